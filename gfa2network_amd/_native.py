@@ -1,0 +1,315 @@
+"""ctypes binding of libg2n.so (include/g2n.h) — the only way Python reaches the GPU path.
+
+The library is built in-tree (gfa2network_amd/_lib/libg2n.so, ``make -C
+gfa2network_amd/csrc`` or ``__graft_entry__.build()``).  There is no fallback: if the
+library or a HIP device is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libg2n.so"
+
+ABI_VERSION = 1
+MAX_PHASES = 24
+
+# status codes (include/g2n.h)
+OK = 0
+E_MALFORMED_L, E_MALFORMED_E, E_MALFORMED_C, E_MALFORMED_P, E_MALFORMED_O = 1, 2, 3, 4, 5
+E_INDEX_LIST, E_INDEX_BYTES, E_UNICODE, E_INT_TOO_LARGE = 6, 7, 8, 9
+E_CAST_OVERFLOW, E_CAST_INF, E_CAST_NAN = 10, 11, 12
+E_ARG, E_IO, E_GZIP, E_DEVICE, E_NOMEM, E_UNSUPPORTED = 13, 14, 15, 16, 17, 18
+
+DTYPE_CODES = {"bool": 0, "int8": 1, "int32": 2, "float32": 3, "float64": 4}
+CODE_DTYPES = {v: np.dtype(k) for k, v in DTYPE_CODES.items()}
+OUT_PARSE, OUT_CSR = 0, 1
+FMT_COO, FMT_CSR = 0, 1
+
+# every symbol include/g2n.h declares (tests check the library exports all of them)
+EXPORTED = [
+    "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_last_error",
+    "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
+    "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
+    "g2n_build_device",
+]
+
+
+class Options(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_uint32),
+        ("directed", ctypes.c_int32),
+        ("bidirected", ctypes.c_int32),
+        ("keep_directed_bidir", ctypes.c_int32),
+        ("asymmetric", ctypes.c_int32),
+        ("strip_orientation", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("output", ctypes.c_int32),
+        ("weight_tag", ctypes.c_char_p),
+        ("want_node_names", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
+    ]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("err_line", ctypes.c_int64),
+        ("err_index", ctypes.c_int64),
+        ("err_value", ctypes.c_double),
+        ("err_detail", ctypes.c_void_p),
+        ("err_detail_len", ctypes.c_int64),
+        ("has_warning", ctypes.c_int32),
+        ("warn_byte", ctypes.c_int32),
+        ("warn_line", ctypes.c_int64),
+        ("n_lines", ctypes.c_int64),
+        ("n_records", ctypes.c_int64),
+        ("n_records_before_error", ctypes.c_int64),
+        ("n_edges", ctypes.c_int64),
+        ("n_nodes", ctypes.c_int64),
+        ("names_blob", ctypes.c_void_p),
+        ("names_offsets", ctypes.c_void_p),
+        ("format", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("index_width", ctypes.c_int32),
+        ("sum_sorted", ctypes.c_int32),
+        ("nnz", ctypes.c_int64),
+        ("rows", ctypes.c_void_p),
+        ("cols", ctypes.c_void_p),
+        ("indptr", ctypes.c_void_p),
+        ("indices", ctypes.c_void_p),
+        ("data", ctypes.c_void_p),
+        ("n_cast_overflow", ctypes.c_int64),
+        ("input_bytes", ctypes.c_uint64),
+        ("n_phases", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("phase_ms", ctypes.c_double * MAX_PHASES),
+        ("phase_names", ctypes.c_char_p * MAX_PHASES),
+        ("host_ms_read", ctypes.c_double),
+        ("host_ms_h2d", ctypes.c_double),
+        ("host_ms_d2h", ctypes.c_double),
+        ("priv_", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+class NativeUnavailable(RuntimeError):
+    """libg2n.so is missing or cannot be loaded (the path has no CPU fallback)."""
+
+
+def load() -> ctypes.CDLL:
+    """Load libg2n.so once; raise NativeUnavailable when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = os.environ.get("G2N_LIB", str(LIB_PATH))
+    if not Path(path).exists():
+        raise NativeUnavailable(
+            f"{path} not found: build it with `make -C gfa2network_amd/csrc` "
+            "(or __graft_entry__.build()); the GFA->CSR path has no CPU fallback")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as exc:  # pragma: no cover - depends on the image
+        raise NativeUnavailable(f"cannot load {path}: {exc}") from exc
+    lib.g2n_version.restype = ctypes.c_char_p
+    lib.g2n_abi_version.restype = ctypes.c_uint32
+    lib.g2n_last_error.restype = ctypes.c_char_p
+    lib.g2n_status_name.restype = ctypes.c_char_p
+    lib.g2n_status_name.argtypes = [ctypes.c_int]
+    lib.g2n_options_init.argtypes = [ctypes.POINTER(Options)]
+    lib.g2n_options_init.restype = None
+    lib.g2n_device_count.restype = ctypes.c_int
+    lib.g2n_build_from_path.argtypes = [ctypes.c_char_p, ctypes.POINTER(Options),
+                                        ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.g2n_build_from_path.restype = ctypes.c_int
+    lib.g2n_build_from_buffer.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Options),
+                                          ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.g2n_build_from_buffer.restype = ctypes.c_int
+    lib.g2n_result_free.argtypes = [ctypes.POINTER(Result)]
+    lib.g2n_result_free.restype = None
+    lib.g2n_coo_to_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.g2n_coo_to_csr.restype = ctypes.c_int
+    lib.g2n_context_create.argtypes = [ctypes.c_int]
+    lib.g2n_context_create.restype = ctypes.c_void_p
+    lib.g2n_context_destroy.argtypes = [ctypes.c_void_p]
+    lib.g2n_context_destroy.restype = None
+    lib.g2n_context_stream.argtypes = [ctypes.c_void_p]
+    lib.g2n_context_stream.restype = ctypes.c_void_p
+    lib.g2n_build_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.POINTER(Options), ctypes.POINTER(Result)]
+    lib.g2n_build_device.restype = ctypes.c_int
+    if lib.g2n_abi_version() != ABI_VERSION:
+        raise NativeUnavailable("libg2n.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().g2n_last_error().decode(errors="replace")
+
+
+def status_name(code: int) -> str:
+    return load().g2n_status_name(code).decode()
+
+
+def make_options(*, directed=True, bidirected=False, keep_directed_bidir=False, asymmetric=False,
+                 strip_orientation=False, dtype="float64", weight_tag=None, output=OUT_PARSE,
+                 want_node_names=True, device=0) -> Options:
+    lib = load()
+    o = Options()
+    lib.g2n_options_init(ctypes.byref(o))
+    o.directed = int(bool(directed))
+    o.bidirected = int(bool(bidirected))
+    o.keep_directed_bidir = int(bool(keep_directed_bidir))
+    o.asymmetric = int(bool(asymmetric))
+    o.strip_orientation = int(bool(strip_orientation))
+    o.dtype = DTYPE_CODES[dtype]
+    o.output = output
+    o.weight_tag = weight_tag.encode("utf-8") if weight_tag else None
+    o.want_node_names = int(bool(want_node_names))
+    o.device = int(device)
+    return o
+
+
+class _Owner:
+    """Frees one g2n_result when the last numpy view of its buffers goes away."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr is not None and _lib is not None:
+            _lib.g2n_result_free(self.ptr)
+            self.ptr = None
+
+
+def _view(addr: int | None, count: int, dtype, owner: _Owner) -> np.ndarray:
+    """Zero-copy numpy view of library-owned host memory, keeping `owner` alive."""
+    dtype = np.dtype(dtype)
+    if not addr or count == 0:
+        return np.zeros(0, dtype=dtype)
+    buf = (ctypes.c_uint8 * (count * dtype.itemsize)).from_address(addr)
+    buf._g2n_owner = owner  # the ctypes buffer (the array's base) pins the result
+    return np.frombuffer(buf, dtype=dtype, count=count)
+
+
+@dataclass
+class RawResult:
+    """What one native build returned, before it is turned into scipy objects."""
+
+    status: int = 0
+    message: str = ""
+    err_line: int = -1
+    err_index: int = -1
+    err_value: float = 0.0
+    err_detail: bytes = b""
+    has_warning: bool = False
+    warn_byte: int = 0
+    warn_line: int = -1
+    n_lines: int = 0
+    n_records: int = 0
+    n_records_before_error: int = 0
+    n_edges: int = 0
+    n_nodes: int = 0
+    names_blob: np.ndarray | None = None
+    names_offsets: np.ndarray | None = None
+    format: str = "coo"
+    dtype: np.dtype = field(default_factory=lambda: np.dtype("float64"))
+    rows: np.ndarray | None = None
+    cols: np.ndarray | None = None
+    indptr: np.ndarray | None = None
+    indices: np.ndarray | None = None
+    data: np.ndarray | None = None
+    sum_sorted: bool = True
+    n_cast_overflow: int = 0
+    phase_ms: dict = field(default_factory=dict)
+    host_ms: dict = field(default_factory=dict)
+
+
+def _from_result(ptr, rc: int) -> RawResult:
+    if not ptr:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    r = ptr.contents
+    owner = _Owner(ptr)
+    out = RawResult(status=r.status, message=last_error() if r.status else "")
+    out.err_line, out.err_index, out.err_value = r.err_line, r.err_index, r.err_value
+    if r.err_detail and r.err_detail_len:
+        out.err_detail = ctypes.string_at(r.err_detail, r.err_detail_len)
+    out.has_warning, out.warn_byte, out.warn_line = bool(r.has_warning), r.warn_byte, r.warn_line
+    out.n_lines, out.n_records = r.n_lines, r.n_records
+    out.n_records_before_error, out.n_edges, out.n_nodes = r.n_records_before_error, r.n_edges, r.n_nodes
+    out.dtype = CODE_DTYPES.get(r.dtype, np.dtype("float64"))
+    out.sum_sorted = bool(r.sum_sorted)
+    out.n_cast_overflow = int(r.n_cast_overflow)
+    if r.status == OK:
+        idx = np.int32 if r.index_width == 4 else np.int64
+        if r.names_offsets:
+            out.names_offsets = _view(r.names_offsets, r.n_nodes + 1, np.int64, owner)
+            out.names_blob = _view(r.names_blob, int(out.names_offsets[-1]), np.uint8, owner)
+        if r.format == FMT_COO:
+            out.format = "coo"
+            out.rows = _view(r.rows, r.nnz, idx, owner)
+            out.cols = _view(r.cols, r.nnz, idx, owner)
+        else:
+            out.format = "csr"
+            out.indptr = _view(r.indptr, r.n_nodes + 1, idx, owner)
+            out.indices = _view(r.indices, r.nnz, idx, owner)
+        out.data = _view(r.data, r.nnz, out.dtype, owner)
+    out.phase_ms = {r.phase_names[k].decode(): r.phase_ms[k] for k in range(r.n_phases)}
+    out.host_ms = {"read": r.host_ms_read, "h2d": r.host_ms_h2d, "d2h": r.host_ms_d2h}
+    return out
+
+
+def build_from_path(path: str, opts: Options) -> RawResult:
+    lib = load()
+    res = ctypes.POINTER(Result)()
+    rc = lib.g2n_build_from_path(os.fsencode(path), ctypes.byref(opts), ctypes.byref(res))
+    return _from_result(res, rc)
+
+
+def build_from_buffer(data: bytes | bytearray | memoryview | np.ndarray, opts: Options) -> RawResult:
+    lib = load()
+    arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    arr = np.ascontiguousarray(arr, dtype=np.uint8)
+    res = ctypes.POINTER(Result)()
+    rc = lib.g2n_build_from_buffer(arr.ctypes.data if arr.size else None, arr.size, ctypes.byref(opts),
+                                   ctypes.byref(res))
+    return _from_result(res, rc)
+
+
+def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int, n_cols: int,
+               device: int = 0) -> RawResult:
+    lib = load()
+    dt = np.dtype(data.dtype)
+    if dt.name not in DTYPE_CODES:
+        raise NotImplementedError(f"GPU COO->CSR supports {sorted(DTYPE_CODES)}, not {dt}")
+    if max(n_rows, n_cols, len(data)) >= 2**31 - 1:
+        raise NotImplementedError("GPU COO->CSR currently needs int32 indices")
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    c = np.ascontiguousarray(cols, dtype=np.int32)
+    d = np.ascontiguousarray(data)
+    res = ctypes.POINTER(Result)()
+    rc = lib.g2n_coo_to_csr(r.ctypes.data, c.ctypes.data, d.ctypes.data, len(d), n_rows, n_cols, 4,
+                            DTYPE_CODES[dt.name], device, ctypes.byref(res))
+    out = _from_result(res, rc)
+    if out.status != OK:
+        raise RuntimeError(f"{status_name(out.status)}: {out.message}")
+    return out
+
+
+def device_count() -> int:
+    return int(load().g2n_device_count())
+
+
+def version() -> str:
+    return load().g2n_version().decode()

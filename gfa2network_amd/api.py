@@ -1,0 +1,268 @@
+"""parse_gfa / convert_format with the reference's call surface, backed by libg2n.so.
+
+Mirrors the matrix subset of sclipman/gfa2network:
+  * ``parse_gfa(path, *, build_graph, build_matrix, ...)``   gfa2network/builders.py:30-299
+  * ``convert_format(A, fmt, *, verbose=False)``             gfa2network/utils.py:40-63
+
+Same keyword names, defaults, returned objects (scipy ``coo_matrix`` in stream order, or
+the MAX-SYM ``csr_matrix``; node list of ``str`` or raw ``bytes``), exception types and
+messages, the one-shot ``RuntimeWarning`` and the ``verbose`` progress strings.  Every
+numeric step runs on the GPU; only the Python objects are assembled here.  Graph-object
+outputs (NetworkX / igraph, split_on_alignment) are outside this port's scope and raise
+``NotImplementedError``.
+"""
+from __future__ import annotations
+
+import gzip
+import os
+import sys
+import time
+import warnings
+import zlib
+from pathlib import Path
+from typing import Any
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _native as nat
+from ._native import RawResult
+
+__all__ = ["parse_gfa", "convert_format", "finalize", "raise_for_status"]
+
+_MALFORMED = {
+    nat.E_MALFORMED_L: "L", nat.E_MALFORMED_E: "E", nat.E_MALFORMED_C: "C",
+    nat.E_MALFORMED_P: "P", nat.E_MALFORMED_O: "O",
+}
+
+
+def raise_for_status(raw: RawResult, dtype: np.dtype, path: Any = None) -> None:
+    """Raise exactly what the reference raises for this failure (type and message)."""
+    s = raw.status
+    if s == nat.OK:
+        return
+    if s in _MALFORMED:  # parser.py:209, 252, 300, 232, 346
+        raise ValueError(f"Malformed {_MALFORMED[s]} record")
+    if s == nat.E_INDEX_LIST:  # parser.py:163 fields[1]
+        raise IndexError("list index out of range")
+    if s == nat.E_INDEX_BYTES:  # parser.py:220-221 u_field[-1] on b""
+        raise IndexError("index out of range")
+    if s == nat.E_UNICODE:  # the same bytes.decode() the reference calls
+        bytes(raw.err_detail).decode()
+        raise AssertionError("decode of the reported bytes unexpectedly succeeded")
+    if s == nat.E_INT_TOO_LARGE:  # builders.py:209 float(int)
+        raise OverflowError("int too large to convert to float")
+    if s == nat.E_CAST_OVERFLOW:  # numpy cast in coo_matrix(..., dtype) (builders.py:281)
+        raise OverflowError(f"Python integer {int(raw.err_value)} out of bounds for {dtype}")
+    if s == nat.E_CAST_INF:
+        raise OverflowError("cannot convert float infinity to integer")
+    if s == nat.E_CAST_NAN:
+        raise ValueError("cannot convert float NaN to integer")
+    if s == nat.E_IO:
+        err = int(raw.err_index)
+        raise OSError(err, os.strerror(err), str(path))
+    if s == nat.E_GZIP:  # gzip.open(...) failures (parser.py:108-109)
+        sub = int(raw.err_index)
+        if sub == 2:
+            raise EOFError(raw.message)
+        if sub == 3:
+            raise zlib.error(raw.message)
+        raise gzip.BadGzipFile(raw.message)
+    raise RuntimeError(f"{nat.status_name(s)}: {raw.message}")
+
+
+def _node_list(raw: RawResult, raw_bytes_id: bool) -> list:
+    """node_list[idx] = node (raw_bytes_id) or node.decode()  (builders.py:284-288)."""
+    offs = raw.names_offsets
+    n = 0 if offs is None else len(offs) - 1
+    if n == 0:
+        return []
+    blob = raw.names_blob
+    # names never contain b"\n" (lines are split on it): join with "\n" and split once
+    total = int(offs[-1])
+    joined = np.empty(total + n - 1, dtype=np.uint8)
+    lens = np.diff(offs)
+    dest = np.arange(total, dtype=np.int64) + np.repeat(np.arange(n, dtype=np.int64), lens)
+    joined[dest] = blob[:total]
+    if n > 1:
+        joined[offs[1:-1] + np.arange(n - 1, dtype=np.int64)] = 0x0A
+    jb = joined.tobytes()
+    if raw_bytes_id:
+        return jb.split(b"\n")
+    try:
+        return jb.decode().split("\n")
+    except UnicodeDecodeError:
+        pass
+    for i in range(n):  # the first undecodable name in id order raises, as in the reference
+        bytes(blob[offs[i]:offs[i + 1]]).decode()
+    raise AssertionError("unreachable")
+
+
+def _progress(n_records: int) -> None:
+    # builders.py:257-258: every 500 000 records yielded
+    for k in range(1, n_records // 500_000 + 1):
+        print(f"\r[{k * 500_000:,} lines]", end="", file=sys.stderr)
+
+
+def finalize(raw: RawResult, *, dtype: np.dtype, return_node_list: bool, raw_bytes_id: bool,
+             verbose: bool, build_matrix: bool = True, path: Any = None):
+    """Turn one native result into the reference's return value / warning / exception."""
+    if raw.status in (nat.E_IO, nat.E_GZIP, nat.E_ARG, nat.E_DEVICE, nat.E_NOMEM, nat.E_UNSUPPORTED):
+        raise_for_status(raw, dtype, path)
+    if raw.has_warning:  # parser.py:124-130
+        warnings.warn(f"Skipping unsupported record: {chr(raw.warn_byte)}", RuntimeWarning, stacklevel=3)
+    parse_failed = nat.OK < raw.status < nat.E_CAST_OVERFLOW
+    if verbose:
+        _progress(raw.n_records_before_error if parse_failed else raw.n_records)
+    if parse_failed:
+        raise_for_status(raw, dtype, path)
+    if verbose:
+        print("\r[parse_gfa] done")
+    if not build_matrix:
+        return None
+    raise_for_status(raw, dtype, path)  # dtype cast errors (after the parse loop)
+    for _ in range(int(raw.n_cast_overflow)):  # numpy's per-element float32 cast warning
+        warnings.warn("overflow encountered in cast", RuntimeWarning, stacklevel=3)
+    n = int(raw.n_nodes)
+    if raw.format == "coo":
+        A = sp.coo_matrix((raw.data, (raw.rows, raw.cols)), shape=(n, n), dtype=dtype)
+    else:
+        A = sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=(n, n), dtype=dtype)
+    if return_node_list:
+        return A, _node_list(raw, raw_bytes_id)
+    return A
+
+
+def _dtype_of(dtype) -> np.dtype:
+    dt = np.dtype(dtype)
+    if dt.name not in nat.DTYPE_CODES:
+        raise NotImplementedError(
+            f"dtype {dt} is not supported by the GPU path (supported: {', '.join(nat.DTYPE_CODES)})")
+    return dt
+
+
+def parse_gfa(
+    path,
+    *,
+    build_graph: bool,
+    build_matrix: bool,
+    directed: bool = True,
+    weight_tag: str | None = None,
+    store_seq: bool = False,
+    store_tags: bool = False,
+    strip_orientation: bool = False,
+    verbose: bool = False,
+    bidirected: bool = False,
+    keep_directed_bidir: bool = False,
+    backend: str = "networkx",
+    dtype: str | object = "float64",
+    asymmetric: bool = False,
+    raw_bytes_id: bool = False,
+    return_node_list: bool = False,
+    max_tag_mb: float = 100.0,
+    split_on_alignment: bool = False,
+    device: int = 0,
+):
+    """GPU ``parse_gfa`` (gfa2network/builders.py:30-299), matrix outputs only.
+
+    Returns ``A`` or ``(A, node_list)`` exactly as the reference does for
+    ``build_graph=False, build_matrix=True``.
+    """
+    if backend == "igraph":
+        raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
+    if split_on_alignment:
+        raise NotImplementedError("split_on_alignment is outside the GPU GFA->CSR path")
+    if return_node_list and not build_matrix:  # builders.py:129-130
+        raise ValueError("return_node_list requires build_matrix=True")
+    if build_graph:
+        raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
+    dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
+    opts = nat.make_options(
+        directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+        asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
+        weight_tag=weight_tag or None, output=nat.OUT_PARSE,
+        want_node_names=bool(return_node_list), device=device)
+    raw = _run(path, opts)
+    return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
+                    verbose=verbose, build_matrix=build_matrix, path=path)
+
+
+def _run(path, opts) -> RawResult:
+    """GFAParser's source rules (parser.py:95-112): file object, '-' = stdin, else a path."""
+    if hasattr(path, "read"):
+        return nat.build_from_buffer(path.read(), opts)
+    p = str(path)
+    if p == "-":
+        return nat.build_from_buffer(sys.stdin.buffer.read(), opts)
+    return nat.build_from_path(p, opts)
+
+
+def _native_tocsr(A, device: int = 0):
+    """scipy coo.tocsr() on the GPU: duplicates summed in dtype in scipy's order."""
+    n_rows, n_cols = A.shape
+    raw = nat.coo_to_csr(A.row, A.col, A.data, n_rows, n_cols, device)
+    return sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype)
+
+
+def _native_tocsc(A, device: int = 0):
+    """scipy coo.tocsc(): the CSR of the transposed coordinates, read as CSC."""
+    n_rows, n_cols = A.shape
+    raw = nat.coo_to_csr(A.col, A.row, A.data, n_cols, n_rows, device)
+    return sp.csc_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype)
+
+
+def convert_format(A, fmt: str, *, verbose: bool = False):
+    """GPU ``convert_format`` (gfa2network/utils.py:40-63)."""
+    fmt = fmt.lower()
+    if fmt not in {"csr", "csc", "coo", "dok"}:
+        raise ValueError("matrix-format must be csr|csc|coo|dok")
+    if fmt == "coo":
+        return A
+    if verbose:
+        start = time.perf_counter()
+        print(f"[convert] -> {fmt} …", end="", file=sys.stderr, flush=True)
+    if fmt == A.format:
+        out = A
+    elif fmt == "dok":
+        raise NotImplementedError("dok output is outside the GPU GFA->CSR path")
+    else:
+        coo = A if A.format == "coo" else A.tocoo()
+        out = _native_tocsr(coo) if fmt == "csr" else _native_tocsc(coo)
+    if verbose:
+        print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
+    return out
+
+
+def save_matrix(A, dest: Path, *, verbose: bool = False, max_dense_gb: float = 5.0):
+    """Writer of ``convert --matrix`` (gfa2network/utils.py:66-105): same guard and formats."""
+    MAX_DENSE_BYTES = max_dense_gb * 1_000_000_000
+    dest = Path(dest)
+    if dest.suffix in {".csv", ".npy"}:
+        nnz = A.nnz if sp.issparse(A) else A.size
+        itemsize = A.dtype.itemsize if hasattr(A, "dtype") else 8
+        if nnz * itemsize > MAX_DENSE_BYTES:
+            raise MemoryError(
+                f"dense export would allocate {nnz*itemsize/1e9:.1f} GB; choose a sparse .npz or write an edge list instead"
+            )
+    if verbose:
+        start = time.perf_counter()
+        print(f"[save] {dest.suffix[1:]} → {dest}", "...", end="", file=sys.stderr, flush=True)
+    if dest.suffix == ".npz":
+        sp.save_npz(dest, A)
+    elif dest.suffix == ".npy":
+        np.save(dest, A.toarray() if sp.issparse(A) else A)
+    elif dest.suffix == ".csv":
+        np.savetxt(dest, A.toarray() if sp.issparse(A) else A, delimiter=",", fmt="%.6g")
+    else:
+        raise ValueError("matrix path must end with .npz, .npy, or .csv")
+    if verbose:
+        print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
+
+
+def save_node_map(nodes, dest: Path) -> None:
+    """``<matrix>.nodes.tsv`` sidecar (gfa2network/utils.py:108-114): ``i\\tname\\n``."""
+    with open(dest, "w") as fh:
+        for i, node in enumerate(nodes):
+            if isinstance(node, (bytes, bytearray)):
+                node = node.decode()
+            fh.write(f"{i}\t{node}\n")

@@ -1,0 +1,150 @@
+// g2n_kernels.h — device-side data layout shared by the kernels and the pipeline driver.
+//
+// HBM layout of one build (all SoA, sized from counts read back between phases):
+//   in[len]                      GFA bytes (read-only)
+//   ls[n_lines + 1]   u64        line start offsets (ls[n_lines] = len)
+//   kind[n_lines]     u8         kSkip / kUnknown / kS / kEdge / kPO
+//   pack[n_lines]     u64        exclusive scan of (touches << 32 | edges) per line
+//   touches (n_t):   noff u64, nlen u32 [, ooff u64, olen u32 when bidirected], slot u32
+//   edges   (n_e):   w f64 (weight before the dtype cast), tb u32 (first touch)
+//   table[cap]        u64        (hash tag << 32 | first touch), cap = pow2 >= 2 n_t
+//   first/nid u32, flen/foff u64 per touch; names blob + offsets
+//   rows/cols i32, data T per triplet; sort keys u64 + stream positions u32
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "stl_sort.h"
+
+namespace g2n {
+
+constexpr int kTPB = 256;
+constexpr int kNlIters = 8;
+constexpr uint64_t kNlTile = (uint64_t)kTPB * 16 * kNlIters;  // 32 KiB of input per block
+
+enum : uint8_t { kSkip = 0, kUnknown = 1, kS = 2, kEdge = 3, kPO = 4 };
+
+// error codes (= G2N_E_* in include/g2n.h)
+enum : uint32_t {
+  kErrMalformedL = 1,
+  kErrMalformedE = 2,
+  kErrMalformedC = 3,
+  kErrMalformedP = 4,
+  kErrMalformedO = 5,
+  kErrIndexList = 6,
+  kErrIndexBytes = 7,
+  kErrUnicode = 8,
+  kErrIntTooLarge = 9,
+  kErrCastOverflow = 10,
+  kErrCastInf = 11,
+  kErrCastNan = 12,
+};
+
+// an orientation span whose offset carries this flag is the constant byte (off & 0xFF)
+constexpr uint64_t kConstFlag = 1ull << 62;
+constexpr unsigned long long kEmptySlot = ~0ull;
+
+// device control block: counters and first-error words (zeroed / ~0 per build)
+struct Ctl {
+  unsigned long long err_key;    // min over (line << 5 | code)
+  unsigned long long warn_line;  // min line whose first byte is not in SLPECOHF
+  unsigned long long cast_key;   // min over (triplet << 4 | code)
+  unsigned long long wl_count;   // deferred weights
+  unsigned long long n_lines;
+  unsigned long long n_records;
+  unsigned long long n_edges;
+  unsigned long long n_s;
+  unsigned long long n_records_before;
+  unsigned long long n_nodes;
+  unsigned long long names_len;
+  unsigned long long table_overflow;
+  unsigned long long detail_off;
+  unsigned long long detail_len;
+  unsigned long long unsorted[2];
+  unsigned long long flagged[2];
+  unsigned long long n_unique[2];
+  unsigned long long n_keep;
+  unsigned long long n_f32_overflow;  // edges whose float32 cast overflowed
+  unsigned long long pad[6];
+};
+
+struct ParseOpts {
+  int bidir, keep, strip, has_wt;
+  uint32_t wt_len;
+  const uint8_t* wt;  // device copy of the weight tag bytes
+};
+
+struct TouchOut {
+  uint64_t* noff;
+  uint32_t* nlen;
+  uint64_t* ooff;
+  uint32_t* olen;
+};
+struct TouchIn {
+  const uint64_t* noff;
+  const uint32_t* nlen;
+  const uint64_t* ooff;
+  const uint32_t* olen;
+};
+struct EdgeOut {
+  double* w;
+  uint32_t* tb;
+};
+struct EdgeIn {
+  const double* w;
+  const uint32_t* tb;
+};
+
+// ---- kernels (g2n_kernels.hip) ----
+__global__ void k_nl_count(const uint8_t* in, uint64_t len, uint64_t* tile_cnt);
+__global__ void k_nl_write(const uint8_t* in, uint64_t len, const uint64_t* tile_base, uint64_t* ls);
+__global__ void k_nl_finish(const uint8_t* in, uint64_t len, const uint64_t* tile_base, const uint64_t* tile_cnt,
+                            uint64_t n_tiles, uint64_t* ls, Ctl* ctl);
+__global__ void k_classify(const uint8_t* in, const uint64_t* ls, uint64_t n_lines, uint32_t tps, uint32_t tpe,
+                           uint8_t* kind, uint64_t* pack, Ctl* ctl);
+__global__ void k_parse(const uint8_t* in, const uint64_t* ls, const uint8_t* kind, const uint64_t* pack_scan,
+                        uint64_t n_lines, ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl, uint64_t* worklist);
+__global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint64_t* pack_scan,
+                               const uint64_t* worklist, uint64_t n_work, ParseOpts op, EdgeOut E, Ctl* ctl);
+__global__ void k_error_detail(const uint8_t* in, const uint64_t* ls, uint64_t line, Ctl* ctl);
+__global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
+__global__ void k_insert(const uint8_t* in, TouchIn T, uint64_t n_t, unsigned long long* table, uint64_t mask,
+                         uint32_t* slot, int bidir, Ctl* ctl);
+__global__ void k_first(TouchIn T, uint64_t n_t, const unsigned long long* table, const uint32_t* slot, int bidir,
+                        uint32_t* first, uint64_t* flen);
+__global__ void k_totals(const uint32_t* first, const uint32_t* nid, const uint64_t* flen, const uint64_t* foff,
+                         uint64_t n_t, Ctl* ctl);
+__global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_t, const uint32_t* first, const uint32_t* nid,
+                        const uint64_t* foff, int bidir, uint8_t* blob, int64_t* offs, const Ctl* ctl);
+template <class T>
+__global__ void k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* slot, const unsigned long long* table,
+                           const uint32_t* nid, int tpe, int gd, int32_t* rows, int32_t* cols, T* data, Ctl* ctl);
+__global__ void k_make_keys(const int32_t* rows, const int32_t* cols, uint64_t n, int nb, int transposed,
+                            unsigned long long* keys, uint32_t* vals);
+__global__ void k_heads(const unsigned long long* keys, const uint32_t* vals, uint64_t n, int nb, uint32_t* head,
+                        Ctl* ctl, int which);
+__global__ void k_count_from_scan(const uint32_t* flag, const uint32_t* pos, uint64_t n, unsigned long long* out);
+template <class T>
+__global__ void k_group_sum(const unsigned long long* keys, const uint32_t* vals, uint64_t n, const uint32_t* head,
+                            const uint32_t* hpos, const T* data, int nb, unsigned long long* ukeys, T* udata,
+                            uint8_t* rowflag, Ctl* ctl, int which);
+template <class I>
+__global__ void k_indptr(const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, int nb,
+                         uint64_t n_rows, I* indptr);
+template <class I>
+__global__ void k_split_keys(const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, int nb,
+                             I* indices);
+template <class T>
+__global__ void k_emulate_rows(const unsigned long long* keys, const uint32_t* vals, uint64_t n, int nb,
+                               uint64_t n_rows, const uint8_t* rowflag, const T* data,
+                               const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, T* udata,
+                               KV<int32_t, T>* kv, uint32_t* ord);
+template <class T>
+__global__ void k_maxsym(const unsigned long long* mk, const uint32_t* mv, uint64_t m, const T* ua, const T* ut,
+                         uint32_t* keep, T* mval);
+template <class T>
+__global__ void k_compact(const unsigned long long* mk, const T* mval, const uint32_t* keep, const uint32_t* kpos,
+                          uint64_t m, unsigned long long* okeys, T* odata);
+__global__ void k_tag_values(uint64_t n, uint32_t tag, uint32_t* v);
+
+}  // namespace g2n

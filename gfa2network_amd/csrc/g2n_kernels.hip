@@ -1,0 +1,1098 @@
+// g2n_kernels.hip — gfx950 kernels of the GFA -> CSR path.
+//
+// Replaces, on the GPU, the reference's per-line Python loops:
+//   K1 nl_count / nl_write   `for line in fh`                    gfa2network/parser.py:114
+//   K2 classify              first-byte dispatch + fields[0]      parser.py:117-134
+//   K3 parse                 split(b"\t") + _parse_link/_edge/... parser.py:133-361,
+//                            tag weight (fast grammar)            parser.py:179-204, builders.py:205-209
+//   K3b weights_slow         exact CPython int()/float() for the rest (pylit.h)
+//   K4 insert                node2idx dict (first-touch ids)      builders.py:190-198, 218-221
+//   K5 first/names           dict insertion order, node_list      builders.py:284-288
+//   K6 triplets              add_mat_edge + dtype cast            builders.py:222-234, 280-281
+//   K7-K9 (sort, group_sum, emulate_rows, maxsym)  coo.tocsr / A.maximum(A.T)
+//                            (scipy sparsetools coo_tocsr, csr_sort_indices,
+//                             csr_sum_duplicates, csr_maximum_csr)  builders.py:281-283, utils.py:55
+// Integer / byte work only; every kernel is HBM- or latency-bound (no MFMA).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "g2n_kernels.h"
+#include "pylit.h"
+#include "stl_sort.h"
+
+namespace g2n {
+
+// ------------------------------------------------------------------ helpers --------
+__device__ inline uint32_t byte_match_mask(uint32_t w, uint32_t pat) {
+  // 0x80 in every byte of w equal to the byte in pat (exact, no false positives)
+  uint32_t x = w ^ pat;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+
+// first '\t' in [p, end), or end
+__device__ inline uint64_t next_tab(const uint8_t* __restrict__ in, uint64_t p, uint64_t end) {
+  while (p < end && (p & 3)) {
+    if (in[p] == '\t') return p;
+    p++;
+  }
+  while (p + 4 <= end) {
+    uint32_t w = *(const uint32_t*)(in + p);
+    uint32_t m = byte_match_mask(w, 0x09090909u);
+    if (m) return p + (uint64_t)(__builtin_ctz(m) >> 3);
+    p += 4;
+  }
+  while (p < end) {
+    if (in[p] == '\t') return p;
+    p++;
+  }
+  return end;
+}
+
+__device__ inline uint64_t next_byte(const uint8_t* __restrict__ in, uint64_t p, uint64_t end, uint8_t c) {
+  while (p < end && in[p] != c) p++;
+  return p;
+}
+
+template <class T>
+__device__ inline T wave_reduce_sum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+template <class T>
+__device__ inline T wave_reduce_min(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_down(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// exclusive scan of one u32 per thread over a 256-thread block; returns the block total
+__device__ inline uint32_t block_excl_scan_u32(uint32_t v, uint32_t* excl, uint32_t* lds /* >= 4 */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  uint32_t wbase = 0, tot = 0;
+  for (int w = 0; w < kTPB / 64; w++) {
+    uint32_t s = lds[w];
+    if (w < wid) wbase += s;
+    tot += s;
+  }
+  __syncthreads();
+  *excl = wbase + x - v;
+  return tot;
+}
+
+// 16 bytes at pos (pos 16-aligned); bytes at or beyond len read as 0
+__device__ inline uint4 load16(const uint8_t* __restrict__ in, uint64_t pos, uint64_t len) {
+  if (pos + 16 <= len) return *(const uint4*)(in + pos);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int b = 0; b < 16; b++)
+    if (pos + b < len) w[b >> 2] |= (uint32_t)in[pos + b] << ((b & 3) * 8);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ================================================================= K1: lines ======
+__global__ void __launch_bounds__(kTPB) k_nl_count(const uint8_t* __restrict__ in, uint64_t len,
+                                                   uint64_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t red[kTPB / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kNlTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kNlIters; j++) {
+    uint64_t pos = base + (uint64_t)j * (kTPB * 16) + (uint64_t)threadIdx.x * 16;
+    if (pos < len) {
+      uint4 v = load16(in, pos, len);
+      c += __popc(byte_match_mask(v.x, 0x0A0A0A0Au)) + __popc(byte_match_mask(v.y, 0x0A0A0A0Au)) +
+           __popc(byte_match_mask(v.z, 0x0A0A0A0Au)) + __popc(byte_match_mask(v.w, 0x0A0A0A0Au));
+    }
+  }
+  c = wave_reduce_sum(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kTPB / 64; w++) t += red[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// ls[r + 1] = 1 + position of the r-th '\n' (0-based over the whole input)
+__global__ void __launch_bounds__(kTPB) k_nl_write(const uint8_t* __restrict__ in, uint64_t len,
+                                                   const uint64_t* __restrict__ tile_base,
+                                                   uint64_t* __restrict__ ls) {
+  __shared__ uint32_t lds[kTPB / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kNlTile;
+  uint64_t run = tile_base[blockIdx.x];
+  for (int j = 0; j < kNlIters; j++) {
+    uint64_t seg = base + (uint64_t)j * (kTPB * 16);
+    if (seg >= len) break;  // uniform over the block
+    uint64_t pos = seg + (uint64_t)threadIdx.x * 16;
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    if (pos < len) {
+      uint4 v = load16(in, pos, len);
+      m0 = byte_match_mask(v.x, 0x0A0A0A0Au);
+      m1 = byte_match_mask(v.y, 0x0A0A0A0Au);
+      m2 = byte_match_mask(v.z, 0x0A0A0A0Au);
+      m3 = byte_match_mask(v.w, 0x0A0A0A0Au);
+    }
+    uint32_t c = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
+    uint32_t off;
+    uint32_t tot = block_excl_scan_u32(c, &off, lds);
+    if (c) {
+      uint64_t r = run + off + 1;
+      uint32_t ms[4] = {m0, m1, m2, m3};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t m = ms[q];
+        while (m) {
+          int b = __builtin_ctz(m) >> 3;
+          m &= m - 1;
+          ls[r++] = pos + (uint64_t)(q * 4 + b) + 1;
+        }
+      }
+    }
+    run += tot;
+  }
+}
+
+// n_lines and the end sentinel (ls[n_lines] = len)
+__global__ void k_nl_finish(const uint8_t* __restrict__ in, uint64_t len, const uint64_t* __restrict__ tile_base,
+                            const uint64_t* __restrict__ tile_cnt, uint64_t n_tiles, uint64_t* __restrict__ ls,
+                            Ctl* ctl) {
+  uint64_t total = n_tiles ? tile_base[n_tiles - 1] + tile_cnt[n_tiles - 1] : 0;
+  uint64_t n_lines = total;
+  if (len > 0 && in[len - 1] != '\n') n_lines++;
+  ls[0] = 0;
+  ls[n_lines] = len;
+  ctl->n_lines = n_lines;
+}
+
+// ================================================================ K2: classify ====
+__global__ void __launch_bounds__(kTPB) k_classify(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
+                                                   uint64_t n_lines, uint32_t tps, uint32_t tpe,
+                                                   uint8_t* __restrict__ kind, uint64_t* __restrict__ pack,
+                                                   Ctl* ctl) {
+  __shared__ unsigned long long s_min[kTPB / 64];
+  __shared__ unsigned long long s_cnt[3][kTPB / 64];
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  unsigned long long unk = ~0ull;
+  unsigned long long nrec = 0, nedge = 0, ns = 0;
+  if (i < n_lines) {
+    uint64_t s = ls[i], e = ls[i + 1];
+    uint8_t c0 = in[s];
+    bool exact = (s + 1 == e);
+    if (!exact) {
+      uint8_t c1 = in[s + 1];
+      exact = (c1 == '\t' || c1 == '\n');
+    }
+    uint8_t k = kSkip;
+    uint64_t pk = 0;
+    switch (c0) {
+      case 'S':
+        if (exact) { k = kS; pk = (uint64_t)tps << 32; ns = 1; nrec = 1; }
+        break;
+      case 'L': case 'E': case 'C':
+        if (exact) { k = kEdge; pk = ((uint64_t)tpe << 32) | 1u; nedge = 1; nrec = 1; }
+        break;
+      case 'P': case 'O':
+        if (exact) { k = kPO; nrec = 1; }
+        break;
+      case 'H': case 'F':
+        break;
+      default:
+        k = kUnknown;
+        unk = i;
+    }
+    kind[i] = k;
+    pack[i] = pk;
+  }
+  unk = wave_reduce_min(unk);
+  nrec = wave_reduce_sum(nrec);
+  nedge = wave_reduce_sum(nedge);
+  ns = wave_reduce_sum(ns);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_min[w] = unk;
+    s_cnt[0][w] = nrec;
+    s_cnt[1][w] = nedge;
+    s_cnt[2][w] = ns;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = ~0ull, a = 0, b = 0, c = 0;
+    for (int q = 0; q < kTPB / 64; q++) {
+      m = s_min[q] < m ? s_min[q] : m;
+      a += s_cnt[0][q];
+      b += s_cnt[1][q];
+      c += s_cnt[2][q];
+    }
+    if (m != ~0ull) atomicMin(&ctl->warn_line, m);
+    if (a) atomicAdd(&ctl->n_records, a);
+    if (b) atomicAdd(&ctl->n_edges, b);
+    if (c) atomicAdd(&ctl->n_s, c);
+  }
+}
+
+// ================================================================ K3: parse =======
+__device__ inline void record_error(Ctl* ctl, uint64_t line, uint32_t code) {
+  atomicMin(&ctl->err_key, (unsigned long long)((line << 5) | code));
+}
+
+struct EdgeLayout {
+  uint64_t uo, vo, ouo, ovo;  // offsets (ou/ov may carry kConstFlag)
+  uint32_t ul, vl, oul, ovl;
+  uint64_t tag_start;          // first tag field start, valid when has_tags
+  bool has_tags;
+  uint32_t err;                // 0 or an error code
+  uint64_t err_off;            // G2N_E_UNICODE: the span whose decode fails
+  uint32_t err_len;
+};
+
+__device__ inline uint64_t rstrip_pm(const uint8_t* __restrict__ in, uint64_t off, uint64_t len) {
+  while (len > 0) {
+    uint8_t c = in[off + len - 1];
+    if (c != '+' && c != '-') break;
+    len--;
+  }
+  return len;
+}
+
+__device__ inline bool int_bytes_ok(const uint8_t* __restrict__ in, uint64_t s, uint64_t e) {
+  return py_int_literal(in + s, e - s, false, nullptr);
+}
+
+// Field layout of an L/E/C line [s, e) ('\n' already stripped): parser.py:206-341.
+__device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_t s, uint64_t e) {
+  EdgeLayout L;
+  L.err = 0;
+  L.has_tags = false;
+  L.tag_start = e;
+  uint64_t fs[10], fe[10];
+  int nf = 0;
+  uint64_t p = s;
+  bool more = true;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    fs[k] = e;
+    fe[k] = e;
+    if (more) {
+      fs[k] = p;
+      fe[k] = next_tab(in, p, e);
+      nf = k + 1;
+      if (fe[k] == e) more = false;
+      else p = fe[k] + 1;
+    }
+  }
+  const uint8_t t = in[s];
+  int tag_from = 0;
+  if (t == 'L') {
+    if (nf < 5) { L.err = kErrMalformedL; return L; }
+    uint8_t c2 = fe[2] > fs[2] ? in[fs[2]] : 0;
+    if (fe[2] - fs[2] == 1 && (c2 == '+' || c2 == '-')) {
+      L.uo = fs[1]; L.ul = (uint32_t)(fe[1] - fs[1]);
+      L.ouo = kConstFlag | c2; L.oul = 1;
+      L.vo = fs[3]; L.vl = (uint32_t)(fe[3] - fs[3]);
+      L.ovo = fs[4]; L.ovl = (uint32_t)(fe[4] - fs[4]);
+      if (!utf8_valid(in + L.ovo, L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
+      tag_from = 6;
+    } else {
+      if (fe[1] == fs[1] || fe[2] == fs[2]) { L.err = kErrIndexBytes; return L; }
+      uint8_t lu = in[fe[1] - 1], lv = in[fe[2] - 1];
+      L.ouo = kConstFlag | ((lu == '+' || lu == '-') ? lu : '+'); L.oul = 1;
+      L.ovo = kConstFlag | ((lv == '+' || lv == '-') ? lv : '+'); L.ovl = 1;
+      L.uo = fs[1]; L.ul = (uint32_t)rstrip_pm(in, fs[1], fe[1] - fs[1]);
+      L.vo = fs[2]; L.vl = (uint32_t)rstrip_pm(in, fs[2], fe[2] - fs[2]);
+      tag_from = 4;
+    }
+  } else {
+    const bool isE = t == 'E';
+    if (nf < (isE ? 6 : 5)) { L.err = isE ? kErrMalformedE : kErrMalformedC; return L; }
+    bool coords = nf >= 9 && int_bytes_ok(in, fs[3], fe[3]) && int_bytes_ok(in, fs[4], fe[4]) &&
+                  int_bytes_ok(in, fs[6], fe[6]) && int_bytes_ok(in, fs[7], fe[7]);
+    if (coords) {
+      uint64_t ul = fe[2] - fs[2], vl = fe[5] - fs[5];
+      L.ouo = kConstFlag | ((ul && in[fe[2] - 1] == '-') ? '-' : '+'); L.oul = 1;
+      L.ovo = kConstFlag | ((vl && in[fe[5] - 1] == '-') ? '-' : '+'); L.ovl = 1;
+      L.uo = fs[2]; L.ul = (uint32_t)rstrip_pm(in, fs[2], ul);
+      L.vo = fs[5]; L.vl = (uint32_t)rstrip_pm(in, fs[5], vl);
+      tag_from = 9;
+    } else if (isE) {
+      L.uo = fs[2]; L.ul = (uint32_t)(fe[2] - fs[2]);
+      L.ouo = fs[3]; L.oul = (uint32_t)(fe[3] - fs[3]);
+      L.vo = fs[4]; L.vl = (uint32_t)(fe[4] - fs[4]);
+      L.ovo = fs[5]; L.ovl = (uint32_t)(fe[5] - fs[5]);
+      tag_from = 6;
+    } else {
+      L.uo = fs[1]; L.ul = (uint32_t)(fe[1] - fs[1]);
+      L.ouo = fs[2]; L.oul = (uint32_t)(fe[2] - fs[2]);
+      L.vo = fs[3]; L.vl = (uint32_t)(fe[3] - fs[3]);
+      L.ovo = fs[4]; L.ovl = (uint32_t)(fe[4] - fs[4]);
+      tag_from = 5;
+    }
+    if (!coords) {
+      if (!utf8_valid(in + L.ouo, L.oul)) { L.err = kErrUnicode; L.err_off = L.ouo; L.err_len = L.oul; return L; }
+      if (!utf8_valid(in + L.ovo, L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
+    }
+  }
+  // fields[tag_from:] (tag_from <= 9, static selects keep fs[] in registers)
+  uint64_t ts = e;
+  bool have = nf > tag_from;
+  switch (tag_from) {
+    case 4: ts = fs[4]; break;
+    case 5: ts = fs[5]; break;
+    case 6: ts = fs[6]; break;
+    default: ts = fs[9]; break;
+  }
+  L.has_tags = have;
+  L.tag_start = ts;
+  return L;
+}
+
+__device__ inline bool span_eq(const uint8_t* __restrict__ in, uint64_t off, uint64_t len,
+                               const uint8_t* __restrict__ w, uint32_t wl) {
+  if (len != wl) return false;
+  for (uint32_t k = 0; k < wl; k++)
+    if (in[off + k] != w[k]) return false;
+  return true;
+}
+
+// Weight by the fast grammar.  Returns false when a matching tag needs the exact path.
+__device__ inline bool weight_fast(const uint8_t* __restrict__ in, uint64_t ts, uint64_t e, bool has_tags,
+                                   const uint8_t* __restrict__ wt, uint32_t wtl, double* w) {
+  *w = 1.0;
+  if (!has_tags) return true;
+  int kind = 0;  // 0 none, 1 number, 2 other
+  double num = 1.0;
+  uint64_t p = ts;
+  while (true) {
+    uint64_t fe = next_tab(in, p, e);
+    uint64_t c1 = next_byte(in, p, fe, ':');
+    if (c1 < fe && c1 - p == wtl && span_eq(in, p, wtl, wt, wtl)) {
+      uint64_t c2 = next_byte(in, c1 + 1, fe, ':');
+      if (c2 < fe) {
+        for (uint64_t q = p; q < fe; q++)
+          if (in[q] >= 0x80) return false;
+        uint64_t tl = c2 - c1 - 1;
+        uint8_t ty = in[c1 + 1];
+        if (tl == 1 && ty == 'i') {
+          double v;
+          if (!fast_int(in + c2 + 1, fe - c2 - 1, &v)) return false;
+          kind = 1;
+          num = v;
+        } else if (tl == 1 && ty == 'f') {
+          double v;
+          if (!fast_float(in + c2 + 1, fe - c2 - 1, &v)) return false;
+          kind = 1;
+          num = v;
+        } else {
+          kind = 2;
+        }
+      }
+    }
+    if (fe >= e) break;
+    p = fe + 1;
+  }
+  *w = kind == 1 ? num : 1.0;
+  return true;
+}
+
+__device__ inline void put_touch(const TouchOut& T, uint64_t t, uint64_t no, uint32_t nl, uint64_t oo, uint32_t ol,
+                                 bool bidir) {
+  T.noff[t] = no;
+  T.nlen[t] = nl;
+  if (bidir) {
+    T.ooff[t] = oo;
+    T.olen[t] = ol;
+  }
+}
+
+__device__ inline uint64_t rev_ori(const uint8_t* __restrict__ in, uint64_t oo, uint32_t ol) {
+  // builders.py:232-233: "-" if orientation == "+" else "+"
+  bool plus = (oo & kConstFlag) ? ((oo & 0xFF) == '+') : (ol == 1 && in[oo] == '+');
+  return kConstFlag | (plus ? '-' : '+');
+}
+
+__global__ void __launch_bounds__(kTPB) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
+                                                const uint8_t* __restrict__ kind,
+                                                const uint64_t* __restrict__ pack_scan, uint64_t n_lines,
+                                                ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl,
+                                                uint64_t* __restrict__ worklist) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n_lines) return;
+  const uint8_t k = kind[i];
+  if (k == kSkip || k == kUnknown) return;
+  uint64_t s = ls[i], e = ls[i + 1];
+  if (e > s && in[e - 1] == '\n') e--;
+  if (k == kPO) {  // parser.py:231-232, 345-346: fewer than 3 fields
+    uint64_t t1 = next_tab(in, s, e);
+    if (t1 >= e || next_tab(in, t1 + 1, e) >= e) record_error(ctl, i, in[s] == 'P' ? kErrMalformedP : kErrMalformedO);
+    return;
+  }
+  const uint64_t pk = pack_scan[i];
+  const uint64_t tb = pk >> 32;
+  if (k == kS) {  // parser.py:163, builders.py:190-198
+    uint64_t t1 = next_tab(in, s, e);
+    if (t1 >= e) {
+      record_error(ctl, i, kErrIndexList);
+      return;
+    }
+    uint64_t ns = t1 + 1;
+    uint64_t ne = next_tab(in, ns, e);
+    uint32_t nl = (uint32_t)(ne - ns);
+    if (!op.bidir) {
+      put_touch(T, tb, ns, nl, 0, 0, false);
+    } else {
+      put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true);
+      put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true);
+    }
+    return;
+  }
+  // L / E / C
+  const uint64_t eb = pk & 0xFFFFFFFFull;
+  EdgeLayout L = edge_layout(in, s, e);
+  if (L.err) {
+    record_error(ctl, i, L.err);
+    return;
+  }
+  if (op.strip) {  // builders.py:202-204
+    L.ul = (uint32_t)rstrip_pm(in, L.uo, L.ul);
+    L.vl = (uint32_t)rstrip_pm(in, L.vo, L.vl);
+  }
+  double w = 1.0;
+  if (op.has_wt) {
+    if (!weight_fast(in, L.tag_start, e, L.has_tags, op.wt, op.wt_len, &w)) {
+      unsigned long long slot = atomicAdd(&ctl->wl_count, 1ull);
+      worklist[slot] = i;
+      w = 0.0;
+    }
+  }
+  E.w[eb] = w;
+  E.tb[eb] = (uint32_t)tb;
+  if (!op.bidir) {
+    put_touch(T, tb, L.uo, L.ul, 0, 0, false);
+    put_touch(T, tb + 1, L.vo, L.vl, 0, 0, false);
+  } else {
+    put_touch(T, tb, L.uo, L.ul, L.ouo, L.oul, true);
+    put_touch(T, tb + 1, L.vo, L.vl, L.ovo, L.ovl, true);
+    if (!op.keep) {  // builders.py:231-234: v:rev(ori_to), u:rev(ori_from)
+      put_touch(T, tb + 2, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, true);
+      put_touch(T, tb + 3, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, true);
+    }
+  }
+}
+
+// Exact weights (CPython int()/float() semantics) for the edges the fast grammar deferred.
+__global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
+                                                     const uint64_t* __restrict__ pack_scan,
+                                                     const uint64_t* __restrict__ worklist, uint64_t n_work,
+                                                     ParseOpts op, EdgeOut E, Ctl* ctl) {
+  const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= n_work) return;
+  const uint64_t i = worklist[j];
+  uint64_t s = ls[i], e = ls[i + 1];
+  if (e > s && in[e - 1] == '\n') e--;
+  EdgeLayout L = edge_layout(in, s, e);
+  const uint64_t eb = pack_scan[i] & 0xFFFFFFFFull;
+  Decimal dec;
+  uint8_t tmp[DEC_TMP];
+  // _parse_tags over fields[tag_from:], keeping only the final value for weight_tag
+  int kind = 0;  // 0 none, 1 int, 2 float, 3 other
+  uint64_t best_s = 0, best_e = 0;
+  double fval = 0.0;
+  if (L.has_tags) {
+    uint64_t p = L.tag_start;
+    while (true) {
+      uint64_t fe = next_tab(in, p, e);
+      if (utf8_valid(in + p, fe - p)) {
+        uint64_t c1 = next_byte(in, p, fe, ':');
+        uint64_t c2 = c1 < fe ? next_byte(in, c1 + 1, fe, ':') : fe;
+        if (c2 < fe && span_eq(in, p, c1 - p, op.wt, op.wt_len)) {
+          uint64_t tl = c2 - c1 - 1;
+          uint8_t ty = in[c1 + 1];
+          if (tl == 1 && ty == 'i') {
+            if (py_int_literal(in + c2 + 1, fe - c2 - 1, true, nullptr)) {
+              kind = 1;
+              best_s = c2 + 1;
+              best_e = fe;
+            }
+          } else if (tl == 1 && ty == 'f') {
+            double v;
+            if (py_float_literal(in + c2 + 1, fe - c2 - 1, true, &v, &dec, tmp)) {
+              kind = 2;
+              fval = v;
+            }
+          } else {
+            kind = 3;
+          }
+        }
+      }
+      if (fe >= e) break;
+      p = fe + 1;
+    }
+  }
+  double w = 1.0;
+  if (kind == 1) {
+    py_int_literal(in + best_s, best_e - best_s, true, &dec);
+    if (!py_int_to_f64(&dec, &w, tmp)) {  // builders.py:209 float(val): OverflowError
+      record_error(ctl, i, kErrIntTooLarge);
+      return;
+    }
+  } else if (kind == 2) {
+    w = fval;
+  }
+  E.w[eb] = w;
+}
+
+// Re-parse the failing line to recover the bytes whose .decode() raised.
+__global__ void k_error_detail(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls, uint64_t line,
+                               Ctl* ctl) {
+  uint64_t s = ls[line], e = ls[line + 1];
+  if (e > s && in[e - 1] == '\n') e--;
+  EdgeLayout L = edge_layout(in, s, e);
+  ctl->detail_off = L.err == kErrUnicode ? L.err_off : s;
+  ctl->detail_len = L.err == kErrUnicode ? L.err_len : 1;
+}
+
+// records on lines before `line` (verbose progress before an error, builders.py:257-258)
+__global__ void __launch_bounds__(kTPB) k_count_records(const uint8_t* __restrict__ kind, uint64_t line, Ctl* ctl) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  unsigned long long c = 0;
+  if (i < line) {
+    uint8_t k = kind[i];
+    c = (k == kS || k == kEdge || k == kPO) ? 1 : 0;
+  }
+  c = wave_reduce_sum(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&ctl->n_records_before, c);
+}
+
+// ============================================================= K4: dictionary =====
+__device__ inline uint8_t touch_byte(const uint8_t* __restrict__ in, uint64_t no, uint32_t nl, uint64_t oo,
+                                     uint64_t j) {
+  if (j < nl) return in[no + j];
+  if (j == nl) return ':';
+  return (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + (j - nl - 1)];
+}
+
+__device__ inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+__device__ inline uint64_t touch_hash(const uint8_t* __restrict__ in, uint64_t no, uint32_t nl, uint64_t oo,
+                                      uint32_t ol, bool bidir) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint32_t j = 0; j < nl; j++) h = (h ^ in[no + j]) * 0x100000001b3ull;
+  if (bidir) {
+    h = (h ^ (uint64_t)':') * 0x100000001b3ull;
+    if (oo & kConstFlag) {
+      h = (h ^ (oo & 0xFF)) * 0x100000001b3ull;
+    } else {
+      for (uint32_t j = 0; j < ol; j++) h = (h ^ in[oo + j]) * 0x100000001b3ull;
+    }
+  }
+  return fmix64(h ^ ((uint64_t)nl << 40) ^ ol);
+}
+
+__device__ inline bool touch_eq(const uint8_t* __restrict__ in, const TouchIn& T, uint64_t a, uint64_t b,
+                                bool bidir) {
+  uint64_t na = T.noff[a], nb = T.noff[b];
+  uint32_t la = T.nlen[a], lb = T.nlen[b];
+  if (!bidir) {
+    if (la != lb) return false;
+    for (uint32_t j = 0; j < la; j++)
+      if (in[na + j] != in[nb + j]) return false;
+    return true;
+  }
+  uint64_t oa = T.ooff[a], ob = T.ooff[b];
+  uint32_t pa = T.olen[a], pb = T.olen[b];
+  uint64_t tl = (uint64_t)la + 1 + pa;
+  if (tl != (uint64_t)lb + 1 + pb) return false;
+  if (la == lb) {  // common case: same split point
+    for (uint32_t j = 0; j < la; j++)
+      if (in[na + j] != in[nb + j]) return false;
+    for (uint32_t j = 0; j < pa; j++) {
+      uint8_t x = (oa & kConstFlag) ? (uint8_t)(oa & 0xFF) : in[oa + j];
+      uint8_t y = (ob & kConstFlag) ? (uint8_t)(ob & 0xFF) : in[ob + j];
+      if (x != y) return false;
+    }
+    return true;
+  }
+  for (uint64_t j = 0; j < tl; j++)
+    if (touch_byte(in, na, la, oa, j) != touch_byte(in, nb, lb, ob, j)) return false;
+  return true;
+}
+
+// Open-addressing table, 64-bit slots = (hash tag << 32) | representative touch.  A slot's
+// representative is lowered by atomicMin to the FIRST touch of its key, which is exactly
+// what Python's dict insertion order needs.
+__global__ void __launch_bounds__(kTPB) k_insert(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_t,
+                                                 unsigned long long* __restrict__ table, uint64_t mask,
+                                                 uint32_t* __restrict__ slot, int bidir, Ctl* ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t >= n_t) return;
+  const uint64_t no = T.noff[t];
+  const uint32_t nl = T.nlen[t];
+  const uint64_t oo = bidir ? T.ooff[t] : 0;
+  const uint32_t ol = bidir ? T.olen[t] : 0;
+  const uint64_t h = touch_hash(in, no, nl, oo, ol, bidir != 0);
+  const uint32_t tag = (uint32_t)(h >> 32);
+  const unsigned long long mine = ((unsigned long long)tag << 32) | (uint32_t)t;
+  uint64_t idx = h & mask;
+  for (uint64_t probe = 0; probe <= mask; probe++) {
+    unsigned long long cur = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == kEmptySlot) {
+      cur = atomicCAS(&table[idx], kEmptySlot, mine);
+      if (cur == kEmptySlot) {
+        slot[t] = (uint32_t)idx;
+        return;
+      }
+    }
+    if ((uint32_t)(cur >> 32) == tag && touch_eq(in, T, t, (uint32_t)cur, bidir != 0)) {
+      if ((uint32_t)cur > (uint32_t)t) atomicMin(&table[idx], mine);
+      slot[t] = (uint32_t)idx;
+      return;
+    }
+    idx = (idx + 1) & mask;
+  }
+  ctl->table_overflow = 1;
+}
+
+// first[t] = 1 iff t is the first touch of its key; flen[t] = key length if first
+__global__ void __launch_bounds__(kTPB) k_first(TouchIn T, uint64_t n_t, const unsigned long long* __restrict__ table,
+                                                const uint32_t* __restrict__ slot, int bidir,
+                                                uint32_t* __restrict__ first, uint64_t* __restrict__ flen) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t >= n_t) return;
+  bool f = (uint32_t)table[slot[t]] == (uint32_t)t;
+  first[t] = f ? 1u : 0u;
+  flen[t] = f ? (uint64_t)T.nlen[t] + (bidir ? 1ull + T.olen[t] : 0ull) : 0ull;
+}
+
+__global__ void k_totals(const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
+                         const uint64_t* __restrict__ flen, const uint64_t* __restrict__ foff, uint64_t n_t,
+                         Ctl* ctl) {
+  ctl->n_nodes = n_t ? (uint64_t)nid[n_t - 1] + first[n_t - 1] : 0;
+  ctl->names_len = n_t ? foff[n_t - 1] + flen[n_t - 1] : 0;
+}
+
+// names blob in id order + offsets (builders.py:284-288 node_list)
+__global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_t,
+                                                const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
+                                                const uint64_t* __restrict__ foff, int bidir,
+                                                uint8_t* __restrict__ blob, int64_t* __restrict__ offs,
+                                                const Ctl* ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t == 0) offs[ctl->n_nodes] = (int64_t)ctl->names_len;
+  if (t >= n_t || !first[t]) return;
+  const uint64_t o = foff[t];
+  offs[nid[t]] = (int64_t)o;
+  const uint64_t no = T.noff[t];
+  const uint32_t nl = T.nlen[t];
+  for (uint32_t j = 0; j < nl; j++) blob[o + j] = in[no + j];
+  if (bidir) {
+    const uint64_t oo = T.ooff[t];
+    const uint32_t ol = T.olen[t];
+    blob[o + nl] = ':';
+    for (uint32_t j = 0; j < ol; j++) blob[o + nl + 1 + j] = (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + j];
+  }
+}
+
+// ============================================================ K6: triplets ========
+// numpy's np.array(list_of_python_floats, dtype) element conversion (builders.py:281)
+template <class T>
+struct Cast;
+template <>
+struct Cast<uint8_t> {  // bool: w != 0
+  __device__ static uint32_t go(double w, uint8_t* o) { *o = (w != 0.0) ? 1 : 0; return 0; }
+};
+template <>
+struct Cast<int8_t> {
+  __device__ static uint32_t go(double w, int8_t* o) {
+    if (w != w) return kErrCastNan;
+    if (__builtin_isinf(w)) return kErrCastInf;
+    double t = __builtin_trunc(w);
+    if (t < -128.0 || t > 127.0) return kErrCastOverflow;
+    *o = (int8_t)(int)t;
+    return 0;
+  }
+};
+template <>
+struct Cast<int32_t> {
+  __device__ static uint32_t go(double w, int32_t* o) {
+    if (w != w) return kErrCastNan;
+    if (__builtin_isinf(w)) return kErrCastInf;
+    double t = __builtin_trunc(w);
+    if (t < -2147483648.0 || t > 2147483647.0) return kErrCastOverflow;
+    *o = (int32_t)t;
+    return 0;
+  }
+};
+template <>
+struct Cast<float> {  // x86 cvtsd2ss: NaN keeps sign, payload truncated, quiet bit set
+  __device__ static uint32_t go(double w, float* o) {
+    if (w != w) {
+      uint64_t b = f64_bits(w);
+      uint32_t f = (uint32_t)(b >> 32 & 0x80000000u) | 0x7FC00000u | (uint32_t)((b >> 29) & 0x3FFFFFu);
+      *o = __uint_as_float(f);
+    } else {
+      *o = (float)w;
+    }
+    return 0;
+  }
+};
+template <>
+struct Cast<double> {
+  __device__ static uint32_t go(double w, double* o) { *o = w; return 0; }
+};
+
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* __restrict__ slot,
+                                                   const unsigned long long* __restrict__ table,
+                                                   const uint32_t* __restrict__ nid, int tpe, int gd,
+                                                   int32_t* __restrict__ rows, int32_t* __restrict__ cols,
+                                                   T* __restrict__ data, Ctl* ctl) {
+  const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (e >= n_e) return;
+  const uint64_t tb = E.tb[e];
+  auto id = [&](uint64_t t) -> int32_t { return (int32_t)nid[(uint32_t)table[slot[t]]]; };
+  T v;
+  const double wv = E.w[e];
+  uint32_t err = Cast<T>::go(wv, &v);
+  if (std::is_same<T, float>::value && !__builtin_isinf(wv) && wv == wv && __builtin_isinf((double)v))
+    atomicAdd(&ctl->n_f32_overflow, 1ull);
+  const int k = tpe == 4 ? 4 : (gd ? 1 : 2);
+  const uint64_t o = e * (uint64_t)k;
+  if (err) {
+    atomicMin(&ctl->cast_key, (unsigned long long)((o << 4) | err));
+    return;
+  }
+  int32_t a = id(tb), b = id(tb + 1);
+  rows[o] = a;
+  cols[o] = b;
+  data[o] = v;
+  if (k >= 2) {
+    rows[o + 1] = b;
+    cols[o + 1] = a;
+    data[o + 1] = v;
+  }
+  if (k == 4) {  // bidirected twin (v:rev(ori_to), u:rev(ori_from)), both directions
+    int32_t c = id(tb + 2), d = id(tb + 3);
+    rows[o + 2] = c;
+    cols[o + 2] = d;
+    data[o + 2] = v;
+    rows[o + 3] = d;
+    cols[o + 3] = c;
+    data[o + 3] = v;
+  }
+}
+
+// ======================================================= K7-K9: COO -> CSR ========
+__global__ void __launch_bounds__(kTPB) k_make_keys(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                                    uint64_t n, int nb, int transposed,
+                                                    unsigned long long* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  uint64_t r = (uint32_t)rows[i], c = (uint32_t)cols[i];
+  if (transposed) {
+    uint64_t t = r;
+    r = c;
+    c = t;
+  }
+  keys[i] = (r << nb) | c;
+  vals[i] = (uint32_t)i;
+}
+
+// group heads; and scipy's has_sorted_indices of the scattered matrix: within a row, the
+// stream order of entries must have non-decreasing columns, i.e. after a stable sort by
+// (row, col) the stream positions must increase along the row.
+__global__ void __launch_bounds__(kTPB) k_heads(const unsigned long long* __restrict__ keys,
+                                                const uint32_t* __restrict__ vals, uint64_t n, int nb,
+                                                uint32_t* __restrict__ head, Ctl* ctl, int which) {
+  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (p >= n) return;
+  bool h = p == 0 || keys[p] != keys[p - 1];
+  head[p] = h ? 1u : 0u;
+  if (p > 0 && (keys[p] >> nb) == (keys[p - 1] >> nb) && vals[p - 1] > vals[p]) ctl->unsorted[which] = 1;
+}
+
+__global__ void k_count_from_scan(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos, uint64_t n,
+                                  unsigned long long* out) {
+  *out = n ? (unsigned long long)pos[n - 1] + flag[n - 1] : 0ull;
+}
+
+// x86-64 SSE semantics of scipy's `x += y` (csr_sum_duplicates), bit for bit
+template <class T>
+struct Acc;
+template <>
+struct Acc<uint8_t> {
+  __device__ static uint8_t add(uint8_t x, uint8_t y) { return (x | y) ? 1 : 0; }  // npy_bool_wrapper
+  __device__ static bool is_float() { return false; }
+  __device__ static double limit() { return 0.0; }
+};
+template <>
+struct Acc<int8_t> {
+  __device__ static int8_t add(int8_t x, int8_t y) { return (int8_t)(uint8_t)((uint8_t)x + (uint8_t)y); }
+  __device__ static bool is_float() { return false; }
+  __device__ static double limit() { return 0.0; }
+};
+template <>
+struct Acc<int32_t> {
+  __device__ static int32_t add(int32_t x, int32_t y) { return (int32_t)((uint32_t)x + (uint32_t)y); }
+  __device__ static bool is_float() { return false; }
+  __device__ static double limit() { return 0.0; }
+};
+template <>
+struct Acc<float> {
+  __device__ static float add(float x, float y) {
+    if (x != x) return __uint_as_float(__float_as_uint(x) | 0x00400000u);
+    if (y != y) return __uint_as_float(__float_as_uint(y) | 0x00400000u);
+    float r = x + y;
+    if (r != r) return __uint_as_float(0xFFC00000u);  // x86 default NaN (inf + -inf)
+    return r;
+  }
+  __device__ static bool is_float() { return true; }
+  __device__ static double limit() { return 16777216.0; }
+};
+template <>
+struct Acc<double> {
+  __device__ static double add(double x, double y) {
+    if (x != x) return bits_f64(f64_bits(x) | 0x0008000000000000ull);
+    if (y != y) return bits_f64(f64_bits(y) | 0x0008000000000000ull);
+    double r = x + y;
+    if (r != r) return bits_f64(0xFFF8000000000000ull);
+    return r;
+  }
+  __device__ static bool is_float() { return true; }
+  __device__ static double limit() { return 9007199254740992.0; }
+};
+
+template <class T>
+__device__ inline bool exact_term(T v) {
+  double d = (double)v;
+  return d == __builtin_trunc(d);  // integral (false for inf/nan)
+}
+
+// Sum each (row, col) group in stream order (= scipy's order whenever it is provably
+// order-independent); flag rows whose float groups could depend on std::sort's order.
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_group_sum(const unsigned long long* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals, uint64_t n,
+                                                    const uint32_t* __restrict__ head,
+                                                    const uint32_t* __restrict__ hpos,
+                                                    const T* __restrict__ data, int nb,
+                                                    unsigned long long* __restrict__ ukeys, T* __restrict__ udata,
+                                                    uint8_t* __restrict__ rowflag, Ctl* ctl, int which) {
+  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (p >= n || !head[p]) return;
+  const unsigned long long key = keys[p];
+  const uint64_t u = hpos[p];
+  T x = data[vals[p]];
+  bool exact = true;
+  double sabs = 0.0;
+  if (Acc<T>::is_float()) {
+    exact = exact_term(x);
+    sabs = __builtin_fabs((double)x);
+  }
+  uint64_t q = p + 1;
+  uint32_t cnt = 1;
+  while (q < n && keys[q] == key) {
+    T y = data[vals[q]];
+    if (Acc<T>::is_float()) {
+      exact = exact && exact_term(y);
+      sabs += __builtin_fabs((double)y);
+    }
+    x = Acc<T>::add(x, y);
+    q++;
+    cnt++;
+  }
+  ukeys[u] = key;
+  udata[u] = x;
+  if (Acc<T>::is_float() && cnt >= 3 && !(exact && sabs < Acc<T>::limit())) {
+    rowflag[key >> nb] = 1;
+    ctl->flagged[which] = 1;
+  }
+}
+
+__device__ inline uint64_t lower_bound_u64(const unsigned long long* __restrict__ a, uint64_t n,
+                                           unsigned long long key) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <class I>
+__global__ void __launch_bounds__(kTPB) k_indptr(const unsigned long long* __restrict__ ukeys,
+                                                 const unsigned long long* __restrict__ n_unique_ptr, int nb,
+                                                 uint64_t n_rows, I* __restrict__ indptr) {
+  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (r > n_rows) return;
+  const uint64_t nu = *n_unique_ptr;
+  indptr[r] = (I)(r == n_rows ? nu : lower_bound_u64(ukeys, nu, (unsigned long long)r << nb));
+}
+
+template <class I>
+__global__ void __launch_bounds__(kTPB) k_split_keys(const unsigned long long* __restrict__ ukeys,
+                                                     const unsigned long long* __restrict__ n_unique_ptr, int nb,
+                                                     I* __restrict__ indices) {
+  const uint64_t u = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (u >= *n_unique_ptr) return;
+  indices[u] = (I)(ukeys[u] & ((1ull << nb) - 1));
+}
+
+// Rows whose sums could depend on the order: redo exactly what scipy does for the row —
+// scatter in stream order (coo_tocsr), std::sort by column (csr_sort_indices, restated in
+// stl_sort.h), left-to-right run sums (csr_sum_duplicates).  Only rows of > 16 entries get
+// here: std::sort on <= 16 elements is an insertion sort, which is stable.
+template <class T>
+__global__ void __launch_bounds__(64) k_emulate_rows(const unsigned long long* __restrict__ keys,
+                                                     const uint32_t* __restrict__ vals, uint64_t n, int nb,
+                                                     uint64_t n_rows, const uint8_t* __restrict__ rowflag,
+                                                     const T* __restrict__ data,
+                                                     const unsigned long long* __restrict__ ukeys,
+                                                     const unsigned long long* __restrict__ n_unique_ptr,
+                                                     T* __restrict__ udata, KV<int32_t, T>* __restrict__ kv,
+                                                     uint32_t* __restrict__ ord) {
+  const uint64_t r = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_rows || !rowflag[r]) return;
+  const uint64_t rs = lower_bound_u64(keys, n, (unsigned long long)r << nb);
+  const uint64_t re = lower_bound_u64(keys, n, (unsigned long long)(r + 1) << nb);
+  const uint64_t len = re - rs;
+  if (len <= 16) return;
+  // stream order of the row: sort its sorted positions (rs..re) by stream index (heap sort)
+  uint32_t* o = ord + rs;
+  for (uint64_t q = 0; q < len; q++) o[q] = (uint32_t)q;
+  const uint32_t* sv = vals + rs;
+  auto sift = [&](int64_t root, int64_t end) {
+    while (true) {
+      int64_t c = 2 * root + 1;
+      if (c >= end) break;
+      if (c + 1 < end && sv[o[c + 1]] > sv[o[c]]) c++;
+      if (sv[o[c]] > sv[o[root]]) {
+        uint32_t t = o[c];
+        o[c] = o[root];
+        o[root] = t;
+        root = c;
+      } else {
+        break;
+      }
+    }
+  };
+  for (int64_t st = (int64_t)len / 2 - 1; st >= 0; st--) sift(st, (int64_t)len);
+  for (int64_t end = (int64_t)len - 1; end > 0; end--) {
+    uint32_t t = o[0];
+    o[0] = o[end];
+    o[end] = t;
+    sift(0, end);
+  }
+  // (col, val) pairs in stream order = coo_tocsr's scatter order for this row
+  KV<int32_t, T>* a = kv + rs;
+  const uint64_t cmask = (1ull << nb) - 1;
+  for (uint64_t q = 0; q < len; q++) {
+    const uint64_t z = rs + o[q];
+    a[q].k = (int32_t)(keys[z] & cmask);
+    a[q].v = data[vals[z]];
+  }
+  stl_sort(a, a + len);
+  const uint64_t us = lower_bound_u64(ukeys, *n_unique_ptr, (unsigned long long)r << nb);
+  uint64_t g = 0, q = 0;
+  while (q < len) {
+    int32_t c = a[q].k;
+    T x = a[q].v;
+    q++;
+    while (q < len && a[q].k == c) {
+      x = Acc<T>::add(x, a[q].v);
+      q++;
+    }
+    udata[us + g] = x;
+    g++;
+  }
+}
+
+// M = maximum(B, B^T') over the merged key streams of B and BT (csr_binop_csr_canonical
+// with std::max: (a < b) ? b : a, missing = 0, results == 0 dropped).
+template <class T>
+__device__ inline bool nonzero(T x) { return x != (T)0; }
+
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_maxsym(const unsigned long long* __restrict__ mk,
+                                                 const uint32_t* __restrict__ mv, uint64_t m,
+                                                 const T* __restrict__ ua, const T* __restrict__ ut,
+                                                 uint32_t* __restrict__ keep, T* __restrict__ mval) {
+  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (p >= m) return;
+  if (p > 0 && mk[p] == mk[p - 1]) {
+    keep[p] = 0;
+    return;
+  }
+  T a = (T)0, b = (T)0;
+  uint32_t v0 = mv[p];
+  if (v0 >> 31) b = ut[v0 & 0x7FFFFFFFu];
+  else a = ua[v0];
+  if (p + 1 < m && mk[p + 1] == mk[p]) {
+    uint32_t v1 = mv[p + 1];
+    if (v1 >> 31) b = ut[v1 & 0x7FFFFFFFu];
+    else a = ua[v1];
+  }
+  T r = (a < b) ? b : a;
+  keep[p] = nonzero(r) ? 1u : 0u;
+  mval[p] = r;
+}
+
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_compact(const unsigned long long* __restrict__ mk,
+                                                  const T* __restrict__ mval, const uint32_t* __restrict__ keep,
+                                                  const uint32_t* __restrict__ kpos, uint64_t m,
+                                                  unsigned long long* __restrict__ okeys, T* __restrict__ odata) {
+  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (p >= m || !keep[p]) return;
+  okeys[kpos[p]] = mk[p];
+  odata[kpos[p]] = mval[p];
+}
+
+__global__ void __launch_bounds__(kTPB) k_tag_values(uint64_t n, uint32_t tag, uint32_t* __restrict__ v) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i | tag;
+}
+
+// ----------------------------------------------------------- explicit instances --
+#define G2N_INST(T)                                                                                              \
+  template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const unsigned long long*,             \
+                                         const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
+  template __global__ void k_group_sum<T>(const unsigned long long*, const uint32_t*, uint64_t, const uint32_t*,  \
+                                          const uint32_t*, const T*, int, unsigned long long*, T*, uint8_t*,      \
+                                          Ctl*, int);                                                            \
+  template __global__ void k_emulate_rows<T>(const unsigned long long*, const uint32_t*, uint64_t, int, uint64_t, \
+                                             const uint8_t*, const T*, const unsigned long long*,                 \
+                                             const unsigned long long*, T*, KV<int32_t, T>*, uint32_t*);          \
+  template __global__ void k_maxsym<T>(const unsigned long long*, const uint32_t*, uint64_t, const T*, const T*,  \
+                                       uint32_t*, T*);                                                           \
+  template __global__ void k_compact<T>(const unsigned long long*, const T*, const uint32_t*, const uint32_t*,    \
+                                        uint64_t, unsigned long long*, T*);
+G2N_INST(uint8_t)
+G2N_INST(int8_t)
+G2N_INST(int32_t)
+G2N_INST(float)
+G2N_INST(double)
+#undef G2N_INST
+template __global__ void k_indptr<int32_t>(const unsigned long long*, const unsigned long long*, int, uint64_t,
+                                           int32_t*);
+template __global__ void k_split_keys<int32_t>(const unsigned long long*, const unsigned long long*, int, int32_t*);
+
+}  // namespace g2n

@@ -1,0 +1,733 @@
+// g2n_pipeline.hip — drives the gfx950 kernels for one GFA -> CSR build.
+//
+// One build = one pass over the input bytes resident in HBM:
+//   lines -> classify -> parse (+ exact weights) -> dictionary -> names -> triplets
+//   -> [COO out]  or  sort + group sums (+ std::sort emulation rows) -> [SUM CSR]
+//   -> transposed sort + sums, merge, maximum -> [MAX-SYM CSR]
+// Scans / radix sort / merge are rocPRIM device primitives; every other step is a
+// hand-written kernel in g2n_kernels.hip.  Counts are read back between phases (a few
+// small synchronous copies per build) to size the next phase's buffers exactly.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <rocprim/rocprim.hpp>
+
+#include "g2n_internal.h"
+#include "g2n_kernels.hip"
+
+#define G2N_HIP(call)                                                                                      \
+  do {                                                                                                     \
+    hipError_t e_ = (call);                                                                                \
+    if (e_ != hipSuccess)                                                                                  \
+      throw ::g2n::Failure(G2N_E_DEVICE, std::string(#call " failed: ") + hipGetErrorString(e_));          \
+  } while (0)
+
+namespace g2n {
+
+// ----------------------------------------------------------------- arena ----------
+enum Slot {
+  S_IN, S_TILE_CNT, S_TILE_BASE, S_LS, S_KIND, S_PACK, S_PACK_SCAN, S_NOFF, S_NLEN, S_OOFF, S_OLEN, S_EW, S_ETB,
+  S_WL, S_TABLE, S_SLOT, S_FIRST, S_NID, S_FLEN, S_FOFF, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1,
+  S_VALS0, S_VALS1, S_HEAD, S_HPOS, S_UKEYS0, S_UDATA0, S_UKEYS1, S_UDATA1, S_ROWFLAG, S_KV, S_ORD, S_MK, S_MV,
+  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_NSLOTS
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace g2n
+
+struct g2n_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<g2n::DevBuf> bufs;
+  g2n::Ctl* ctl = nullptr;    // device
+  g2n::Ctl* h_ctl = nullptr;  // pinned host mirror
+  hipEvent_t ev[G2N_MAX_PHASES + 1];
+  int n_ev = 0;
+  const char* ev_name[G2N_MAX_PHASES];
+  std::mutex mu;
+};
+
+namespace g2n {
+
+static void* dbuf(g2n_context* c, int slot, size_t bytes) {
+  DevBuf& b = c->bufs[slot];
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) G2N_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 8 + 256;
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+      (void)hipGetLastError();
+      throw Failure(G2N_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+    }
+    b.cap = want;
+  }
+  return b.p;
+}
+template <class T>
+static T* dget(g2n_context* c, int slot, uint64_t count) {
+  return (T*)dbuf(c, slot, (size_t)count * sizeof(T));
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned tpb = kTPB) {
+  uint64_t g = (n + tpb - 1) / tpb;
+  return (unsigned)(g ? g : 1);
+}
+
+static void phase(g2n_context* c, const char* name) {
+  if (c->n_ev >= G2N_MAX_PHASES) return;
+  c->ev_name[c->n_ev] = name;
+  G2N_HIP(hipEventRecord(c->ev[c->n_ev + 1], c->stream));
+  c->n_ev++;
+}
+
+static void sync_ctl(g2n_context* c) {
+  G2N_HIP(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+template <class T>
+static T read_dev(g2n_context* c, const T* p) {
+  T v;
+  G2N_HIP(hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  return v;
+}
+
+// rocPRIM wrappers (query temp size, grow the TEMP slot, run)
+template <class T>
+static void excl_scan(g2n_context* c, const T* in, T* out, uint64_t n) {
+  if (n == 0) return;
+  size_t tb = 0;
+  G2N_HIP(rocprim::exclusive_scan(nullptr, tb, in, out, T(0), (size_t)n, rocprim::plus<T>(), c->stream));
+  void* tmp = dbuf(c, S_TEMP, tb);
+  G2N_HIP(rocprim::exclusive_scan(tmp, tb, in, out, T(0), (size_t)n, rocprim::plus<T>(), c->stream));
+}
+
+static void sort_pairs(g2n_context* c, const unsigned long long* kin, unsigned long long* kout, const uint32_t* vin,
+                       uint32_t* vout, uint64_t n, int bits) {
+  if (n == 0) return;
+  size_t tb = 0;
+  G2N_HIP(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, c->stream));
+  void* tmp = dbuf(c, S_TEMP, tb);
+  G2N_HIP(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, c->stream));
+}
+
+static void merge_pairs(g2n_context* c, const unsigned long long* k1, const unsigned long long* k2,
+                        unsigned long long* ko, const uint32_t* v1, const uint32_t* v2, uint32_t* vo, uint64_t n1,
+                        uint64_t n2) {
+  if (n1 + n2 == 0) return;
+  size_t tb = 0;
+  G2N_HIP(rocprim::merge(nullptr, tb, k1, k2, ko, v1, v2, vo, (size_t)n1, (size_t)n2,
+                         rocprim::less<unsigned long long>(), c->stream));
+  void* tmp = dbuf(c, S_TEMP, tb);
+  G2N_HIP(rocprim::merge(tmp, tb, k1, k2, ko, v1, v2, vo, (size_t)n1, (size_t)n2,
+                         rocprim::less<unsigned long long>(), c->stream));
+}
+
+static int bits_for(uint64_t n) {  // bits to hold values 0..n-1 (>= 1)
+  int b = 1;
+  while (b < 63 && (1ull << b) < n) b++;
+  return b;
+}
+
+static size_t dtype_size(int dt) {
+  switch (dt) {
+    case G2N_BOOL: case G2N_INT8: return 1;
+    case G2N_INT32: case G2N_FLOAT32: return 4;
+    default: return 8;
+  }
+}
+
+// ------------------------------------------------- SUM (coo.tocsr) on device -------
+struct SumOut {
+  unsigned long long* ukeys;
+  void* udata;
+  uint64_t n_unique;
+  bool unsorted, flagged;
+};
+
+template <class T>
+static SumOut sum_duplicates(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n,
+                             uint64_t n_rows, int nb, int which) {
+  SumOut o{};
+  auto* k0 = dget<unsigned long long>(c, S_KEYS0, n);
+  auto* k1 = dget<unsigned long long>(c, S_KEYS1, n);
+  auto* v0 = dget<uint32_t>(c, S_VALS0, n);
+  auto* v1 = dget<uint32_t>(c, S_VALS1, n);
+  auto* head = dget<uint32_t>(c, S_HEAD, n);
+  auto* hpos = dget<uint32_t>(c, S_HPOS, n);
+  auto* uk = dget<unsigned long long>(c, which ? S_UKEYS1 : S_UKEYS0, n);
+  T* ud = dget<T>(c, which ? S_UDATA1 : S_UDATA0, n);
+  auto* rowflag = dget<uint8_t>(c, S_ROWFLAG, n_rows);
+  G2N_HIP(hipMemsetAsync(rowflag, 0, n_rows ? n_rows : 1, c->stream));
+  if (n) {
+    hipLaunchKernelGGL(k_make_keys, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, nb, which, k0, v0);
+    sort_pairs(c, k0, k1, v0, v1, n, 2 * nb);
+    hipLaunchKernelGGL(k_heads, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, k1, v1, n, nb, head, c->ctl, which);
+    excl_scan<uint32_t>(c, head, hpos, n);
+    hipLaunchKernelGGL(k_count_from_scan, dim3(1), dim3(1), 0, c->stream, head, hpos, n, &c->ctl->n_unique[which]);
+    hipLaunchKernelGGL((k_group_sum<T>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, k1, v1, n, head, hpos, data,
+                       nb, uk, ud, rowflag, c->ctl, which);
+  }
+  sync_ctl(c);
+  o.n_unique = n ? c->h_ctl->n_unique[which] : 0;
+  o.unsorted = c->h_ctl->unsorted[which] != 0;
+  o.flagged = c->h_ctl->flagged[which] != 0;
+  if (n && o.unsorted && o.flagged) {
+    auto* kv = dget<KV<int32_t, T>>(c, S_KV, n);
+    auto* ord = dget<uint32_t>(c, S_ORD, n);
+    hipLaunchKernelGGL((k_emulate_rows<T>), dim3(grid_for(n_rows, 64)), dim3(64), 0, c->stream, k1, v1, n, nb,
+                       n_rows, rowflag, data, uk, &c->ctl->n_unique[which], ud, kv, ord);
+  }
+  o.ukeys = uk;
+  o.udata = ud;
+  return o;
+}
+
+static void csr_from_keys(g2n_context* c, const unsigned long long* uk, const unsigned long long* n_unique_dev,
+                          uint64_t nnz, uint64_t n_rows, int nb, int32_t** indptr, int32_t** indices) {
+  *indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
+  *indices = dget<int32_t>(c, S_INDICES, nnz);
+  hipLaunchKernelGGL(k_indptr<int32_t>, dim3(grid_for(n_rows + 1)), dim3(kTPB), 0, c->stream, uk, n_unique_dev, nb,
+                     n_rows, *indptr);
+  if (nnz)
+    hipLaunchKernelGGL(k_split_keys<int32_t>, dim3(grid_for(nnz)), dim3(kTPB), 0, c->stream, uk, n_unique_dev, nb,
+                       *indices);
+}
+
+// SUM CSR, or MAX-SYM CSR when maxsym, from device COO triplets.
+template <class T>
+static void assemble(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
+                     uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
+  const int nb = bits_for(n_rows > n_cols ? n_rows : n_cols);
+  SumOut A = sum_duplicates<T>(c, rows, cols, data, n_trip, n_rows, nb, 0);
+  R->sum_sorted = A.unsorted ? 0 : 1;
+  phase(c, "sum");
+  int32_t *indptr, *indices;
+  if (!maxsym) {
+    csr_from_keys(c, A.ukeys, &c->ctl->n_unique[0], A.n_unique, n_rows, nb, &indptr, &indices);
+    R->format = G2N_FMT_CSR;
+    R->nnz = (int64_t)A.n_unique;
+    R->indptr = indptr;
+    R->indices = indices;
+    R->data = A.udata;
+    phase(c, "csr");
+    return;
+  }
+  // A.maximum(A.T): B = SUM(A) above, BT = SUM(A.T) with A.T's own scatter order
+  SumOut B = sum_duplicates<T>(c, rows, cols, data, n_trip, n_rows, nb, 1);
+  phase(c, "sum_t");
+  const uint64_t m = A.n_unique + B.n_unique;
+  auto* va = dget<uint32_t>(c, S_TVALS0, A.n_unique);
+  auto* vb = dget<uint32_t>(c, S_TVALS1, B.n_unique);
+  if (A.n_unique)
+    hipLaunchKernelGGL(k_tag_values, dim3(grid_for(A.n_unique)), dim3(kTPB), 0, c->stream, A.n_unique, 0u, va);
+  if (B.n_unique)
+    hipLaunchKernelGGL(k_tag_values, dim3(grid_for(B.n_unique)), dim3(kTPB), 0, c->stream, B.n_unique,
+                       0x80000000u, vb);
+  auto* mk = dget<unsigned long long>(c, S_MK, m);
+  auto* mv = dget<uint32_t>(c, S_MV, m);
+  merge_pairs(c, A.ukeys, B.ukeys, mk, va, vb, mv, A.n_unique, B.n_unique);
+  T* mval = dget<T>(c, S_MVAL, m);
+  auto* keep = dget<uint32_t>(c, S_KEEP, m);
+  auto* kpos = dget<uint32_t>(c, S_KPOS, m);
+  auto* okeys = dget<unsigned long long>(c, S_OKEYS, m);
+  T* odata = dget<T>(c, S_ODATA, m);
+  uint64_t nk = 0;
+  if (m) {
+    hipLaunchKernelGGL((k_maxsym<T>), dim3(grid_for(m)), dim3(kTPB), 0, c->stream, mk, mv, m, (const T*)A.udata,
+                       (const T*)B.udata, keep, mval);
+    excl_scan<uint32_t>(c, keep, kpos, m);
+    hipLaunchKernelGGL(k_count_from_scan, dim3(1), dim3(1), 0, c->stream, keep, kpos, m, &c->ctl->n_keep);
+    hipLaunchKernelGGL((k_compact<T>), dim3(grid_for(m)), dim3(kTPB), 0, c->stream, mk, mval, keep, kpos, m, okeys,
+                       odata);
+    nk = read_dev(c, &c->ctl->n_keep);
+  } else {
+    G2N_HIP(hipMemsetAsync(&c->ctl->n_keep, 0, sizeof(unsigned long long), c->stream));
+  }
+  phase(c, "maxsym");
+  csr_from_keys(c, okeys, &c->ctl->n_keep, nk, n_rows, nb, &indptr, &indices);
+  R->format = G2N_FMT_CSR;
+  R->nnz = (int64_t)nk;
+  R->indptr = indptr;
+  R->indices = indices;
+  R->data = odata;
+  phase(c, "csr");
+}
+
+template <class T>
+static void run_triplets(g2n_context* c, EdgeIn E, uint64_t n_e, const uint32_t* slot,
+                         const unsigned long long* table, const uint32_t* nid, int tpe, int gd, int32_t* rows,
+                         int32_t* cols, void* data) {
+  if (n_e)
+    hipLaunchKernelGGL((k_triplets<T>), dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E, n_e, slot, table, nid, tpe,
+                       gd, rows, cols, (T*)data, c->ctl);
+}
+
+static void reset_ctl(g2n_context* c) {
+  std::memset(c->h_ctl, 0, sizeof(Ctl));
+  c->h_ctl->err_key = ~0ull;
+  c->h_ctl->warn_line = ~0ull;
+  c->h_ctl->cast_key = ~0ull;
+  G2N_HIP(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+}
+
+static void finish_timings(g2n_context* c, g2n_result* R) {
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  R->n_phases = c->n_ev;
+  for (int k = 0; k < c->n_ev; k++) {
+    float ms = 0.f;
+    G2N_HIP(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
+    R->phase_ms[k] = ms;
+    R->phase_names[k] = c->ev_name[k];
+  }
+}
+
+// The pipeline.  R's pointers are device pointers into the context's arena.
+static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
+  fill_defaults(R);
+  R->input_bytes = len;
+  c->n_ev = 0;
+  G2N_HIP(hipEventRecord(c->ev[0], c->stream));
+  reset_ctl(c);
+  const bool bidir = o->bidirected != 0, keep = o->keep_directed_bidir != 0;
+  const bool gd = keep || (!bidir && o->directed != 0);  // builders.py:143
+  const bool maxsym = gd && !o->asymmetric;              // builders.py:282
+  const uint32_t tps = bidir ? 2 : 1;
+  const uint32_t tpe = (bidir && !keep) ? 4 : 2;
+  const int dt = o->dtype;
+  R->dtype = dt;
+  R->index_width = 4;
+
+  // ---- lines
+  const uint64_t n_tiles = (len + kNlTile - 1) / kNlTile;
+  auto* tile_cnt = dget<uint64_t>(c, S_TILE_CNT, n_tiles + 1);
+  auto* tile_base = dget<uint64_t>(c, S_TILE_BASE, n_tiles + 1);
+  if (n_tiles) {
+    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tile_cnt);
+    excl_scan<uint64_t>(c, tile_cnt, tile_base, n_tiles);
+  }
+  uint64_t total_nl = 0;
+  if (n_tiles) total_nl = read_dev(c, tile_base + n_tiles - 1) + read_dev(c, tile_cnt + n_tiles - 1);
+  auto* ls = dget<uint64_t>(c, S_LS, total_nl + 2);
+  if (n_tiles)
+    hipLaunchKernelGGL(k_nl_write, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tile_base, ls);
+  hipLaunchKernelGGL(k_nl_finish, dim3(1), dim3(1), 0, c->stream, in, len, tile_base, tile_cnt, n_tiles, ls, c->ctl);
+  const uint64_t n_lines = read_dev(c, &c->ctl->n_lines);
+  R->n_lines = (int64_t)n_lines;
+  phase(c, "lines");
+
+  // ---- classify (K2) + per-line touch/edge offsets
+  auto* kind = dget<uint8_t>(c, S_KIND, n_lines);
+  auto* pack = dget<uint64_t>(c, S_PACK, n_lines);
+  auto* pack_scan = dget<uint64_t>(c, S_PACK_SCAN, n_lines);
+  if (n_lines) {
+    hipLaunchKernelGGL(k_classify, dim3(grid_for(n_lines)), dim3(kTPB), 0, c->stream, in, ls, n_lines, tps, tpe,
+                       kind, pack, c->ctl);
+    excl_scan<uint64_t>(c, pack, pack_scan, n_lines);
+  }
+  sync_ctl(c);
+  const uint64_t n_e = c->h_ctl->n_edges, n_s = c->h_ctl->n_s;
+  const uint64_t n_t = n_s * tps + n_e * tpe;
+  R->n_edges = (int64_t)n_e;
+  R->n_records = (int64_t)c->h_ctl->n_records;
+  if (n_t >= 0xFFFFFFFFull || n_e >= 0xFFFFFFFFull)
+    throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 node touches in one build");
+  phase(c, "classify");
+
+  // ---- parse (K3)
+  ParseOpts op{};
+  op.bidir = bidir;
+  op.keep = keep;
+  op.strip = o->strip_orientation != 0;
+  const size_t wtl = o->weight_tag ? std::strlen(o->weight_tag) : 0;
+  op.has_wt = wtl > 0;
+  op.wt_len = (uint32_t)wtl;
+  if (wtl) {
+    auto* wt = dget<uint8_t>(c, S_WT, wtl);
+    G2N_HIP(hipMemcpyAsync(wt, o->weight_tag, wtl, hipMemcpyHostToDevice, c->stream));
+    op.wt = wt;
+  }
+  TouchOut T{dget<uint64_t>(c, S_NOFF, n_t), dget<uint32_t>(c, S_NLEN, n_t),
+             bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr};
+  EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
+  auto* wl = dget<uint64_t>(c, S_WL, n_e);
+  if (n_lines)
+    hipLaunchKernelGGL(k_parse, dim3(grid_for(n_lines)), dim3(kTPB), 0, c->stream, in, ls, kind, pack_scan, n_lines,
+                       op, T, E, c->ctl, wl);
+  sync_ctl(c);
+  phase(c, "parse");
+  const uint64_t n_work = c->h_ctl->wl_count;
+  if (n_work) {
+    hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, ls, pack_scan, wl,
+                       n_work, op, E, c->ctl);
+    sync_ctl(c);
+    phase(c, "weights_slow");
+  }
+
+  // ---- first error in stream order; the one-shot unsupported-record warning
+  uint64_t err_key = c->h_ctl->err_key;
+  uint64_t err_line = err_key == ~0ull ? ~0ull : (err_key >> 5);
+  int err_code = err_key == ~0ull ? 0 : (int)(err_key & 31);
+  const uint64_t warn_line = c->h_ctl->warn_line;
+  if (warn_line != ~0ull && warn_line < err_line) {
+    uint64_t off = read_dev(c, ls + warn_line);
+    uint8_t b = read_dev(c, in + off);
+    if (b >= 0x80) {  // parser.py:127 line[:1].decode() raises
+      err_line = warn_line;
+      err_code = G2N_E_UNICODE;
+      c->h_ctl->detail_off = off;
+      c->h_ctl->detail_len = 1;
+    } else {
+      R->has_warning = 1;
+      R->warn_byte = b;
+      R->warn_line = (int64_t)warn_line;
+    }
+  }
+  if (err_code) {
+    R->status = err_code;
+    R->err_line = (int64_t)err_line;
+    if (err_code == G2N_E_UNICODE && err_line != warn_line) {
+      hipLaunchKernelGGL(k_error_detail, dim3(1), dim3(1), 0, c->stream, in, ls, err_line, c->ctl);
+      sync_ctl(c);
+    }
+    if (err_code == G2N_E_UNICODE) {
+      R->err_detail = in + c->h_ctl->detail_off;  // device pointer
+      R->err_detail_len = (int64_t)c->h_ctl->detail_len;
+    }
+    hipLaunchKernelGGL(k_count_records, dim3(grid_for(err_line)), dim3(kTPB), 0, c->stream, kind, err_line, c->ctl);
+    R->n_records_before_error = (int64_t)read_dev(c, &c->ctl->n_records_before);
+    finish_timings(c, R);
+    return R->status;
+  }
+  R->n_records_before_error = R->n_records;
+
+  // ---- dictionary: first-touch node ids (K4, K5)
+  uint64_t cap = 1024;
+  while (cap < 2 * n_t) cap <<= 1;
+  auto* table = dget<unsigned long long>(c, S_TABLE, cap);
+  auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
+  auto* first = dget<uint32_t>(c, S_FIRST, n_t);
+  auto* nid = dget<uint32_t>(c, S_NID, n_t);
+  auto* flen = dget<uint64_t>(c, S_FLEN, n_t);
+  auto* foff = dget<uint64_t>(c, S_FOFF, n_t);
+  TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
+  if (n_t) {
+    G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(k_insert, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, table, cap - 1, slot,
+                       (int)bidir, c->ctl);
+    phase(c, "insert");
+    hipLaunchKernelGGL(k_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, TI, n_t, table, slot, (int)bidir,
+                       first, flen);
+    excl_scan<uint32_t>(c, first, nid, n_t);
+    excl_scan<uint64_t>(c, flen, foff, n_t);
+    hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, c->stream, first, nid, flen, foff, n_t, c->ctl);
+  }
+  sync_ctl(c);
+  if (c->h_ctl->table_overflow) throw Failure(G2N_E_DEVICE, "node table overflow");
+  const uint64_t n_nodes = n_t ? c->h_ctl->n_nodes : 0;
+  const uint64_t names_len = n_t ? c->h_ctl->names_len : 0;
+  if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
+  R->n_nodes = (int64_t)n_nodes;
+  phase(c, "ids");
+  if (o->want_node_names) {
+    auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
+    auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
+    if (n_t)
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, first, nid, foff,
+                         (int)bidir, blob, offs, c->ctl);
+    else
+      G2N_HIP(hipMemsetAsync(offs, 0, sizeof(int64_t), c->stream));
+    R->names_blob = blob;
+    R->names_offsets = offs;
+    phase(c, "names");
+  }
+
+  // ---- triplets (K6): stream-order COO with the dtype cast
+  const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
+  const uint64_t n_trip = n_e * (uint64_t)ktrip;
+  if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 matrix entries");
+  auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
+  auto* cols = dget<int32_t>(c, S_COLS, n_trip);
+  void* data = dbuf(c, S_DATA, n_trip * dtype_size(dt));
+  EdgeIn EI{E.w, E.tb};
+  switch (dt) {
+    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+    default: run_triplets<double>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+  }
+  sync_ctl(c);
+  const uint64_t cast_key = c->h_ctl->cast_key;
+  R->n_cast_overflow = (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip);
+  phase(c, "triplets");
+  if (cast_key != ~0ull) {  // np.array(data, dtype) raises at the first bad element
+    R->status = (int)(cast_key & 15);
+    R->err_index = (int64_t)(cast_key >> 4);
+    R->err_value = read_dev(c, E.w + (cast_key >> 4) / ktrip);
+    finish_timings(c, R);
+    return R->status;
+  }
+  if (o->output == G2N_OUT_PARSE && !maxsym) {  // builders.py:281: the COO itself
+    R->format = G2N_FMT_COO;
+    R->nnz = (int64_t)n_trip;
+    R->rows = rows;
+    R->cols = cols;
+    R->data = data;
+    finish_timings(c, R);
+    return G2N_OK;
+  }
+  switch (dt) {
+    case G2N_BOOL: assemble<uint8_t>(c, rows, cols, (const uint8_t*)data, n_trip, n_nodes, n_nodes, maxsym, R); break;
+    case G2N_INT8: assemble<int8_t>(c, rows, cols, (const int8_t*)data, n_trip, n_nodes, n_nodes, maxsym, R); break;
+    case G2N_INT32: assemble<int32_t>(c, rows, cols, (const int32_t*)data, n_trip, n_nodes, n_nodes, maxsym, R); break;
+    case G2N_FLOAT32: assemble<float>(c, rows, cols, (const float*)data, n_trip, n_nodes, n_nodes, maxsym, R); break;
+    default: assemble<double>(c, rows, cols, (const double*)data, n_trip, n_nodes, n_nodes, maxsym, R); break;
+  }
+  finish_timings(c, R);
+  return G2N_OK;
+}
+
+// --------------------------------------------------------------- contexts ----------
+static g2n_context* context_create(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    throw Failure(G2N_E_DEVICE, "no HIP device available (the GFA->CSR path runs only on the GPU)");
+  }
+  if (device < 0 || device >= n) throw Failure(G2N_E_ARG, "device ordinal out of range");
+  std::unique_ptr<g2n_context> c(new g2n_context());
+  c->device = device;
+  G2N_HIP(hipSetDevice(device));
+  G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->bufs.resize(S_NSLOTS);
+  G2N_HIP(hipMalloc(&c->ctl, sizeof(Ctl)));
+  G2N_HIP(hipHostMalloc(&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
+  for (int k = 0; k <= G2N_MAX_PHASES; k++) G2N_HIP(hipEventCreate(&c->ev[k]));
+  return c.release();
+}
+
+static void context_destroy(g2n_context* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& b : c->bufs)
+    if (b.p) (void)hipFree(b.p);
+  if (c->ctl) (void)hipFree(c->ctl);
+  if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+  for (int k = 0; k <= G2N_MAX_PHASES; k++)
+    if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+// one cached context per device for the host entry points
+static std::mutex g_ctx_mu;
+static std::map<int, g2n_context*> g_ctx;
+
+static g2n_context* shared_context(int device) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto it = g_ctx.find(device);
+  if (it != g_ctx.end()) return it->second;
+  g2n_context* c = context_create(device);
+  g_ctx[device] = c;
+  return c;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <class V>
+static const void* download(g2n_context* c, V& dst, const void* src, size_t bytes) {
+  dst.resize(bytes / sizeof(typename V::value_type) + 1);
+  if (bytes) G2N_HIP(hipMemcpyAsync(dst.data(), src, bytes, hipMemcpyDeviceToHost, c->stream));
+  return dst.data();
+}
+
+static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) {
+  g2n_result& R = H->r;
+  std::memcpy(&R, &D, sizeof(g2n_result));
+  R.priv_ = H;
+  R.err_detail = nullptr;
+  R.names_blob = nullptr;
+  R.names_offsets = nullptr;
+  R.rows = R.cols = R.indptr = R.indices = R.data = nullptr;
+  if (D.err_detail) R.err_detail = (const uint8_t*)download(c, H->detail, D.err_detail, (size_t)D.err_detail_len);
+  if (D.status == G2N_OK) {
+    if (D.names_blob) {
+      H->offs.resize((size_t)D.n_nodes + 1);
+      G2N_HIP(hipMemcpyAsync(H->offs.data(), D.names_offsets, (size_t)(D.n_nodes + 1) * sizeof(int64_t),
+                             hipMemcpyDeviceToHost, c->stream));
+      G2N_HIP(hipStreamSynchronize(c->stream));
+      const size_t blen = (size_t)H->offs[(size_t)D.n_nodes];
+      R.names_blob = (const uint8_t*)download(c, H->blob, D.names_blob, blen);
+      R.names_offsets = H->offs.data();
+    }
+    const size_t w = dtype_size(D.dtype);
+    if (D.format == G2N_FMT_COO) {
+      R.rows = download(c, H->rows, D.rows, (size_t)D.nnz * 4);
+      R.cols = download(c, H->cols, D.cols, (size_t)D.nnz * 4);
+    } else {
+      R.indptr = download(c, H->indptr, D.indptr, (size_t)(D.n_nodes + 1) * 4);
+      R.indices = download(c, H->indices, D.indices, (size_t)D.nnz * 4);
+    }
+    R.data = download(c, H->data, D.data, (size_t)D.nnz * w);
+  }
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+int build_host(const void* buf, size_t len, const g2n_options* opts, g2n_result** out, double read_ms) {
+  g2n_context* c = shared_context(opts->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  G2N_HIP(hipSetDevice(c->device));
+  double t0 = now_ms();
+  auto* din = dget<uint8_t>(c, S_IN, len + 16);
+  if (len) G2N_HIP(hipMemcpyAsync(din, buf, len, hipMemcpyHostToDevice, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  double t1 = now_ms();
+  g2n_result D;
+  run_pipeline(c, din, len, opts, &D);
+  double t2 = now_ms();
+  HostResult* H = new_host_result();
+  try {
+    download_result(c, D, H);
+  } catch (...) {
+    delete H;
+    throw;
+  }
+  H->r.host_ms_read = read_ms;
+  H->r.host_ms_h2d = t1 - t0;
+  H->r.host_ms_d2h = now_ms() - t2;
+  *out = &H->r;
+  return H->r.status;
+}
+
+// --------------------------------------------------------- convert_format ------
+template <class T>
+static void coo_to_csr_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t nnz,
+                         uint64_t n_rows, uint64_t n_cols, g2n_result* R) {
+  assemble<T>(c, rows, cols, data, nnz, n_rows, n_cols, false, R);
+}
+
+int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows, int64_t n_cols,
+               int32_t index_width, int32_t dtype, int32_t device, g2n_result** out) {
+  if (index_width != 4) throw Failure(G2N_E_UNSUPPORTED, "only int32 COO indices are supported");
+  if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) throw Failure(G2N_E_ARG, "unsupported dtype");
+  if (nnz < 0 || n_rows < 0 || n_cols < 0) throw Failure(G2N_E_ARG, "negative size");
+  if (nnz >= 0x7FFFFFFF) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 entries");
+  g2n_context* c = shared_context(device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  G2N_HIP(hipSetDevice(c->device));
+  const size_t w = dtype_size(dtype);
+  auto* dr = dget<int32_t>(c, S_ROWS, (uint64_t)nnz);
+  auto* dc = dget<int32_t>(c, S_COLS, (uint64_t)nnz);
+  void* dd = dbuf(c, S_DATA, (size_t)nnz * w);
+  if (nnz) {
+    G2N_HIP(hipMemcpyAsync(dr, rows, (size_t)nnz * 4, hipMemcpyHostToDevice, c->stream));
+    G2N_HIP(hipMemcpyAsync(dc, cols, (size_t)nnz * 4, hipMemcpyHostToDevice, c->stream));
+    G2N_HIP(hipMemcpyAsync(dd, data, (size_t)nnz * w, hipMemcpyHostToDevice, c->stream));
+  }
+  g2n_result D;
+  fill_defaults(&D);
+  c->n_ev = 0;
+  G2N_HIP(hipEventRecord(c->ev[0], c->stream));
+  reset_ctl(c);
+  D.dtype = dtype;
+  D.index_width = 4;
+  D.n_nodes = n_rows;
+  switch (dtype) {
+    case G2N_BOOL: coo_to_csr_t<uint8_t>(c, dr, dc, (const uint8_t*)dd, nnz, n_rows, n_cols, &D); break;
+    case G2N_INT8: coo_to_csr_t<int8_t>(c, dr, dc, (const int8_t*)dd, nnz, n_rows, n_cols, &D); break;
+    case G2N_INT32: coo_to_csr_t<int32_t>(c, dr, dc, (const int32_t*)dd, nnz, n_rows, n_cols, &D); break;
+    case G2N_FLOAT32: coo_to_csr_t<float>(c, dr, dc, (const float*)dd, nnz, n_rows, n_cols, &D); break;
+    default: coo_to_csr_t<double>(c, dr, dc, (const double*)dd, nnz, n_rows, n_cols, &D); break;
+  }
+  finish_timings(c, &D);
+  HostResult* H = new_host_result();
+  try {
+    download_result(c, D, H);
+  } catch (...) {
+    delete H;
+    throw;
+  }
+  *out = &H->r;
+  return G2N_OK;
+}
+
+}  // namespace g2n
+
+// ------------------------------------------------------------------ C ABI --------
+extern "C" {
+
+g2n_context* g2n_context_create(int device) {
+  try {
+    return g2n::context_create(device);
+  } catch (const g2n::Failure& f) {
+    g2n::set_last_error(f.what());
+  } catch (const std::exception& e) {
+    g2n::set_last_error(e.what());
+  }
+  return nullptr;
+}
+
+void g2n_context_destroy(g2n_context* ctx) { g2n::context_destroy(ctx); }
+
+void* g2n_context_stream(g2n_context* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int g2n_build_device(g2n_context* ctx, const void* d_input, size_t len, const g2n_options* opts, g2n_result* out) {
+  if (!ctx || !opts || !out || (len && !d_input)) {
+    g2n::set_last_error("g2n_build_device: null argument");
+    return G2N_E_ARG;
+  }
+  try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    G2N_HIP(hipSetDevice(ctx->device));
+    return g2n::run_pipeline(ctx, (const uint8_t*)d_input, len, opts, out);
+  } catch (const g2n::Failure& f) {
+    g2n::set_last_error(f.what());
+    out->status = f.status;
+    return f.status;
+  } catch (const std::exception& e) {
+    g2n::set_last_error(e.what());
+    out->status = G2N_E_DEVICE;
+    return G2N_E_DEVICE;
+  }
+}
+
+int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows,
+                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, g2n_result** out) {
+  if (!out) return G2N_E_ARG;
+  *out = nullptr;
+  try {
+    return g2n::coo_to_csr(rows, cols, data, nnz, n_rows, n_cols, index_width, dtype, device, out);
+  } catch (const g2n::Failure& f) {
+    g2n::set_last_error(f.what());
+    return f.status;
+  } catch (const std::exception& e) {
+    g2n::set_last_error(e.what());
+    return G2N_E_DEVICE;
+  }
+}
+
+int g2n_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+}  // extern "C"

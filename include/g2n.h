@@ -1,0 +1,167 @@
+/*
+ * g2n.h — C-ABI of the MI355X-native GFA -> CSR ingest path (libg2n.so).
+ *
+ * Drop-in boundary for the hot path of sclipman/gfa2network (reference @ 2025-07-04).
+ * The reference is pure Python and has no FFI of its own; these entry
+ * points are what its Python call surface binds through ctypes (INTEGRATION.md shows the
+ * stub a maintainer adds).  Plain pointers and sizes only: no torch / numpy types.
+ *
+ *   g2n_build_from_path    replaces GFAParser(path) iteration + the build_matrix=True
+ *                          branch of parse_gfa      gfa2network/parser.py:95-176,
+ *                                                    gfa2network/builders.py:129-299
+ *   g2n_build_from_buffer  same, for an in-memory / already-read file object
+ *                          (GFAParser(BinaryIO) parser.py:90-92, stdin parser.py:104-105)
+ *   g2n_build_device       same, input already resident in HBM (the measured hot path)
+ *   g2n_coo_to_csr         replaces convert_format(A, "csr") = A.asformat("csr")
+ *                          for a COO matrix   gfa2network/utils.py:40-63 (scipy coo.tocsr)
+ *
+ * Output selection (g2n_options.output):
+ *   G2N_OUT_PARSE  exactly what parse_gfa(..., build_matrix=True) returns: the MAX-SYM
+ *                  CSR when graph_directed and not asymmetric (builders.py:282-283),
+ *                  otherwise the stream-order, unsummed COO (builders.py:281).
+ *   G2N_OUT_CSR    what convert_format(parse_gfa(...), "csr") returns (cli.py:239).
+ *
+ * Errors: a non-zero status is one of G2N_E_*; each maps 1:1 to the exception the
+ * reference raises for the same input (type + message; the Python shim re-raises it).
+ * Everything runs on the GPU: there is no CPU fallback.  Without a usable HIP device the
+ * build entry points return G2N_E_DEVICE.
+ */
+#ifndef G2N_H
+#define G2N_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define G2N_ABI_VERSION 1u
+
+/* ---- status codes ------------------------------------------------------------------ */
+enum {
+  G2N_OK = 0,
+  G2N_E_MALFORMED_L = 1,   /* ValueError("Malformed L record")   parser.py:208-209 */
+  G2N_E_MALFORMED_E = 2,   /* ValueError("Malformed E record")   parser.py:251-252 */
+  G2N_E_MALFORMED_C = 3,   /* ValueError("Malformed C record")   parser.py:299-300 */
+  G2N_E_MALFORMED_P = 4,   /* ValueError("Malformed P record")   parser.py:231-232 */
+  G2N_E_MALFORMED_O = 5,   /* ValueError("Malformed O record")   parser.py:345-346 */
+  G2N_E_INDEX_LIST = 6,    /* IndexError("list index out of range"): S without a name, parser.py:163 */
+  G2N_E_INDEX_BYTES = 7,   /* IndexError("index out of range"): u_field[-1] on b"", parser.py:220-221 */
+  G2N_E_UNICODE = 8,       /* UnicodeDecodeError: err_detail bytes .decode() (parser.py:127,212,214,291,293,337,339) */
+  G2N_E_INT_TOO_LARGE = 9, /* OverflowError("int too large to convert to float"), builders.py:209 */
+  G2N_E_CAST_OVERFLOW = 10,/* OverflowError("Python integer X out of bounds for <dtype>"), builders.py:281 */
+  G2N_E_CAST_INF = 11,     /* OverflowError("cannot convert float infinity to integer"), builders.py:281 */
+  G2N_E_CAST_NAN = 12,     /* ValueError("cannot convert float NaN to integer"), builders.py:281 */
+  G2N_E_ARG = 13,          /* invalid options / arguments */
+  G2N_E_IO = 14,           /* OSError opening/reading the input; errno in err_index */
+  G2N_E_GZIP = 15,         /* corrupt gzip stream (gzip.open path, parser.py:108-109) */
+  G2N_E_DEVICE = 16,       /* no usable HIP device / HIP runtime failure */
+  G2N_E_NOMEM = 17,        /* host or device allocation failure */
+  G2N_E_UNSUPPORTED = 18   /* input exceeds a documented implementation limit */
+};
+
+/* ---- matrix dtypes (cli.py:92-97 --dtype choices) ------------------------------------ */
+enum { G2N_BOOL = 0, G2N_INT8 = 1, G2N_INT32 = 2, G2N_FLOAT32 = 3, G2N_FLOAT64 = 4 };
+
+enum { G2N_OUT_PARSE = 0, G2N_OUT_CSR = 1 };
+enum { G2N_FMT_COO = 0, G2N_FMT_CSR = 1 };
+
+/* Mirrors parse_gfa's keyword arguments that affect the matrix (builders.py:30-50). */
+typedef struct g2n_options {
+  uint32_t abi_version;        /* = G2N_ABI_VERSION */
+  int32_t directed;            /* default 1 */
+  int32_t bidirected;          /* default 0 */
+  int32_t keep_directed_bidir; /* default 0 */
+  int32_t asymmetric;          /* default 0 */
+  int32_t strip_orientation;   /* default 0 */
+  int32_t dtype;               /* G2N_* dtype, default G2N_FLOAT64 */
+  int32_t output;              /* G2N_OUT_PARSE (default) | G2N_OUT_CSR */
+  const char *weight_tag;      /* UTF-8, NUL-terminated; NULL or "" = no weights */
+  int32_t want_node_names;     /* 1 (default): produce the names blob in id order */
+  int32_t device;              /* HIP device ordinal, default 0 */
+  int32_t reserved[6];
+} g2n_options;
+
+#define G2N_MAX_PHASES 24
+
+/* Result of one build.  All pointers are owned by the result (host memory for the
+ * host entry points, device memory for g2n_build_device) and stay valid until
+ * g2n_result_free (or, for g2n_build_device, until the next build on the context). */
+typedef struct g2n_result {
+  uint32_t abi_version;
+  int32_t status;              /* G2N_OK or G2N_E_* */
+  int64_t err_line;            /* 0-based input line of the failing record (parse errors) */
+  int64_t err_index;           /* cast errors: element index in the triplet stream; IO: errno */
+  double err_value;            /* cast errors: the offending float64 value */
+  const uint8_t *err_detail;   /* G2N_E_UNICODE: the bytes whose .decode() raises */
+  int64_t err_detail_len;
+  int32_t has_warning;         /* RuntimeWarning("Skipping unsupported record: <c>") */
+  int32_t warn_byte;           /* <c> (first byte of the first unsupported line) */
+  int64_t warn_line;
+  int64_t n_lines;             /* lines seen (Python binary line iteration) */
+  int64_t n_records;           /* records the parser yielded (S/L/E/C/P/O) */
+  int64_t n_records_before_error;
+  int64_t n_edges;             /* L + E + C records */
+  int64_t n_nodes;             /* matrix is n_nodes x n_nodes */
+  const uint8_t *names_blob;   /* node keys in id order (builders.py:284-288), concatenated */
+  const int64_t *names_offsets;/* n_nodes + 1 offsets into names_blob */
+  int32_t format;              /* G2N_FMT_COO | G2N_FMT_CSR */
+  int32_t dtype;
+  int32_t index_width;         /* 4 (int32) or 8 (int64) for rows/cols/indptr/indices */
+  int32_t sum_sorted;          /* scipy has_sorted_indices of the scattered COO (diagnostic) */
+  int64_t nnz;                 /* COO: triplet count; CSR: stored entries */
+  const void *rows;            /* COO */
+  const void *cols;            /* COO */
+  const void *indptr;          /* CSR: n_nodes + 1 */
+  const void *indices;         /* CSR */
+  const void *data;            /* nnz elements of dtype */
+  int64_t n_cast_overflow;     /* float32 casts that overflowed to +-inf: numpy warns
+                                  RuntimeWarning("overflow encountered in cast") once each */
+  uint64_t input_bytes;        /* uncompressed GFA bytes parsed */
+  int32_t n_phases;            /* device phase timings (hipEvent, pipeline stream) */
+  int32_t pad_;
+  double phase_ms[G2N_MAX_PHASES];
+  const char *phase_names[G2N_MAX_PHASES];
+  double host_ms_read;         /* host ingest (read / inflate) */
+  double host_ms_h2d;          /* host -> device copy of the input */
+  double host_ms_d2h;          /* device -> host copy of the outputs */
+  void *priv_;
+} g2n_result;
+
+/* ---- library ------------------------------------------------------------------------- */
+const char *g2n_version(void);
+uint32_t g2n_abi_version(void);
+void g2n_options_init(g2n_options *opts);      /* reference defaults (builders.py:30-50) */
+int g2n_device_count(void);                    /* HIP devices visible (0 without a GPU) */
+const char *g2n_last_error(void);              /* thread-local message of the last failure */
+const char *g2n_status_name(int status);
+
+/* ---- host entry points (results in host memory) ---------------------------------------- */
+/* path: "-" = stdin; a name ending in ".gz" is gunzipped (multi-member); anything else is
+ * read raw — the same rule as parser.py:100-112 (by name, not by magic bytes). */
+int g2n_build_from_path(const char *path, const g2n_options *opts, g2n_result **out);
+int g2n_build_from_buffer(const void *buf, size_t len, const g2n_options *opts, g2n_result **out);
+void g2n_result_free(g2n_result *res);
+
+/* convert_format(A, "csr") for a COO matrix (utils.py:40-63 -> scipy coo.tocsr):
+ * sums duplicates in dtype with scipy's summation order, keeps explicit zeros.
+ * rows/cols have index_width bytes per element, data has dtype elements; n_rows x n_cols. */
+int g2n_coo_to_csr(const void *rows, const void *cols, const void *data, int64_t nnz, int64_t n_rows,
+                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, g2n_result **out);
+
+/* ---- device-resident entry points (the measured hot path) ------------------------------ */
+typedef struct g2n_context g2n_context;
+g2n_context *g2n_context_create(int device);   /* NULL on failure (see g2n_last_error) */
+void g2n_context_destroy(g2n_context *ctx);
+void *g2n_context_stream(g2n_context *ctx);    /* the hipStream_t the pipeline runs on */
+/* d_input: len bytes already in this device's HBM.  The result's pointers are DEVICE
+ * pointers owned by ctx, valid until the next build on ctx.  The call returns after the
+ * stream has drained (counts must be read back); phase timings are hipEvent-based. */
+int g2n_build_device(g2n_context *ctx, const void *d_input, size_t len, const g2n_options *opts,
+                     g2n_result *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* G2N_H */

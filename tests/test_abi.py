@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library builds/loads and exports every symbol include/g2n.h declares;
+the product path fails loudly (no CPU fallback) when no GPU is visible."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def declared_functions() -> list[str]:
+    names = []
+    for h in (ROOT / "include").glob("*.h"):
+        text = h.read_text()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names += re.findall(r"\b(g2n_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    from gfa2network_amd import _native
+
+    lib = _native.load()
+    decl = declared_functions()
+    assert decl, "no declarations found"
+    missing = [n for n in decl if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_native.EXPORTED) <= set(decl)
+
+
+def test_abi_version_and_defaults():
+    from gfa2network_amd import _native
+
+    assert _native.load().g2n_abi_version() == _native.ABI_VERSION
+    o = _native.make_options()
+    assert (o.directed, o.bidirected, o.keep_directed_bidir, o.asymmetric, o.strip_orientation) == (1, 0, 0, 0, 0)
+    assert o.dtype == _native.DTYPE_CODES["float64"] and o.want_node_names == 1
+
+
+def test_struct_sizes_match_header():
+    """ctypes layouts agree with the C structs (offsets of the last fields)."""
+    from gfa2network_amd import _native
+
+    assert ctypes.sizeof(_native.Options) == 4 * 8 + 8 + 4 * 8
+    r = _native.Result
+    assert r.priv_.offset + 8 == ctypes.sizeof(r)
+    assert r.phase_ms.offset % 8 == 0
+
+
+@pytest.mark.skipif(__import__("gfa2network_amd._native", fromlist=["x"]).device_count() > 0,
+                    reason="a GPU is visible")
+def test_no_gpu_fails_loudly(tmp_path):
+    from gfa2network_amd import parse_gfa
+
+    p = tmp_path / "a.gfa"
+    p.write_bytes(b"S\ta\nL\ta\t+\tb\t+\t*\n")
+    with pytest.raises(RuntimeError, match="G2N_E_DEVICE"):
+        parse_gfa(p, build_graph=False, build_matrix=True)
+
+
+def test_out_of_scope_options_raise(tmp_path):
+    from gfa2network_amd import parse_gfa
+
+    p = tmp_path / "a.gfa"
+    p.write_bytes(b"S\ta\n")
+    with pytest.raises(NotImplementedError):
+        parse_gfa(p, build_graph=True, build_matrix=False)
+    with pytest.raises(NotImplementedError):
+        parse_gfa(p, build_graph=False, build_matrix=True, backend="igraph")
+    with pytest.raises(ValueError, match="return_node_list requires build_matrix=True"):
+        parse_gfa(p, build_graph=False, build_matrix=False, return_node_list=True)
+    with pytest.raises(NotImplementedError):
+        parse_gfa(p, build_graph=False, build_matrix=True, dtype="float16")
