@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X GFA -> CSR path (BASELINE.json metric).
+
+One "step" = one full pass of the hot path over one HBM-resident synthetic GFA: raw bytes
+already in HBM -> CSR (indptr / indices / data) in HBM, i.e. g2n_build_device() — lines,
+classify, parse + weights, first-touch node ids, node-name blob, triplets, radix sort,
+duplicate sums and (default mode) the A.maximum(A.T) symmetrisation.  Workload = C4 of
+BASELINE.json (50M S / 200M L, default flags), the north star's 200M-edge config; the
+gzip inflate and the PCIe copy are host ingest, measured separately.
+
+`python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run: one
+rank per GPU, weak scaling — every rank builds its own independently seeded C4 input).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="C4", choices=["C2", "C3", "C4"])
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-links", type=int, default=12_000_000)
+    ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
+    return ap.parse_args()
+
+
+def _dist_setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def _max_over_ranks(world, value: float) -> float:
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def algorithmic_bytes(input_bytes: int, n_nodes: int, nnz: int, w_dtype: int, w_idx: int = 4) -> int:
+    """B_alg = B_in + (n+1) w_idx + nnz (w_idx + w_dtype)."""
+    return input_bytes + (n_nodes + 1) * w_idx + nnz * (w_idx + w_dtype)
+
+
+def cpu_baseline(workload, links: int) -> dict:
+    """The oracle (C++ restatement of the reference, 1 thread) on a bounded sample of the
+    same generator: segments scaled with the links so the S:L ratio is kept."""
+    from gfa2network_amd import synth
+    from oracle import oracle
+
+    oracle.build()
+    segs = max(1, int(workload.n_segments * links / workload.n_links))
+    data = synth.host_bytes(segs, links, seed=0, rc_tag=workload.rc_tag)
+    mode = dict(workload.mode)
+    t0 = time.perf_counter()
+    o = oracle.run(data, **mode)
+    dt = time.perf_counter() - t0
+    assert o.status == 0
+    return {"value": round(links / dt / 1e6, 4), "unit": "M edges/s", "cores": 1, "kind": "port",
+            "sample": f"{segs} S / {links} L lines of the {workload.name} generator ({len(data) / 1e9:.2f} GB), "
+                      f"oracle/g2n_oracle.cpp single thread, {dt:.1f} s"}
+
+
+def main():
+    args = _args()
+    world, rank, local = _dist_setup(args.gpus)
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    lib = nat.load()
+    wl = synth.WORKLOADS[args.workload]
+    n_s = max(1, int(wl.n_segments * args.scale))
+    n_l = max(1, int(wl.n_links * args.scale))
+    dev_in = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local)
+    ctx = lib.g2n_context_create(local)
+    if not ctx:
+        raise RuntimeError(nat.last_error())
+    mode = dict(wl.mode)
+    opts = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=local,
+                            directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+                            weight_tag=mode.get("weight_tag"))
+    res = nat.Result()
+
+    def step():
+        rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(opts), ctypes.byref(res))
+        if rc != 0:
+            raise RuntimeError(f"{nat.status_name(rc)}: {nat.last_error()}")
+        return {res.phase_names[k].decode(): res.phase_ms[k] for k in range(res.n_phases)}
+
+    for _ in range(args.warmup):
+        step()
+    _barrier(world)
+    lib.g2n_context_stream(ctx)
+    phases = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        phases.append(step())  # returns after the pipeline stream drained
+    _barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = _max_over_ranks(world, elapsed)
+
+    n_edges, n_nodes, nnz, in_bytes = int(res.n_edges), int(res.n_nodes), int(res.nnz), int(res.input_bytes)
+    w_dtype = 8
+    ms_step = elapsed / args.steps * 1e3
+    edges_total = n_edges * args.steps * world
+    value = edges_total / elapsed / 1e6
+    gbs = in_bytes * args.steps * world / elapsed / 1e9
+    # per-phase device time (hipEvents on the pipeline stream), averaged over the steps
+    avg = {k: sum(p[k] for p in phases) / len(phases) for k in phases[0]}
+    dev_ms = sum(avg.values())
+    b_alg = algorithmic_bytes(in_bytes, n_nodes, nnz, w_dtype)
+    # the dominant phase and its own algorithmic bytes
+    dom = max(avg, key=avg.get)
+    dom_bytes = phase_bytes(dom, in_bytes, int(res.n_lines), n_edges, n_nodes, nnz, wl)
+    achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
+    line = {
+        "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
+        "value": round(value, 2),
+        "unit": "M edge records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int64 (float64 weights)",
+        "data": "synthetic (deterministic generator, gfa2network_amd/csrc/synth.h), generated in HBM",
+        "config": {"workload": f"{wl.name}: {wl.note}" + (f" x{args.scale}" if args.scale != 1 else ""),
+                   "n_segments": n_s, "n_links": n_l, "input_bytes_per_gpu": in_bytes, "n_nodes": n_nodes,
+                   "nnz": nnz, "mode": mode or "default", "output": "csr", "parallelism": f"replica x{world}"},
+        "gb_per_s_ingested": round(gbs, 2),
+        "device_ms_per_step": round(dev_ms, 3),
+        "phase_ms": {k: round(v, 3) for k, v in avg.items()},
+        "pipeline_roofline": {"bound": "hbm", "b_alg_bytes": b_alg,
+                              "achieved_gbs": round(b_alg / (dev_ms / 1e3) / 1e9, 1),
+                              "peak_gbs": HBM_PEAK_GBS,
+                              "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
+    if rank == 0:
+        if args.phases:
+            print(json.dumps(avg, indent=1), file=sys.stderr)
+        print(json.dumps(line))
+    lib.g2n_context_destroy(ctx)
+    dev_in.free()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+def phase_bytes(phase: str, in_bytes: int, n_lines: int, n_edges: int, n_nodes: int, nnz: int, wl) -> int:
+    """Minimal HBM bytes a phase must move (read its inputs once, write its outputs once).
+    Per-phase formulas: DESIGN.md §Roofline."""
+    tpe = 4 if wl.mode.get("bidirected") else 2
+    n_s = wl.n_segments
+    n_t = n_s * (2 if wl.mode.get("bidirected") else 1) + n_edges * tpe
+    if phase == "lines":
+        return in_bytes + 8 * (n_lines + 1)
+    if phase == "classify":
+        return 8 * n_lines + 2 * n_lines + n_lines + 16 * n_lines
+    if phase == "parse":
+        return in_bytes + 8 * n_lines + n_lines + 8 * n_lines + 12 * n_t + 12 * n_edges
+    if phase == "insert":
+        return 12 * n_t + 8 * n_nodes + 4 * n_t
+    return in_bytes
+
+
+if __name__ == "__main__":
+    main()

@@ -90,6 +90,12 @@ struct EdgeOut {
   double* w;
   uint32_t* tb;
 };
+struct BlockCounts {  // per-block partials of k_classify
+  unsigned long long* unk;
+  unsigned long long* rec;
+  unsigned long long* edges;
+  unsigned long long* segs;
+};
 struct EdgeIn {
   const double* w;
   const uint32_t* tb;
@@ -101,7 +107,8 @@ __global__ void k_nl_write(const uint8_t* in, uint64_t len, const uint64_t* tile
 __global__ void k_nl_finish(const uint8_t* in, uint64_t len, const uint64_t* tile_base, const uint64_t* tile_cnt,
                             uint64_t n_tiles, uint64_t* ls, Ctl* ctl);
 __global__ void k_classify(const uint8_t* in, const uint64_t* ls, uint64_t n_lines, uint32_t tps, uint32_t tpe,
-                           uint8_t* kind, uint64_t* pack, Ctl* ctl);
+                           uint8_t* kind, uint64_t* pack, BlockCounts bc);
+__global__ void k_reduce_blocks(BlockCounts bc, uint64_t n_blocks, Ctl* ctl);
 __global__ void k_parse(const uint8_t* in, const uint64_t* ls, const uint8_t* kind, const uint64_t* pack_scan,
                         uint64_t n_lines, ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl, uint64_t* worklist);
 __global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint64_t* pack_scan,
@@ -109,9 +116,10 @@ __global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint
 __global__ void k_error_detail(const uint8_t* in, const uint64_t* ls, uint64_t line, Ctl* ctl);
 __global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
 __global__ void k_insert(const uint8_t* in, TouchIn T, uint64_t n_t, unsigned long long* table, uint64_t mask,
-                         uint32_t* slot, int bidir, Ctl* ctl);
-__global__ void k_first(TouchIn T, uint64_t n_t, const unsigned long long* table, const uint32_t* slot, int bidir,
-                        uint32_t* first, uint64_t* flen);
+                         uint64_t max_probes, uint32_t* slot, int bidir, Ctl* ctl);
+__global__ void k_mark_first(TouchIn T, const unsigned long long* table, uint64_t cap, int bidir, uint32_t* first,
+                             uint64_t* flen);
+__global__ void k_assign_ids(unsigned long long* table, uint64_t cap, const uint32_t* nid);
 __global__ void k_totals(const uint32_t* first, const uint32_t* nid, const uint64_t* flen, const uint64_t* foff,
                          uint64_t n_t, Ctl* ctl);
 __global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_t, const uint32_t* first, const uint32_t* nid,

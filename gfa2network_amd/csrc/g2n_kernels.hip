@@ -179,7 +179,7 @@ __global__ void k_nl_finish(const uint8_t* __restrict__ in, uint64_t len, const 
 __global__ void __launch_bounds__(kTPB) k_classify(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
                                                    uint64_t n_lines, uint32_t tps, uint32_t tpe,
                                                    uint8_t* __restrict__ kind, uint64_t* __restrict__ pack,
-                                                   Ctl* ctl) {
+                                                   BlockCounts bc) {
   __shared__ unsigned long long s_min[kTPB / 64];
   __shared__ unsigned long long s_cnt[3][kTPB / 64];
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kTPB) k_classify(const uint8_t* __restrict__ i
     s_cnt[2][w] = ns;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // per-block partials (one word per block, no same-address atomics)
     unsigned long long m = ~0ull, a = 0, b = 0, c = 0;
     for (int q = 0; q < kTPB / 64; q++) {
       m = s_min[q] < m ? s_min[q] : m;
@@ -234,10 +234,46 @@ __global__ void __launch_bounds__(kTPB) k_classify(const uint8_t* __restrict__ i
       b += s_cnt[1][q];
       c += s_cnt[2][q];
     }
-    if (m != ~0ull) atomicMin(&ctl->warn_line, m);
-    if (a) atomicAdd(&ctl->n_records, a);
-    if (b) atomicAdd(&ctl->n_edges, b);
-    if (c) atomicAdd(&ctl->n_s, c);
+    bc.unk[blockIdx.x] = m;
+    bc.rec[blockIdx.x] = a;
+    bc.edges[blockIdx.x] = b;
+    bc.segs[blockIdx.x] = c;
+  }
+}
+
+// fold the per-block partials of k_classify into the control block (one 1024-thread block)
+__global__ void __launch_bounds__(1024) k_reduce_blocks(BlockCounts bc, uint64_t n_blocks, Ctl* ctl) {
+  __shared__ unsigned long long s[4][1024 / 64];
+  unsigned long long m = ~0ull, a = 0, b = 0, c = 0;
+  for (uint64_t i = threadIdx.x; i < n_blocks; i += 1024) {
+    unsigned long long u = bc.unk[i];
+    m = u < m ? u : m;
+    a += bc.rec[i];
+    b += bc.edges[i];
+    c += bc.segs[i];
+  }
+  m = wave_reduce_min(m);
+  a = wave_reduce_sum(a);
+  b = wave_reduce_sum(b);
+  c = wave_reduce_sum(c);
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = m;
+    s[1][threadIdx.x >> 6] = a;
+    s[2][threadIdx.x >> 6] = b;
+    s[3][threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 1024 / 64; q++) {
+      s[0][0] = s[0][q] < s[0][0] ? s[0][q] : s[0][0];
+      s[1][0] += s[1][q];
+      s[2][0] += s[2][q];
+      s[3][0] += s[3][q];
+    }
+    ctl->warn_line = s[0][0];
+    ctl->n_records = s[1][0];
+    ctl->n_edges = s[2][0];
+    ctl->n_s = s[3][0];
   }
 }
 
@@ -639,7 +675,8 @@ __device__ inline bool touch_eq(const uint8_t* __restrict__ in, const TouchIn& T
 // what Python's dict insertion order needs.
 __global__ void __launch_bounds__(kTPB) k_insert(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_t,
                                                  unsigned long long* __restrict__ table, uint64_t mask,
-                                                 uint32_t* __restrict__ slot, int bidir, Ctl* ctl) {
+                                                 uint64_t max_probes, uint32_t* __restrict__ slot, int bidir,
+                                                 Ctl* ctl) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (t >= n_t) return;
   const uint64_t no = T.noff[t];
@@ -650,7 +687,7 @@ __global__ void __launch_bounds__(kTPB) k_insert(const uint8_t* __restrict__ in,
   const uint32_t tag = (uint32_t)(h >> 32);
   const unsigned long long mine = ((unsigned long long)tag << 32) | (uint32_t)t;
   uint64_t idx = h & mask;
-  for (uint64_t probe = 0; probe <= mask; probe++) {
+  for (uint64_t probe = 0; probe < max_probes; probe++) {
     unsigned long long cur = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == kEmptySlot) {
       cur = atomicCAS(&table[idx], kEmptySlot, mine);
@@ -666,18 +703,30 @@ __global__ void __launch_bounds__(kTPB) k_insert(const uint8_t* __restrict__ in,
     }
     idx = (idx + 1) & mask;
   }
-  ctl->table_overflow = 1;
+  ctl->table_overflow = 1;  // the host retries with a table sized for every touch
 }
 
-// first[t] = 1 iff t is the first touch of its key; flen[t] = key length if first
-__global__ void __launch_bounds__(kTPB) k_first(TouchIn T, uint64_t n_t, const unsigned long long* __restrict__ table,
-                                                const uint32_t* __restrict__ slot, int bidir,
-                                                uint32_t* __restrict__ first, uint64_t* __restrict__ flen) {
-  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (t >= n_t) return;
-  bool f = (uint32_t)table[slot[t]] == (uint32_t)t;
-  first[t] = f ? 1u : 0u;
-  flen[t] = f ? (uint64_t)T.nlen[t] + (bidir ? 1ull + T.olen[t] : 0ull) : 0ull;
+// After all inserts, every occupied slot holds the FIRST touch of its key: mark it.
+__global__ void __launch_bounds__(kTPB) k_mark_first(TouchIn T, const unsigned long long* __restrict__ table,
+                                                     uint64_t cap, int bidir, uint32_t* __restrict__ first,
+                                                     uint64_t* __restrict__ flen) {
+  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (s >= cap) return;
+  const unsigned long long v = table[s];
+  if (v == kEmptySlot) return;
+  const uint32_t rep = (uint32_t)v;
+  first[rep] = 1u;
+  flen[rep] = (uint64_t)T.nlen[rep] + (bidir ? 1ull + T.olen[rep] : 0ull);
+}
+
+// Replace each slot's representative by its node id (= rank of its first touch).
+__global__ void __launch_bounds__(kTPB) k_assign_ids(unsigned long long* __restrict__ table, uint64_t cap,
+                                                     const uint32_t* __restrict__ nid) {
+  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (s >= cap) return;
+  const unsigned long long v = table[s];
+  if (v == kEmptySlot) return;
+  table[s] = (v & 0xFFFFFFFF00000000ull) | nid[(uint32_t)v];
 }
 
 __global__ void k_totals(const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
@@ -766,7 +815,7 @@ __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const
   const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (e >= n_e) return;
   const uint64_t tb = E.tb[e];
-  auto id = [&](uint64_t t) -> int32_t { return (int32_t)nid[(uint32_t)table[slot[t]]]; };
+  auto id = [&](uint64_t t) -> int32_t { return (int32_t)(uint32_t)table[slot[t]]; };  // slot -> node id
   T v;
   const double wv = E.w[e];
   uint32_t err = Cast<T>::go(wv, &v);

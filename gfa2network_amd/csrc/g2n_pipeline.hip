@@ -33,7 +33,7 @@ enum Slot {
   S_IN, S_TILE_CNT, S_TILE_BASE, S_LS, S_KIND, S_PACK, S_PACK_SCAN, S_NOFF, S_NLEN, S_OOFF, S_OLEN, S_EW, S_ETB,
   S_WL, S_TABLE, S_SLOT, S_FIRST, S_NID, S_FLEN, S_FOFF, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1,
   S_VALS0, S_VALS1, S_HEAD, S_HPOS, S_UKEYS0, S_UDATA0, S_UKEYS1, S_UDATA1, S_ROWFLAG, S_KV, S_ORD, S_MK, S_MV,
-  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_NSLOTS
+  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_BLK, S_NSLOTS
 };
 
 struct DevBuf {
@@ -332,8 +332,12 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   auto* pack = dget<uint64_t>(c, S_PACK, n_lines);
   auto* pack_scan = dget<uint64_t>(c, S_PACK_SCAN, n_lines);
   if (n_lines) {
-    hipLaunchKernelGGL(k_classify, dim3(grid_for(n_lines)), dim3(kTPB), 0, c->stream, in, ls, n_lines, tps, tpe,
-                       kind, pack, c->ctl);
+    const uint64_t nb = grid_for(n_lines);
+    auto* blk = dget<unsigned long long>(c, S_BLK, 4 * nb);
+    BlockCounts bc{blk, blk + nb, blk + 2 * nb, blk + 3 * nb};
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(kTPB), 0, c->stream, in, ls, n_lines, tps, tpe, kind,
+                       pack, bc);
+    hipLaunchKernelGGL(k_reduce_blocks, dim3(1), dim3(1024), 0, c->stream, bc, nb, c->ctl);
     excl_scan<uint64_t>(c, pack, pack_scan, n_lines);
   }
   sync_ctl(c);
@@ -413,25 +417,43 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   R->n_records_before_error = R->n_records;
 
   // ---- dictionary: first-touch node ids (K4, K5)
+  // Table sized for the expected number of distinct keys (S names + a fraction of the edge
+  // touches); a bounded probe sequence flags overflow and the insert is redone with a table
+  // sized for every touch (load <= 1/2, unbounded probes).
+  const uint64_t est = n_s * tps + (n_e * tpe) / 16 + 1024;
+  uint64_t full_cap = 1024;
+  while (full_cap < 2 * n_t) full_cap <<= 1;
   uint64_t cap = 1024;
-  while (cap < 2 * n_t) cap <<= 1;
-  auto* table = dget<unsigned long long>(c, S_TABLE, cap);
+  while (cap < 2 * est) cap <<= 1;
+  if (cap > full_cap) cap = full_cap;
   auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
   auto* first = dget<uint32_t>(c, S_FIRST, n_t);
   auto* nid = dget<uint32_t>(c, S_NID, n_t);
   auto* flen = dget<uint64_t>(c, S_FLEN, n_t);
   auto* foff = dget<uint64_t>(c, S_FOFF, n_t);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
+  unsigned long long* table = nullptr;
   if (n_t) {
-    G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(unsigned long long), c->stream));
-    hipLaunchKernelGGL(k_insert, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, table, cap - 1, slot,
-                       (int)bidir, c->ctl);
+    while (true) {
+      table = dget<unsigned long long>(c, S_TABLE, cap);
+      G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(unsigned long long), c->stream));
+      const uint64_t max_probes = cap >= full_cap ? cap : 4096;
+      hipLaunchKernelGGL(k_insert, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, table, cap - 1,
+                         max_probes, slot, (int)bidir, c->ctl);
+      if (cap >= full_cap) break;
+      if (read_dev(c, &c->ctl->table_overflow) == 0) break;
+      G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
+      cap = full_cap;
+    }
     phase(c, "insert");
-    hipLaunchKernelGGL(k_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, TI, n_t, table, slot, (int)bidir,
+    G2N_HIP(hipMemsetAsync(first, 0, n_t * sizeof(uint32_t), c->stream));
+    G2N_HIP(hipMemsetAsync(flen, 0, n_t * sizeof(uint64_t), c->stream));
+    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, TI, table, cap, (int)bidir,
                        first, flen);
     excl_scan<uint32_t>(c, first, nid, n_t);
     excl_scan<uint64_t>(c, flen, foff, n_t);
     hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, c->stream, first, nid, flen, foff, n_t, c->ctl);
+    hipLaunchKernelGGL(k_assign_ids, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, nid);
   }
   sync_ctl(c);
   if (c->h_ctl->table_overflow) throw Failure(G2N_E_DEVICE, "node table overflow");

@@ -1,0 +1,181 @@
+"""GPU vs the oracle on inputs the reference's own fixtures do not cover.
+
+* randomized GFA texts full of parse quirks (fuzz_gfa.make), every mode x dtype family;
+* the synthetic generator at 10^5 - 10^7 edges, bit-exact COO / CSR / MAX-SYM / names;
+* bench-size properties (C4: 200M edges) that hold whatever the size: symmetry of the
+  MAX-SYM CSR, canonical CSR, node names = "1".."N" in S order.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import fuzz_gfa
+import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+MODES = [
+    {},
+    {"directed": False},
+    {"asymmetric": True},
+    {"bidirected": True},
+    {"bidirected": True, "keep_directed_bidir": True},
+    {"keep_directed_bidir": True, "asymmetric": True},
+    {"strip_orientation": True, "bidirected": True},
+]
+
+
+def outcome(run):
+    res, exc, warns, so, se = G.run_python(run)
+    if exc is not None:
+        return ("exc", type(exc).__name__, str(exc), tuple(w["msg"] for w in warns), so, se)
+    A, nodes = res
+    M = A.tocoo() if A.format == "csr" else A
+    key = [A.format, str(A.dtype), A.shape, tuple(w["msg"] for w in warns), so, se, nodes]
+    if A.format == "coo":
+        key += [A.row.tobytes(), A.col.tobytes(), A.data.tobytes()]
+    else:
+        key += [A.indptr.tobytes(), A.indices.tobytes(), A.data.tobytes()]
+    del M
+    return tuple(key)
+
+
+def gpu_run(data: bytes, mode: dict, dtype: str, wt, raw_bytes_id=True, verbose=False):
+    import io
+
+    from gfa2network_amd import parse_gfa
+
+    return lambda: parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, return_node_list=True,
+                             raw_bytes_id=raw_bytes_id, verbose=verbose, dtype=dtype, weight_tag=wt, **mode)
+
+
+def oracle_run(oracle_mod, data: bytes, mode: dict, dtype: str, wt, raw_bytes_id=True, verbose=False):
+    from gfa2network_amd.api import finalize
+
+    def run():
+        o = oracle_mod.run(data, dtype=dtype, weight_tag=wt, **mode)
+        return finalize(oracle_mod.to_raw(o, "parse"), dtype=np.dtype(dtype), return_node_list=True,
+                        raw_bytes_id=raw_bytes_id, verbose=verbose)
+
+    return run
+
+
+@pytest.mark.parametrize("block", range(8))
+def test_fuzz_gpu_equals_oracle(gpu, oracle_lib, block):
+    bad = []
+    for seed in range(block * 40, block * 40 + 40):
+        data = fuzz_gfa.make(seed, n_lines=50, allow_errors=seed % 3 == 0)
+        mode = MODES[seed % len(MODES)]
+        dtype = ["float64", "float32", "int8", "int32", "bool"][seed % 5]
+        for wt in (None, "RC"):
+            for rbi in (True, False):
+                a = outcome(gpu_run(data, mode, dtype, wt, rbi, verbose=seed % 2 == 0))
+                b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt, rbi, verbose=seed % 2 == 0))
+                if a != b:
+                    bad.append((seed, mode, dtype, wt, rbi, a[:3], b[:3]))
+    assert not bad, bad[:3]
+
+
+def test_fuzz_convert_format_equals_oracle(gpu, oracle_lib):
+    """convert_format(A, "csr") on the GPU == scipy's tocsr, on the COO outputs."""
+    from gfa2network_amd import convert_format
+
+    bad = []
+    for seed in range(300, 420):
+        data = fuzz_gfa.make(seed, n_lines=80, allow_errors=False)
+        for dtype in ("float64", "float32", "int8", "bool"):
+            o = oracle_lib.run(data, dtype=dtype, weight_tag="RC", directed=False)
+            if o.status:
+                continue
+            A = sp.coo_matrix((o.data, (o.rows.astype(np.int32), o.cols.astype(np.int32))),
+                              shape=(o.n_nodes, o.n_nodes), dtype=dtype)
+            C = convert_format(A, "csr")
+            R = A.tocsr()
+            if not (C.indptr.tobytes() == R.indptr.tobytes() and C.indices.tobytes() == R.indices.tobytes()
+                    and C.data.tobytes() == R.data.tobytes() and C.dtype == R.dtype):
+                bad.append((seed, dtype))
+            Cc = convert_format(A, "csc")
+            Rc = A.tocsc()
+            if not (Cc.indptr.tobytes() == Rc.indptr.tobytes() and Cc.indices.tobytes() == Rc.indices.tobytes()
+                    and Cc.data.tobytes() == Rc.data.tobytes()):
+                bad.append((seed, dtype, "csc"))
+    assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("n_s,n_l,rc", [(1000, 4000, True), (100_000, 400_000, True), (1_000_000, 4_000_000, False)])
+def test_synthetic_gpu_equals_oracle(gpu, oracle_lib, n_s, n_l, rc):
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(n_s, n_l, seed=11, rc_tag=rc)
+    modes = MODES if n_l <= 400_000 else [{}, {"directed": False}, {"bidirected": True}]
+    for mode in modes:
+        for dtype in (["float64", "float32", "int32"] if n_l <= 400_000 else ["float64"]):
+            wt = "RC" if rc else None
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
+            assert a == b, (mode, dtype)
+
+
+def test_float_duplicate_sums_match_scipy_order(gpu, oracle_lib):
+    """Rows of > 16 entries with >= 3 inexact float duplicates: the GPU re-runs scipy's
+    std::sort order (stl_sort.h) and matches scipy bit for bit."""
+    import random
+
+    r = random.Random(5)
+    lines = []
+    vals = ["1e16", "1", "-1e16", "0.1", "3.3", "-2.7", "1e-3", "7.25", "1e300", "-1e300"]
+    for _ in range(4000):
+        lines.append(f"L\tr{r.randint(0, 6)}\t+\tc{r.randint(0, 40)}\t+\t*\tRC:f:{r.choice(vals)}\n")
+    data = "".join(lines).encode()
+    for mode in ({}, {"directed": False}, {"asymmetric": True}):
+        for dtype in ("float64", "float32"):
+            a = outcome(gpu_run(data, mode, dtype, "RC"))
+            b = outcome(oracle_run(oracle_lib, data, mode, dtype, "RC"))
+            assert a == b, (mode, dtype)
+    from gfa2network_amd import convert_format, parse_gfa
+    import io
+
+    A = parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, directed=False, weight_tag="RC")
+    C, R = convert_format(A, "csr"), A.tocsr()
+    assert C.data.tobytes() == R.data.tobytes() and C.indices.tobytes() == R.indices.tobytes()
+
+
+def test_c4_properties_on_device(gpu):
+    """Full C4 size (50M S / 200M L, 6.3 GB) on the device: size-independent properties."""
+    import ctypes
+
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    lib = nat.load()
+    dev = synth.DeviceInput(50_000_000, 200_000_000, seed=0)
+    ctx = lib.g2n_context_create(0)
+    try:
+        opts = nat.make_options(output=nat.OUT_CSR)
+        res = nat.Result()
+        assert lib.g2n_build_device(ctx, dev.ptr, dev.len, ctypes.byref(opts), ctypes.byref(res)) == 0
+        n, nnz = res.n_nodes, res.nnz
+        assert res.n_edges == 200_000_000 and n == 50_000_000 and res.format == nat.FMT_CSR
+        indptr = np.empty(n + 1, np.int32)
+        indices = np.empty(nnz, np.int32)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(indptr.ctypes.data, res.indptr, indptr.nbytes, 2) == 0
+        assert hip.hipMemcpy(indices.ctypes.data, res.indices, indices.nbytes, 2) == 0
+        offs = np.empty(n + 1, np.int64)
+        assert hip.hipMemcpy(offs.ctypes.data, res.names_offsets, offs.nbytes, 2) == 0
+        blob = np.empty(int(offs[-1]), np.uint8)
+        assert hip.hipMemcpy(blob.ctypes.data, res.names_blob, blob.nbytes, 2) == 0
+    finally:
+        lib.g2n_context_destroy(ctx)
+        dev.free()
+    assert indptr[0] == 0 and indptr[-1] == nnz and np.all(np.diff(indptr) >= 0)
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    k1 = rows * n + indices  # canonical CSR: strictly increasing (row, col)
+    assert np.all(np.diff(k1) > 0)
+    k2 = np.sort(indices.astype(np.int64) * n + rows)
+    assert np.array_equal(k1, k2)  # MAX-SYM result is structurally symmetric
+    # S lines define "1".."N" in order, so node k is named str(k+1)
+    names = blob.tobytes()
+    want = "".join(str(k) for k in range(1, n + 1)).encode()
+    assert names == want
