@@ -120,7 +120,12 @@ def main():
         rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(opts), ctypes.byref(res))
         if rc != 0:
             raise RuntimeError(f"{nat.status_name(rc)}: {nat.last_error()}")
-        return {res.phase_names[k].decode(): res.phase_ms[k] for k in range(res.n_phases)}
+        ph = {}
+        for k in range(res.n_phases):  # "_"-phases are host gaps between measured kernels
+            name = res.phase_names[k].decode()
+            if not name.startswith("_"):
+                ph[name] = ph.get(name, 0.0) + res.phase_ms[k]
+        return ph
 
     for _ in range(args.warmup):
         step()
@@ -141,13 +146,20 @@ def main():
     value = edges_total / elapsed / 1e6
     gbs = in_bytes * args.steps * world / elapsed / 1e9
     # per-phase device time (hipEvents on the pipeline stream), averaged over the steps
-    avg = {k: sum(p[k] for p in phases) / len(phases) for k in phases[0]}
+    avg = {k: sum(p.get(k, 0.0) for p in phases) / len(phases) for k in phases[0]}
     dev_ms = sum(avg.values())
     b_alg = algorithmic_bytes(in_bytes, n_nodes, nnz, w_dtype)
-    # the dominant phase and its own algorithmic bytes
-    dom = max(avg, key=avg.get)
-    dom_bytes = phase_bytes(dom, in_bytes, int(res.n_lines), n_edges, n_nodes, nnz, wl)
+    # roofline of the dominant single kernel: its algorithmic bytes per launch / its event time
+    counts = dict(n_lines=int(res.n_lines), n_edges=n_edges, n_nodes=n_nodes, in_bytes=in_bytes,
+                  names_bytes=int(res.names_bytes), bidir=bool(mode.get("bidirected")),
+                  keep=bool(mode.get("keep_directed_bidir")), n_s=n_s, w_dtype=w_dtype,
+                  directed_csr=bool(mode.get("keep_directed_bidir")) or (not mode.get("bidirected")
+                                                                        and mode.get("directed", True)))
+    cand = {ph: avg[ph] for ph in KERNEL_OF_PHASE if ph in avg}
+    dom = max(cand, key=cand.get)
+    dom_bytes, unit_desc = kernel_bytes(dom, **counts)
     achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
+    traffic = measured_traffic(KERNEL_OF_PHASE[dom])
     line = {
         "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
         "value": round(value, 2),
@@ -171,8 +183,10 @@ def main():
                               "achieved_gbs": round(b_alg / (dev_ms / 1e3) / 1e9, 1),
                               "peak_gbs": HBM_PEAK_GBS,
                               "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+        "roofline": {"bound": "hbm", "kernel": KERNEL_OF_PHASE[dom], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "per_unit": unit_desc,
+                     "ms_per_launch": round(avg[dom], 3)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
@@ -188,21 +202,48 @@ def main():
         dist.destroy_process_group()
 
 
-def phase_bytes(phase: str, in_bytes: int, n_lines: int, n_edges: int, n_nodes: int, nnz: int, wl) -> int:
-    """Minimal HBM bytes a phase must move (read its inputs once, write its outputs once).
-    Per-phase formulas: DESIGN.md §Roofline."""
-    tpe = 4 if wl.mode.get("bidirected") else 2
-    n_s = wl.n_segments
-    n_t = n_s * (2 if wl.mode.get("bidirected") else 1) + n_edges * tpe
-    if phase == "lines":
-        return in_bytes + 8 * (n_lines + 1)
-    if phase == "classify":
-        return 8 * n_lines + 2 * n_lines + n_lines + 16 * n_lines
-    if phase == "parse":
-        return in_bytes + 8 * n_lines + n_lines + 8 * n_lines + 12 * n_t + 12 * n_edges
-    if phase == "insert":
-        return 12 * n_t + 8 * n_nodes + 4 * n_t
-    return in_bytes
+KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
+    "parse": "g2n::k_parse",
+    "insert_claim": "g2n::k_insert_round<true>",
+    "insert_lookup": "g2n::k_insert_round<false>",
+    "triplets": "g2n::k_triplets<double>",
+}
+
+
+def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bidir, keep, n_s, w_dtype,
+                 directed_csr=True):
+    """Algorithmic bytes one launch must move (inputs read once, outputs written once) and the
+    per-unit figure it is built from."""
+    tps = 2 if bidir else 1
+    tpe = 4 if (bidir and not keep) else 2
+    n_t = n_s * tps + n_edges * tpe
+    d_o = 12 if bidir else 0  # orientation descriptor (u64 off + u32 len) per touch
+    avg_key = names_bytes / max(n_nodes, 1)
+    if phase == "parse":  # every input byte, ls pair, kind, pack; per touch / edge descriptors out
+        per_t, per_e = 13 + d_o, 12
+        return (in_bytes + 17 * n_lines + per_t * n_t + per_e * n_edges,
+                f"B_in + 17 B/line + {per_t} B/touch + {per_e} B/edge")
+    if phase in ("insert_claim", "insert_lookup"):
+        k = n_s * tps if phase == "insert_claim" else n_edges * tpe
+        per = 1 + 1 + 12 + d_o + avg_key + 32 + 4  # state r/w, descriptor, key bytes, 32-B entry, slot
+        return (int(n_t * 1 + k * (per - 1)), f"1 B/touch + {per - 1:.1f} B per processed touch ({k} touches)")
+    if phase == "triplets":
+        k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
+        per = 4 + 8 + tpe * (4 + 8) + k_trip * (4 + 4 + w_dtype)  # tb, w, slot+entry per touch, COO out
+        return n_edges * per, f"{per} B/edge"
+    return in_bytes, "B_in"
+
+
+def measured_traffic(kernel: str):
+    """HBM bytes per launch for `kernel` from the committed rocprofv3 PMC summary
+    (profiles/latest_pmc.json, FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or None."""
+    p = ROOT / "profiles" / "latest_pmc.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get("kernels", {}).get(kernel, {}).get("traffic_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

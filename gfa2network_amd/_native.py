@@ -16,7 +16,7 @@ import numpy as np
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libg2n.so"
 
 ABI_VERSION = 1
-MAX_PHASES = 24
+MAX_PHASES = 40
 
 # status codes (include/g2n.h)
 OK = 0
@@ -85,6 +85,7 @@ class Result(ctypes.Structure):
         ("indptr", ctypes.c_void_p),
         ("indices", ctypes.c_void_p),
         ("data", ctypes.c_void_p),
+        ("names_bytes", ctypes.c_uint64),
         ("n_cast_overflow", ctypes.c_int64),
         ("input_bytes", ctypes.c_uint64),
         ("n_phases", ctypes.c_int32),
@@ -265,7 +266,10 @@ def _from_result(ptr, rc: int) -> RawResult:
             out.indptr = _view(r.indptr, r.n_nodes + 1, idx, owner)
             out.indices = _view(r.indices, r.nnz, idx, owner)
         out.data = _view(r.data, r.nnz, out.dtype, owner)
-    out.phase_ms = {r.phase_names[k].decode(): r.phase_ms[k] for k in range(r.n_phases)}
+    for k in range(r.n_phases):  # repeated phases (e.g. several insert rounds) add up
+        name = r.phase_names[k].decode()
+        if not name.startswith("_"):
+            out.phase_ms[name] = out.phase_ms.get(name, 0.0) + r.phase_ms[k]
     out.host_ms = {"read": r.host_ms_read, "h2d": r.host_ms_h2d, "d2h": r.host_ms_d2h}
     return out
 

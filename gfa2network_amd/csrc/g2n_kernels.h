@@ -65,7 +65,8 @@ struct Ctl {
   unsigned long long n_unique[2];
   unsigned long long n_keep;
   unsigned long long n_f32_overflow;  // edges whose float32 cast overflowed
-  unsigned long long pad[6];
+  unsigned long long deferred;        // touches left for the next insert round
+  unsigned long long pad[5];
 };
 
 struct ParseOpts {
@@ -79,6 +80,13 @@ struct TouchOut {
   uint32_t* nlen;
   uint64_t* ooff;
   uint32_t* olen;
+  uint8_t* tkind;
+};
+// dictionary entry (32 B): see k_insert_round
+struct DictEntry {
+  unsigned long long hdr;   // (hash tag << 32) | first touch, later | node id; ~0 = empty
+  unsigned long long meta;  // (publication round << 32) | key length; ~0 = unpublished
+  unsigned long long k0, k1;  // first 16 key bytes, zero padded
 };
 struct TouchIn {
   const uint64_t* noff;
@@ -115,17 +123,19 @@ __global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint
                                const uint64_t* worklist, uint64_t n_work, ParseOpts op, EdgeOut E, Ctl* ctl);
 __global__ void k_error_detail(const uint8_t* in, const uint64_t* ls, uint64_t line, Ctl* ctl);
 __global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
-__global__ void k_insert(const uint8_t* in, TouchIn T, uint64_t n_t, unsigned long long* table, uint64_t mask,
-                         uint64_t max_probes, uint32_t* slot, int bidir, Ctl* ctl);
-__global__ void k_mark_first(TouchIn T, const unsigned long long* table, uint64_t cap, int bidir, uint32_t* first,
+template <bool kClaim>
+__global__ void k_insert_round(const uint8_t* in, uint64_t in_len, TouchIn T, uint64_t n_t, DictEntry* table,
+                               uint64_t mask, uint64_t max_probes, uint32_t* slot, uint8_t* tstate, uint32_t round,
+                               int bidir, Ctl* ctl);
+__global__ void k_mark_first(TouchIn T, const DictEntry* table, uint64_t cap, int bidir, uint32_t* first,
                              uint64_t* flen);
-__global__ void k_assign_ids(unsigned long long* table, uint64_t cap, const uint32_t* nid);
+__global__ void k_assign_ids(DictEntry* table, uint64_t cap, const uint32_t* nid);
 __global__ void k_totals(const uint32_t* first, const uint32_t* nid, const uint64_t* flen, const uint64_t* foff,
                          uint64_t n_t, Ctl* ctl);
 __global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_t, const uint32_t* first, const uint32_t* nid,
                         const uint64_t* foff, int bidir, uint8_t* blob, int64_t* offs, const Ctl* ctl);
 template <class T>
-__global__ void k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* slot, const unsigned long long* table,
+__global__ void k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* slot, const DictEntry* table,
                            const uint32_t* nid, int tpe, int gd, int32_t* rows, int32_t* cols, T* data, Ctl* ctl);
 __global__ void k_make_keys(const int32_t* rows, const int32_t* cols, uint64_t n, int nb, int transposed,
                             unsigned long long* keys, uint32_t* vals);

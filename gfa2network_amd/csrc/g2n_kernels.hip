@@ -441,9 +441,10 @@ __device__ inline bool weight_fast(const uint8_t* __restrict__ in, uint64_t ts, 
 }
 
 __device__ inline void put_touch(const TouchOut& T, uint64_t t, uint64_t no, uint32_t nl, uint64_t oo, uint32_t ol,
-                                 bool bidir) {
+                                 bool bidir, uint8_t kind = 2) {
   T.noff[t] = no;
   T.nlen[t] = nl;
+  T.tkind[t] = kind;  // 1: S touch (first insert round), 2: edge touch
   if (bidir) {
     T.ooff[t] = oo;
     T.olen[t] = ol;
@@ -484,10 +485,10 @@ __global__ void __launch_bounds__(kTPB) k_parse(const uint8_t* __restrict__ in, 
     uint64_t ne = next_tab(in, ns, e);
     uint32_t nl = (uint32_t)(ne - ns);
     if (!op.bidir) {
-      put_touch(T, tb, ns, nl, 0, 0, false);
+      put_touch(T, tb, ns, nl, 0, 0, false, 1);
     } else {
-      put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true);
-      put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true);
+      put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
+      put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true, 1);
     }
     return;
   }
@@ -610,12 +611,6 @@ __global__ void __launch_bounds__(kTPB) k_count_records(const uint8_t* __restric
 }
 
 // ============================================================= K4: dictionary =====
-__device__ inline uint8_t touch_byte(const uint8_t* __restrict__ in, uint64_t no, uint32_t nl, uint64_t oo,
-                                     uint64_t j) {
-  if (j < nl) return in[no + j];
-  if (j == nl) return ':';
-  return (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + (j - nl - 1)];
-}
 
 __device__ inline uint64_t fmix64(uint64_t k) {
   k ^= k >> 33;
@@ -626,107 +621,180 @@ __device__ inline uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-__device__ inline uint64_t touch_hash(const uint8_t* __restrict__ in, uint64_t no, uint32_t nl, uint64_t oo,
-                                      uint32_t ol, bool bidir) {
-  uint64_t h = 0xcbf29ce484222325ull;
-  for (uint32_t j = 0; j < nl; j++) h = (h ^ in[no + j]) * 0x100000001b3ull;
-  if (bidir) {
-    h = (h ^ (uint64_t)':') * 0x100000001b3ull;
-    if (oo & kConstFlag) {
-      h = (h ^ (oo & 0xFF)) * 0x100000001b3ull;
-    } else {
-      for (uint32_t j = 0; j < ol; j++) h = (h ^ in[oo + j]) * 0x100000001b3ull;
-    }
-  }
-  return fmix64(h ^ ((uint64_t)nl << 40) ^ ol);
+typedef unsigned __int128 u128;
+
+// 8 bytes at aligned address a (a % 8 == 0); bytes at or past in_len read as 0
+__device__ inline uint64_t rd64(const uint8_t* __restrict__ in, uint64_t in_len, uint64_t a) {
+  if (a + 8 <= in_len) return *(const uint64_t*)(in + a);
+  uint64_t w = 0;
+  for (int b = 0; b < 8; b++)
+    if (a + b < in_len) w |= (uint64_t)in[a + b] << (8 * b);
+  return w;
 }
 
-__device__ inline bool touch_eq(const uint8_t* __restrict__ in, const TouchIn& T, uint64_t a, uint64_t b,
-                                bool bidir) {
-  uint64_t na = T.noff[a], nb = T.noff[b];
-  uint32_t la = T.nlen[a], lb = T.nlen[b];
-  if (!bidir) {
-    if (la != lb) return false;
-    for (uint32_t j = 0; j < la; j++)
-      if (in[na + j] != in[nb + j]) return false;
-    return true;
-  }
-  uint64_t oa = T.ooff[a], ob = T.ooff[b];
-  uint32_t pa = T.olen[a], pb = T.olen[b];
-  uint64_t tl = (uint64_t)la + 1 + pa;
-  if (tl != (uint64_t)lb + 1 + pb) return false;
-  if (la == lb) {  // common case: same split point
-    for (uint32_t j = 0; j < la; j++)
-      if (in[na + j] != in[nb + j]) return false;
-    for (uint32_t j = 0; j < pa; j++) {
-      uint8_t x = (oa & kConstFlag) ? (uint8_t)(oa & 0xFF) : in[oa + j];
-      uint8_t y = (ob & kConstFlag) ? (uint8_t)(ob & 0xFF) : in[ob + j];
-      if (x != y) return false;
+// first min(n, 16) bytes at `off`, little-endian, zero padded (aligned 8-byte loads)
+__device__ inline u128 load_span16(const uint8_t* __restrict__ in, uint64_t in_len, uint64_t off, uint64_t n) {
+  if (n == 0) return 0;
+  const uint64_t m = n < 16 ? n : 16;
+  const uint64_t a = off & ~7ull, end = off + m;
+  const uint32_t sh = (uint32_t)(off & 7) * 8;
+  uint64_t w0 = rd64(in, in_len, a);
+  uint64_t w1 = a + 8 < end ? rd64(in, in_len, a + 8) : 0;
+  uint64_t w2 = a + 16 < end ? rd64(in, in_len, a + 16) : 0;
+  uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  u128 k = ((u128)hi << 64) | lo;
+  if (m < 16) k &= (((u128)1) << (8 * m)) - 1;
+  return k;
+}
+
+// The first 16 bytes of a node key (name, or name + ":" + orientation when bidirected)
+// and its length.  builders.py:211-212, 234: keys are byte strings compared exactly.
+struct KeyHead {
+  u128 k;
+  uint32_t len;
+};
+
+__device__ inline KeyHead key_head(const uint8_t* __restrict__ in, uint64_t in_len, uint64_t no, uint32_t nl,
+                                   uint64_t oo, uint32_t ol, bool bidir) {
+  KeyHead kh;
+  kh.k = load_span16(in, in_len, no, nl);
+  kh.len = nl;
+  if (bidir) {
+    kh.len = nl + 1 + ol;
+    if (nl < 16) {
+      kh.k |= ((u128)':') << (8 * nl);
+      if (nl + 1 < 16) {
+        u128 o = (oo & kConstFlag) ? (u128)(oo & 0xFF) : load_span16(in, in_len, oo, ol);
+        kh.k |= o << (8 * (nl + 1));
+      }
     }
-    return true;
   }
-  for (uint64_t j = 0; j < tl; j++)
+  return kh;
+}
+
+__device__ inline uint8_t touch_byte(const uint8_t* __restrict__ in, uint64_t no, uint32_t nl, uint64_t oo,
+                                     uint64_t j) {
+  if (j < nl) return in[no + j];
+  if (j == nl) return ':';
+  return (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + (j - nl - 1)];
+}
+
+__device__ inline uint64_t key_hash(const uint8_t* __restrict__ in, const KeyHead& kh, uint64_t no, uint32_t nl,
+                                    uint64_t oo) {
+  const uint64_t lo = (uint64_t)kh.k, hi = (uint64_t)(kh.k >> 64);
+  uint64_t h = lo * 0x9E3779B97F4A7C15ull;
+  h ^= ((hi * 0xC2B2AE3D27D4EB4Full) << 31) | ((hi * 0xC2B2AE3D27D4EB4Full) >> 33);
+  h ^= (uint64_t)kh.len * 0x165667B19E3779F9ull;
+  for (uint64_t j = 16; j < kh.len; j++) h = (h ^ touch_byte(in, no, nl, oo, j)) * 0x100000001b3ull;  // long keys
+  return fmix64(h);
+}
+
+// bytes [16, len) of two keys of equal length (only for keys longer than the inline head)
+__device__ inline bool tail_eq(const uint8_t* __restrict__ in, const TouchIn& T, uint64_t a, uint64_t b, bool bidir,
+                               uint32_t len) {
+  const uint64_t na = T.noff[a], nb = T.noff[b];
+  const uint32_t la = T.nlen[a], lb = T.nlen[b];
+  const uint64_t oa = bidir ? T.ooff[a] : 0, ob = bidir ? T.ooff[b] : 0;
+  for (uint64_t j = 16; j < len; j++)
     if (touch_byte(in, na, la, oa, j) != touch_byte(in, nb, lb, ob, j)) return false;
   return true;
 }
 
-// Open-addressing table, 64-bit slots = (hash tag << 32) | representative touch.  A slot's
-// representative is lowered by atomicMin to the FIRST touch of its key, which is exactly
-// what Python's dict insertion order needs.
-__global__ void __launch_bounds__(kTPB) k_insert(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_t,
-                                                 unsigned long long* __restrict__ table, uint64_t mask,
-                                                 uint64_t max_probes, uint32_t* __restrict__ slot, int bidir,
-                                                 Ctl* ctl) {
+// Open-addressing dictionary, 32-byte entries: hdr = (hash tag << 32 | first touch),
+// meta = (round << 32 | key length), then the first 16 key bytes.  A touch compares its
+// key against an entry only when the entry was published in an EARLIER round (launch):
+// the inline bytes are then visible, and one random access resolves the touch.  Touches
+// meeting a same-tag entry claimed in the current round retry next round.  The
+// representative is lowered with atomicMin to the FIRST touch of the key — the order of
+// Python dict insertion (builders.py:194-198, 219-221).
+template <bool kClaim>  // kClaim: round 1 (touches of S lines); else: rounds >= 2 (everything left)
+__global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict__ in, uint64_t in_len, TouchIn T,
+                                                       uint64_t n_t, DictEntry* __restrict__ table, uint64_t mask,
+                                                       uint64_t max_probes, uint32_t* __restrict__ slot,
+                                                       uint8_t* __restrict__ tstate, uint32_t round, int bidir,
+                                                       Ctl* ctl) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (t >= n_t) return;
-  const uint64_t no = T.noff[t];
-  const uint32_t nl = T.nlen[t];
-  const uint64_t oo = bidir ? T.ooff[t] : 0;
-  const uint32_t ol = bidir ? T.olen[t] : 0;
-  const uint64_t h = touch_hash(in, no, nl, oo, ol, bidir != 0);
-  const uint32_t tag = (uint32_t)(h >> 32);
-  const unsigned long long mine = ((unsigned long long)tag << 32) | (uint32_t)t;
-  uint64_t idx = h & mask;
-  for (uint64_t probe = 0; probe < max_probes; probe++) {
-    unsigned long long cur = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == kEmptySlot) {
-      cur = atomicCAS(&table[idx], kEmptySlot, mine);
-      if (cur == kEmptySlot) {
-        slot[t] = (uint32_t)idx;
-        return;
+  bool deferred = false;
+  if (t < n_t) {
+    const uint8_t st = tstate[t];
+    if (st != 0 && !(kClaim && st != 1)) {
+      const uint64_t no = T.noff[t];
+      const uint32_t nl = T.nlen[t];
+      const uint64_t oo = bidir ? T.ooff[t] : 0;
+      const uint32_t ol = bidir ? T.olen[t] : 0;
+      const KeyHead kh = key_head(in, in_len, no, nl, oo, ol, bidir != 0);
+      const uint64_t h = key_hash(in, kh, no, nl, oo);
+      const uint32_t tag = (uint32_t)(h >> 32);
+      const unsigned long long mine = ((unsigned long long)tag << 32) | (uint32_t)t;
+      uint64_t idx = h & mask;
+      bool done = false;
+      for (uint64_t probe = 0; probe < max_probes && !done && !deferred; probe++) {
+        DictEntry* e = table + idx;
+        unsigned long long cur = __hip_atomic_load(&e->hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kEmptySlot) {
+          cur = atomicCAS(&e->hdr, kEmptySlot, mine);
+          if (cur == kEmptySlot) {  // claimed: publish the key for later rounds
+            e->k0 = (uint64_t)kh.k;
+            e->k1 = (uint64_t)(kh.k >> 64);
+            e->meta = ((unsigned long long)round << 32) | kh.len;
+            slot[t] = (uint32_t)idx;
+            tstate[t] = 0;
+            done = true;
+            break;
+          }
+        }
+        if ((uint32_t)(cur >> 32) == tag) {
+          const unsigned long long meta = __hip_atomic_load(&e->meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((meta >> 32) >= round) {  // published in this launch (or not yet): next round
+            deferred = true;
+            break;
+          }
+          if ((uint32_t)meta == kh.len && e->k0 == (uint64_t)kh.k && e->k1 == (uint64_t)(kh.k >> 64) &&
+              (kh.len <= 16 || tail_eq(in, T, t, (uint32_t)cur, bidir != 0, kh.len))) {
+            if ((uint32_t)cur > (uint32_t)t) atomicMin(&e->hdr, mine);
+            slot[t] = (uint32_t)idx;
+            tstate[t] = 0;
+            done = true;
+            break;
+          }
+        }
+        idx = (idx + 1) & mask;
       }
+      if (!done && !deferred) ctl->table_overflow = 1;  // the host retries with a larger table
     }
-    if ((uint32_t)(cur >> 32) == tag && touch_eq(in, T, t, (uint32_t)cur, bidir != 0)) {
-      if ((uint32_t)cur > (uint32_t)t) atomicMin(&table[idx], mine);
-      slot[t] = (uint32_t)idx;
-      return;
-    }
-    idx = (idx + 1) & mask;
   }
-  ctl->table_overflow = 1;  // the host retries with a table sized for every touch
+  // one atomic per wave for the deferred count
+  unsigned long long d = __ballot(deferred);
+  if ((threadIdx.x & 63) == 0 && d) atomicAdd(&ctl->deferred, (unsigned long long)__popcll(d));
 }
 
-// After all inserts, every occupied slot holds the FIRST touch of its key: mark it.
-__global__ void __launch_bounds__(kTPB) k_mark_first(TouchIn T, const unsigned long long* __restrict__ table,
-                                                     uint64_t cap, int bidir, uint32_t* __restrict__ first,
+template __global__ void k_insert_round<true>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,
+                                              uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*);
+template __global__ void k_insert_round<false>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,
+                                               uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*);
+
+// After all rounds, every occupied entry holds the FIRST touch of its key: mark it.
+__global__ void __launch_bounds__(kTPB) k_mark_first(TouchIn T, const DictEntry* __restrict__ table, uint64_t cap,
+                                                     int bidir, uint32_t* __restrict__ first,
                                                      uint64_t* __restrict__ flen) {
   const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (s >= cap) return;
-  const unsigned long long v = table[s];
+  const unsigned long long v = table[s].hdr;
   if (v == kEmptySlot) return;
   const uint32_t rep = (uint32_t)v;
   first[rep] = 1u;
-  flen[rep] = (uint64_t)T.nlen[rep] + (bidir ? 1ull + T.olen[rep] : 0ull);
+  flen[rep] = (uint32_t)table[s].meta;  // key length
 }
 
-// Replace each slot's representative by its node id (= rank of its first touch).
-__global__ void __launch_bounds__(kTPB) k_assign_ids(unsigned long long* __restrict__ table, uint64_t cap,
+// Replace each entry's representative by its node id (= rank of its first touch).
+__global__ void __launch_bounds__(kTPB) k_assign_ids(DictEntry* __restrict__ table, uint64_t cap,
                                                      const uint32_t* __restrict__ nid) {
   const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (s >= cap) return;
-  const unsigned long long v = table[s];
+  const unsigned long long v = table[s].hdr;
   if (v == kEmptySlot) return;
-  table[s] = (v & 0xFFFFFFFF00000000ull) | nid[(uint32_t)v];
+  table[s].hdr = (v & 0xFFFFFFFF00000000ull) | nid[(uint32_t)v];
 }
 
 __global__ void k_totals(const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
@@ -808,14 +876,14 @@ struct Cast<double> {
 
 template <class T>
 __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* __restrict__ slot,
-                                                   const unsigned long long* __restrict__ table,
+                                                   const DictEntry* __restrict__ table,
                                                    const uint32_t* __restrict__ nid, int tpe, int gd,
                                                    int32_t* __restrict__ rows, int32_t* __restrict__ cols,
                                                    T* __restrict__ data, Ctl* ctl) {
   const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (e >= n_e) return;
   const uint64_t tb = E.tb[e];
-  auto id = [&](uint64_t t) -> int32_t { return (int32_t)(uint32_t)table[slot[t]]; };  // slot -> node id
+  auto id = [&](uint64_t t) -> int32_t { return (int32_t)(uint32_t)table[slot[t]].hdr; };  // slot -> node id
   T v;
   const double wv = E.w[e];
   uint32_t err = Cast<T>::go(wv, &v);
@@ -1122,7 +1190,7 @@ __global__ void __launch_bounds__(kTPB) k_tag_values(uint64_t n, uint32_t tag, u
 
 // ----------------------------------------------------------- explicit instances --
 #define G2N_INST(T)                                                                                              \
-  template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const unsigned long long*,             \
+  template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
   template __global__ void k_group_sum<T>(const unsigned long long*, const uint32_t*, uint64_t, const uint32_t*,  \
                                           const uint32_t*, const T*, int, unsigned long long*, T*, uint8_t*,      \

@@ -33,7 +33,7 @@ enum Slot {
   S_IN, S_TILE_CNT, S_TILE_BASE, S_LS, S_KIND, S_PACK, S_PACK_SCAN, S_NOFF, S_NLEN, S_OOFF, S_OLEN, S_EW, S_ETB,
   S_WL, S_TABLE, S_SLOT, S_FIRST, S_NID, S_FLEN, S_FOFF, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1,
   S_VALS0, S_VALS1, S_HEAD, S_HPOS, S_UKEYS0, S_UDATA0, S_UKEYS1, S_UDATA1, S_ROWFLAG, S_KV, S_ORD, S_MK, S_MV,
-  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_BLK, S_NSLOTS
+  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_BLK, S_TKIND, S_TSTATE, S_NSLOTS
 };
 
 struct DevBuf {
@@ -267,7 +267,7 @@ static void assemble(g2n_context* c, const int32_t* rows, const int32_t* cols, c
 
 template <class T>
 static void run_triplets(g2n_context* c, EdgeIn E, uint64_t n_e, const uint32_t* slot,
-                         const unsigned long long* table, const uint32_t* nid, int tpe, int gd, int32_t* rows,
+                         const DictEntry* table, const uint32_t* nid, int tpe, int gd, int32_t* rows,
                          int32_t* cols, void* data) {
   if (n_e)
     hipLaunchKernelGGL((k_triplets<T>), dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E, n_e, slot, table, nid, tpe,
@@ -363,14 +363,16 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     op.wt = wt;
   }
   TouchOut T{dget<uint64_t>(c, S_NOFF, n_t), dget<uint32_t>(c, S_NLEN, n_t),
-             bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr};
+             bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr,
+             dget<uint8_t>(c, S_TKIND, n_t)};
   EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
   auto* wl = dget<uint64_t>(c, S_WL, n_e);
+  phase(c, "_prep");
   if (n_lines)
     hipLaunchKernelGGL(k_parse, dim3(grid_for(n_lines)), dim3(kTPB), 0, c->stream, in, ls, kind, pack_scan, n_lines,
                        op, T, E, c->ctl, wl);
-  sync_ctl(c);
   phase(c, "parse");
+  sync_ctl(c);
   const uint64_t n_work = c->h_ctl->wl_count;
   if (n_work) {
     hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, ls, pack_scan, wl,
@@ -424,7 +426,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   uint64_t full_cap = 1024;
   while (full_cap < 2 * n_t) full_cap <<= 1;
   uint64_t cap = 1024;
-  while (cap < 2 * est) cap <<= 1;
+  while (cap < est + est / 2) cap <<= 1;
   if (cap > full_cap) cap = full_cap;
   auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
   auto* first = dget<uint32_t>(c, S_FIRST, n_t);
@@ -432,20 +434,36 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   auto* flen = dget<uint64_t>(c, S_FLEN, n_t);
   auto* foff = dget<uint64_t>(c, S_FOFF, n_t);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
-  unsigned long long* table = nullptr;
+  DictEntry* table = nullptr;
+  auto* tstate = dget<uint8_t>(c, S_TSTATE, n_t);
   if (n_t) {
     while (true) {
-      table = dget<unsigned long long>(c, S_TABLE, cap);
-      G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(unsigned long long), c->stream));
+      table = dget<DictEntry>(c, S_TABLE, cap);
+      G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
+      G2N_HIP(hipMemcpyAsync(tstate, T.tkind, n_t, hipMemcpyDeviceToDevice, c->stream));
+      phase(c, "table_init");
       const uint64_t max_probes = cap >= full_cap ? cap : 4096;
-      hipLaunchKernelGGL(k_insert, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, table, cap - 1,
-                         max_probes, slot, (int)bidir, c->ctl);
-      if (cap >= full_cap) break;
-      if (read_dev(c, &c->ctl->table_overflow) == 0) break;
+      bool overflow = false;
+      for (uint32_t round = 1;; round++) {  // round 1: S touches; then every unresolved touch
+        G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
+        phase(c, "_prep");
+        if (round == 1)
+          hipLaunchKernelGGL(k_insert_round<true>, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, len, TI, n_t,
+                             table, cap - 1, max_probes, slot, tstate, round, (int)bidir, c->ctl);
+        else
+          hipLaunchKernelGGL(k_insert_round<false>, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, len, TI, n_t,
+                             table, cap - 1, max_probes, slot, tstate, round, (int)bidir, c->ctl);
+        phase(c, round == 1 ? "insert_claim" : "insert_lookup");
+        sync_ctl(c);
+        if (c->h_ctl->table_overflow) { overflow = true; break; }
+        if (round > 1 && c->h_ctl->deferred == 0) break;
+        if (round > 100000) throw Failure(G2N_E_DEVICE, "dictionary insert did not converge");
+      }
+      if (!overflow) break;
+      if (cap >= full_cap) throw Failure(G2N_E_DEVICE, "node table overflow");
       G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
       cap = full_cap;
     }
-    phase(c, "insert");
     G2N_HIP(hipMemsetAsync(first, 0, n_t * sizeof(uint32_t), c->stream));
     G2N_HIP(hipMemsetAsync(flen, 0, n_t * sizeof(uint64_t), c->stream));
     hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, TI, table, cap, (int)bidir,
@@ -461,6 +479,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   const uint64_t names_len = n_t ? c->h_ctl->names_len : 0;
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
+  R->names_bytes = names_len;
   phase(c, "ids");
   if (o->want_node_names) {
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
@@ -483,6 +502,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   auto* cols = dget<int32_t>(c, S_COLS, n_trip);
   void* data = dbuf(c, S_DATA, n_trip * dtype_size(dt));
   EdgeIn EI{E.w, E.tb};
+  phase(c, "_prep");
   switch (dt) {
     case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
     case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
@@ -490,10 +510,10 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
     default: run_triplets<double>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
   }
+  phase(c, "triplets");
   sync_ctl(c);
   const uint64_t cast_key = c->h_ctl->cast_key;
   R->n_cast_overflow = (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip);
-  phase(c, "triplets");
   if (cast_key != ~0ull) {  // np.array(data, dtype) raises at the first bad element
     R->status = (int)(cast_key & 15);
     R->err_index = (int64_t)(cast_key >> 4);

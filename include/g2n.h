@@ -83,7 +83,7 @@ typedef struct g2n_options {
   int32_t reserved[6];
 } g2n_options;
 
-#define G2N_MAX_PHASES 24
+#define G2N_MAX_PHASES 40
 
 /* Result of one build.  All pointers are owned by the result (host memory for the
  * host entry points, device memory for g2n_build_device) and stay valid until
@@ -116,6 +116,7 @@ typedef struct g2n_result {
   const void *indptr;          /* CSR: n_nodes + 1 */
   const void *indices;         /* CSR */
   const void *data;            /* nnz elements of dtype */
+  uint64_t names_bytes;        /* total bytes of all node keys (names blob length) */
   int64_t n_cast_overflow;     /* float32 casts that overflowed to +-inf: numpy warns
                                   RuntimeWarning("overflow encountered in cast") once each */
   uint64_t input_bytes;        /* uncompressed GFA bytes parsed */
