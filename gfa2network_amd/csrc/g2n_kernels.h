@@ -137,32 +137,6 @@ __global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_t, const uint32
 template <class T>
 __global__ void k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* slot, const DictEntry* table,
                            const uint32_t* nid, int tpe, int gd, int32_t* rows, int32_t* cols, T* data, Ctl* ctl);
-__global__ void k_make_keys(const int32_t* rows, const int32_t* cols, uint64_t n, int nb, int transposed,
-                            unsigned long long* keys, uint32_t* vals);
-__global__ void k_heads(const unsigned long long* keys, const uint32_t* vals, uint64_t n, int nb, uint32_t* head,
-                        Ctl* ctl, int which);
-__global__ void k_count_from_scan(const uint32_t* flag, const uint32_t* pos, uint64_t n, unsigned long long* out);
-template <class T>
-__global__ void k_group_sum(const unsigned long long* keys, const uint32_t* vals, uint64_t n, const uint32_t* head,
-                            const uint32_t* hpos, const T* data, int nb, unsigned long long* ukeys, T* udata,
-                            uint8_t* rowflag, Ctl* ctl, int which);
-template <class I>
-__global__ void k_indptr(const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, int nb,
-                         uint64_t n_rows, I* indptr);
-template <class I>
-__global__ void k_split_keys(const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, int nb,
-                             I* indices);
-template <class T>
-__global__ void k_emulate_rows(const unsigned long long* keys, const uint32_t* vals, uint64_t n, int nb,
-                               uint64_t n_rows, const uint8_t* rowflag, const T* data,
-                               const unsigned long long* ukeys, const unsigned long long* n_unique_ptr, T* udata,
-                               KV<int32_t, T>* kv, uint32_t* ord);
-template <class T>
-__global__ void k_maxsym(const unsigned long long* mk, const uint32_t* mv, uint64_t m, const T* ua, const T* ut,
-                         uint32_t* keep, T* mval);
-template <class T>
-__global__ void k_compact(const unsigned long long* mk, const T* mval, const uint32_t* keep, const uint32_t* kpos,
-                          uint64_t m, unsigned long long* okeys, T* odata);
-__global__ void k_tag_values(uint64_t n, uint32_t tag, uint32_t* v);
+// K7-K9 (COO -> CSR) kernels are templates defined in g2n_kernels.hip (same translation unit).
 
 }  // namespace g2n

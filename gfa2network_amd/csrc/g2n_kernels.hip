@@ -916,40 +916,13 @@ __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const
 }
 
 // ======================================================= K7-K9: COO -> CSR ========
-__global__ void __launch_bounds__(kTPB) k_make_keys(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
-                                                    uint64_t n, int nb, int transposed,
-                                                    unsigned long long* __restrict__ keys,
-                                                    uint32_t* __restrict__ vals) {
-  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (i >= n) return;
-  uint64_t r = (uint32_t)rows[i], c = (uint32_t)cols[i];
-  if (transposed) {
-    uint64_t t = r;
-    r = c;
-    c = t;
-  }
-  keys[i] = (r << nb) | c;
-  vals[i] = (uint32_t)i;
-}
-
-// group heads; and scipy's has_sorted_indices of the scattered matrix: within a row, the
-// stream order of entries must have non-decreasing columns, i.e. after a stable sort by
-// (row, col) the stream positions must increase along the row.
-__global__ void __launch_bounds__(kTPB) k_heads(const unsigned long long* __restrict__ keys,
-                                                const uint32_t* __restrict__ vals, uint64_t n, int nb,
-                                                uint32_t* __restrict__ head, Ctl* ctl, int which) {
-  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (p >= n) return;
-  bool h = p == 0 || keys[p] != keys[p - 1];
-  head[p] = h ? 1u : 0u;
-  if (p > 0 && (keys[p] >> nb) == (keys[p - 1] >> nb) && vals[p - 1] > vals[p]) ctl->unsorted[which] = 1;
-}
-
-__global__ void k_count_from_scan(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos, uint64_t n,
-                                  unsigned long long* out) {
-  *out = n ? (unsigned long long)pos[n - 1] + flag[n - 1] : 0ull;
-}
-
+// scipy's coo.tocsr() = coo_tocsr (scatter rows in stream order) + csr_sort_indices
+// (std::sort by column, only when some row is unsorted) + csr_sum_duplicates (left-to-right
+// run sums, in dtype).  On the GPU: a STABLE radix sort by row alone (32-bit keys; the column
+// and value travel as the payload) reproduces coo_tocsr's per-row stream order; one thread per
+// row then sorts its entries by column (stably: equal to std::sort whenever the result can
+// not depend on it) and sums runs.  Rows whose float sums could depend on std::sort's exact
+// permutation are re-run with the restated libstdc++ introsort (stl_sort.h).
 // x86-64 SSE semantics of scipy's `x += y` (csr_sum_duplicates), bit for bit
 template <class T>
 struct Acc;
@@ -1002,49 +975,57 @@ __device__ inline bool exact_term(T v) {
   return d == __builtin_trunc(d);  // integral (false for inf/nan)
 }
 
-// Sum each (row, col) group in stream order (= scipy's order whenever it is provably
-// order-independent); flag rows whose float groups could depend on std::sort's order.
+
 template <class T>
-__global__ void __launch_bounds__(kTPB) k_group_sum(const unsigned long long* __restrict__ keys,
-                                                    const uint32_t* __restrict__ vals, uint64_t n,
-                                                    const uint32_t* __restrict__ head,
-                                                    const uint32_t* __restrict__ hpos,
-                                                    const T* __restrict__ data, int nb,
-                                                    unsigned long long* __restrict__ ukeys, T* __restrict__ udata,
-                                                    uint8_t* __restrict__ rowflag, Ctl* ctl, int which) {
-  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (p >= n || !head[p]) return;
-  const unsigned long long key = keys[p];
-  const uint64_t u = hpos[p];
-  T x = data[vals[p]];
-  bool exact = true;
-  double sabs = 0.0;
-  if (Acc<T>::is_float()) {
-    exact = exact_term(x);
-    sabs = __builtin_fabs((double)x);
-  }
-  uint64_t q = p + 1;
-  uint32_t cnt = 1;
-  while (q < n && keys[q] == key) {
-    T y = data[vals[q]];
-    if (Acc<T>::is_float()) {
-      exact = exact && exact_term(y);
-      sabs += __builtin_fabs((double)y);
-    }
-    x = Acc<T>::add(x, y);
-    q++;
-    cnt++;
-  }
-  ukeys[u] = key;
-  udata[u] = x;
-  if (Acc<T>::is_float() && cnt >= 3 && !(exact && sabs < Acc<T>::limit())) {
-    rowflag[key >> nb] = 1;
-    ctl->flagged[which] = 1;
+struct PV {  // sort payload: the other coordinate and the value
+  uint32_t c;
+  T v;
+};
+
+// Sum of k copies of one value (the unweighted build: every entry is dtype(1.0)), exactly as
+// the left-to-right `x += y` of csr_sum_duplicates would produce it.
+template <class T>
+__device__ inline T sum_copies(T one, uint64_t k);
+template <>
+__device__ inline uint8_t sum_copies<uint8_t>(uint8_t one, uint64_t k) { return one; }
+template <>
+__device__ inline int8_t sum_copies<int8_t>(int8_t one, uint64_t k) {
+  return (int8_t)(uint8_t)((uint64_t)(uint8_t)one * k);
+}
+template <>
+__device__ inline int32_t sum_copies<int32_t>(int32_t one, uint64_t k) {
+  return (int32_t)(uint32_t)((uint64_t)(uint32_t)one * k);
+}
+template <>
+__device__ inline float sum_copies<float>(float one, uint64_t k) {  // one == 1.0f: stalls at 2^24
+  return (float)(k < 16777216ull ? k : 16777216ull);
+}
+template <>
+__device__ inline double sum_copies<double>(double one, uint64_t k) {  // one == 1.0: stalls at 2^53
+  return (double)(k < 9007199254740992ull ? k : 9007199254740992ull);
+}
+
+// sort inputs: key = row (column when transposed); payload = column (row) [+ value]
+template <class T, bool kUniform>
+__global__ void __launch_bounds__(kTPB) k_pack(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                               const T* __restrict__ data, uint64_t n, int transposed,
+                                               uint32_t* __restrict__ key, PV<T>* __restrict__ pv,
+                                               uint32_t* __restrict__ pc) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = (uint32_t)rows[i], c = (uint32_t)cols[i];
+  key[i] = transposed ? c : r;
+  if (kUniform) {
+    pc[i] = transposed ? r : c;
+  } else {
+    PV<T> x;
+    x.c = transposed ? r : c;
+    x.v = data[i];
+    pv[i] = x;
   }
 }
 
-__device__ inline uint64_t lower_bound_u64(const unsigned long long* __restrict__ a, uint64_t n,
-                                           unsigned long long key) {
+__device__ inline uint64_t lower_bound_u32(const uint32_t* __restrict__ a, uint64_t n, uint32_t key) {
   uint64_t lo = 0, hi = n;
   while (lo < hi) {
     uint64_t mid = (lo + hi) >> 1;
@@ -1054,81 +1035,133 @@ __device__ inline uint64_t lower_bound_u64(const unsigned long long* __restrict_
   return lo;
 }
 
-template <class I>
-__global__ void __launch_bounds__(kTPB) k_indptr(const unsigned long long* __restrict__ ukeys,
-                                                 const unsigned long long* __restrict__ n_unique_ptr, int nb,
-                                                 uint64_t n_rows, I* __restrict__ indptr) {
+// start[r] = first sorted position of row r (start[n_rows] = n)
+__global__ void __launch_bounds__(kTPB) k_row_start(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_rows,
+                                                    uint32_t* __restrict__ start) {
   const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (r > n_rows) return;
-  const uint64_t nu = *n_unique_ptr;
-  indptr[r] = (I)(r == n_rows ? nu : lower_bound_u64(ukeys, nu, (unsigned long long)r << nb));
+  start[r] = (uint32_t)(r == n_rows ? n : lower_bound_u32(key, n, (uint32_t)r));
 }
 
-template <class I>
-__global__ void __launch_bounds__(kTPB) k_split_keys(const unsigned long long* __restrict__ ukeys,
-                                                     const unsigned long long* __restrict__ n_unique_ptr, int nb,
-                                                     I* __restrict__ indices) {
-  const uint64_t u = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (u >= *n_unique_ptr) return;
-  indices[u] = (I)(ukeys[u] & ((1ull << nb) - 1));
+// One thread per row: the row's entries (stream order) -> sorted unique (column, sum)
+// written at the front of the row's segment of `out`; ucnt[r] = unique entries.
+template <class T, bool kUniform>
+__global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ start, uint64_t n_rows,
+                                                  const PV<T>* __restrict__ pv, const uint32_t* __restrict__ pc,
+                                                  PV<T>* __restrict__ out, PV<T>* __restrict__ scr,
+                                                  uint32_t* __restrict__ ucnt, T one, uint8_t* __restrict__ rowflag,
+                                                  Ctl* ctl, int which) {
+  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (r >= n_rows) return;
+  const uint32_t s = start[r], e = start[r + 1];
+  const uint32_t len = e - s;
+  if (len == 0) {
+    ucnt[r] = 0;
+    return;
+  }
+  PV<T>* o = out + s;
+  // copy in stream order and note scipy's has_sorted_indices for this row
+  bool sorted = true;
+  uint32_t prev = 0;
+  for (uint32_t q = 0; q < len; q++) {
+    PV<T> x;
+    if (kUniform) {
+      x.c = pc[s + q];
+      x.v = one;
+    } else {
+      x = pv[s + q];
+    }
+    if (q && x.c < prev) sorted = false;
+    prev = x.c;
+    o[q] = x;
+  }
+  if (!sorted) {
+    ctl->unsorted[which] = 1;
+    if (len <= 32) {  // stable insertion sort by column
+      for (uint32_t q = 1; q < len; q++) {
+        PV<T> x = o[q];
+        int32_t z = (int32_t)q - 1;
+        while (z >= 0 && o[z].c > x.c) {
+          o[z + 1] = o[z];
+          z--;
+        }
+        o[z + 1] = x;
+      }
+    } else {  // long row: stable bottom-up merge sort, ping-pong with the row's scratch segment
+      PV<T>* src = o;
+      PV<T>* dst = scr + s;
+      for (uint32_t width = 1; width < len; width <<= 1) {
+        for (uint32_t lo = 0; lo < len; lo += 2 * width) {
+          const uint32_t mid = lo + width < len ? lo + width : len;
+          const uint32_t hi = lo + 2 * width < len ? lo + 2 * width : len;
+          uint32_t a = lo, b = mid, w = lo;
+          while (a < mid && b < hi) dst[w++] = (src[b].c < src[a].c) ? src[b++] : src[a++];
+          while (a < mid) dst[w++] = src[a++];
+          while (b < hi) dst[w++] = src[b++];
+        }
+        PV<T>* t = src;
+        src = dst;
+        dst = t;
+      }
+      if (src != o)
+        for (uint32_t q = 0; q < len; q++) o[q] = src[q];
+    }
+  }
+  // left-to-right run sums
+  uint32_t u = 0, q = 0;
+  bool flag = false;
+  while (q < len) {
+    const uint32_t c = o[q].c;
+    uint32_t q0 = q;
+    T x = o[q].v;
+    bool exact = true;
+    double sabs = 0.0;
+    if (!kUniform && Acc<T>::is_float()) {
+      exact = exact_term(x);
+      sabs = __builtin_fabs((double)x);
+    }
+    q++;
+    while (q < len && o[q].c == c) {
+      if (!kUniform) {
+        T y = o[q].v;
+        if (Acc<T>::is_float()) {
+          exact = exact && exact_term(y);
+          sabs += __builtin_fabs((double)y);
+        }
+        x = Acc<T>::add(x, y);
+      }
+      q++;
+    }
+    if (kUniform) x = sum_copies<T>(one, q - q0);
+    if (!kUniform && Acc<T>::is_float() && q - q0 >= 3 && !(exact && sabs < Acc<T>::limit())) flag = true;
+    PV<T> y;
+    y.c = c;
+    y.v = x;
+    o[u++] = y;
+  }
+  ucnt[r] = u;
+  if (flag && len > 16) {  // std::sort on > 16 elements is not an insertion sort
+    rowflag[r] = 1;
+    ctl->flagged[which] = 1;
+  }
 }
 
-// Rows whose sums could depend on the order: redo exactly what scipy does for the row —
-// scatter in stream order (coo_tocsr), std::sort by column (csr_sort_indices, restated in
-// stl_sort.h), left-to-right run sums (csr_sum_duplicates).  Only rows of > 16 entries get
-// here: std::sort on <= 16 elements is an insertion sort, which is stable.
+// Flagged rows when the matrix is unsorted: exactly scipy's per-row std::sort + run sums.
 template <class T>
-__global__ void __launch_bounds__(64) k_emulate_rows(const unsigned long long* __restrict__ keys,
-                                                     const uint32_t* __restrict__ vals, uint64_t n, int nb,
-                                                     uint64_t n_rows, const uint8_t* __restrict__ rowflag,
-                                                     const T* __restrict__ data,
-                                                     const unsigned long long* __restrict__ ukeys,
-                                                     const unsigned long long* __restrict__ n_unique_ptr,
-                                                     T* __restrict__ udata, KV<int32_t, T>* __restrict__ kv,
-                                                     uint32_t* __restrict__ ord) {
+__global__ void __launch_bounds__(64) k_row_emulate(const uint32_t* __restrict__ start, uint64_t n_rows,
+                                                    const uint8_t* __restrict__ rowflag,
+                                                    const PV<T>* __restrict__ pv, PV<T>* __restrict__ out,
+                                                    KV<int32_t, T>* __restrict__ kv) {
   const uint64_t r = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (r >= n_rows || !rowflag[r]) return;
-  const uint64_t rs = lower_bound_u64(keys, n, (unsigned long long)r << nb);
-  const uint64_t re = lower_bound_u64(keys, n, (unsigned long long)(r + 1) << nb);
-  const uint64_t len = re - rs;
-  if (len <= 16) return;
-  // stream order of the row: sort its sorted positions (rs..re) by stream index (heap sort)
-  uint32_t* o = ord + rs;
-  for (uint64_t q = 0; q < len; q++) o[q] = (uint32_t)q;
-  const uint32_t* sv = vals + rs;
-  auto sift = [&](int64_t root, int64_t end) {
-    while (true) {
-      int64_t c = 2 * root + 1;
-      if (c >= end) break;
-      if (c + 1 < end && sv[o[c + 1]] > sv[o[c]]) c++;
-      if (sv[o[c]] > sv[o[root]]) {
-        uint32_t t = o[c];
-        o[c] = o[root];
-        o[root] = t;
-        root = c;
-      } else {
-        break;
-      }
-    }
-  };
-  for (int64_t st = (int64_t)len / 2 - 1; st >= 0; st--) sift(st, (int64_t)len);
-  for (int64_t end = (int64_t)len - 1; end > 0; end--) {
-    uint32_t t = o[0];
-    o[0] = o[end];
-    o[end] = t;
-    sift(0, end);
-  }
-  // (col, val) pairs in stream order = coo_tocsr's scatter order for this row
-  KV<int32_t, T>* a = kv + rs;
-  const uint64_t cmask = (1ull << nb) - 1;
-  for (uint64_t q = 0; q < len; q++) {
-    const uint64_t z = rs + o[q];
-    a[q].k = (int32_t)(keys[z] & cmask);
-    a[q].v = data[vals[z]];
+  const uint32_t s = start[r], len = start[r + 1] - s;
+  KV<int32_t, T>* a = kv + s;
+  for (uint32_t q = 0; q < len; q++) {
+    a[q].k = (int32_t)pv[s + q].c;
+    a[q].v = pv[s + q].v;
   }
   stl_sort(a, a + len);
-  const uint64_t us = lower_bound_u64(ukeys, *n_unique_ptr, (unsigned long long)r << nb);
-  uint64_t g = 0, q = 0;
+  uint32_t u = 0, q = 0;
   while (q < len) {
     int32_t c = a[q].k;
     T x = a[q].v;
@@ -1137,79 +1170,110 @@ __global__ void __launch_bounds__(64) k_emulate_rows(const unsigned long long* _
       x = Acc<T>::add(x, a[q].v);
       q++;
     }
-    udata[us + g] = x;
-    g++;
+    out[s + u].c = (uint32_t)c;
+    out[s + u].v = x;
+    u++;
   }
 }
 
-// M = maximum(B, B^T') over the merged key streams of B and BT (csr_binop_csr_canonical
-// with std::max: (a < b) ? b : a, missing = 0, results == 0 dropped).
+// SUM CSR: row r's unique entries -> indices/data at indptr[r]
 template <class T>
-__device__ inline bool nonzero(T x) { return x != (T)0; }
-
-template <class T>
-__global__ void __launch_bounds__(kTPB) k_maxsym(const unsigned long long* __restrict__ mk,
-                                                 const uint32_t* __restrict__ mv, uint64_t m,
-                                                 const T* __restrict__ ua, const T* __restrict__ ut,
-                                                 uint32_t* __restrict__ keep, T* __restrict__ mval) {
-  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (p >= m) return;
-  if (p > 0 && mk[p] == mk[p - 1]) {
-    keep[p] = 0;
-    return;
+__global__ void __launch_bounds__(kTPB) k_row_compact(const uint32_t* __restrict__ start,
+                                                      const uint32_t* __restrict__ ucnt,
+                                                      const uint32_t* __restrict__ uoff, uint64_t n_rows,
+                                                      const PV<T>* __restrict__ out, int32_t* __restrict__ indptr,
+                                                      int32_t* __restrict__ indices, T* __restrict__ data) {
+  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (r >= n_rows) return;
+  const uint32_t s = start[r], u = ucnt[r], o = uoff[r];
+  indptr[r] = (int32_t)o;
+  if (r == n_rows - 1) indptr[n_rows] = (int32_t)(o + u);
+  for (uint32_t j = 0; j < u; j++) {
+    indices[o + j] = (int32_t)out[s + j].c;
+    data[o + j] = out[s + j].v;
   }
-  T a = (T)0, b = (T)0;
-  uint32_t v0 = mv[p];
-  if (v0 >> 31) b = ut[v0 & 0x7FFFFFFFu];
-  else a = ua[v0];
-  if (p + 1 < m && mk[p + 1] == mk[p]) {
-    uint32_t v1 = mv[p + 1];
-    if (v1 >> 31) b = ut[v1 & 0x7FFFFFFFu];
-    else a = ua[v1];
-  }
-  T r = (a < b) ? b : a;
-  keep[p] = nonzero(r) ? 1u : 0u;
-  mval[p] = r;
 }
 
-template <class T>
-__global__ void __launch_bounds__(kTPB) k_compact(const unsigned long long* __restrict__ mk,
-                                                  const T* __restrict__ mval, const uint32_t* __restrict__ keep,
-                                                  const uint32_t* __restrict__ kpos, uint64_t m,
-                                                  unsigned long long* __restrict__ okeys, T* __restrict__ odata) {
-  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (p >= m || !keep[p]) return;
-  okeys[kpos[p]] = mk[p];
-  odata[kpos[p]] = mval[p];
+// M = A.maximum(A.T) row by row: merge row r of B (= SUM(A)) and of BT (= SUM(A.T)), both sorted
+// by column; csr_binop_csr_canonical with std::max ((a < b) ? b : a), missing = 0, zeros dropped.
+template <class T, bool kWrite>
+__global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ ua,
+                                                  const PV<T>* __restrict__ oa, const uint32_t* __restrict__ st,
+                                                  const uint32_t* __restrict__ ut, const PV<T>* __restrict__ ot,
+                                                  uint64_t n_rows, uint32_t* __restrict__ mcnt,
+                                                  const uint32_t* __restrict__ moff, int32_t* __restrict__ indptr,
+                                                  int32_t* __restrict__ indices, T* __restrict__ data) {
+  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (r >= n_rows) return;
+  const PV<T>* A = oa + sa[r];
+  const PV<T>* B = ot + st[r];
+  const uint32_t na = ua[r], nb = ut[r];
+  uint32_t i = 0, j = 0, m = 0;
+  const uint32_t base = kWrite ? moff[r] : 0;
+  if (kWrite) {
+    indptr[r] = (int32_t)base;
+    if (r == n_rows - 1) indptr[n_rows] = (int32_t)(base + mcnt[r]);
+  }
+  auto emit = [&](uint32_t c, T x, T y) {
+    T v = (x < y) ? y : x;
+    if (v != (T)0) {
+      if (kWrite) {
+        indices[base + m] = (int32_t)c;
+        data[base + m] = v;
+      }
+      m++;
+    }
+  };
+  while (i < na && j < nb) {
+    if (A[i].c == B[j].c) {
+      emit(A[i].c, A[i].v, B[j].v);
+      i++;
+      j++;
+    } else if (A[i].c < B[j].c) {
+      emit(A[i].c, A[i].v, (T)0);
+      i++;
+    } else {
+      emit(B[j].c, (T)0, B[j].v);
+      j++;
+    }
+  }
+  for (; i < na; i++) emit(A[i].c, A[i].v, (T)0);
+  for (; j < nb; j++) emit(B[j].c, (T)0, B[j].v);
+  if (!kWrite) mcnt[r] = m;
 }
 
-__global__ void __launch_bounds__(kTPB) k_tag_values(uint64_t n, uint32_t tag, uint32_t* __restrict__ v) {
-  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (i < n) v[i] = (uint32_t)i | tag;
+__global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, uint64_t n,
+                             unsigned long long* out) {
+  *out = n ? (unsigned long long)off[n - 1] + cnt[n - 1] : 0ull;
 }
 
 // ----------------------------------------------------------- explicit instances --
 #define G2N_INST(T)                                                                                              \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
-  template __global__ void k_group_sum<T>(const unsigned long long*, const uint32_t*, uint64_t, const uint32_t*,  \
-                                          const uint32_t*, const T*, int, unsigned long long*, T*, uint8_t*,      \
-                                          Ctl*, int);                                                            \
-  template __global__ void k_emulate_rows<T>(const unsigned long long*, const uint32_t*, uint64_t, int, uint64_t, \
-                                             const uint8_t*, const T*, const unsigned long long*,                 \
-                                             const unsigned long long*, T*, KV<int32_t, T>*, uint32_t*);          \
-  template __global__ void k_maxsym<T>(const unsigned long long*, const uint32_t*, uint64_t, const T*, const T*,  \
-                                       uint32_t*, T*);                                                           \
-  template __global__ void k_compact<T>(const unsigned long long*, const T*, const uint32_t*, const uint32_t*,    \
-                                        uint64_t, unsigned long long*, T*);
+  template __global__ void k_pack<T, true>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*,     \
+                                           PV<T>*, uint32_t*);                                                    \
+  template __global__ void k_pack<T, false>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*,    \
+                                            PV<T>*, uint32_t*);                                                   \
+  template __global__ void k_row_sum<T, true>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, PV<T>*,    \
+                                              PV<T>*, uint32_t*, T, uint8_t*, Ctl*, int);                         \
+  template __global__ void k_row_sum<T, false>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, PV<T>*,   \
+                                               PV<T>*, uint32_t*, T, uint8_t*, Ctl*, int);                        \
+  template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, PV<T>*,       \
+                                            KV<int32_t, T>*);                                                     \
+  template __global__ void k_row_compact<T>(const uint32_t*, const uint32_t*, const uint32_t*, uint64_t,          \
+                                            const PV<T>*, int32_t*, int32_t*, T*);                                \
+  template __global__ void k_row_max<T, false>(const uint32_t*, const uint32_t*, const PV<T>*, const uint32_t*,    \
+                                               const uint32_t*, const PV<T>*, uint64_t, uint32_t*,                \
+                                               const uint32_t*, int32_t*, int32_t*, T*);                          \
+  template __global__ void k_row_max<T, true>(const uint32_t*, const uint32_t*, const PV<T>*, const uint32_t*,     \
+                                              const uint32_t*, const PV<T>*, uint64_t, uint32_t*,                 \
+                                              const uint32_t*, int32_t*, int32_t*, T*);
 G2N_INST(uint8_t)
 G2N_INST(int8_t)
 G2N_INST(int32_t)
 G2N_INST(float)
 G2N_INST(double)
 #undef G2N_INST
-template __global__ void k_indptr<int32_t>(const unsigned long long*, const unsigned long long*, int, uint64_t,
-                                           int32_t*);
-template __global__ void k_split_keys<int32_t>(const unsigned long long*, const unsigned long long*, int, int32_t*);
 
 }  // namespace g2n
