@@ -8,7 +8,7 @@
 //   touches (n_t):   noff u64, nlen u32 [, ooff u64, olen u32 when bidirected], slot u32
 //   edges   (n_e):   w f64 (weight before the dtype cast), tb u32 (first touch)
 //   table[cap]        u64        (hash tag << 32 | first touch), cap = pow2 >= 2 n_t
-//   first/nid u32, flen/foff u64 per touch; names blob + offsets
+//   first u8, nid/tid u32 per touch; inv/klen u32 per node id; names blob + offsets
 //   rows/cols i32, data T per triplet; sort keys u64 + stream positions u32
 #pragma once
 #include <hip/hip_runtime.h>
@@ -66,7 +66,8 @@ struct Ctl {
   unsigned long long n_keep;
   unsigned long long n_f32_overflow;  // edges whose float32 cast overflowed
   unsigned long long deferred;        // touches left for the next insert round
-  unsigned long long pad[5];
+  unsigned long long dict_general;    // the S-first dictionary fast path does not apply
+  unsigned long long pad[4];
 };
 
 struct ParseOpts {
@@ -123,20 +124,22 @@ __global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint
                                const uint64_t* worklist, uint64_t n_work, ParseOpts op, EdgeOut E, Ctl* ctl);
 __global__ void k_error_detail(const uint8_t* in, const uint64_t* ls, uint64_t line, Ctl* ctl);
 __global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
-template <bool kClaim>
+template <int kMode>
 __global__ void k_insert_round(const uint8_t* in, uint64_t in_len, TouchIn T, uint64_t n_t, DictEntry* table,
                                uint64_t mask, uint64_t max_probes, uint32_t* slot, uint8_t* tstate, uint32_t round,
-                               int bidir, Ctl* ctl);
-__global__ void k_mark_first(TouchIn T, const DictEntry* table, uint64_t cap, int bidir, uint32_t* first,
-                             uint64_t* flen);
-__global__ void k_assign_ids(DictEntry* table, uint64_t cap, const uint32_t* nid);
-__global__ void k_totals(const uint32_t* first, const uint32_t* nid, const uint64_t* flen, const uint64_t* foff,
-                         uint64_t n_t, Ctl* ctl);
-__global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_t, const uint32_t* first, const uint32_t* nid,
-                        const uint64_t* foff, int bidir, uint8_t* blob, int64_t* offs, const Ctl* ctl);
+                               int bidir, Ctl* ctl, uint8_t* first, const uint32_t* nid, const uint32_t* inv,
+                               uint32_t* tid);
+__global__ void k_assign_first(DictEntry* table, TouchIn T, uint64_t n_t, int bidir, const uint8_t* first,
+                               const uint32_t* slot, const uint32_t* nid, uint32_t* inv, uint32_t* klen);
+__global__ void k_mark_first(const DictEntry* table, uint64_t cap, uint8_t* first);
+__global__ void k_assign_ids(DictEntry* table, uint64_t cap, const uint32_t* nid, uint32_t* inv, uint32_t* klen);
+__global__ void k_node_count(const uint8_t* first, const uint32_t* nid, uint64_t n_t, Ctl* ctl);
+__global__ void k_names_total(const uint32_t* klen, uint64_t n_nodes, int64_t* offs, Ctl* ctl);
+__global__ void k_names(const uint8_t* in, TouchIn T, uint64_t n_nodes, const uint32_t* inv, const int64_t* offs,
+                        int bidir, uint8_t* blob);
 template <class T>
 __global__ void k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* slot, const DictEntry* table,
-                           const uint32_t* nid, int tpe, int gd, int32_t* rows, int32_t* cols, T* data, Ctl* ctl);
+                           const uint32_t* tid, int tpe, int gd, int32_t* rows, int32_t* cols, T* data, Ctl* ctl);
 // K7-K9 (COO -> CSR) kernels are templates defined in g2n_kernels.hip (same translation unit).
 
 }  // namespace g2n

@@ -708,17 +708,38 @@ __device__ inline bool tail_eq(const uint8_t* __restrict__ in, const TouchIn& T,
 // meeting a same-tag entry claimed in the current round retry next round.  The
 // representative is lowered with atomicMin to the FIRST touch of the key — the order of
 // Python dict insertion (builders.py:194-198, 219-221).
-template <bool kClaim>  // kClaim: round 1 (touches of S lines); else: rounds >= 2 (everything left)
+//
+// Probing reads the whole entry with one plain 32-byte load: everything an earlier launch
+// wrote is visible to it, and a line fetched during this launch can only show an entry that
+// is empty (-> atomic CAS), or claimed in this round (meta round >= this round: retried next
+// round), or published earlier (immutable except for the representative, which only ever
+// decreases — a stale one costs at most a redundant atomicMin).
+//
+// Modes.  kClaim: round 1, the S-line touches claim or find their keys; it also records
+// first[t] (claimed here) for every touch.  kLookup: the general rounds
+// >= 2 (representatives lowered, new keys claimed).  kFast: the single lookup round of the
+// S-first fast path — after round 1 every claimed entry holds the node id its S touch ranks
+// to (k_assign_first), so an edge touch reads its node id straight into tid[t].  That is the
+// final id only if the key's first touch is the S touch: a touch with no key (new node) or one
+// preceding the S touch (rank >= nid[t], the firsts before it) sets ctl->dict_general and the
+// host redoes the dictionary with the general rounds.
+enum : int { kModeClaim = 0, kModeLookup = 1, kModeFast = 2 };
+
+template <int kMode>
 __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict__ in, uint64_t in_len, TouchIn T,
                                                        uint64_t n_t, DictEntry* __restrict__ table, uint64_t mask,
                                                        uint64_t max_probes, uint32_t* __restrict__ slot,
                                                        uint8_t* __restrict__ tstate, uint32_t round, int bidir,
-                                                       Ctl* ctl) {
+                                                       Ctl* ctl, uint8_t* __restrict__ first,
+                                                       const uint32_t* __restrict__ nid,
+                                                       const uint32_t* __restrict__ inv, uint32_t* __restrict__ tid) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   bool deferred = false;
   if (t < n_t) {
     const uint8_t st = tstate[t];
-    if (st != 0 && !(kClaim && st != 1)) {
+    bool claimed = false;
+    const bool active = kMode == kModeClaim ? st == 1 : st != 0;
+    if (active) {
       const uint64_t no = T.noff[t];
       const uint32_t nl = T.nlen[t];
       const uint64_t oo = bidir ? T.ooff[t] : 0;
@@ -727,34 +748,52 @@ __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict
       const uint64_t h = key_hash(in, kh, no, nl, oo);
       const uint32_t tag = (uint32_t)(h >> 32);
       const unsigned long long mine = ((unsigned long long)tag << 32) | (uint32_t)t;
+      const uint64_t k0 = (uint64_t)kh.k, k1 = (uint64_t)(kh.k >> 64);
       uint64_t idx = h & mask;
       bool done = false;
-      for (uint64_t probe = 0; probe < max_probes && !done && !deferred; probe++) {
+      for (uint64_t probe = 0; probe < max_probes; probe++) {
         DictEntry* e = table + idx;
-        unsigned long long cur = __hip_atomic_load(&e->hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint4 lo = ((const uint4*)e)[0], hi = ((const uint4*)e)[1];  // one plain 32-byte load
+        unsigned long long cur = ((unsigned long long)lo.y << 32) | lo.x;
+        unsigned long long meta = ((unsigned long long)lo.w << 32) | lo.z;
+        uint64_t e0 = ((uint64_t)hi.y << 32) | hi.x, e1 = ((uint64_t)hi.w << 32) | hi.z;
         if (cur == kEmptySlot) {
-          cur = atomicCAS(&e->hdr, kEmptySlot, mine);
-          if (cur == kEmptySlot) {  // claimed: publish the key for later rounds
-            e->k0 = (uint64_t)kh.k;
-            e->k1 = (uint64_t)(kh.k >> 64);
-            e->meta = ((unsigned long long)round << 32) | kh.len;
-            slot[t] = (uint32_t)idx;
-            tstate[t] = 0;
+          if (kMode == kModeFast) {  // a key no S line defined: a new node
+            ctl->dict_general = 1;
             done = true;
             break;
           }
+          cur = atomicCAS(&e->hdr, kEmptySlot, mine);
+          if (cur == kEmptySlot) {  // claimed: publish the key for later rounds
+            e->k0 = k0;
+            e->k1 = k1;
+            e->meta = ((unsigned long long)round << 32) | kh.len;
+            slot[t] = (uint32_t)idx;
+            tstate[t] = 0;
+            claimed = true;
+            done = true;
+            break;
+          }
+          // lost the race: the entry was claimed during this launch
+          meta = __hip_atomic_load(&e->meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if ((uint32_t)(cur >> 32) == tag) {
-          const unsigned long long meta = __hip_atomic_load(&e->meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((meta >> 32) >= round) {  // published in this launch (or not yet): next round
             deferred = true;
             break;
           }
-          if ((uint32_t)meta == kh.len && e->k0 == (uint64_t)kh.k && e->k1 == (uint64_t)(kh.k >> 64) &&
-              (kh.len <= 16 || tail_eq(in, T, t, (uint32_t)cur, bidir != 0, kh.len))) {
-            if ((uint32_t)cur > (uint32_t)t) atomicMin(&e->hdr, mine);
-            slot[t] = (uint32_t)idx;
-            tstate[t] = 0;
+          if ((uint32_t)meta == kh.len && e0 == k0 && e1 == k1 &&
+              (kh.len <= 16 ||
+               tail_eq(in, T, t, kMode == kModeFast ? inv[(uint32_t)cur] : (uint32_t)cur, bidir != 0, kh.len))) {
+            if (kMode == kModeFast) {
+              const uint32_t id = (uint32_t)cur;  // rank of the key's S touch among the firsts
+              if (id >= nid[t]) ctl->dict_general = 1;  // this touch precedes it
+              tid[t] = id;
+            } else {
+              if ((uint32_t)cur > (uint32_t)t) atomicMin(&e->hdr, mine);
+              slot[t] = (uint32_t)idx;
+              tstate[t] = 0;
+            }
             done = true;
             break;
           }
@@ -763,58 +802,84 @@ __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict
       }
       if (!done && !deferred) ctl->table_overflow = 1;  // the host retries with a larger table
     }
+    if (kMode == kModeClaim) first[t] = claimed ? 1 : 0;  // S-first fast path: the claimers are the first touches
   }
   // one atomic per wave for the deferred count
   unsigned long long d = __ballot(deferred);
   if ((threadIdx.x & 63) == 0 && d) atomicAdd(&ctl->deferred, (unsigned long long)__popcll(d));
 }
 
-template __global__ void k_insert_round<true>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,
-                                              uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*);
-template __global__ void k_insert_round<false>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,
-                                               uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*);
+#define G2N_INS(M)                                                                                               \
+  template __global__ void k_insert_round<M>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,  \
+                                             uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*, uint8_t*,       \
+                                             const uint32_t*, const uint32_t*, uint32_t*);
+G2N_INS(kModeClaim)
+G2N_INS(kModeLookup)
+G2N_INS(kModeFast)
+#undef G2N_INS
 
-// After all rounds, every occupied entry holds the FIRST touch of its key: mark it.
-__global__ void __launch_bounds__(kTPB) k_mark_first(TouchIn T, const DictEntry* __restrict__ table, uint64_t cap,
-                                                     int bidir, uint32_t* __restrict__ first,
-                                                     uint64_t* __restrict__ flen) {
-  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (s >= cap) return;
-  const unsigned long long v = table[s].hdr;
-  if (v == kEmptySlot) return;
-  const uint32_t rep = (uint32_t)v;
-  first[rep] = 1u;
-  flen[rep] = (uint32_t)table[s].meta;  // key length
+__device__ inline uint32_t touch_key_len(const TouchIn& T, uint64_t t, int bidir) {
+  return T.nlen[t] + (bidir ? 1 + T.olen[t] : 0);  // name [+ ":" + orientation]
 }
 
-// Replace each entry's representative by its node id (= rank of its first touch).
-__global__ void __launch_bounds__(kTPB) k_assign_ids(DictEntry* __restrict__ table, uint64_t cap,
-                                                     const uint32_t* __restrict__ nid) {
-  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (s >= cap) return;
-  const unsigned long long v = table[s].hdr;
-  if (v == kEmptySlot) return;
-  table[s].hdr = (v & 0xFFFFFFFF00000000ull) | nid[(uint32_t)v];
-}
-
-__global__ void k_totals(const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
-                         const uint64_t* __restrict__ flen, const uint64_t* __restrict__ foff, uint64_t n_t,
-                         Ctl* ctl) {
-  ctl->n_nodes = n_t ? (uint64_t)nid[n_t - 1] + first[n_t - 1] : 0;
-  ctl->names_len = n_t ? foff[n_t - 1] + flen[n_t - 1] : 0;
-}
-
-// names blob in id order + offsets (builders.py:284-288 node_list)
-__global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_t,
-                                                const uint32_t* __restrict__ first, const uint32_t* __restrict__ nid,
-                                                const uint64_t* __restrict__ foff, int bidir,
-                                                uint8_t* __restrict__ blob, int64_t* __restrict__ offs,
-                                                const Ctl* ctl) {
+// S-first fast path: each round-1 claimer's entry takes its node id (its rank among the firsts);
+// inv[id] = the touch holding the key's bytes, klen[id] = its length (names blob).
+__global__ void __launch_bounds__(kTPB) k_assign_first(DictEntry* __restrict__ table, TouchIn T, uint64_t n_t,
+                                                       int bidir, const uint8_t* __restrict__ first,
+                                                       const uint32_t* __restrict__ slot,
+                                                       const uint32_t* __restrict__ nid, uint32_t* __restrict__ inv,
+                                                       uint32_t* __restrict__ klen) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (t == 0) offs[ctl->n_nodes] = (int64_t)ctl->names_len;
   if (t >= n_t || !first[t]) return;
-  const uint64_t o = foff[t];
-  offs[nid[t]] = (int64_t)o;
+  const uint32_t id = nid[t];
+  ((uint32_t*)&table[slot[t]].hdr)[0] = id;  // the low half of hdr (little endian): no read back
+  inv[id] = (uint32_t)t;
+  klen[id] = touch_key_len(T, t, bidir);
+}
+
+// General path, after all rounds: every occupied entry holds the FIRST touch of its key.
+__global__ void __launch_bounds__(kTPB) k_mark_first(const DictEntry* __restrict__ table, uint64_t cap,
+                                                     uint8_t* __restrict__ first) {
+  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (s >= cap) return;
+  const unsigned long long v = table[s].hdr;
+  if (v != kEmptySlot) first[(uint32_t)v] = 1;
+}
+
+// General path: each entry's representative -> its node id (= rank of the first touch).
+__global__ void __launch_bounds__(kTPB) k_assign_ids(DictEntry* __restrict__ table, uint64_t cap,
+                                                     const uint32_t* __restrict__ nid, uint32_t* __restrict__ inv,
+                                                     uint32_t* __restrict__ klen) {
+  const uint64_t s = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (s >= cap) return;
+  const unsigned long long v = table[s].hdr;
+  if (v == kEmptySlot) return;
+  const uint32_t rep = (uint32_t)v, id = nid[rep];
+  table[s].hdr = (v & 0xFFFFFFFF00000000ull) | id;
+  inv[id] = rep;
+  klen[id] = (uint32_t)table[s].meta;
+}
+
+__global__ void k_node_count(const uint8_t* __restrict__ first, const uint32_t* __restrict__ nid, uint64_t n_t,
+                             Ctl* ctl) {
+  ctl->n_nodes = n_t ? (uint64_t)nid[n_t - 1] + first[n_t - 1] : 0;
+}
+
+__global__ void k_names_total(const uint32_t* __restrict__ klen, uint64_t n_nodes, int64_t* __restrict__ offs,
+                              Ctl* ctl) {
+  const uint64_t total = n_nodes ? (uint64_t)offs[n_nodes - 1] + klen[n_nodes - 1] : 0;
+  offs[n_nodes] = (int64_t)total;
+  ctl->names_len = total;
+}
+
+// names blob in id order (builders.py:284-288 node_list): node `id` <- the key bytes of inv[id]
+__global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_nodes,
+                                                const uint32_t* __restrict__ inv, const int64_t* __restrict__ offs,
+                                                int bidir, uint8_t* __restrict__ blob) {
+  const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (id >= n_nodes) return;
+  const uint64_t t = inv[id];
+  const uint64_t o = (uint64_t)offs[id];
   const uint64_t no = T.noff[t];
   const uint32_t nl = T.nlen[t];
   for (uint32_t j = 0; j < nl; j++) blob[o + j] = in[no + j];
@@ -874,16 +939,19 @@ struct Cast<double> {
   __device__ static uint32_t go(double w, double* o) { *o = w; return 0; }
 };
 
+// tid: node id per touch (S-first fast path, a streaming read) — else slot -> table entry -> id.
 template <class T>
 __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const uint32_t* __restrict__ slot,
                                                    const DictEntry* __restrict__ table,
-                                                   const uint32_t* __restrict__ nid, int tpe, int gd,
+                                                   const uint32_t* __restrict__ tid, int tpe, int gd,
                                                    int32_t* __restrict__ rows, int32_t* __restrict__ cols,
                                                    T* __restrict__ data, Ctl* ctl) {
   const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (e >= n_e) return;
   const uint64_t tb = E.tb[e];
-  auto id = [&](uint64_t t) -> int32_t { return (int32_t)(uint32_t)table[slot[t]].hdr; };  // slot -> node id
+  auto id = [&](uint64_t t) -> int32_t {
+    return tid ? (int32_t)tid[t] : (int32_t)(uint32_t)table[slot[t]].hdr;
+  };
   T v;
   const double wv = E.w[e];
   uint32_t err = Cast<T>::go(wv, &v);
@@ -1043,104 +1111,266 @@ __global__ void __launch_bounds__(kTPB) k_row_start(const uint32_t* __restrict__
   start[r] = (uint32_t)(r == n_rows ? n : lower_bound_u32(key, n, (uint32_t)r));
 }
 
-// One thread per row: the row's entries (stream order) -> sorted unique (column, sum)
-// written at the front of the row's segment of `out`; ucnt[r] = unique entries.
+// Row sums keep the unique entries of row r at [start[r], start[r] + ucnt[r]) of structure-of-
+// arrays outputs: ocol (column) and, per entry, the run length (uniform build: every value is
+// dtype(1), so the sum is a function of the count) or the summed value (weighted build).
+template <class T, bool kUniform>
+struct RowVal {
+  using type = typename std::conditional<kUniform, uint32_t, T>::type;
+};
+
+template <class T, bool kUniform>
+__device__ inline T row_value(const typename RowVal<T, kUniform>::type* ov, uint32_t j, T one) {
+  if constexpr (kUniform) return sum_copies<T>(one, ov[j]);
+  else return ov[j];
+}
+
+// Bitonic sorting network on the first N of M register slots (indices are compile-time after
+// unrolling, so the arrays stay in VGPRs).  Keys are unique or payload-free, so stability is moot.
+template <int N, int M, class K>
+__device__ inline void net_sort(K (&k)[M]) {
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const K a = k[i], b = k[j];
+          const bool asc = (i & size) == 0;
+          const bool sw = asc ? (a > b) : (a < b);
+          k[i] = sw ? b : a;
+          k[j] = sw ? a : b;
+        }
+      }
+}
+template <int N, int M, class K, class V>
+__device__ inline void net_sort_kv(K (&k)[M], V (&v)[M]) {
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const K a = k[i], b = k[j];
+          const V x = v[i], y = v[j];
+          const bool asc = (i & size) == 0;
+          const bool sw = asc ? (a > b) : (a < b);
+          k[i] = sw ? b : a;
+          k[j] = sw ? a : b;
+          v[i] = sw ? y : x;
+          v[j] = sw ? x : y;
+        }
+      }
+}
+
+constexpr uint32_t kRegRow = 16;  // rows up to this many entries are sorted in registers
+
+// One thread per row: the row's entries (stream order, after the stable row-bucket sort) ->
+// sorted unique (column, count | sum).  Rows <= kRegRow entries: register sorting network on
+// (column, stream position) keys, i.e. a stable sort.  Longer rows: stable bottom-up merge sort
+// in global memory, ping-ponging between two scratch buffers the row-bucket sort left free.
 template <class T, bool kUniform>
 __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ start, uint64_t n_rows,
                                                   const PV<T>* __restrict__ pv, const uint32_t* __restrict__ pc,
-                                                  PV<T>* __restrict__ out, PV<T>* __restrict__ scr,
-                                                  uint32_t* __restrict__ ucnt, T one, uint8_t* __restrict__ rowflag,
+                                                  uint32_t* __restrict__ ocol,
+                                                  typename RowVal<T, kUniform>::type* __restrict__ oval,
+                                                  void* __restrict__ scr_a, void* __restrict__ scr_b,
+                                                  uint32_t* __restrict__ ucnt, uint8_t* __restrict__ rowflag,
                                                   Ctl* ctl, int which) {
   const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (r >= n_rows) return;
   const uint32_t s = start[r], e = start[r + 1];
   const uint32_t len = e - s;
-  if (len == 0) {
-    ucnt[r] = 0;
+  if (len <= 1) {
+    ucnt[r] = len;
+    if (len) {
+      if constexpr (kUniform) {
+        ocol[s] = pc[s];
+        oval[s] = 1u;
+      } else {
+        const PV<T> x = pv[s];
+        ocol[s] = x.c;
+        oval[s] = x.v;
+      }
+    }
     return;
   }
-  PV<T>* o = out + s;
-  // copy in stream order and note scipy's has_sorted_indices for this row
-  bool sorted = true;
-  uint32_t prev = 0;
-  for (uint32_t q = 0; q < len; q++) {
-    PV<T> x;
-    if (kUniform) {
-      x.c = pc[s + q];
-      x.v = one;
-    } else {
-      x = pv[s + q];
-    }
-    if (q && x.c < prev) sorted = false;
-    prev = x.c;
-    o[q] = x;
-  }
-  if (!sorted) {
-    ctl->unsorted[which] = 1;
-    if (len <= 32) {  // stable insertion sort by column
-      for (uint32_t q = 1; q < len; q++) {
-        PV<T> x = o[q];
-        int32_t z = (int32_t)q - 1;
-        while (z >= 0 && o[z].c > x.c) {
-          o[z + 1] = o[z];
-          z--;
-        }
-        o[z + 1] = x;
+  if (len <= kRegRow) {
+    uint32_t u = 0;
+    bool sorted = true;
+    if constexpr (kUniform) {
+      uint32_t k[kRegRow];
+#pragma unroll
+      for (uint32_t q = 0; q < kRegRow; q++) k[q] = q < len ? pc[s + q] : 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t q = 1; q < kRegRow; q++)
+        if (q < len && k[q] < k[q - 1]) sorted = false;
+      if (!sorted) {
+        if (len <= 8) net_sort<8>(k);
+        else net_sort<16>(k);
       }
-    } else {  // long row: stable bottom-up merge sort, ping-pong with the row's scratch segment
-      PV<T>* src = o;
-      PV<T>* dst = scr + s;
+      uint32_t cur = k[0], cnt = 1;
+#pragma unroll
+      for (uint32_t q = 1; q < kRegRow; q++) {
+        if (q < len) {
+          if (k[q] != cur) {
+            ocol[s + u] = cur;
+            oval[s + u] = cnt;
+            u++;
+            cur = k[q];
+            cnt = 0;
+          }
+          cnt++;
+        }
+      }
+      ocol[s + u] = cur;
+      oval[s + u] = cnt;
+      u++;
+    } else {
+      uint64_t k[kRegRow];
+      T v[kRegRow];
+#pragma unroll
+      for (uint32_t q = 0; q < kRegRow; q++) {
+        if (q < len) {
+          const PV<T> x = pv[s + q];
+          k[q] = ((uint64_t)x.c << 32) | q;
+          v[q] = x.v;
+        } else {
+          k[q] = ~0ull;
+          v[q] = (T)0;
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 1; q < kRegRow; q++)
+        if (q < len && (k[q] >> 32) < (k[q - 1] >> 32)) sorted = false;
+      if (!sorted) {
+        if (len <= 8) net_sort_kv<8>(k, v);
+        else net_sort_kv<16>(k, v);
+      }
+      uint32_t cur = (uint32_t)(k[0] >> 32);
+      T acc = v[0];
+#pragma unroll
+      for (uint32_t q = 1; q < kRegRow; q++) {
+        if (q < len) {
+          const uint32_t c = (uint32_t)(k[q] >> 32);
+          if (c != cur) {
+            ocol[s + u] = cur;
+            oval[s + u] = acc;
+            u++;
+            cur = c;
+            acc = v[q];
+          } else {
+            acc = Acc<T>::add(acc, v[q]);
+          }
+        }
+      }
+      ocol[s + u] = cur;
+      oval[s + u] = acc;
+      u++;
+    }
+    if (!sorted) ctl->unsorted[which] = 1;
+    ucnt[r] = u;
+    return;
+  }
+  // ---- long row
+  bool sorted = true;
+  uint32_t u = 0;
+  bool flag = false;
+  if constexpr (kUniform) {
+    uint32_t* a = (uint32_t*)scr_a + s;
+    uint32_t* b = (uint32_t*)scr_b + s;
+    uint32_t prev = 0;
+    for (uint32_t q = 0; q < len; q++) {
+      const uint32_t c = pc[s + q];
+      if (q && c < prev) sorted = false;
+      prev = c;
+      a[q] = c;
+    }
+    const uint32_t* src = pc + s;
+    if (!sorted) {
       for (uint32_t width = 1; width < len; width <<= 1) {
         for (uint32_t lo = 0; lo < len; lo += 2 * width) {
           const uint32_t mid = lo + width < len ? lo + width : len;
           const uint32_t hi = lo + 2 * width < len ? lo + 2 * width : len;
-          uint32_t a = lo, b = mid, w = lo;
-          while (a < mid && b < hi) dst[w++] = (src[b].c < src[a].c) ? src[b++] : src[a++];
-          while (a < mid) dst[w++] = src[a++];
-          while (b < hi) dst[w++] = src[b++];
+          uint32_t x = lo, y = mid, w = lo;
+          while (x < mid && y < hi) b[w++] = (a[y] < a[x]) ? a[y++] : a[x++];
+          while (x < mid) b[w++] = a[x++];
+          while (y < hi) b[w++] = a[y++];
         }
-        PV<T>* t = src;
-        src = dst;
-        dst = t;
+        uint32_t* t = a;
+        a = b;
+        b = t;
       }
-      if (src != o)
-        for (uint32_t q = 0; q < len; q++) o[q] = src[q];
+      src = a;
     }
-  }
-  // left-to-right run sums
-  uint32_t u = 0, q = 0;
-  bool flag = false;
-  while (q < len) {
-    const uint32_t c = o[q].c;
-    uint32_t q0 = q;
-    T x = o[q].v;
-    bool exact = true;
-    double sabs = 0.0;
-    if (!kUniform && Acc<T>::is_float()) {
-      exact = exact_term(x);
-      sabs = __builtin_fabs((double)x);
+    uint32_t q = 0;
+    while (q < len) {
+      const uint32_t c = src[q], q0 = q;
+      while (q < len && src[q] == c) q++;
+      ocol[s + u] = c;
+      oval[s + u] = q - q0;
+      u++;
     }
-    q++;
-    while (q < len && o[q].c == c) {
-      if (!kUniform) {
-        T y = o[q].v;
+  } else {
+    PV<T>* a = (PV<T>*)scr_a + s;
+    PV<T>* b = (PV<T>*)scr_b + s;
+    uint32_t prev = 0;
+    for (uint32_t q = 0; q < len; q++) {
+      const PV<T> x = pv[s + q];
+      if (q && x.c < prev) sorted = false;
+      prev = x.c;
+      a[q] = x;
+    }
+    if (!sorted) {
+      for (uint32_t width = 1; width < len; width <<= 1) {
+        for (uint32_t lo = 0; lo < len; lo += 2 * width) {
+          const uint32_t mid = lo + width < len ? lo + width : len;
+          const uint32_t hi = lo + 2 * width < len ? lo + 2 * width : len;
+          uint32_t x = lo, y = mid, w = lo;
+          while (x < mid && y < hi) b[w++] = (a[y].c < a[x].c) ? a[y++] : a[x++];
+          while (x < mid) b[w++] = a[x++];
+          while (y < hi) b[w++] = a[y++];
+        }
+        PV<T>* t = a;
+        a = b;
+        b = t;
+      }
+    }
+    uint32_t q = 0;
+    while (q < len) {  // left-to-right run sums
+      const uint32_t c = a[q].c, q0 = q;
+      T x = a[q].v;
+      bool exact = true;
+      double sabs = 0.0;
+      if (Acc<T>::is_float()) {
+        exact = exact_term(x);
+        sabs = __builtin_fabs((double)x);
+      }
+      q++;
+      while (q < len && a[q].c == c) {
+        const T y = a[q].v;
         if (Acc<T>::is_float()) {
           exact = exact && exact_term(y);
           sabs += __builtin_fabs((double)y);
         }
         x = Acc<T>::add(x, y);
+        q++;
       }
-      q++;
+      // a group of >= 3 terms whose sum depends on their order (std::sort on > 16 elements is
+      // not an insertion sort, so scipy's order is not the stable one)
+      if (Acc<T>::is_float() && q - q0 >= 3 && !(exact && sabs < Acc<T>::limit())) flag = true;
+      ocol[s + u] = c;
+      oval[s + u] = x;
+      u++;
     }
-    if (kUniform) x = sum_copies<T>(one, q - q0);
-    if (!kUniform && Acc<T>::is_float() && q - q0 >= 3 && !(exact && sabs < Acc<T>::limit())) flag = true;
-    PV<T> y;
-    y.c = c;
-    y.v = x;
-    o[u++] = y;
   }
+  if (!sorted) ctl->unsorted[which] = 1;
   ucnt[r] = u;
-  if (flag && len > 16) {  // std::sort on > 16 elements is not an insertion sort
+  if (flag) {
     rowflag[r] = 1;
     ctl->flagged[which] = 1;
   }
@@ -1150,8 +1380,8 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
 template <class T>
 __global__ void __launch_bounds__(64) k_row_emulate(const uint32_t* __restrict__ start, uint64_t n_rows,
                                                     const uint8_t* __restrict__ rowflag,
-                                                    const PV<T>* __restrict__ pv, PV<T>* __restrict__ out,
-                                                    KV<int32_t, T>* __restrict__ kv) {
+                                                    const PV<T>* __restrict__ pv, uint32_t* __restrict__ ocol,
+                                                    T* __restrict__ oval, KV<int32_t, T>* __restrict__ kv) {
   const uint64_t r = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (r >= n_rows || !rowflag[r]) return;
   const uint32_t s = start[r], len = start[r + 1] - s;
@@ -1170,18 +1400,20 @@ __global__ void __launch_bounds__(64) k_row_emulate(const uint32_t* __restrict__
       x = Acc<T>::add(x, a[q].v);
       q++;
     }
-    out[s + u].c = (uint32_t)c;
-    out[s + u].v = x;
+    ocol[s + u] = (uint32_t)c;
+    oval[s + u] = x;
     u++;
   }
 }
 
 // SUM CSR: row r's unique entries -> indices/data at indptr[r]
-template <class T>
+template <class T, bool kUniform>
 __global__ void __launch_bounds__(kTPB) k_row_compact(const uint32_t* __restrict__ start,
                                                       const uint32_t* __restrict__ ucnt,
                                                       const uint32_t* __restrict__ uoff, uint64_t n_rows,
-                                                      const PV<T>* __restrict__ out, int32_t* __restrict__ indptr,
+                                                      const uint32_t* __restrict__ ocol,
+                                                      const typename RowVal<T, kUniform>::type* __restrict__ oval,
+                                                      T one, int32_t* __restrict__ indptr,
                                                       int32_t* __restrict__ indices, T* __restrict__ data) {
   const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (r >= n_rows) return;
@@ -1189,24 +1421,26 @@ __global__ void __launch_bounds__(kTPB) k_row_compact(const uint32_t* __restrict
   indptr[r] = (int32_t)o;
   if (r == n_rows - 1) indptr[n_rows] = (int32_t)(o + u);
   for (uint32_t j = 0; j < u; j++) {
-    indices[o + j] = (int32_t)out[s + j].c;
-    data[o + j] = out[s + j].v;
+    indices[o + j] = (int32_t)ocol[s + j];
+    data[o + j] = row_value<T, kUniform>(oval, s + j, one);
   }
 }
 
 // M = A.maximum(A.T) row by row: merge row r of B (= SUM(A)) and of BT (= SUM(A.T)), both sorted
 // by column; csr_binop_csr_canonical with std::max ((a < b) ? b : a), missing = 0, zeros dropped.
-template <class T, bool kWrite>
+template <class T, bool kUniform, bool kWrite>
 __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ ua,
-                                                  const PV<T>* __restrict__ oa, const uint32_t* __restrict__ st,
-                                                  const uint32_t* __restrict__ ut, const PV<T>* __restrict__ ot,
-                                                  uint64_t n_rows, uint32_t* __restrict__ mcnt,
+                                                  const uint32_t* __restrict__ ca,
+                                                  const typename RowVal<T, kUniform>::type* __restrict__ va,
+                                                  const uint32_t* __restrict__ st, const uint32_t* __restrict__ ut,
+                                                  const uint32_t* __restrict__ ct,
+                                                  const typename RowVal<T, kUniform>::type* __restrict__ vt,
+                                                  T one, uint64_t n_rows, uint32_t* __restrict__ mcnt,
                                                   const uint32_t* __restrict__ moff, int32_t* __restrict__ indptr,
                                                   int32_t* __restrict__ indices, T* __restrict__ data) {
   const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (r >= n_rows) return;
-  const PV<T>* A = oa + sa[r];
-  const PV<T>* B = ot + st[r];
+  const uint32_t a0 = sa[r], b0 = st[r];
   const uint32_t na = ua[r], nb = ut[r];
   uint32_t i = 0, j = 0, m = 0;
   const uint32_t base = kWrite ? moff[r] : 0;
@@ -1215,7 +1449,7 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
     if (r == n_rows - 1) indptr[n_rows] = (int32_t)(base + mcnt[r]);
   }
   auto emit = [&](uint32_t c, T x, T y) {
-    T v = (x < y) ? y : x;
+    const T v = (x < y) ? y : x;
     if (v != (T)0) {
       if (kWrite) {
         indices[base + m] = (int32_t)c;
@@ -1224,21 +1458,26 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
       m++;
     }
   };
+  uint32_t cA = i < na ? ca[a0] : 0, cB = j < nb ? ct[b0] : 0;
   while (i < na && j < nb) {
-    if (A[i].c == B[j].c) {
-      emit(A[i].c, A[i].v, B[j].v);
+    if (cA == cB) {
+      emit(cA, row_value<T, kUniform>(va, a0 + i, one), row_value<T, kUniform>(vt, b0 + j, one));
       i++;
       j++;
-    } else if (A[i].c < B[j].c) {
-      emit(A[i].c, A[i].v, (T)0);
+      if (i < na) cA = ca[a0 + i];
+      if (j < nb) cB = ct[b0 + j];
+    } else if (cA < cB) {
+      emit(cA, row_value<T, kUniform>(va, a0 + i, one), (T)0);
       i++;
+      if (i < na) cA = ca[a0 + i];
     } else {
-      emit(B[j].c, (T)0, B[j].v);
+      emit(cB, (T)0, row_value<T, kUniform>(vt, b0 + j, one));
       j++;
+      if (j < nb) cB = ct[b0 + j];
     }
   }
-  for (; i < na; i++) emit(A[i].c, A[i].v, (T)0);
-  for (; j < nb; j++) emit(B[j].c, (T)0, B[j].v);
+  for (; i < na; i++) emit(ca[a0 + i], row_value<T, kUniform>(va, a0 + i, one), (T)0);
+  for (; j < nb; j++) emit(ct[b0 + j], (T)0, row_value<T, kUniform>(vt, b0 + j, one));
   if (!kWrite) mcnt[r] = m;
 }
 
@@ -1248,32 +1487,35 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
 }
 
 // ----------------------------------------------------------- explicit instances --
+#define G2N_INST_U(T, U)                                                                                         \
+  template __global__ void k_pack<T, U>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*, PV<T>*, \
+                                        uint32_t*);                                                              \
+  template __global__ void k_row_sum<T, U>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, uint32_t*,   \
+                                           RowVal<T, U>::type*, void*, void*, uint32_t*, uint8_t*, Ctl*, int);   \
+  template __global__ void k_row_compact<T, U>(const uint32_t*, const uint32_t*, const uint32_t*, uint64_t,      \
+                                               const uint32_t*, const RowVal<T, U>::type*, T, int32_t*,          \
+                                               int32_t*, T*);                                                    \
+  template __global__ void k_row_max<T, U, false>(const uint32_t*, const uint32_t*, const uint32_t*,              \
+                                                  const RowVal<T, U>::type*, const uint32_t*, const uint32_t*,   \
+                                                  const uint32_t*, const RowVal<T, U>::type*, T, uint64_t,       \
+                                                  uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);           \
+  template __global__ void k_row_max<T, U, true>(const uint32_t*, const uint32_t*, const uint32_t*,               \
+                                                 const RowVal<T, U>::type*, const uint32_t*, const uint32_t*,    \
+                                                 const uint32_t*, const RowVal<T, U>::type*, T, uint64_t,        \
+                                                 uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);
 #define G2N_INST(T)                                                                                              \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
-  template __global__ void k_pack<T, true>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*,     \
-                                           PV<T>*, uint32_t*);                                                    \
-  template __global__ void k_pack<T, false>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*,    \
-                                            PV<T>*, uint32_t*);                                                   \
-  template __global__ void k_row_sum<T, true>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, PV<T>*,    \
-                                              PV<T>*, uint32_t*, T, uint8_t*, Ctl*, int);                         \
-  template __global__ void k_row_sum<T, false>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, PV<T>*,   \
-                                               PV<T>*, uint32_t*, T, uint8_t*, Ctl*, int);                        \
-  template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, PV<T>*,       \
-                                            KV<int32_t, T>*);                                                     \
-  template __global__ void k_row_compact<T>(const uint32_t*, const uint32_t*, const uint32_t*, uint64_t,          \
-                                            const PV<T>*, int32_t*, int32_t*, T*);                                \
-  template __global__ void k_row_max<T, false>(const uint32_t*, const uint32_t*, const PV<T>*, const uint32_t*,    \
-                                               const uint32_t*, const PV<T>*, uint64_t, uint32_t*,                \
-                                               const uint32_t*, int32_t*, int32_t*, T*);                          \
-  template __global__ void k_row_max<T, true>(const uint32_t*, const uint32_t*, const PV<T>*, const uint32_t*,     \
-                                              const uint32_t*, const PV<T>*, uint64_t, uint32_t*,                 \
-                                              const uint32_t*, int32_t*, int32_t*, T*);
+  template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, uint32_t*,    \
+                                            T*, KV<int32_t, T>*);                                                 \
+  G2N_INST_U(T, true)                                                                                            \
+  G2N_INST_U(T, false)
 G2N_INST(uint8_t)
 G2N_INST(int8_t)
 G2N_INST(int32_t)
 G2N_INST(float)
 G2N_INST(double)
 #undef G2N_INST
+#undef G2N_INST_U
 
 }  // namespace g2n

@@ -34,7 +34,7 @@ enum Slot {
   S_WL, S_TABLE, S_SLOT, S_FIRST, S_NID, S_FLEN, S_FOFF, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1,
   S_VALS0, S_VALS1, S_HEAD, S_HPOS, S_UKEYS0, S_UDATA0, S_UKEYS1, S_UDATA1, S_ROWFLAG, S_KV, S_ORD, S_MK, S_MV,
   S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_BLK, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0, S_ROUT1,
-  S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_NSLOTS
+  S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID, S_INV, S_NSLOTS
 };
 
 struct DevBuf {
@@ -129,11 +129,13 @@ static size_t dtype_size(int dt) {
 }
 
 // ------------------------------------------------- SUM (coo.tocsr) on device -------
-template <class T>
-struct RowSide {  // one orientation's per-row sums: row r's unique entries at out[start[r]], ucnt[r] of them
+template <class T, bool kU>
+struct RowSide {  // one orientation's per-row sums: row r's unique entries at [start[r], +ucnt[r])
+  using V = typename RowVal<T, kU>::type;  // run length (uniform build) or summed value
   uint32_t* start;
   uint32_t* ucnt;
-  PV<T>* out;
+  uint32_t* ocol;
+  V* oval;
   bool unsorted, flagged;
 };
 
@@ -149,19 +151,21 @@ static void sort_pairs_u32(g2n_context* c, const uint32_t* kin, uint32_t* kout, 
 
 // coo.tocsr() of one orientation (transposed: of A.T), up to the per-row sorted unique entries.
 template <class T, bool kU>
-static RowSide<T> row_sums(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n,
-                           uint64_t n_rows, int transposed, T one) {
+static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n,
+                               uint64_t n_rows, int transposed) {
   const int w = transposed;
-  RowSide<T> S{};
+  using V = typename RowVal<T, kU>::type;
+  RowSide<T, kU> S{};
   auto* key_in = dget<uint32_t>(c, S_KEYS0, n);
   auto* key_out = dget<uint32_t>(c, S_KEYS1, n);
   S.start = dget<uint32_t>(c, w ? S_RSTART1 : S_RSTART0, n_rows + 1);
   S.ucnt = dget<uint32_t>(c, w ? S_UCNT1 : S_UCNT0, n_rows);
-  S.out = dget<PV<T>>(c, w ? S_ROUT1 : S_ROUT0, n);
+  S.ocol = dget<uint32_t>(c, w ? S_ROUT1 : S_ROUT0, n);
+  S.oval = dget<V>(c, w ? S_RVAL1 : S_RVAL0, n);
   auto* rowflag = dget<uint8_t>(c, w ? S_RFLAG1 : S_RFLAG0, n_rows);
-  auto* scr = dget<PV<T>>(c, S_RSCR, n);
   PV<T>* pv_out = nullptr;
   uint32_t* pc_out = nullptr;
+  void *scr_a = nullptr, *scr_b = nullptr;  // long-row merge scratch: buffers the sort no longer needs
   G2N_HIP(hipMemsetAsync(rowflag, 0, n_rows ? n_rows : 1, c->stream));
   const int bits = bits_for(n_rows);
   if (n) {
@@ -171,25 +175,31 @@ static RowSide<T> row_sums(g2n_context* c, const int32_t* rows, const int32_t* c
       hipLaunchKernelGGL((k_pack<T, true>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n, w,
                          key_in, (PV<T>*)nullptr, pc_in);
       sort_pairs_u32<uint32_t>(c, key_in, key_out, pc_in, pc_out, n, bits);
+      scr_a = key_in;
+      scr_b = pc_in;
     } else {
       auto* pv_in = dget<PV<T>>(c, S_VALS0, n);
       pv_out = dget<PV<T>>(c, S_VALS1, n);
       hipLaunchKernelGGL((k_pack<T, false>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n, w,
                          key_in, pv_in, (uint32_t*)nullptr);
       sort_pairs_u32<PV<T>>(c, key_in, key_out, pv_in, pv_out, n, bits);
+      scr_a = pv_in;
+      scr_b = dget<PV<T>>(c, S_RSCR, n);
     }
   }
   hipLaunchKernelGGL(k_row_start, dim3(grid_for(n_rows + 1)), dim3(kTPB), 0, c->stream, key_out, n, n_rows, S.start);
   if (n_rows)
     hipLaunchKernelGGL((k_row_sum<T, kU>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, S.start, n_rows, pv_out,
-                       pc_out, S.out, scr, S.ucnt, one, rowflag, c->ctl, w);
+                       pc_out, S.ocol, S.oval, scr_a, scr_b, S.ucnt, rowflag, c->ctl, w);
   sync_ctl(c);
   S.unsorted = c->h_ctl->unsorted[w] != 0;
   S.flagged = c->h_ctl->flagged[w] != 0;
-  if (!kU && n && S.unsorted && S.flagged) {  // scipy std::sort-ed these rows: redo them exactly
-    auto* kv = dget<KV<int32_t, T>>(c, S_KV, n);
-    hipLaunchKernelGGL((k_row_emulate<T>), dim3(grid_for(n_rows, 64)), dim3(64), 0, c->stream, S.start, n_rows,
-                       rowflag, pv_out, S.out, kv);
+  if constexpr (!kU) {
+    if (n && S.unsorted && S.flagged) {  // scipy std::sort-ed these rows: redo them exactly
+      auto* kv = dget<KV<int32_t, T>>(c, S_KV, n);
+      hipLaunchKernelGGL((k_row_emulate<T>), dim3(grid_for(n_rows, 64)), dim3(64), 0, c->stream, S.start, n_rows,
+                         rowflag, pv_out, S.ocol, S.oval, kv);
+    }
   }
   return S;
 }
@@ -199,7 +209,7 @@ template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   const T one = (T)1;
-  RowSide<T> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, one);
+  RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0);
   R->sum_sorted = A.unsorted ? 0 : 1;
   phase(c, "sum");
   auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
@@ -212,8 +222,8 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
     auto* indices = dget<int32_t>(c, S_INDICES, n_trip);
     T* odata = dget<T>(c, S_ODATA, n_trip);
     if (n_rows) {
-      hipLaunchKernelGGL((k_row_compact<T>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt, uoff,
-                         n_rows, A.out, indptr, indices, odata);
+      hipLaunchKernelGGL((k_row_compact<T, kU>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                         uoff, n_rows, A.ocol, A.oval, one, indptr, indices, odata);
       hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, A.ucnt, uoff, n_rows, &c->ctl->n_keep);
     }
     R->nnz = n_rows ? (int64_t)read_dev(c, &c->ctl->n_keep) : 0;
@@ -223,19 +233,20 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
     return;
   }
   // A.maximum(A.T): B = SUM(A) above, BT = SUM(A.T) with A.T's own scatter order
-  RowSide<T> B = row_sums<T, kU>(c, rows, cols, data, n_trip, n_cols, 1, one);
+  RowSide<T, kU> B = row_sums<T, kU>(c, rows, cols, data, n_trip, n_cols, 1);
   phase(c, "sum_t");
   auto* mcnt = dget<uint32_t>(c, S_MCNT, n_rows);
   auto* moff = dget<uint32_t>(c, S_MOFF, n_rows);
   auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_trip);
   T* odata = dget<T>(c, S_ODATA, 2 * n_trip);
   if (n_rows) {
-    hipLaunchKernelGGL((k_row_max<T, false>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
-                       A.out, B.start, B.ucnt, B.out, n_rows, mcnt, (const uint32_t*)nullptr, (int32_t*)nullptr,
-                       (int32_t*)nullptr, (T*)nullptr);
+    hipLaunchKernelGGL((k_row_max<T, kU, false>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                       A.ocol, A.oval, B.start, B.ucnt, B.ocol, B.oval, one, n_rows, mcnt, (const uint32_t*)nullptr,
+                       (int32_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
     excl_scan<uint32_t>(c, mcnt, moff, n_rows);
-    hipLaunchKernelGGL((k_row_max<T, true>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
-                       A.out, B.start, B.ucnt, B.out, n_rows, mcnt, moff, indptr, indices, odata);
+    hipLaunchKernelGGL((k_row_max<T, kU, true>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                       A.ocol, A.oval, B.start, B.ucnt, B.ocol, B.oval, one, n_rows, mcnt, moff, indptr, indices,
+                       odata);
     hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, mcnt, moff, n_rows, &c->ctl->n_keep);
   }
   R->nnz = n_rows ? (int64_t)read_dev(c, &c->ctl->n_keep) : 0;
@@ -253,10 +264,10 @@ static void assemble(g2n_context* c, const int32_t* rows, const int32_t* cols, c
 
 template <class T>
 static void run_triplets(g2n_context* c, EdgeIn E, uint64_t n_e, const uint32_t* slot,
-                         const DictEntry* table, const uint32_t* nid, int tpe, int gd, int32_t* rows,
+                         const DictEntry* table, const uint32_t* tid, int tpe, int gd, int32_t* rows,
                          int32_t* cols, void* data) {
   if (n_e)
-    hipLaunchKernelGGL((k_triplets<T>), dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E, n_e, slot, table, nid, tpe,
+    hipLaunchKernelGGL((k_triplets<T>), dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E, n_e, slot, table, tid, tpe,
                        gd, rows, cols, (T*)data, c->ctl);
 }
 
@@ -415,66 +426,116 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   while (cap < est + est / 2) cap <<= 1;
   if (cap > full_cap) cap = full_cap;
   auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
-  auto* first = dget<uint32_t>(c, S_FIRST, n_t);
+  auto* first = dget<uint8_t>(c, S_FIRST, n_t);
   auto* nid = dget<uint32_t>(c, S_NID, n_t);
-  auto* flen = dget<uint64_t>(c, S_FLEN, n_t);
-  auto* foff = dget<uint64_t>(c, S_FOFF, n_t);
+  auto* inv = dget<uint32_t>(c, S_INV, n_t);    // node id -> touch holding its key bytes
+  auto* klen = dget<uint32_t>(c, S_FLEN, n_t);  // node id -> key length
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
   DictEntry* table = nullptr;
+  uint32_t* tid = nullptr;  // node id per touch when the S-first fast path holds
   auto* tstate = dget<uint8_t>(c, S_TSTATE, n_t);
+  auto insert = [&](int mode, uint32_t round, uint64_t max_probes, uint32_t* tid_out) {
+    G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
+    phase(c, "_prep");
+    const dim3 g(grid_for(n_t)), b(kTPB);
+    if (mode == kModeClaim)
+      hipLaunchKernelGGL(k_insert_round<kModeClaim>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+    else if (mode == kModeLookup)
+      hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+    else
+      hipLaunchKernelGGL(k_insert_round<kModeFast>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+    phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
+    sync_ctl(c);
+  };
+  auto init_table = [&]() {
+    table = dget<DictEntry>(c, S_TABLE, cap);
+    G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
+    G2N_HIP(hipMemcpyAsync(tstate, T.tkind, n_t, hipMemcpyDeviceToDevice, c->stream));
+    phase(c, "table_init");
+  };
+  auto rank_firsts = [&]() {  // nid[t] = first touches before t; n_nodes
+    size_t tb = 0;
+    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
+                                    c->stream));
+    void* tmp = dbuf(c, S_TEMP, tb);
+    G2N_HIP(rocprim::exclusive_scan(tmp, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
+                                    c->stream));
+    hipLaunchKernelGGL(k_node_count, dim3(1), dim3(1), 0, c->stream, first, nid, n_t, c->ctl);
+  };
   if (n_t) {
-    while (true) {
-      table = dget<DictEntry>(c, S_TABLE, cap);
-      G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
-      G2N_HIP(hipMemcpyAsync(tstate, T.tkind, n_t, hipMemcpyDeviceToDevice, c->stream));
-      phase(c, "table_init");
-      const uint64_t max_probes = cap >= full_cap ? cap : 4096;
-      bool overflow = false;
-      for (uint32_t round = 1;; round++) {  // round 1: S touches; then every unresolved touch
-        G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
-        phase(c, "_prep");
-        if (round == 1)
-          hipLaunchKernelGGL(k_insert_round<true>, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, len, TI, n_t,
-                             table, cap - 1, max_probes, slot, tstate, round, (int)bidir, c->ctl);
-        else
-          hipLaunchKernelGGL(k_insert_round<false>, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, len, TI, n_t,
-                             table, cap - 1, max_probes, slot, tstate, round, (int)bidir, c->ctl);
-        phase(c, round == 1 ? "insert_claim" : "insert_lookup");
-        sync_ctl(c);
-        if (c->h_ctl->table_overflow) { overflow = true; break; }
-        if (round > 1 && c->h_ctl->deferred == 0) break;
-        if (round > 100000) throw Failure(G2N_E_DEVICE, "dictionary insert did not converge");
-      }
-      if (!overflow) break;
-      if (cap >= full_cap) throw Failure(G2N_E_DEVICE, "node table overflow");
-      G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
-      cap = full_cap;
+    // S-first fast path (a GFA whose S lines define every key before any other line uses it):
+    // round 1 claims the S keys, their ranks are the node ids, one lookup round resolves every
+    // other touch to its id.  Anything else is redone by the general rounds below.
+    bool fast = !std::getenv("G2N_DICT_GENERAL");
+    if (fast) {
+      init_table();
+      insert(kModeClaim, 1, cap >= full_cap ? cap : 4096, nullptr);
+      fast = !c->h_ctl->table_overflow;
     }
-    G2N_HIP(hipMemsetAsync(first, 0, n_t * sizeof(uint32_t), c->stream));
-    G2N_HIP(hipMemsetAsync(flen, 0, n_t * sizeof(uint64_t), c->stream));
-    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, TI, table, cap, (int)bidir,
-                       first, flen);
-    excl_scan<uint32_t>(c, first, nid, n_t);
-    excl_scan<uint64_t>(c, flen, foff, n_t);
-    hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, c->stream, first, nid, flen, foff, n_t, c->ctl);
-    hipLaunchKernelGGL(k_assign_ids, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, nid);
+    if (fast) {
+      rank_firsts();
+      hipLaunchKernelGGL(k_assign_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, table, TI, n_t, (int)bidir,
+                         first, slot, nid, inv, klen);
+      phase(c, "ids_fast");
+      tid = dget<uint32_t>(c, S_TID, n_t);
+      insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
+      fast = !c->h_ctl->dict_general && !c->h_ctl->table_overflow && c->h_ctl->deferred == 0;
+      if (!fast) {
+        tid = nullptr;
+        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
+      }
+    }
+    if (!fast) {
+      while (true) {
+        init_table();
+        const uint64_t max_probes = cap >= full_cap ? cap : 4096;
+        bool overflow = false;
+        for (uint32_t round = 1;; round++) {  // round 1: S touches; then every unresolved touch
+          insert(round == 1 ? kModeClaim : kModeLookup, round, max_probes, nullptr);
+          if (c->h_ctl->table_overflow) { overflow = true; break; }
+          if (round > 1 && c->h_ctl->deferred == 0) break;
+          if (round > 100000) throw Failure(G2N_E_DEVICE, "dictionary insert did not converge");
+        }
+        if (!overflow) break;
+        if (cap >= full_cap) throw Failure(G2N_E_DEVICE, "node table overflow");
+        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
+        cap = full_cap;
+      }
+      G2N_HIP(hipMemsetAsync(first, 0, n_t, c->stream));
+      hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, first);
+      rank_firsts();
+      hipLaunchKernelGGL(k_assign_ids, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, nid, inv, klen);
+      phase(c, "ids_general");
+    }
   }
   sync_ctl(c);
   if (c->h_ctl->table_overflow) throw Failure(G2N_E_DEVICE, "node table overflow");
   const uint64_t n_nodes = n_t ? c->h_ctl->n_nodes : 0;
-  const uint64_t names_len = n_t ? c->h_ctl->names_len : 0;
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
-  R->names_bytes = names_len;
   phase(c, "ids");
-  if (o->want_node_names) {
-    auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
+  if (o->want_node_names) {  // names blob + offsets in id order
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
-    if (n_t)
-      hipLaunchKernelGGL(k_names, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, in, TI, n_t, first, nid, foff,
-                         (int)bidir, blob, offs, c->ctl);
-    else
-      G2N_HIP(hipMemsetAsync(offs, 0, sizeof(int64_t), c->stream));
+    {
+      size_t tb = 0;
+      if (n_nodes) {
+        G2N_HIP(rocprim::exclusive_scan(nullptr, tb, klen, offs, (int64_t)0, (size_t)n_nodes,
+                                        rocprim::plus<int64_t>(), c->stream));
+        void* tmp = dbuf(c, S_TEMP, tb);
+        G2N_HIP(rocprim::exclusive_scan(tmp, tb, klen, offs, (int64_t)0, (size_t)n_nodes, rocprim::plus<int64_t>(),
+                                        c->stream));
+      }
+      hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, klen, n_nodes, offs, c->ctl);
+    }
+    const uint64_t names_len = read_dev(c, &c->ctl->names_len);
+    auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
+    if (n_nodes)
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, inv, offs,
+                         (int)bidir, blob);
+    R->names_bytes = names_len;
     R->names_blob = blob;
     R->names_offsets = offs;
     phase(c, "names");
@@ -490,11 +551,11 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
   switch (dt) {
-    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
-    default: run_triplets<double>(c, EI, n_e, slot, table, nid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
+    default: run_triplets<double>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
   }
   phase(c, "triplets");
   sync_ctl(c);

@@ -116,7 +116,7 @@ typedef struct g2n_result {
   const void *indptr;          /* CSR: n_nodes + 1 */
   const void *indices;         /* CSR */
   const void *data;            /* nnz elements of dtype */
-  uint64_t names_bytes;        /* total bytes of all node keys (names blob length) */
+  uint64_t names_bytes;        /* names blob length (0 when want_node_names is 0) */
   int64_t n_cast_overflow;     /* float32 casts that overflowed to +-inf: numpy warns
                                   RuntimeWarning("overflow encountered in cast") once each */
   uint64_t input_bytes;        /* uncompressed GFA bytes parsed */

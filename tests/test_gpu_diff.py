@@ -179,3 +179,78 @@ def test_c4_properties_on_device(gpu):
     names = blob.tobytes()
     want = "".join(str(k) for k in range(1, n + 1)).encode()
     assert names == want
+
+
+def _canonical_gfa(seed: int, n_s: int, n_l: int, long_names: bool) -> bytes:
+    """S lines first (distinct names, some longer than the 16 inline key bytes), then L lines
+    that only name defined segments: the input the S-first dictionary fast path is for."""
+    import random
+
+    r = random.Random(seed)
+    names = []
+    for k in range(n_s):
+        if long_names and k % 3 == 0:
+            names.append(f"chr{r.randint(1, 22)}_segment_{k:08d}_" + "x" * r.randint(0, 40))
+        else:
+            names.append(f"{k + 1}")
+    lines = [f"H\tVN:Z:1.0\n"] + [f"S\t{n}\t*\n" for n in names]
+    for _ in range(n_l):
+        a, b = r.choice(names), r.choice(names)
+        lines.append(f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t*\tRC:i:{r.randint(-3, 9)}\n")
+    return "".join(lines).encode()
+
+
+def _phases(data: bytes, **kw):
+    from gfa2network_amd import _native as nat
+
+    raw = nat.build_from_buffer(data, nat.make_options(**kw))
+    return raw.status, raw.phase_ms
+
+
+@pytest.mark.parametrize("long_names", [False, True])
+def test_s_first_fast_path_taken_and_exact(gpu, oracle_lib, long_names):
+    data = _canonical_gfa(7 + long_names, 3000, 12000, long_names)
+    for mode in MODES:
+        st, ph = _phases(data, **mode)
+        assert st == 0 and "ids_fast" in ph and "ids_general" not in ph, (mode, sorted(ph))
+        for dtype, wt in (("float64", "RC"), ("int8", None), ("float32", "RC")):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
+            assert a == b, (mode, dtype, wt)
+
+
+@pytest.mark.parametrize("case", ["l_before_s", "missing_segment", "duplicate_s"])
+def test_s_first_fallback_to_general_dictionary(gpu, oracle_lib, case):
+    """Inputs where a key's first touch is not its S line: the fast path must notice and the
+    general insert rounds must give the reference's first-touch ids."""
+    base = _canonical_gfa(3, 500, 3000, True).decode().splitlines(keepends=True)
+    s_lines = [x for x in base if x.startswith("S")]
+    l_lines = [x for x in base if x.startswith("L")]
+    if case == "l_before_s":
+        text = l_lines[:50] + s_lines + l_lines[50:]
+    elif case == "missing_segment":
+        text = s_lines + l_lines[:100] + ["L\tnot_a_segment\t+\t1\t-\t*\tRC:i:2\n"] + l_lines[100:]
+    else:  # a later S line repeats an earlier name
+        text = s_lines + [s_lines[10], s_lines[0]] + l_lines
+    data = "".join(text).encode()
+    for mode in MODES:
+        st, ph = _phases(data, **mode)
+        assert st == 0
+        if case != "duplicate_s":  # there the earlier S line may win the claim: fast path stays exact
+            assert "ids_general" in ph, (case, mode, sorted(ph))
+        for dtype, wt in (("float64", "RC"), ("int32", None)):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
+            assert a == b, (case, mode, dtype, wt)
+
+
+def test_general_dictionary_forced(gpu, oracle_lib, monkeypatch):
+    """G2N_DICT_GENERAL=1 keeps the general insert rounds covered on canonical inputs too."""
+    monkeypatch.setenv("G2N_DICT_GENERAL", "1")
+    data = _canonical_gfa(11, 2000, 8000, True)
+    for mode in MODES:
+        st, ph = _phases(data, **mode)
+        assert st == 0 and "ids_general" in ph and "ids_fast" not in ph
+        a = outcome(gpu_run(data, mode, "float64", "RC"))
+        b = outcome(oracle_run(oracle_lib, data, mode, "float64", "RC"))
+        assert a == b, mode
