@@ -67,7 +67,9 @@ struct Ctl {
   unsigned long long n_f32_overflow;  // edges whose float32 cast overflowed
   unsigned long long deferred;        // touches left for the next insert round
   unsigned long long dict_general;    // the S-first dictionary fast path does not apply
-  unsigned long long pad[4];
+  unsigned long long s_late;          // an S-line touch follows an edge touch (claim round)
+  unsigned long long row_gap;         // k_row_bounds met a run of empty rows too long to fill
+  unsigned long long pad[2];
 };
 
 struct ParseOpts {
@@ -127,8 +129,9 @@ __global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
 template <int kMode>
 __global__ void k_insert_round(const uint8_t* in, uint64_t in_len, TouchIn T, uint64_t n_t, DictEntry* table,
                                uint64_t mask, uint64_t max_probes, uint32_t* slot, uint8_t* tstate, uint32_t round,
-                               int bidir, Ctl* ctl, uint8_t* first, const uint32_t* nid, const uint32_t* inv,
-                               uint32_t* tid);
+                               int bidir, Ctl* ctl, uint8_t* first, const uint32_t* nid, uint32_t n_first,
+                               const uint32_t* inv, uint32_t* tid);
+__global__ void k_key_len(TouchIn T, uint64_t n, int bidir, uint32_t* klen);
 __global__ void k_assign_first(DictEntry* table, TouchIn T, uint64_t n_t, int bidir, const uint8_t* first,
                                const uint32_t* slot, const uint32_t* nid, uint32_t* inv, uint32_t* klen);
 __global__ void k_mark_first(const DictEntry* table, uint64_t cap, uint8_t* first);

@@ -732,13 +732,16 @@ __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict
                                                        uint8_t* __restrict__ tstate, uint32_t round, int bidir,
                                                        Ctl* ctl, uint8_t* __restrict__ first,
                                                        const uint32_t* __restrict__ nid,
+                                                       uint32_t n_first,  // claim: S touches; fast: firsts
                                                        const uint32_t* __restrict__ inv, uint32_t* __restrict__ tid) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   bool deferred = false;
+  bool s_touch = false;
   if (t < n_t) {
     const uint8_t st = tstate[t];
     bool claimed = false;
     const bool active = kMode == kModeClaim ? st == 1 : st != 0;
+    s_touch = kMode == kModeClaim && active;
     if (active) {
       const uint64_t no = T.noff[t];
       const uint32_t nl = T.nlen[t];
@@ -784,10 +787,11 @@ __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict
           }
           if ((uint32_t)meta == kh.len && e0 == k0 && e1 == k1 &&
               (kh.len <= 16 ||
-               tail_eq(in, T, t, kMode == kModeFast ? inv[(uint32_t)cur] : (uint32_t)cur, bidir != 0, kh.len))) {
+               tail_eq(in, T, t, (kMode == kModeFast && inv) ? inv[(uint32_t)cur] : (uint32_t)cur, bidir != 0,
+                      kh.len))) {
             if (kMode == kModeFast) {
               const uint32_t id = (uint32_t)cur;  // rank of the key's S touch among the firsts
-              if (id >= nid[t]) ctl->dict_general = 1;  // this touch precedes it
+              if (id >= (nid ? nid[t] : n_first)) ctl->dict_general = 1;  // this touch precedes it
               tid[t] = id;
             } else {
               if ((uint32_t)cur > (uint32_t)t) atomicMin(&e->hdr, mine);
@@ -807,12 +811,16 @@ __global__ void __launch_bounds__(kTPB) k_insert_round(const uint8_t* __restrict
   // one atomic per wave for the deferred count
   unsigned long long d = __ballot(deferred);
   if ((threadIdx.x & 63) == 0 && d) atomicAdd(&ctl->deferred, (unsigned long long)__popcll(d));
+  if (kMode == kModeClaim) {  // an S touch after the first n_first touches: not an S prefix (rare store)
+    const unsigned long long m = __ballot(s_touch && t >= n_first);
+    if ((threadIdx.x & 63) == 0 && m) ctl->s_late = 1;
+  }
 }
 
 #define G2N_INS(M)                                                                                               \
   template __global__ void k_insert_round<M>(const uint8_t*, uint64_t, TouchIn, uint64_t, DictEntry*, uint64_t,  \
                                              uint64_t, uint32_t*, uint8_t*, uint32_t, int, Ctl*, uint8_t*,       \
-                                             const uint32_t*, const uint32_t*, uint32_t*);
+                                             const uint32_t*, uint32_t, const uint32_t*, uint32_t*);
 G2N_INS(kModeClaim)
 G2N_INS(kModeLookup)
 G2N_INS(kModeFast)
@@ -820,6 +828,13 @@ G2N_INS(kModeFast)
 
 __device__ inline uint32_t touch_key_len(const TouchIn& T, uint64_t t, int bidir) {
   return T.nlen[t] + (bidir ? 1 + T.olen[t] : 0);  // name [+ ":" + orientation]
+}
+
+// S-prefix dictionary (every S touch precedes every edge touch, no S key repeated): the node id
+// of an S touch is its touch index; klen[id] for the names blob.
+__global__ void __launch_bounds__(kTPB) k_key_len(TouchIn T, uint64_t n, int bidir, uint32_t* __restrict__ klen) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t < n) klen[t] = touch_key_len(T, t, bidir);
 }
 
 // S-first fast path: each round-1 claimer's entry takes its node id (its rank among the firsts);
@@ -878,7 +893,7 @@ __global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, 
                                                 int bidir, uint8_t* __restrict__ blob) {
   const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (id >= n_nodes) return;
-  const uint64_t t = inv[id];
+  const uint64_t t = inv ? inv[id] : id;  // S-prefix dictionary: id == touch
   const uint64_t o = (uint64_t)offs[id];
   const uint64_t no = T.noff[t];
   const uint32_t nl = T.nlen[t];
@@ -1093,6 +1108,26 @@ __global__ void __launch_bounds__(kTPB) k_pack(const int32_t* __restrict__ rows,
   }
 }
 
+constexpr uint32_t kRowGapCap = 64;  // empty rows one k_row_bounds thread fills
+
+// start[r] = first sorted position of row r (start[n_rows] = n), from the row changes of the
+// sorted keys: position p (0 <= p <= n) where key[p-1] != key[p] starts rows key[p-1]+1 ..
+// key[p] (the empty ones in between included).  A gap wider than kRowGapCap sets ctl->row_gap
+// and k_row_start (binary search per row) redoes the whole array.
+__global__ void __launch_bounds__(kTPB) k_row_bounds(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_rows,
+                                                     uint32_t* __restrict__ start, Ctl* ctl) {
+  const uint64_t p = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (p > n) return;
+  const int64_t prev = p ? (int64_t)key[p - 1] : -1;
+  const int64_t cur = p < n ? (int64_t)key[p] : (int64_t)n_rows;
+  if (cur == prev) return;
+  if (cur - prev > (int64_t)kRowGapCap) {
+    ctl->row_gap = 1;
+    return;
+  }
+  for (int64_t r = prev + 1; r <= cur; r++) start[r] = (uint32_t)p;
+}
+
 __device__ inline uint64_t lower_bound_u32(const uint32_t* __restrict__ a, uint64_t n, uint32_t key) {
   uint64_t lo = 0, hi = n;
   while (lo < hi) {
@@ -1103,9 +1138,9 @@ __device__ inline uint64_t lower_bound_u32(const uint32_t* __restrict__ a, uint6
   return lo;
 }
 
-// start[r] = first sorted position of row r (start[n_rows] = n)
 __global__ void __launch_bounds__(kTPB) k_row_start(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_rows,
-                                                    uint32_t* __restrict__ start) {
+                                                    uint32_t* __restrict__ start, const Ctl* ctl) {
+  if (!ctl->row_gap) return;  // k_row_bounds covered every row
   const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (r > n_rows) return;
   start[r] = (uint32_t)(r == n_rows ? n : lower_bound_u32(key, n, (uint32_t)r));
@@ -1169,43 +1204,58 @@ __device__ inline void net_sort_kv(K (&k)[M], V (&v)[M]) {
 
 constexpr uint32_t kRegRow = 16;  // rows up to this many entries are sorted in registers
 
-// One thread per row: the row's entries (stream order, after the stable row-bucket sort) ->
-// sorted unique (column, count | sum).  Rows <= kRegRow entries: register sorting network on
-// (column, stream position) keys, i.e. a stable sort.  Longer rows: stable bottom-up merge sort
-// in global memory, ping-ponging between two scratch buffers the row-bucket sort left free.
-template <class T, bool kUniform>
-__global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ start, uint64_t n_rows,
-                                                  const PV<T>* __restrict__ pv, const uint32_t* __restrict__ pc,
-                                                  uint32_t* __restrict__ ocol,
-                                                  typename RowVal<T, kUniform>::type* __restrict__ oval,
-                                                  void* __restrict__ scr_a, void* __restrict__ scr_b,
-                                                  uint32_t* __restrict__ ucnt, uint8_t* __restrict__ rowflag,
-                                                  Ctl* ctl, int which) {
-  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (r >= n_rows) return;
-  const uint32_t s = start[r], e = start[r + 1];
-  const uint32_t len = e - s;
-  if (len <= 1) {
-    ucnt[r] = len;
-    if (len) {
-      if constexpr (kUniform) {
-        ocol[s] = pc[s];
-        oval[s] = 1u;
-      } else {
-        const PV<T> x = pv[s];
-        ocol[s] = x.c;
-        oval[s] = x.v;
-      }
+// Rows are processed one per thread, but a block's 256 rows own ONE contiguous range of the
+// sorted entries (start[r0] .. start[r0 + 256]) and of every per-row output, so the block stages
+// its ranges through LDS: coalesced loads and stores of the whole range, lane-strided accesses
+// only in LDS.  A block whose range exceeds the LDS capacity works on global memory directly.
+constexpr uint32_t kStageSumU = 4096;  // entries a k_row_sum block stages (unweighted / weighted)
+constexpr uint32_t kStageSumW = 2048;
+constexpr uint32_t kStageMaxU = 2048;  // entries per staged range in k_row_max / k_row_compact
+constexpr uint32_t kStageMaxW = 1024;
+
+// Staging in two phases so that every load of a block's ranges is in flight at once:
+// fetch (global -> registers, unrolled) for all ranges, then put (registers -> LDS).
+template <uint32_t kCap, class E>
+struct Stage {
+  static constexpr uint32_t kN = (kCap + kTPB - 1) / kTPB;
+  E r[kN];
+  __device__ inline void fetch(const E* __restrict__ g, uint64_t base, uint32_t n) {
+#pragma unroll
+    for (uint32_t k = 0; k < kN; k++) {
+      const uint32_t i = threadIdx.x + k * kTPB;
+      if (i < n) r[k] = g[base + i];
     }
-    return;
   }
+  __device__ inline void put(E* __restrict__ lds, uint32_t n) const {
+#pragma unroll
+    for (uint32_t k = 0; k < kN; k++) {
+      const uint32_t i = threadIdx.x + k * kTPB;
+      if (i < n) lds[i] = r[k];
+    }
+  }
+};
+template <class E>
+__device__ inline void block_store(E* __restrict__ g, const E* __restrict__ lds, uint64_t base, uint32_t n) {
+  for (uint32_t i = threadIdx.x; i < n; i += kTPB) g[base + i] = lds[i];
+}
+
+// One row: entries in stream order (at(q), q < len; after the stable row-bucket sort) -> sorted
+// unique (column, count | sum), put(j, column, value).  Rows <= kRegRow entries: register
+// sorting network on (column, stream position) keys, i.e. a stable sort.  Longer rows: stable
+// bottom-up merge sort in global scratch (a, b: the row's own slices of two buffers the
+// row-bucket sort left free).  flag: the row's float sums could depend on std::sort's order.
+template <class T, bool kUniform, class At, class Put>
+__device__ inline uint32_t row_sum_one(uint32_t len, At at, Put put, void* scr_a, void* scr_b, uint64_t s,
+                                       bool& sorted, bool& flag) {
+  using V = typename RowVal<T, kUniform>::type;
+  uint32_t u = 0;
+  sorted = true;
+  flag = false;
   if (len <= kRegRow) {
-    uint32_t u = 0;
-    bool sorted = true;
     if constexpr (kUniform) {
       uint32_t k[kRegRow];
 #pragma unroll
-      for (uint32_t q = 0; q < kRegRow; q++) k[q] = q < len ? pc[s + q] : 0xFFFFFFFFu;
+      for (uint32_t q = 0; q < kRegRow; q++) k[q] = q < len ? at(q) : 0xFFFFFFFFu;
 #pragma unroll
       for (uint32_t q = 1; q < kRegRow; q++)
         if (q < len && k[q] < k[q - 1]) sorted = false;
@@ -1218,25 +1268,21 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
       for (uint32_t q = 1; q < kRegRow; q++) {
         if (q < len) {
           if (k[q] != cur) {
-            ocol[s + u] = cur;
-            oval[s + u] = cnt;
-            u++;
+            put(u++, cur, (V)cnt);
             cur = k[q];
             cnt = 0;
           }
           cnt++;
         }
       }
-      ocol[s + u] = cur;
-      oval[s + u] = cnt;
-      u++;
+      put(u++, cur, (V)cnt);
     } else {
       uint64_t k[kRegRow];
       T v[kRegRow];
 #pragma unroll
       for (uint32_t q = 0; q < kRegRow; q++) {
         if (q < len) {
-          const PV<T> x = pv[s + q];
+          const PV<T> x = at(q);
           k[q] = ((uint64_t)x.c << 32) | q;
           v[q] = x.v;
         } else {
@@ -1258,9 +1304,7 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
         if (q < len) {
           const uint32_t c = (uint32_t)(k[q] >> 32);
           if (c != cur) {
-            ocol[s + u] = cur;
-            oval[s + u] = acc;
-            u++;
+            put(u++, cur, acc);
             cur = c;
             acc = v[q];
           } else {
@@ -1268,29 +1312,21 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
           }
         }
       }
-      ocol[s + u] = cur;
-      oval[s + u] = acc;
-      u++;
+      put(u++, cur, acc);
     }
-    if (!sorted) ctl->unsorted[which] = 1;
-    ucnt[r] = u;
-    return;
+    return u;
   }
   // ---- long row
-  bool sorted = true;
-  uint32_t u = 0;
-  bool flag = false;
   if constexpr (kUniform) {
     uint32_t* a = (uint32_t*)scr_a + s;
     uint32_t* b = (uint32_t*)scr_b + s;
     uint32_t prev = 0;
     for (uint32_t q = 0; q < len; q++) {
-      const uint32_t c = pc[s + q];
+      const uint32_t c = at(q);
       if (q && c < prev) sorted = false;
       prev = c;
       a[q] = c;
     }
-    const uint32_t* src = pc + s;
     if (!sorted) {
       for (uint32_t width = 1; width < len; width <<= 1) {
         for (uint32_t lo = 0; lo < len; lo += 2 * width) {
@@ -1305,22 +1341,19 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
         a = b;
         b = t;
       }
-      src = a;
     }
     uint32_t q = 0;
     while (q < len) {
-      const uint32_t c = src[q], q0 = q;
-      while (q < len && src[q] == c) q++;
-      ocol[s + u] = c;
-      oval[s + u] = q - q0;
-      u++;
+      const uint32_t c = a[q], q0 = q;
+      while (q < len && a[q] == c) q++;
+      put(u++, c, (V)(q - q0));
     }
   } else {
     PV<T>* a = (PV<T>*)scr_a + s;
     PV<T>* b = (PV<T>*)scr_b + s;
     uint32_t prev = 0;
     for (uint32_t q = 0; q < len; q++) {
-      const PV<T> x = pv[s + q];
+      const PV<T> x = at(q);
       if (q && x.c < prev) sorted = false;
       prev = x.c;
       a[q] = x;
@@ -1363,16 +1396,89 @@ __global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ s
       // a group of >= 3 terms whose sum depends on their order (std::sort on > 16 elements is
       // not an insertion sort, so scipy's order is not the stable one)
       if (Acc<T>::is_float() && q - q0 >= 3 && !(exact && sabs < Acc<T>::limit())) flag = true;
-      ocol[s + u] = c;
-      oval[s + u] = x;
-      u++;
+      put(u++, c, x);
+    }
+  }
+  return u;
+}
+
+// coo.tocsr() per row after the row-bucket sort: row r's unique entries at
+// [start[r], start[r] + ucnt[r]) of ocol / oval.
+template <class T, bool kUniform>
+__global__ void __launch_bounds__(kTPB) k_row_sum(const uint32_t* __restrict__ start, uint64_t n_rows,
+                                                  const PV<T>* __restrict__ pv, const uint32_t* __restrict__ pc,
+                                                  uint32_t* __restrict__ ocol,
+                                                  typename RowVal<T, kUniform>::type* __restrict__ oval,
+                                                  void* __restrict__ scr_a, void* __restrict__ scr_b,
+                                                  uint32_t* __restrict__ ucnt, uint8_t* __restrict__ rowflag,
+                                                  Ctl* ctl, int which) {
+  using V = typename RowVal<T, kUniform>::type;
+  using In = typename std::conditional<kUniform, uint32_t, PV<T>>::type;
+  constexpr uint32_t kCap = kUniform ? kStageSumU : kStageSumW;
+  // the row loads are independent (unrolled) and stay direct; only the lane-strided stores of
+  // the unique entries are staged
+  __shared__ uint32_t s_col[kCap];
+  __shared__ V s_val[kCap];
+  const In* gin = kUniform ? (const In*)(const void*)pc : (const In*)(const void*)pv;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kTPB;
+  const uint64_t r1 = r0 + kTPB < n_rows ? r0 + kTPB : n_rows;
+  const uint32_t b0 = start[r0], nseg = start[r1] - b0;
+  const bool staged = nseg <= kCap;  // block-uniform
+  const uint64_t r = r0 + threadIdx.x;
+  bool sorted = true, flag = false;
+  if (r < n_rows) {
+    const uint32_t s = start[r], len = start[r + 1] - s;
+    uint32_t u = 0;
+    if (len == 1) {
+      const In x = gin[s];
+      uint32_t c;
+      V v;
+      if constexpr (kUniform) {
+        c = x;
+        v = 1u;
+      } else {
+        c = x.c;
+        v = x.v;
+      }
+      if (staged) {
+        s_col[s - b0] = c;
+        s_val[s - b0] = v;
+      } else {
+        ocol[s] = c;
+        oval[s] = v;
+      }
+      u = 1;
+    } else if (len > 1) {
+      if (staged) {
+        const uint32_t o = s - b0;
+        u = row_sum_one<T, kUniform>(
+            len, [&](uint32_t q) { return gin[s + q]; },
+            [&](uint32_t j, uint32_t c, V v) {
+              s_col[o + j] = c;
+              s_val[o + j] = v;
+            },
+            scr_a, scr_b, s, sorted, flag);
+      } else {
+        u = row_sum_one<T, kUniform>(
+            len, [&](uint32_t q) { return gin[s + q]; },
+            [&](uint32_t j, uint32_t c, V v) {
+              ocol[s + j] = c;
+              oval[s + j] = v;
+            },
+            scr_a, scr_b, s, sorted, flag);
+      }
+    }
+    ucnt[r] = u;
+    if (flag) {
+      rowflag[r] = 1;
+      ctl->flagged[which] = 1;
     }
   }
   if (!sorted) ctl->unsorted[which] = 1;
-  ucnt[r] = u;
-  if (flag) {
-    rowflag[r] = 1;
-    ctl->flagged[which] = 1;
+  if (staged) {
+    __syncthreads();
+    block_store(ocol, s_col, b0, nseg);
+    block_store(oval, s_val, b0, nseg);
   }
 }
 
@@ -1415,19 +1521,51 @@ __global__ void __launch_bounds__(kTPB) k_row_compact(const uint32_t* __restrict
                                                       const typename RowVal<T, kUniform>::type* __restrict__ oval,
                                                       T one, int32_t* __restrict__ indptr,
                                                       int32_t* __restrict__ indices, T* __restrict__ data) {
-  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (r >= n_rows) return;
-  const uint32_t s = start[r], u = ucnt[r], o = uoff[r];
-  indptr[r] = (int32_t)o;
-  if (r == n_rows - 1) indptr[n_rows] = (int32_t)(o + u);
-  for (uint32_t j = 0; j < u; j++) {
-    indices[o + j] = (int32_t)ocol[s + j];
-    data[o + j] = row_value<T, kUniform>(oval, s + j, one);
+  using V = typename RowVal<T, kUniform>::type;
+  constexpr uint32_t kCap = kUniform ? kStageMaxU : kStageMaxW;
+  __shared__ uint32_t s_c[kCap];
+  __shared__ V s_v[kCap];
+  __shared__ int32_t s_i[kCap];
+  __shared__ T s_d[kCap];
+  const uint64_t r0 = (uint64_t)blockIdx.x * kTPB;
+  const uint64_t r1 = r0 + kTPB < n_rows ? r0 + kTPB : n_rows;
+  const uint32_t b0 = start[r0], nin = start[r1] - b0;
+  const uint32_t o0 = uoff[r0], nout = uoff[r1 - 1] + ucnt[r1 - 1] - o0;
+  const bool staged = nin <= kCap && nout <= kCap;
+  if (staged) {
+    Stage<kCap, uint32_t> sc;
+    Stage<kCap, V> sv;
+    sc.fetch(ocol, b0, nin);
+    sv.fetch(oval, b0, nin);
+    sc.put(s_c, nin);
+    sv.put(s_v, nin);
+    __syncthreads();
+  }
+  const uint64_t r = r0 + threadIdx.x;
+  if (r < n_rows) {
+    const uint32_t s = start[r], u = ucnt[r], o = uoff[r];
+    indptr[r] = (int32_t)o;
+    if (r == n_rows - 1) indptr[n_rows] = (int32_t)(o + u);
+    for (uint32_t j = 0; j < u; j++) {
+      if (staged) {
+        s_i[o - o0 + j] = (int32_t)s_c[s - b0 + j];
+        s_d[o - o0 + j] = row_value<T, kUniform>(s_v, s - b0 + j, one);
+      } else {
+        indices[o + j] = (int32_t)ocol[s + j];
+        data[o + j] = row_value<T, kUniform>(oval, s + j, one);
+      }
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    block_store(indices, s_i, o0, nout);
+    block_store(data, s_d, o0, nout);
   }
 }
 
 // M = A.maximum(A.T) row by row: merge row r of B (= SUM(A)) and of BT (= SUM(A.T)), both sorted
 // by column; csr_binop_csr_canonical with std::max ((a < b) ? b : a), missing = 0, zeros dropped.
+// kWrite = false: count pass (mcnt); true: write pass at moff[r].
 template <class T, bool kUniform, bool kWrite>
 __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ ua,
                                                   const uint32_t* __restrict__ ca,
@@ -1438,47 +1576,88 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
                                                   T one, uint64_t n_rows, uint32_t* __restrict__ mcnt,
                                                   const uint32_t* __restrict__ moff, int32_t* __restrict__ indptr,
                                                   int32_t* __restrict__ indices, T* __restrict__ data) {
-  const uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (r >= n_rows) return;
-  const uint32_t a0 = sa[r], b0 = st[r];
-  const uint32_t na = ua[r], nb = ut[r];
-  uint32_t i = 0, j = 0, m = 0;
-  const uint32_t base = kWrite ? moff[r] : 0;
-  if (kWrite) {
-    indptr[r] = (int32_t)base;
-    if (r == n_rows - 1) indptr[n_rows] = (int32_t)(base + mcnt[r]);
+  using V = typename RowVal<T, kUniform>::type;
+  constexpr uint32_t kCap = kUniform ? kStageMaxU : kStageMaxW;
+  __shared__ uint32_t s_ca[kCap], s_ct[kCap];
+  __shared__ V s_va[kCap], s_vt[kCap];
+  __shared__ int32_t s_i[kWrite ? kCap : 1];
+  __shared__ T s_d[kWrite ? kCap : 1];
+  const uint64_t r0 = (uint64_t)blockIdx.x * kTPB;
+  const uint64_t r1 = r0 + kTPB < n_rows ? r0 + kTPB : n_rows;
+  const uint32_t a_0 = sa[r0], na_seg = sa[r1] - a_0;
+  const uint32_t t_0 = st[r0], nt_seg = st[r1] - t_0;
+  const uint32_t o0 = kWrite ? moff[r0] : 0;
+  const uint32_t nout = kWrite ? moff[r1 - 1] + mcnt[r1 - 1] - o0 : 0;
+  const bool staged = na_seg <= kCap && nt_seg <= kCap && nout <= kCap;
+  if (staged) {
+    Stage<kCap, uint32_t> c1, c2;
+    Stage<kCap, V> v1, v2;
+    c1.fetch(ca, a_0, na_seg);
+    v1.fetch(va, a_0, na_seg);
+    c2.fetch(ct, t_0, nt_seg);
+    v2.fetch(vt, t_0, nt_seg);
+    c1.put(s_ca, na_seg);
+    v1.put(s_va, na_seg);
+    c2.put(s_ct, nt_seg);
+    v2.put(s_vt, nt_seg);
+    __syncthreads();
   }
-  auto emit = [&](uint32_t c, T x, T y) {
-    const T v = (x < y) ? y : x;
-    if (v != (T)0) {
-      if (kWrite) {
-        indices[base + m] = (int32_t)c;
-        data[base + m] = v;
+  const uint64_t r = r0 + threadIdx.x;
+  if (r < n_rows) {
+    const uint32_t na = ua[r], nb = ut[r];
+    const uint32_t ga = sa[r], gb = st[r];
+    const uint32_t base = kWrite ? moff[r] : 0;
+    if (kWrite) {
+      indptr[r] = (int32_t)base;
+      if (r == n_rows - 1) indptr[n_rows] = (int32_t)(base + mcnt[r]);
+    }
+    auto merge = [&](const uint32_t* CA, const V* VA, const uint32_t* CB, const V* VB, int32_t* OI, T* OD) {
+      uint32_t i = 0, j = 0, m = 0;
+      auto emit = [&](uint32_t c, T x, T y) {
+        const T v = (x < y) ? y : x;
+        if (v != (T)0) {
+          if (kWrite) {
+            OI[m] = (int32_t)c;
+            OD[m] = v;
+          }
+          m++;
+        }
+      };
+      uint32_t cA = na ? CA[0] : 0, cB = nb ? CB[0] : 0;
+      while (i < na && j < nb) {
+        if (cA == cB) {
+          emit(cA, row_value<T, kUniform>(VA, i, one), row_value<T, kUniform>(VB, j, one));
+          i++;
+          j++;
+          if (i < na) cA = CA[i];
+          if (j < nb) cB = CB[j];
+        } else if (cA < cB) {
+          emit(cA, row_value<T, kUniform>(VA, i, one), (T)0);
+          i++;
+          if (i < na) cA = CA[i];
+        } else {
+          emit(cB, (T)0, row_value<T, kUniform>(VB, j, one));
+          j++;
+          if (j < nb) cB = CB[j];
+        }
       }
-      m++;
-    }
-  };
-  uint32_t cA = i < na ? ca[a0] : 0, cB = j < nb ? ct[b0] : 0;
-  while (i < na && j < nb) {
-    if (cA == cB) {
-      emit(cA, row_value<T, kUniform>(va, a0 + i, one), row_value<T, kUniform>(vt, b0 + j, one));
-      i++;
-      j++;
-      if (i < na) cA = ca[a0 + i];
-      if (j < nb) cB = ct[b0 + j];
-    } else if (cA < cB) {
-      emit(cA, row_value<T, kUniform>(va, a0 + i, one), (T)0);
-      i++;
-      if (i < na) cA = ca[a0 + i];
-    } else {
-      emit(cB, (T)0, row_value<T, kUniform>(vt, b0 + j, one));
-      j++;
-      if (j < nb) cB = ct[b0 + j];
-    }
+      for (; i < na; i++) emit(CA[i], row_value<T, kUniform>(VA, i, one), (T)0);
+      for (; j < nb; j++) emit(CB[j], (T)0, row_value<T, kUniform>(VB, j, one));
+      return m;
+    };
+    uint32_t m;
+    if (staged)
+      m = merge(s_ca + (ga - a_0), s_va + (ga - a_0), s_ct + (gb - t_0), s_vt + (gb - t_0), s_i + (base - o0),
+                s_d + (base - o0));
+    else
+      m = merge(ca + ga, va + ga, ct + gb, vt + gb, indices + base, data + base);
+    if (!kWrite) mcnt[r] = m;
   }
-  for (; i < na; i++) emit(ca[a0 + i], row_value<T, kUniform>(va, a0 + i, one), (T)0);
-  for (; j < nb; j++) emit(ct[b0 + j], (T)0, row_value<T, kUniform>(vt, b0 + j, one));
-  if (!kWrite) mcnt[r] = m;
+  if (kWrite && staged) {
+    __syncthreads();
+    block_store(indices, s_i, o0, nout);
+    block_store(data, s_d, o0, nout);
+  }
 }
 
 __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, uint64_t n,

@@ -187,7 +187,11 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
       scr_b = dget<PV<T>>(c, S_RSCR, n);
     }
   }
-  hipLaunchKernelGGL(k_row_start, dim3(grid_for(n_rows + 1)), dim3(kTPB), 0, c->stream, key_out, n, n_rows, S.start);
+  G2N_HIP(hipMemsetAsync(&c->ctl->row_gap, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(k_row_bounds, dim3(grid_for(n + 1)), dim3(kTPB), 0, c->stream, key_out, n, n_rows, S.start,
+                     c->ctl);
+  hipLaunchKernelGGL(k_row_start, dim3(grid_for(n_rows + 1)), dim3(kTPB), 0, c->stream, key_out, n, n_rows, S.start,
+                     (const Ctl*)c->ctl);
   if (n_rows)
     hipLaunchKernelGGL((k_row_sum<T, kU>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, S.start, n_rows, pv_out,
                        pc_out, S.ocol, S.oval, scr_a, scr_b, S.ucnt, rowflag, c->ctl, w);
@@ -434,19 +438,22 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   DictEntry* table = nullptr;
   uint32_t* tid = nullptr;  // node id per touch when the S-first fast path holds
   auto* tstate = dget<uint8_t>(c, S_TSTATE, n_t);
+  const uint32_t* nid_in = nid;  // fast lookup: firsts before each touch (null: n_first for every touch)
+  const uint32_t* inv_in = inv;
+  uint32_t n_first = 0;
   auto insert = [&](int mode, uint32_t round, uint64_t max_probes, uint32_t* tid_out) {
     G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
     phase(c, "_prep");
     const dim3 g(grid_for(n_t)), b(kTPB);
     if (mode == kModeClaim)
       hipLaunchKernelGGL(k_insert_round<kModeClaim>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
     else if (mode == kModeLookup)
       hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
     else
       hipLaunchKernelGGL(k_insert_round<kModeFast>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid, inv, tid_out);
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
     phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
     sync_ctl(c);
   };
@@ -472,19 +479,36 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     bool fast = !std::getenv("G2N_DICT_GENERAL");
     if (fast) {
       init_table();
+      n_first = (uint32_t)(n_s * tps);  // claim round: flags S touches past the first n_s * tps
       insert(kModeClaim, 1, cap >= full_cap ? cap : 4096, nullptr);
       fast = !c->h_ctl->table_overflow;
     }
+    bool sprefix = false;  // ids are touch indices: no ranking pass
     if (fast) {
-      rank_firsts();
-      hipLaunchKernelGGL(k_assign_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, table, TI, n_t, (int)bidir,
-                         first, slot, nid, inv, klen);
+      const uint64_t n_st = n_s * tps;  // S touches
+      sprefix = c->h_ctl->deferred == 0 && !c->h_ctl->s_late;
+      if (sprefix) {
+        nid_in = nullptr;
+        inv_in = nullptr;
+        n_first = (uint32_t)n_st;
+        hipLaunchKernelGGL(k_key_len, dim3(grid_for(n_st)), dim3(kTPB), 0, c->stream, TI, n_st, (int)bidir, klen);
+        c->h_ctl->n_nodes = n_st;
+        G2N_HIP(hipMemcpyAsync(&c->ctl->n_nodes, &c->h_ctl->n_nodes, sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, c->stream));
+      } else {
+        rank_firsts();
+        hipLaunchKernelGGL(k_assign_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, table, TI, n_t,
+                           (int)bidir, first, slot, nid, inv, klen);
+      }
       phase(c, "ids_fast");
       tid = dget<uint32_t>(c, S_TID, n_t);
       insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
       fast = !c->h_ctl->dict_general && !c->h_ctl->table_overflow && c->h_ctl->deferred == 0;
       if (!fast) {
         tid = nullptr;
+        sprefix = false;
+        nid_in = nid;
+        inv_in = inv;
         G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
       }
     }
@@ -533,8 +557,8 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     const uint64_t names_len = read_dev(c, &c->ctl->names_len);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
     if (n_nodes)
-      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, inv, offs,
-                         (int)bidir, blob);
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, inv_in,
+                         offs, (int)bidir, blob);
     R->names_bytes = names_len;
     R->names_blob = blob;
     R->names_offsets = offs;

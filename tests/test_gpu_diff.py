@@ -181,9 +181,10 @@ def test_c4_properties_on_device(gpu):
     assert names == want
 
 
-def _canonical_gfa(seed: int, n_s: int, n_l: int, long_names: bool) -> bytes:
+def _canonical_gfa(seed: int, n_s: int, n_l: int, long_names: bool, interleave: bool = False) -> bytes:
     """S lines first (distinct names, some longer than the 16 inline key bytes), then L lines
-    that only name defined segments: the input the S-first dictionary fast path is for."""
+    that only name defined segments: the input the S-first dictionary fast path is for.
+    interleave: S and L lines mixed, every L line naming segments defined above it."""
     import random
 
     r = random.Random(seed)
@@ -193,10 +194,20 @@ def _canonical_gfa(seed: int, n_s: int, n_l: int, long_names: bool) -> bytes:
             names.append(f"chr{r.randint(1, 22)}_segment_{k:08d}_" + "x" * r.randint(0, 40))
         else:
             names.append(f"{k + 1}")
-    lines = [f"H\tVN:Z:1.0\n"] + [f"S\t{n}\t*\n" for n in names]
-    for _ in range(n_l):
-        a, b = r.choice(names), r.choice(names)
-        lines.append(f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t*\tRC:i:{r.randint(-3, 9)}\n")
+
+    def link(pool):
+        a, b = r.choice(pool), r.choice(pool)
+        return f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t*\tRC:i:{r.randint(-3, 9)}\n"
+
+    lines = [f"H\tVN:Z:1.0\n"]
+    if interleave:
+        per = max(1, n_l // n_s)
+        for k, n in enumerate(names):
+            lines.append(f"S\t{n}\t*\n")
+            lines += [link(names[:k + 1]) for _ in range(per)]
+    else:
+        lines += [f"S\t{n}\t*\n" for n in names]
+        lines += [link(names) for _ in range(n_l)]
     return "".join(lines).encode()
 
 
@@ -207,9 +218,9 @@ def _phases(data: bytes, **kw):
     return raw.status, raw.phase_ms
 
 
-@pytest.mark.parametrize("long_names", [False, True])
-def test_s_first_fast_path_taken_and_exact(gpu, oracle_lib, long_names):
-    data = _canonical_gfa(7 + long_names, 3000, 12000, long_names)
+@pytest.mark.parametrize("long_names,interleave", [(False, False), (True, False), (True, True)])
+def test_s_first_fast_path_taken_and_exact(gpu, oracle_lib, long_names, interleave):
+    data = _canonical_gfa(7 + long_names, 3000, 12000, long_names, interleave)
     for mode in MODES:
         st, ph = _phases(data, **mode)
         assert st == 0 and "ids_fast" in ph and "ids_general" not in ph, (mode, sorted(ph))
@@ -254,3 +265,27 @@ def test_general_dictionary_forced(gpu, oracle_lib, monkeypatch):
         a = outcome(gpu_run(data, mode, "float64", "RC"))
         b = outcome(oracle_run(oracle_lib, data, mode, "float64", "RC"))
         assert a == b, mode
+
+
+def test_long_runs_of_empty_rows(gpu, oracle_lib):
+    """Thousands of consecutive node ids with no entries in a row (or column): the row-start
+    pass falls back to a binary search per row; the CSR must not change."""
+    import io
+    import random
+
+    from gfa2network_amd import convert_format, parse_gfa
+
+    r = random.Random(2)
+    lines = [f"S\t{k}\t*\n" for k in range(1, 3001)]
+    lines += [f"L\t{r.randint(1, 10)}\t+\t{r.randint(2990, 3000)}\t-\t*\tRC:i:{r.randint(1, 5)}\n"
+              for _ in range(500)]
+    data = "".join(lines).encode()
+    for mode in ({}, {"directed": False}, {"bidirected": True}):
+        a = outcome(gpu_run(data, mode, "float64", "RC"))
+        b = outcome(oracle_run(oracle_lib, data, mode, "float64", "RC"))
+        assert a == b, mode
+    A = parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, directed=False, weight_tag="RC")
+    for fmt, ref in (("csr", A.tocsr()), ("csc", A.tocsc())):
+        C = convert_format(A, fmt)
+        assert C.indptr.tobytes() == ref.indptr.tobytes() and C.indices.tobytes() == ref.indices.tobytes()
+        assert C.data.tobytes() == ref.data.tobytes()
