@@ -2,9 +2,9 @@
 //
 // HBM layout of one build (all SoA, sized from counts read back between phases):
 //   in[len]                      GFA bytes (read-only)
+//   tiles[len / 32 KiB]          per-tile counts (lines, touches, edges, ...) and their scan
 //   ls[n_lines + 1]   u64        line start offsets (ls[n_lines] = len)
 //   kind[n_lines]     u8         kSkip / kUnknown / kS / kEdge / kPO
-//   pack[n_lines]     u64        exclusive scan of (touches << 32 | edges) per line
 //   touches (n_t):   noff u64, nlen u32 [, ooff u64, olen u32 when bidirected], slot u32
 //   edges   (n_e):   w f64 (weight before the dtype cast), tb u32 (first touch)
 //   table[cap]        u64        (hash tag << 32 | first touch), cap = pow2 >= 2 n_t
@@ -19,8 +19,8 @@
 namespace g2n {
 
 constexpr int kTPB = 256;
-constexpr int kNlIters = 8;
-constexpr uint64_t kNlTile = (uint64_t)kTPB * 16 * kNlIters;  // 32 KiB of input per block
+constexpr uint64_t kTile = 32768;     // input bytes per front-end block (K1, K2)
+constexpr uint32_t kTileHalo = 4096;  // bytes staged past the tile for lines that end beyond it
 
 enum : uint8_t { kSkip = 0, kUnknown = 1, kS = 2, kEdge = 3, kPO = 4 };
 
@@ -69,7 +69,8 @@ struct Ctl {
   unsigned long long dict_general;    // the S-first dictionary fast path does not apply
   unsigned long long s_late;          // an S-line touch follows an edge touch (claim round)
   unsigned long long row_gap;         // k_row_bounds met a run of empty rows too long to fill
-  unsigned long long pad[2];
+  unsigned long long n_deferred;      // lines parsed from global memory after k_tile_parse
+  unsigned long long pad[1];
 };
 
 struct ParseOpts {
@@ -101,31 +102,14 @@ struct EdgeOut {
   double* w;
   uint32_t* tb;
 };
-struct BlockCounts {  // per-block partials of k_classify
-  unsigned long long* unk;
-  unsigned long long* rec;
-  unsigned long long* edges;
-  unsigned long long* segs;
-};
 struct EdgeIn {
   const double* w;
   const uint32_t* tb;
 };
 
 // ---- kernels (g2n_kernels.hip) ----
-__global__ void k_nl_count(const uint8_t* in, uint64_t len, uint64_t* tile_cnt);
-__global__ void k_nl_write(const uint8_t* in, uint64_t len, const uint64_t* tile_base, uint64_t* ls);
-__global__ void k_nl_finish(const uint8_t* in, uint64_t len, const uint64_t* tile_base, const uint64_t* tile_cnt,
-                            uint64_t n_tiles, uint64_t* ls, Ctl* ctl);
-__global__ void k_classify(const uint8_t* in, const uint64_t* ls, uint64_t n_lines, uint32_t tps, uint32_t tpe,
-                           uint8_t* kind, uint64_t* pack, BlockCounts bc);
-__global__ void k_reduce_blocks(BlockCounts bc, uint64_t n_blocks, Ctl* ctl);
-__global__ void k_parse(const uint8_t* in, const uint64_t* ls, const uint8_t* kind, const uint64_t* pack_scan,
-                        uint64_t n_lines, ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl, uint64_t* worklist);
-__global__ void k_weights_slow(const uint8_t* in, const uint64_t* ls, const uint64_t* pack_scan,
-                               const uint64_t* worklist, uint64_t n_work, ParseOpts op, EdgeOut E, Ctl* ctl);
-__global__ void k_error_detail(const uint8_t* in, const uint64_t* ls, uint64_t line, Ctl* ctl);
-__global__ void k_count_records(const uint8_t* kind, uint64_t line, Ctl* ctl);
+// K1-K2 (tile front end: k_tile_count, k_tile_parse, k_parse_deferred, k_weights_slow,
+// k_error_detail, k_count_records) are defined in g2n_kernels.hip (same translation unit).
 template <int kMode>
 __global__ void k_insert_round(const uint8_t* in, uint64_t in_len, TouchIn T, uint64_t n_t, DictEntry* table,
                                uint64_t mask, uint64_t max_probes, uint32_t* slot, uint8_t* tstate, uint32_t round,

@@ -1,11 +1,11 @@
 // g2n_kernels.hip — gfx950 kernels of the GFA -> CSR path.
 //
 // Replaces, on the GPU, the reference's per-line Python loops:
-//   K1 nl_count / nl_write   `for line in fh`                    gfa2network/parser.py:114
-//   K2 classify              first-byte dispatch + fields[0]      parser.py:117-134
-//   K3 parse                 split(b"\t") + _parse_link/_edge/... parser.py:133-361,
+//   K1 tile_count            `for line in fh` + first-byte dispatch, counted per 32 KiB tile
+//                                                                 gfa2network/parser.py:114-134
+//   K2 tile_parse            split(b"\t") + _parse_link/_edge/... parser.py:133-361,
 //                            tag weight (fast grammar)            parser.py:179-204, builders.py:205-209
-//   K3b weights_slow         exact CPython int()/float() for the rest (pylit.h)
+//   K2b weights_slow         exact CPython int()/float() for the rest (pylit.h)
 //   K4 insert                node2idx dict (first-touch ids)      builders.py:190-198, 218-221
 //   K5 first/names           dict insertion order, node_list      builders.py:284-288
 //   K6 triplets              add_mat_edge + dtype cast            builders.py:222-234, 280-281
@@ -31,15 +31,64 @@ __device__ inline uint32_t byte_match_mask(uint32_t w, uint32_t pat) {
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
 
+// A byte source: input byte i is p[i - o].  Global memory: {in, 0}; a block's LDS-staged
+// window: {lds, window start}.  The parsing code below reads through it, so one copy of the
+// field logic serves both (inlined per call site, each with its own address space).
+struct Src {
+  const uint8_t* p;
+  uint64_t o;
+  uint64_t lim;  // word(i) may read [i, i + 4) when i + 4 <= lim
+  __device__ uint8_t operator[](uint64_t i) const { return p[i - o]; }
+  __device__ const uint8_t* ptr(uint64_t i) const { return p + (i - o); }
+  __device__ uint32_t word(uint64_t i) const { return *(const uint32_t*)(p + (i - o)); }  // i, o % 4 == 0
+  // 4 bytes at aligned i, zero past lim
+  __device__ uint32_t word_z(uint64_t i) const {
+    if (i + 4 <= lim) return word(i);
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 4; b++)
+      if (i + b < lim) w |= (uint32_t)(*this)[i + b] << (8 * b);
+    return w;
+  }
+};
+
+__device__ inline uint32_t match_bits4(uint32_t w, uint32_t pat) {  // bit b: byte b of w == pat's byte
+  const uint32_t m = byte_match_mask(w, pat);
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+
+constexpr uint32_t kMaskSpan = 64;  // bytes a delimiter mask covers
+
+// Bit q: byte s + q (q < min(n, 64)) is '\t' (or '\n' too, with_nl).  The words covering the span
+// are loaded independently (no dependent scan), then the bits are assembled in registers.
+__device__ inline uint64_t delim_mask(const Src& in, uint64_t s, uint64_t n, bool with_nl) {
+  const uint64_t a = s & ~3ull;
+  const uint32_t sh = (uint32_t)(s - a);
+  const uint64_t end = s + (n < kMaskSpan ? n : kMaskSpan);
+  unsigned __int128 m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kMaskSpan / 4 + 1; j++) {
+    const uint64_t q = a + 4 * j;
+    if (q < end) {
+      const uint32_t w = in.word_z(q);
+      uint32_t b = match_bits4(w, 0x09090909u);
+      if (with_nl) b |= match_bits4(w, 0x0A0A0A0Au);
+      m |= (unsigned __int128)b << (4 * j);
+    }
+  }
+  uint64_t r = (uint64_t)(m >> sh);
+  const uint64_t len = end - s;
+  if (len < 64) r &= (1ull << len) - 1;
+  return r;
+}
+
 // first '\t' in [p, end), or end
-__device__ inline uint64_t next_tab(const uint8_t* __restrict__ in, uint64_t p, uint64_t end) {
+__device__ inline uint64_t next_tab(const Src& in, uint64_t p, uint64_t end) {
   while (p < end && (p & 3)) {
     if (in[p] == '\t') return p;
     p++;
   }
   while (p + 4 <= end) {
-    uint32_t w = *(const uint32_t*)(in + p);
-    uint32_t m = byte_match_mask(w, 0x09090909u);
+    uint32_t m = byte_match_mask(in.word(p), 0x09090909u);
     if (m) return p + (uint64_t)(__builtin_ctz(m) >> 3);
     p += 4;
   }
@@ -50,7 +99,44 @@ __device__ inline uint64_t next_tab(const uint8_t* __restrict__ in, uint64_t p, 
   return end;
 }
 
-__device__ inline uint64_t next_byte(const uint8_t* __restrict__ in, uint64_t p, uint64_t end, uint8_t c) {
+// first '\n' in [p, end), or end
+__device__ inline uint64_t next_nl(const Src& in, uint64_t p, uint64_t end) {
+  while (p < end && (p & 3)) {
+    if (in[p] == '\n') return p;
+    p++;
+  }
+  while (p + 4 <= end) {
+    uint32_t m = byte_match_mask(in.word(p), 0x0A0A0A0Au);
+    if (m) return p + (uint64_t)(__builtin_ctz(m) >> 3);
+    p += 4;
+  }
+  while (p < end) {
+    if (in[p] == '\n') return p;
+    p++;
+  }
+  return end;
+}
+
+// first '\t' or '\n' in [p, end), or end
+__device__ inline uint64_t next_delim(const Src& in, uint64_t p, uint64_t end) {
+  while (p < end && (p & 3)) {
+    if (in[p] == '\t' || in[p] == '\n') return p;
+    p++;
+  }
+  while (p + 4 <= end) {
+    const uint32_t w = in.word(p);
+    uint32_t m = byte_match_mask(w, 0x09090909u) | byte_match_mask(w, 0x0A0A0A0Au);
+    if (m) return p + (uint64_t)(__builtin_ctz(m) >> 3);
+    p += 4;
+  }
+  while (p < end) {
+    if (in[p] == '\t' || in[p] == '\n') return p;
+    p++;
+  }
+  return end;
+}
+
+__device__ inline uint64_t next_byte(const Src& in, uint64_t p, uint64_t end, uint8_t c) {
   while (p < end && in[p] != c) p++;
   return p;
 }
@@ -99,185 +185,153 @@ __device__ inline uint4 load16(const uint8_t* __restrict__ in, uint64_t pos, uin
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// ================================================================= K1: lines ======
-__global__ void __launch_bounds__(kTPB) k_nl_count(const uint8_t* __restrict__ in, uint64_t len,
-                                                   uint64_t* __restrict__ tile_cnt) {
-  __shared__ uint32_t red[kTPB / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kNlTile;
-  uint32_t c = 0;
+// ================================================= K1: tiles (lines, classify) ======
+// The input is cut into 32 KiB tiles, one block each.  A block stages its tile (and a halo
+// past it) in LDS with coalesced 16-byte loads and scans it in the same order: thread t takes
+// the 16-byte chunks 256 j + t (conflict-free LDS reads).  A line belongs to the tile holding
+// its first byte; its index is the number of '\n' before it (parser.py:114 `for line in fh`),
+// its record kind the first-byte dispatch of parser.py:117-134 (a record type must be followed
+// by '\t', '\n' or the end of input).
+constexpr uint32_t kTileChunks = (uint32_t)(kTile / 16);  // 2048
+constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // 8
+
+template <uint32_t kHalo>
+__device__ inline void stage_tile(const uint8_t* __restrict__ in, uint64_t len, uint64_t t0, uint8_t* lds) {
+  constexpr uint32_t kChunks = (uint32_t)((kTile + kHalo) / 16);
+  constexpr uint32_t kPer = (kChunks + kTPB - 1) / kTPB;
+  uint4 r[kPer];
 #pragma unroll
-  for (int j = 0; j < kNlIters; j++) {
-    uint64_t pos = base + (uint64_t)j * (kTPB * 16) + (uint64_t)threadIdx.x * 16;
-    if (pos < len) {
-      uint4 v = load16(in, pos, len);
-      c += __popc(byte_match_mask(v.x, 0x0A0A0A0Au)) + __popc(byte_match_mask(v.y, 0x0A0A0A0Au)) +
-           __popc(byte_match_mask(v.z, 0x0A0A0A0Au)) + __popc(byte_match_mask(v.w, 0x0A0A0A0Au));
-    }
+  for (uint32_t j = 0; j < kPer; j++) {  // every load in flight before the first LDS write
+    const uint32_t c = j * kTPB + threadIdx.x;
+    const uint64_t pos = t0 + (uint64_t)c * 16;
+    r[j] = (c < kChunks && pos < len) ? load16(in, pos, len) : make_uint4(0, 0, 0, 0);
   }
-  c = wave_reduce_sum(c);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kTPB / 64; w++) t += red[w];
-    tile_cnt[blockIdx.x] = t;
-  }
-}
-
-// ls[r + 1] = 1 + position of the r-th '\n' (0-based over the whole input)
-__global__ void __launch_bounds__(kTPB) k_nl_write(const uint8_t* __restrict__ in, uint64_t len,
-                                                   const uint64_t* __restrict__ tile_base,
-                                                   uint64_t* __restrict__ ls) {
-  __shared__ uint32_t lds[kTPB / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kNlTile;
-  uint64_t run = tile_base[blockIdx.x];
-  for (int j = 0; j < kNlIters; j++) {
-    uint64_t seg = base + (uint64_t)j * (kTPB * 16);
-    if (seg >= len) break;  // uniform over the block
-    uint64_t pos = seg + (uint64_t)threadIdx.x * 16;
-    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-    if (pos < len) {
-      uint4 v = load16(in, pos, len);
-      m0 = byte_match_mask(v.x, 0x0A0A0A0Au);
-      m1 = byte_match_mask(v.y, 0x0A0A0A0Au);
-      m2 = byte_match_mask(v.z, 0x0A0A0A0Au);
-      m3 = byte_match_mask(v.w, 0x0A0A0A0Au);
-    }
-    uint32_t c = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
-    uint32_t off;
-    uint32_t tot = block_excl_scan_u32(c, &off, lds);
-    if (c) {
-      uint64_t r = run + off + 1;
-      uint32_t ms[4] = {m0, m1, m2, m3};
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        uint32_t m = ms[q];
-        while (m) {
-          int b = __builtin_ctz(m) >> 3;
-          m &= m - 1;
-          ls[r++] = pos + (uint64_t)(q * 4 + b) + 1;
-        }
-      }
-    }
-    run += tot;
+  for (uint32_t j = 0; j < kPer; j++) {
+    const uint32_t c = j * kTPB + threadIdx.x;
+    if (c < kChunks) *(uint4*)(lds + (uint64_t)c * 16) = r[j];
   }
 }
 
-// n_lines and the end sentinel (ls[n_lines] = len)
-__global__ void k_nl_finish(const uint8_t* __restrict__ in, uint64_t len, const uint64_t* __restrict__ tile_base,
-                            const uint64_t* __restrict__ tile_cnt, uint64_t n_tiles, uint64_t* __restrict__ ls,
-                            Ctl* ctl) {
-  uint64_t total = n_tiles ? tile_base[n_tiles - 1] + tile_cnt[n_tiles - 1] : 0;
-  uint64_t n_lines = total;
-  if (len > 0 && in[len - 1] != '\n') n_lines++;
-  ls[0] = 0;
-  ls[n_lines] = len;
-  ctl->n_lines = n_lines;
+__device__ inline uint8_t line_kind(uint8_t c0, bool exact) {
+  switch (c0) {
+    case 'S': return exact ? kS : kSkip;
+    case 'L': case 'E': case 'C': return exact ? kEdge : kSkip;
+    case 'P': case 'O': return exact ? kPO : kSkip;
+    case 'H': case 'F': return kSkip;
+    default: return kUnknown;  // parser.py:125-131: warned about once
+  }
 }
 
-// ================================================================ K2: classify ====
-__global__ void __launch_bounds__(kTPB) k_classify(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
-                                                   uint64_t n_lines, uint32_t tps, uint32_t tpe,
-                                                   uint8_t* __restrict__ kind, uint64_t* __restrict__ pack,
-                                                   BlockCounts bc) {
-  __shared__ unsigned long long s_min[kTPB / 64];
-  __shared__ unsigned long long s_cnt[3][kTPB / 64];
-  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  unsigned long long unk = ~0ull;
-  unsigned long long nrec = 0, nedge = 0, ns = 0;
-  if (i < n_lines) {
-    uint64_t s = ls[i], e = ls[i + 1];
-    uint8_t c0 = in[s];
-    bool exact = (s + 1 == e);
-    if (!exact) {
-      uint8_t c1 = in[s + 1];
-      exact = (c1 == '\t' || c1 == '\n');
-    }
-    uint8_t k = kSkip;
-    uint64_t pk = 0;
-    switch (c0) {
-      case 'S':
-        if (exact) { k = kS; pk = (uint64_t)tps << 32; ns = 1; nrec = 1; }
-        break;
-      case 'L': case 'E': case 'C':
-        if (exact) { k = kEdge; pk = ((uint64_t)tpe << 32) | 1u; nedge = 1; nrec = 1; }
-        break;
-      case 'P': case 'O':
-        if (exact) { k = kPO; nrec = 1; }
-        break;
-      case 'H': case 'F':
-        break;
-      default:
-        k = kUnknown;
-        unk = i;
-    }
-    kind[i] = k;
-    pack[i] = pk;
+// kind of the line starting at tile offset o (input position p)
+__device__ inline uint8_t kind_at(const uint8_t* buf, uint32_t o, uint64_t p, uint64_t len) {
+  const uint8_t c0 = buf[o];
+  return line_kind(c0, p + 1 >= len || c0 == '\n' || buf[o + 1] == '\t' || buf[o + 1] == '\n');
+}
+
+__device__ inline uint32_t nl_bits4(uint32_t w) {  // bit b: byte b of w is '\n'
+  const uint32_t m = byte_match_mask(w, 0x0A0A0A0Au);
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+
+// Newlines (bit b = byte b) and line starts of chunk c of the staged tile.  Bytes at or past
+// len hold neither; a start needs the byte before it to be '\n' (or to be the input's start).
+__device__ inline void chunk_masks(const uint8_t* buf, uint32_t c, uint64_t t0, uint64_t len, bool tile_prev_nl,
+                                   uint32_t& nl, uint32_t& st) {
+  const uint4 v = *(const uint4*)(buf + 16 * c);
+  nl = nl_bits4(v.x) | (nl_bits4(v.y) << 4) | (nl_bits4(v.z) << 8) | (nl_bits4(v.w) << 12);
+  const bool prev = c ? buf[16 * c - 1] == '\n' : tile_prev_nl;
+  st = ((nl << 1) | (prev ? 1u : 0u)) & 0xFFFFu;
+  const uint64_t pos = t0 + 16ull * c;
+  if (pos + 16 > len) {
+    const uint32_t keep = pos >= len ? 0u : ((1u << (uint32_t)(len - pos)) - 1u);
+    nl &= keep;
+    st &= keep;
   }
-  unk = wave_reduce_min(unk);
-  nrec = wave_reduce_sum(nrec);
-  nedge = wave_reduce_sum(nedge);
-  ns = wave_reduce_sum(ns);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s_min[w] = unk;
-    s_cnt[0][w] = nrec;
-    s_cnt[1][w] = nedge;
-    s_cnt[2][w] = ns;
+}
+
+struct TileCnt {
+  unsigned long long nl, lines, touches, edges, segs, recs;
+};
+struct TileCntPlus {
+  __device__ __host__ TileCnt operator()(const TileCnt& a, const TileCnt& b) const {
+    return TileCnt{a.nl + b.nl, a.lines + b.lines, a.touches + b.touches, a.edges + b.edges, a.segs + b.segs,
+                   a.recs + b.recs};
+  }
+};
+
+template <class T>
+__device__ inline T block_sum(T v, T* lds /* >= kTPB / 64 */) {
+  v = wave_reduce_sum(v);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T t = 0;
+#pragma unroll
+  for (int w = 0; w < kTPB / 64; w++) t += lds[w];
+  __syncthreads();
+  return t;
+}
+
+// exclusive scan over the block (thread order) of one u64 per thread; *tot = block total
+__device__ inline unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long* tot,
+                                                         unsigned long long* lds /* >= kTPB / 64 */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  unsigned long long wbase = 0, t = 0;
+#pragma unroll
+  for (int q = 0; q < kTPB / 64; q++) {
+    const unsigned long long y = lds[q];
+    if (q < wid) wbase += y;
+    t += y;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // per-block partials (one word per block, no same-address atomics)
-    unsigned long long m = ~0ull, a = 0, b = 0, c = 0;
-    for (int q = 0; q < kTPB / 64; q++) {
-      m = s_min[q] < m ? s_min[q] : m;
-      a += s_cnt[0][q];
-      b += s_cnt[1][q];
-      c += s_cnt[2][q];
-    }
-    bc.unk[blockIdx.x] = m;
-    bc.rec[blockIdx.x] = a;
-    bc.edges[blockIdx.x] = b;
-    bc.segs[blockIdx.x] = c;
-  }
+  *tot = t;
+  return wbase + x - v;
 }
 
-// fold the per-block partials of k_classify into the control block (one 1024-thread block)
-__global__ void __launch_bounds__(1024) k_reduce_blocks(BlockCounts bc, uint64_t n_blocks, Ctl* ctl) {
-  __shared__ unsigned long long s[4][1024 / 64];
-  unsigned long long m = ~0ull, a = 0, b = 0, c = 0;
-  for (uint64_t i = threadIdx.x; i < n_blocks; i += 1024) {
-    unsigned long long u = bc.unk[i];
-    m = u < m ? u : m;
-    a += bc.rec[i];
-    b += bc.edges[i];
-    c += bc.segs[i];
-  }
-  m = wave_reduce_min(m);
-  a = wave_reduce_sum(a);
-  b = wave_reduce_sum(b);
-  c = wave_reduce_sum(c);
-  if ((threadIdx.x & 63) == 0) {
-    s[0][threadIdx.x >> 6] = m;
-    s[1][threadIdx.x >> 6] = a;
-    s[2][threadIdx.x >> 6] = b;
-    s[3][threadIdx.x >> 6] = c;
-  }
+// pass 1: per tile, the '\n', lines, touches, edges, S lines and records it holds
+__global__ void __launch_bounds__(kTPB) k_tile_count(const uint8_t* __restrict__ in, uint64_t len, uint32_t tps,
+                                                     uint32_t tpe, TileCnt* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + 16];
+  __shared__ unsigned long long red[kTPB / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  stage_tile<16>(in, len, t0, buf);
+  const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int q = 1; q < 1024 / 64; q++) {
-      s[0][0] = s[0][q] < s[0][0] ? s[0][q] : s[0][0];
-      s[1][0] += s[1][q];
-      s[2][0] += s[2][q];
-      s[3][0] += s[3][q];
+  unsigned long long nl = 0, lines = 0, touches = 0, edges = 0, segs = 0, recs = 0;
+#pragma unroll 2
+  for (uint32_t j = 0; j < kChunkIters; j++) {
+    const uint32_t c = j * kTPB + threadIdx.x;
+    uint32_t m, st;
+    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
+    nl += __popc(m);
+    lines += __popc(st);
+    while (st) {
+      const uint32_t o = 16 * c + __builtin_ctz(st);
+      st &= st - 1;
+      const uint8_t k = kind_at(buf, o, t0 + o, len);
+      if (k == kS) { touches += tps; segs++; recs++; }
+      else if (k == kEdge) { touches += tpe; edges++; recs++; }
+      else if (k == kPO) recs++;
     }
-    ctl->warn_line = s[0][0];
-    ctl->n_records = s[1][0];
-    ctl->n_edges = s[2][0];
-    ctl->n_s = s[3][0];
   }
+  TileCnt cnt;
+  cnt.nl = block_sum(nl, red);
+  cnt.lines = block_sum(lines, red);
+  cnt.touches = block_sum(touches, red);
+  cnt.edges = block_sum(edges, red);
+  cnt.segs = block_sum(segs, red);
+  cnt.recs = block_sum(recs, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = cnt;
 }
 
-// ================================================================ K3: parse =======
+// ================================================================ K2: parse =======
 __device__ inline void record_error(Ctl* ctl, uint64_t line, uint32_t code) {
   atomicMin(&ctl->err_key, (unsigned long long)((line << 5) | code));
 }
@@ -292,7 +346,7 @@ struct EdgeLayout {
   uint32_t err_len;
 };
 
-__device__ inline uint64_t rstrip_pm(const uint8_t* __restrict__ in, uint64_t off, uint64_t len) {
+__device__ inline uint64_t rstrip_pm(const Src& in, uint64_t off, uint64_t len) {
   while (len > 0) {
     uint8_t c = in[off + len - 1];
     if (c != '+' && c != '-') break;
@@ -301,12 +355,12 @@ __device__ inline uint64_t rstrip_pm(const uint8_t* __restrict__ in, uint64_t of
   return len;
 }
 
-__device__ inline bool int_bytes_ok(const uint8_t* __restrict__ in, uint64_t s, uint64_t e) {
-  return py_int_literal(in + s, e - s, false, nullptr);
+__device__ inline bool int_bytes_ok(const Src& in, uint64_t s, uint64_t e) {
+  return py_int_literal(in.ptr(s), e - s, false, nullptr);
 }
 
 // Field layout of an L/E/C line [s, e) ('\n' already stripped): parser.py:206-341.
-__device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_t s, uint64_t e) {
+__device__ inline EdgeLayout edge_layout(const Src& in, uint64_t s, uint64_t e) {
   EdgeLayout L;
   L.err = 0;
   L.has_tags = false;
@@ -315,16 +369,36 @@ __device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_
   int nf = 0;
   uint64_t p = s;
   bool more = true;
+  if (e - s <= kMaskSpan) {  // short line: every tab from one register mask
+    uint64_t m = delim_mask(in, s, e - s, false);
 #pragma unroll
-  for (int k = 0; k < 10; k++) {
-    fs[k] = e;
-    fe[k] = e;
-    if (more) {
-      fs[k] = p;
-      fe[k] = next_tab(in, p, e);
-      nf = k + 1;
-      if (fe[k] == e) more = false;
-      else p = fe[k] + 1;
+    for (int k = 0; k < 10; k++) {
+      fs[k] = e;
+      fe[k] = e;
+      if (more) {
+        fs[k] = p;
+        nf = k + 1;
+        if (m) {
+          fe[k] = s + __builtin_ctzll(m);
+          m &= m - 1;
+          p = fe[k] + 1;
+        } else {
+          more = false;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      fs[k] = e;
+      fe[k] = e;
+      if (more) {
+        fs[k] = p;
+        fe[k] = next_tab(in, p, e);
+        nf = k + 1;
+        if (fe[k] == e) more = false;
+        else p = fe[k] + 1;
+      }
     }
   }
   const uint8_t t = in[s];
@@ -337,7 +411,7 @@ __device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_
       L.ouo = kConstFlag | c2; L.oul = 1;
       L.vo = fs[3]; L.vl = (uint32_t)(fe[3] - fs[3]);
       L.ovo = fs[4]; L.ovl = (uint32_t)(fe[4] - fs[4]);
-      if (!utf8_valid(in + L.ovo, L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
+      if (!utf8_valid(in.ptr(L.ovo), L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
       tag_from = 6;
     } else {
       if (fe[1] == fs[1] || fe[2] == fs[2]) { L.err = kErrIndexBytes; return L; }
@@ -374,8 +448,8 @@ __device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_
       tag_from = 5;
     }
     if (!coords) {
-      if (!utf8_valid(in + L.ouo, L.oul)) { L.err = kErrUnicode; L.err_off = L.ouo; L.err_len = L.oul; return L; }
-      if (!utf8_valid(in + L.ovo, L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
+      if (!utf8_valid(in.ptr(L.ouo), L.oul)) { L.err = kErrUnicode; L.err_off = L.ouo; L.err_len = L.oul; return L; }
+      if (!utf8_valid(in.ptr(L.ovo), L.ovl)) { L.err = kErrUnicode; L.err_off = L.ovo; L.err_len = L.ovl; return L; }
     }
   }
   // fields[tag_from:] (tag_from <= 9, static selects keep fs[] in registers)
@@ -392,8 +466,8 @@ __device__ inline EdgeLayout edge_layout(const uint8_t* __restrict__ in, uint64_
   return L;
 }
 
-__device__ inline bool span_eq(const uint8_t* __restrict__ in, uint64_t off, uint64_t len,
-                               const uint8_t* __restrict__ w, uint32_t wl) {
+__device__ inline bool span_eq(const Src& in, uint64_t off, uint64_t len, const uint8_t* __restrict__ w,
+                               uint32_t wl) {
   if (len != wl) return false;
   for (uint32_t k = 0; k < wl; k++)
     if (in[off + k] != w[k]) return false;
@@ -401,7 +475,7 @@ __device__ inline bool span_eq(const uint8_t* __restrict__ in, uint64_t off, uin
 }
 
 // Weight by the fast grammar.  Returns false when a matching tag needs the exact path.
-__device__ inline bool weight_fast(const uint8_t* __restrict__ in, uint64_t ts, uint64_t e, bool has_tags,
+__device__ inline bool weight_fast(const Src& in, uint64_t ts, uint64_t e, bool has_tags,
                                    const uint8_t* __restrict__ wt, uint32_t wtl, double* w) {
   *w = 1.0;
   if (!has_tags) return true;
@@ -420,12 +494,12 @@ __device__ inline bool weight_fast(const uint8_t* __restrict__ in, uint64_t ts, 
         uint8_t ty = in[c1 + 1];
         if (tl == 1 && ty == 'i') {
           double v;
-          if (!fast_int(in + c2 + 1, fe - c2 - 1, &v)) return false;
+          if (!fast_int(in.ptr(c2 + 1), fe - c2 - 1, &v)) return false;
           kind = 1;
           num = v;
         } else if (tl == 1 && ty == 'f') {
           double v;
-          if (!fast_float(in + c2 + 1, fe - c2 - 1, &v)) return false;
+          if (!fast_float(in.ptr(c2 + 1), fe - c2 - 1, &v)) return false;
           kind = 1;
           num = v;
         } else {
@@ -451,49 +525,27 @@ __device__ inline void put_touch(const TouchOut& T, uint64_t t, uint64_t no, uin
   }
 }
 
-__device__ inline uint64_t rev_ori(const uint8_t* __restrict__ in, uint64_t oo, uint32_t ol) {
+__device__ inline uint64_t rev_ori(const Src& in, uint64_t oo, uint32_t ol) {
   // builders.py:232-233: "-" if orientation == "+" else "+"
   bool plus = (oo & kConstFlag) ? ((oo & 0xFF) == '+') : (ol == 1 && in[oo] == '+');
   return kConstFlag | (plus ? '-' : '+');
 }
 
-__global__ void __launch_bounds__(kTPB) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
-                                                const uint8_t* __restrict__ kind,
-                                                const uint64_t* __restrict__ pack_scan, uint64_t n_lines,
-                                                ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl,
-                                                uint64_t* __restrict__ worklist) {
-  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (i >= n_lines) return;
-  const uint8_t k = kind[i];
-  if (k == kSkip || k == kUnknown) return;
-  uint64_t s = ls[i], e = ls[i + 1];
-  if (e > s && in[e - 1] == '\n') e--;
-  if (k == kPO) {  // parser.py:231-232, 345-346: fewer than 3 fields
-    uint64_t t1 = next_tab(in, s, e);
-    if (t1 >= e || next_tab(in, t1 + 1, e) >= e) record_error(ctl, i, in[s] == 'P' ? kErrMalformedP : kErrMalformedO);
-    return;
+// S line i, name = [ns, ne): parser.py:163, builders.py:190-198
+__device__ inline void put_segment(const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t ns, uint64_t ne) {
+  const uint32_t nl = (uint32_t)(ne - ns);
+  if (!op.bidir) {
+    put_touch(T, tb, ns, nl, 0, 0, false, 1);
+  } else {
+    put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
+    put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true, 1);
   }
-  const uint64_t pk = pack_scan[i];
-  const uint64_t tb = pk >> 32;
-  if (k == kS) {  // parser.py:163, builders.py:190-198
-    uint64_t t1 = next_tab(in, s, e);
-    if (t1 >= e) {
-      record_error(ctl, i, kErrIndexList);
-      return;
-    }
-    uint64_t ns = t1 + 1;
-    uint64_t ne = next_tab(in, ns, e);
-    uint32_t nl = (uint32_t)(ne - ns);
-    if (!op.bidir) {
-      put_touch(T, tb, ns, nl, 0, 0, false, 1);
-    } else {
-      put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
-      put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true, 1);
-    }
-    return;
-  }
-  // L / E / C
-  const uint64_t eb = pk & 0xFFFFFFFFull;
+}
+
+// L / E / C line i = [s, e) ('\n' stripped), its touches from tb, its edge eb
+__device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_t e, uint64_t tb, uint64_t eb,
+                                  const ParseOpts& op, const TouchOut& T, const EdgeOut& E, Ctl* ctl,
+                                  uint64_t* __restrict__ worklist) {
   EdgeLayout L = edge_layout(in, s, e);
   if (L.err) {
     record_error(ctl, i, L.err);
@@ -507,7 +559,8 @@ __global__ void __launch_bounds__(kTPB) k_parse(const uint8_t* __restrict__ in, 
   if (op.has_wt) {
     if (!weight_fast(in, L.tag_start, e, L.has_tags, op.wt, op.wt_len, &w)) {
       unsigned long long slot = atomicAdd(&ctl->wl_count, 1ull);
-      worklist[slot] = i;
+      worklist[2 * slot] = i;
+      worklist[2 * slot + 1] = eb;
       w = 0.0;
     }
   }
@@ -526,18 +579,158 @@ __global__ void __launch_bounds__(kTPB) k_parse(const uint8_t* __restrict__ in, 
   }
 }
 
+// Line i of kind k starting at s.  The source holds the bytes [.., bound); when nl_at_bound
+// the line's '\n' is byte bound - 1 (its end is known).  Returns false when the line's fields
+// run past bound < len: the line is deferred.
+__device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, bool nl_at_bound, uint64_t i,
+                                  uint8_t k, uint64_t s, uint64_t tb, uint64_t eb, const ParseOpts& op,
+                                  const TouchOut& T, const EdgeOut& E, Ctl* ctl, uint64_t* __restrict__ worklist) {
+  const bool cut = bound < len;
+  if (k == kS || k == kPO) {  // the first two (S) / three (P, O) fields
+    uint64_t t1, t2;
+    const uint64_t m = delim_mask(in, s, bound - s, true);
+    if (__popcll(m) >= 2) {  // both delimiters among the first 64 bytes
+      t1 = s + __builtin_ctzll(m);
+      t2 = s + __builtin_ctzll(m & (m - 1));
+    } else {
+      t1 = next_delim(in, s, bound);
+      if (t1 == bound && cut) return false;
+      t2 = t1 < bound ? next_delim(in, t1 + 1, bound) : bound;
+    }
+    if (t1 == bound || in[t1] == '\n') {  // one field: parser.py:163 IndexError / :231 too few fields
+      record_error(ctl, i, k == kS ? kErrIndexList : (in[s] == 'P' ? kErrMalformedP : kErrMalformedO));
+      return true;
+    }
+    if (t2 == bound && cut) return false;
+    if (k == kS) {
+      put_segment(op, T, tb, t1 + 1, t2);
+    } else if (t2 == bound || in[t2] == '\n') {
+      record_error(ctl, i, in[s] == 'P' ? kErrMalformedP : kErrMalformedO);
+    }
+    return true;
+  }
+  const uint64_t e = nl_at_bound ? bound - 1 : next_nl(in, s, bound);
+  if (e == bound && cut) return false;
+  parse_edge(in, i, s, e, tb, eb, op, T, E, ctl, worklist);
+  return true;
+}
+
+struct DeferredLine {
+  unsigned long long line;
+  uint32_t tb, eb;
+};
+
+// pass 2: line starts, kinds, touches, edges of every line starting in the tile.  The tile's
+// line starts are compacted into an LDS list (in windows of kTileLines), then lanes take
+// consecutive lines and parse them from the staged bytes.
+constexpr uint32_t kTileLines = 4096;
+
+__global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__ in, uint64_t len,
+                                                     const TileCnt* __restrict__ base, uint32_t tps, uint32_t tpe,
+                                                     ParseOpts op, uint64_t* __restrict__ ls,
+                                                     uint8_t* __restrict__ kind, TouchOut T, EdgeOut E, Ctl* ctl,
+                                                     uint64_t* __restrict__ worklist,
+                                                     DeferredLine* __restrict__ deferred) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
+  __shared__ uint16_t starts[kTileLines];
+  __shared__ unsigned long long red[kTPB / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  stage_tile<kTileHalo>(in, len, t0, buf);
+  const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
+  __syncthreads();
+  const uint64_t w1 = t0 + kTile + kTileHalo < len ? t0 + kTile + kTileHalo : len;
+  const Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
+  const TileCnt b = base[blockIdx.x];
+  const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
+  uint64_t t_run = b.touches, e_run = b.edges;
+  unsigned long long unk = ~0ull;
+  for (uint32_t w0 = 0;; w0 += kTileLines) {
+    // compact the starts ranked [w0, w0 + kTileLines) into `starts`
+    uint32_t run = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < kChunkIters; j++) {
+      const uint32_t c = j * kTPB + threadIdx.x;
+      uint32_t m, st;
+      chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
+      unsigned long long tot;
+      uint32_t r = run + (uint32_t)block_excl_scan_u64(__popc(st), &tot, red);
+      run += (uint32_t)tot;
+      while (st) {
+        const uint32_t o = 16 * c + __builtin_ctz(st);
+        st &= st - 1;
+        if (r >= w0 && r < w0 + kTileLines) starts[r - w0] = (uint16_t)o;
+        r++;
+      }
+    }
+    __syncthreads();
+    const uint32_t n_win = run - w0 < kTileLines ? run - w0 : kTileLines;
+    const bool last_win = w0 + n_win >= run;
+#pragma unroll 1
+    for (uint32_t k0 = 0; k0 < n_win; k0 += kTPB) {
+      const uint32_t j = k0 + threadIdx.x;
+      uint8_t k = kSkip;
+      uint32_t o = 0;
+      if (j < n_win) {
+        o = starts[j];
+        k = kind_at(buf, o, t0 + o, len);
+      }
+      const unsigned long long cnt = k == kS ? (unsigned long long)tps << 20
+                                    : k == kEdge ? ((unsigned long long)tpe << 20) | 1ull : 0ull;
+      unsigned long long tot;
+      const unsigned long long ex = block_excl_scan_u64(cnt, &tot, red);
+      if (j < n_win) {
+        const uint64_t i = idx0 + w0 + j;
+        const uint64_t p = t0 + o;
+        ls[i] = p;
+        kind[i] = k;
+        if (k == kUnknown) unk = i < unk ? i : unk;
+        if (k == kS || k == kEdge || k == kPO) {
+          const uint64_t tb = t_run + (ex >> 20), eb = e_run + (ex & 0xFFFFF);
+          // the line ends where the next one starts; the window's last line: search the staged bytes
+          const bool known = j + 1 < n_win;
+          const uint64_t bound = known ? t0 + starts[j + 1] : w1;
+          if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist)) {
+            const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
+            deferred[d] = DeferredLine{i, (uint32_t)tb, (uint32_t)eb};
+          }
+        }
+      }
+      t_run += tot >> 20;
+      e_run += tot & 0xFFFFF;
+    }
+    if (last_win) break;
+    __syncthreads();  // before the next window overwrites `starts`
+  }
+  unk = wave_reduce_min(unk);
+  if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
+}
+
+// Lines whose fields run past their tile's staged window: parsed from global memory.
+__global__ void __launch_bounds__(64) k_parse_deferred(const uint8_t* __restrict__ in, uint64_t len,
+                                                       const uint64_t* __restrict__ ls,
+                                                       const uint8_t* __restrict__ kind,
+                                                       const DeferredLine* __restrict__ deferred, uint64_t n,
+                                                       ParseOpts op, TouchOut T, EdgeOut E, Ctl* ctl,
+                                                       uint64_t* __restrict__ worklist) {
+  const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= n) return;
+  const DeferredLine d = deferred[j];
+  const Src G{in, 0, len};
+  parse_line(G, len, len, false, d.line, kind[d.line], ls[d.line], d.tb, d.eb, op, T, E, ctl, worklist);
+}
+
 // Exact weights (CPython int()/float() semantics) for the edges the fast grammar deferred.
-__global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls,
-                                                     const uint64_t* __restrict__ pack_scan,
+__global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__ in_, uint64_t len,
+                                                     const uint64_t* __restrict__ ls,
                                                      const uint64_t* __restrict__ worklist, uint64_t n_work,
                                                      ParseOpts op, EdgeOut E, Ctl* ctl) {
   const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (j >= n_work) return;
-  const uint64_t i = worklist[j];
+  const Src in{in_, 0, len};
+  const uint64_t i = worklist[2 * j], eb = worklist[2 * j + 1];
   uint64_t s = ls[i], e = ls[i + 1];
   if (e > s && in[e - 1] == '\n') e--;
   EdgeLayout L = edge_layout(in, s, e);
-  const uint64_t eb = pack_scan[i] & 0xFFFFFFFFull;
   Decimal dec;
   uint8_t tmp[DEC_TMP];
   // _parse_tags over fields[tag_from:], keeping only the final value for weight_tag
@@ -548,21 +741,21 @@ __global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__
     uint64_t p = L.tag_start;
     while (true) {
       uint64_t fe = next_tab(in, p, e);
-      if (utf8_valid(in + p, fe - p)) {
+      if (utf8_valid(in.ptr(p), fe - p)) {
         uint64_t c1 = next_byte(in, p, fe, ':');
         uint64_t c2 = c1 < fe ? next_byte(in, c1 + 1, fe, ':') : fe;
         if (c2 < fe && span_eq(in, p, c1 - p, op.wt, op.wt_len)) {
           uint64_t tl = c2 - c1 - 1;
           uint8_t ty = in[c1 + 1];
           if (tl == 1 && ty == 'i') {
-            if (py_int_literal(in + c2 + 1, fe - c2 - 1, true, nullptr)) {
+            if (py_int_literal(in.ptr(c2 + 1), fe - c2 - 1, true, nullptr)) {
               kind = 1;
               best_s = c2 + 1;
               best_e = fe;
             }
           } else if (tl == 1 && ty == 'f') {
             double v;
-            if (py_float_literal(in + c2 + 1, fe - c2 - 1, true, &v, &dec, tmp)) {
+            if (py_float_literal(in.ptr(c2 + 1), fe - c2 - 1, true, &v, &dec, tmp)) {
               kind = 2;
               fval = v;
             }
@@ -577,7 +770,7 @@ __global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__
   }
   double w = 1.0;
   if (kind == 1) {
-    py_int_literal(in + best_s, best_e - best_s, true, &dec);
+    py_int_literal(in.ptr(best_s), best_e - best_s, true, &dec);
     if (!py_int_to_f64(&dec, &w, tmp)) {  // builders.py:209 float(val): OverflowError
       record_error(ctl, i, kErrIntTooLarge);
       return;
@@ -589,8 +782,9 @@ __global__ void __launch_bounds__(64) k_weights_slow(const uint8_t* __restrict__
 }
 
 // Re-parse the failing line to recover the bytes whose .decode() raised.
-__global__ void k_error_detail(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ls, uint64_t line,
-                               Ctl* ctl) {
+__global__ void k_error_detail(const uint8_t* __restrict__ in_, uint64_t len, const uint64_t* __restrict__ ls,
+                               uint64_t line, Ctl* ctl) {
+  const Src in{in_, 0, len};
   uint64_t s = ls[line], e = ls[line + 1];
   if (e > s && in[e - 1] == '\n') e--;
   EdgeLayout L = edge_layout(in, s, e);

@@ -30,11 +30,11 @@ namespace g2n {
 
 // ----------------------------------------------------------------- arena ----------
 enum Slot {
-  S_IN, S_TILE_CNT, S_TILE_BASE, S_LS, S_KIND, S_PACK, S_PACK_SCAN, S_NOFF, S_NLEN, S_OOFF, S_OLEN, S_EW, S_ETB,
-  S_WL, S_TABLE, S_SLOT, S_FIRST, S_NID, S_FLEN, S_FOFF, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1,
-  S_VALS0, S_VALS1, S_HEAD, S_HPOS, S_UKEYS0, S_UDATA0, S_UKEYS1, S_UDATA1, S_ROWFLAG, S_KV, S_ORD, S_MK, S_MV,
-  S_MVAL, S_KEEP, S_KPOS, S_OKEYS, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TVALS0, S_TVALS1, S_BLK, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0, S_ROUT1,
-  S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID, S_INV, S_NSLOTS
+  S_IN, S_TILE_CNT, S_TILE_BASE, S_LS, S_KIND, S_NOFF, S_NLEN, S_OOFF, S_OLEN, S_EW, S_ETB, S_WL, S_TABLE,
+  S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
+  S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
+  S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
+  S_INV, S_DEFER, S_NSLOTS
 };
 
 struct DevBuf {
@@ -310,47 +310,34 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   R->dtype = dt;
   R->index_width = 4;
 
-  // ---- lines
-  const uint64_t n_tiles = (len + kNlTile - 1) / kNlTile;
-  auto* tile_cnt = dget<uint64_t>(c, S_TILE_CNT, n_tiles + 1);
-  auto* tile_base = dget<uint64_t>(c, S_TILE_BASE, n_tiles + 1);
+  // ---- K1: per-tile counts -> tile bases
+  const uint64_t n_tiles = (len + kTile - 1) / kTile;
+  auto* tcnt = dget<TileCnt>(c, S_TILE_CNT, n_tiles + 1);
+  auto* tbase = dget<TileCnt>(c, S_TILE_BASE, n_tiles + 1);
+  TileCnt tot{};
   if (n_tiles) {
-    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tile_cnt);
-    excl_scan<uint64_t>(c, tile_cnt, tile_base, n_tiles);
+    hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
+    size_t tb = 0;
+    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, tcnt, tbase, TileCnt{}, (size_t)n_tiles, TileCntPlus(),
+                                    c->stream));
+    void* tmp = dbuf(c, S_TEMP, tb);
+    G2N_HIP(rocprim::exclusive_scan(tmp, tb, tcnt, tbase, TileCnt{}, (size_t)n_tiles, TileCntPlus(), c->stream));
+    const TileCnt last_b = read_dev(c, tbase + n_tiles - 1), last_c = read_dev(c, tcnt + n_tiles - 1);
+    tot = TileCntPlus()(last_b, last_c);
   }
-  uint64_t total_nl = 0;
-  if (n_tiles) total_nl = read_dev(c, tile_base + n_tiles - 1) + read_dev(c, tile_cnt + n_tiles - 1);
-  auto* ls = dget<uint64_t>(c, S_LS, total_nl + 2);
-  if (n_tiles)
-    hipLaunchKernelGGL(k_nl_write, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tile_base, ls);
-  hipLaunchKernelGGL(k_nl_finish, dim3(1), dim3(1), 0, c->stream, in, len, tile_base, tile_cnt, n_tiles, ls, c->ctl);
-  const uint64_t n_lines = read_dev(c, &c->ctl->n_lines);
-  R->n_lines = (int64_t)n_lines;
-  phase(c, "lines");
-
-  // ---- classify (K2) + per-line touch/edge offsets
-  auto* kind = dget<uint8_t>(c, S_KIND, n_lines);
-  auto* pack = dget<uint64_t>(c, S_PACK, n_lines);
-  auto* pack_scan = dget<uint64_t>(c, S_PACK_SCAN, n_lines);
-  if (n_lines) {
-    const uint64_t nb = grid_for(n_lines);
-    auto* blk = dget<unsigned long long>(c, S_BLK, 4 * nb);
-    BlockCounts bc{blk, blk + nb, blk + 2 * nb, blk + 3 * nb};
-    hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(kTPB), 0, c->stream, in, ls, n_lines, tps, tpe, kind,
-                       pack, bc);
-    hipLaunchKernelGGL(k_reduce_blocks, dim3(1), dim3(1024), 0, c->stream, bc, nb, c->ctl);
-    excl_scan<uint64_t>(c, pack, pack_scan, n_lines);
-  }
-  sync_ctl(c);
-  const uint64_t n_e = c->h_ctl->n_edges, n_s = c->h_ctl->n_s;
+  const uint64_t n_lines = tot.lines;
+  const uint64_t n_e = tot.edges, n_s = tot.segs;
   const uint64_t n_t = n_s * tps + n_e * tpe;
+  R->n_lines = (int64_t)n_lines;
   R->n_edges = (int64_t)n_e;
-  R->n_records = (int64_t)c->h_ctl->n_records;
+  R->n_records = (int64_t)tot.recs;
   if (n_t >= 0xFFFFFFFFull || n_e >= 0xFFFFFFFFull)
     throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 node touches in one build");
-  phase(c, "classify");
+  phase(c, "tiles");
 
-  // ---- parse (K3)
+  // ---- K2: parse every line from its tile's LDS window
+  auto* ls = dget<uint64_t>(c, S_LS, n_lines + 1);
+  auto* kind = dget<uint8_t>(c, S_KIND, n_lines);
   ParseOpts op{};
   op.bidir = bidir;
   op.keep = keep;
@@ -367,17 +354,24 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
              bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr,
              dget<uint8_t>(c, S_TKIND, n_t)};
   EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
-  auto* wl = dget<uint64_t>(c, S_WL, n_e);
+  auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
+  auto* deferred = dget<DeferredLine>(c, S_DEFER, n_lines);
+  G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   phase(c, "_prep");
-  if (n_lines)
-    hipLaunchKernelGGL(k_parse, dim3(grid_for(n_lines)), dim3(kTPB), 0, c->stream, in, ls, kind, pack_scan, n_lines,
-                       op, T, E, c->ctl, wl);
+  if (n_tiles)
+    hipLaunchKernelGGL(k_tile_parse, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe, op,
+                       ls, kind, T, E, c->ctl, wl, deferred);
+  sync_ctl(c);
+  const uint64_t n_def = c->h_ctl->n_deferred;
+  if (n_def)
+    hipLaunchKernelGGL(k_parse_deferred, dim3(grid_for(n_def, 64)), dim3(64), 0, c->stream, in, len, ls, kind,
+                       deferred, n_def, op, T, E, c->ctl, wl);
   phase(c, "parse");
   sync_ctl(c);
   const uint64_t n_work = c->h_ctl->wl_count;
   if (n_work) {
-    hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, ls, pack_scan, wl,
-                       n_work, op, E, c->ctl);
+    hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, len, ls, wl, n_work, op, E,
+                       c->ctl);
     sync_ctl(c);
     phase(c, "weights_slow");
   }
@@ -405,7 +399,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     R->status = err_code;
     R->err_line = (int64_t)err_line;
     if (err_code == G2N_E_UNICODE && err_line != warn_line) {
-      hipLaunchKernelGGL(k_error_detail, dim3(1), dim3(1), 0, c->stream, in, ls, err_line, c->ctl);
+      hipLaunchKernelGGL(k_error_detail, dim3(1), dim3(1), 0, c->stream, in, len, ls, err_line, c->ctl);
       sync_ctl(c);
     }
     if (err_code == G2N_E_UNICODE) {

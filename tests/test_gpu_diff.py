@@ -289,3 +289,31 @@ def test_long_runs_of_empty_rows(gpu, oracle_lib):
         C = convert_format(A, fmt)
         assert C.indptr.tobytes() == ref.indptr.tobytes() and C.indices.tobytes() == ref.indices.tobytes()
         assert C.data.tobytes() == ref.data.tobytes()
+
+
+def test_field_boundaries_near_mask_span_and_tiles(gpu, oracle_lib):
+    """Lines of 40-90 bytes (the field masks cover 64), names ending near byte 64, and S lines
+    long enough to cross a 32 KiB tile and its halo: the LDS front end must match the oracle."""
+    import random
+
+    r = random.Random(9)
+    names = []
+    lines = []
+    for k in range(400):
+        n = f"n{k}_" + "a" * r.randint(0, 70)
+        names.append(n)
+        seq = "ACGT" * r.choice([0, 1, 10, 3000, 9000])  # up to 36 KB: crosses tiles and halos
+        lines.append(f"S\t{n}\t{seq or '*'}\tLN:i:{len(seq)}\n")
+    for _ in range(3000):
+        a, b = r.choice(names), r.choice(names)
+        tags = "\t".join(f"X{q}:i:{r.randint(0, 9)}" for q in range(r.randint(0, 4)))
+        w = f"\tRC:i:{r.randint(-5, 50)}" if r.random() < 0.8 else ""
+        lines.append(f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t{r.randint(0, 99)}M{w}" +
+                     (f"\t{tags}" if tags else "") + "\n")
+    r.shuffle(lines)  # S lines after the links that name them: the general dictionary too
+    data = "".join(lines).encode()
+    for mode in MODES[:4]:
+        for wt in (None, "RC"):
+            a = outcome(gpu_run(data, mode, "float64", wt))
+            b = outcome(oracle_run(oracle_lib, data, mode, "float64", wt))
+            assert a == b, (mode, wt)
