@@ -37,45 +37,48 @@ __device__ inline uint32_t byte_match_mask(uint32_t w, uint32_t pat) {
 struct Src {
   const uint8_t* p;
   uint64_t o;
-  uint64_t lim;  // word(i) may read [i, i + 4) when i + 4 <= lim
+  uint64_t lim;  // word8_z(i) reads memory only below lim
   __device__ uint8_t operator[](uint64_t i) const { return p[i - o]; }
   __device__ const uint8_t* ptr(uint64_t i) const { return p + (i - o); }
   __device__ uint32_t word(uint64_t i) const { return *(const uint32_t*)(p + (i - o)); }  // i, o % 4 == 0
-  // 4 bytes at aligned i, zero past lim
-  __device__ uint32_t word_z(uint64_t i) const {
-    if (i + 4 <= lim) return word(i);
-    uint32_t w = 0;
-    for (uint32_t b = 0; b < 4; b++)
-      if (i + b < lim) w |= (uint32_t)(*this)[i + b] << (8 * b);
+  // 8 bytes at i (i, o % 8 == 0), zero past lim
+  __device__ uint64_t word8_z(uint64_t i) const {
+    if (i + 8 <= lim) return *(const uint64_t*)(p + (i - o));
+    uint64_t w = 0;
+    for (uint32_t b = 0; b < 8; b++)
+      if (i + b < lim) w |= (uint64_t)(*this)[i + b] << (8 * b);
     return w;
   }
 };
 
-__device__ inline uint32_t match_bits4(uint32_t w, uint32_t pat) {  // bit b: byte b of w == pat's byte
-  const uint32_t m = byte_match_mask(w, pat);
-  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+// bit b: byte b of w equals pat's byte (pat = byte * 0x0101010101010101)
+__device__ inline uint32_t match_bits8(uint64_t w, uint64_t pat) {
+  const uint64_t x = w ^ pat;
+  const uint64_t hi = ~(((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x | 0x7F7F7F7F7F7F7F7Full);
+  return (uint32_t)(((hi >> 7) * 0x0102040810204080ull) >> 56);  // movemask of the 8 top bits
 }
 
 constexpr uint32_t kMaskSpan = 64;  // bytes a delimiter mask covers
 
-// Bit q: byte s + q (q < min(n, 64)) is '\t' (or '\n' too, with_nl).  The words covering the span
-// are loaded independently (no dependent scan), then the bits are assembled in registers.
+// Bit q: byte s + q (q < min(n, 64)) is '\t' (or '\n' too, with_nl).  The 8-byte words covering
+// the span are loaded independently (no dependent scan), then the bits are assembled in registers.
 __device__ inline uint64_t delim_mask(const Src& in, uint64_t s, uint64_t n, bool with_nl) {
-  const uint64_t a = s & ~3ull;
+  const uint64_t a = s & ~7ull;
   const uint32_t sh = (uint32_t)(s - a);
   const uint64_t end = s + (n < kMaskSpan ? n : kMaskSpan);
-  unsigned __int128 m = 0;
+  uint64_t lo = 0, hi = 0;  // bits of bytes a .. a+63, a+64 .. a+71
 #pragma unroll
-  for (uint32_t j = 0; j < kMaskSpan / 4 + 1; j++) {
-    const uint64_t q = a + 4 * j;
+  for (uint32_t j = 0; j < kMaskSpan / 8 + 1; j++) {
+    const uint64_t q = a + 8 * j;
     if (q < end) {
-      const uint32_t w = in.word_z(q);
-      uint32_t b = match_bits4(w, 0x09090909u);
-      if (with_nl) b |= match_bits4(w, 0x0A0A0A0Au);
-      m |= (unsigned __int128)b << (4 * j);
+      const uint64_t w = in.word8_z(q);
+      uint64_t b = match_bits8(w, 0x0909090909090909ull);
+      if (with_nl) b |= match_bits8(w, 0x0A0A0A0A0A0A0A0Aull);
+      if (j < 8) lo |= b << (8 * j);
+      else hi = b;
     }
   }
-  uint64_t r = (uint64_t)(m >> sh);
+  uint64_t r = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
   const uint64_t len = end - s;
   if (len < 64) r &= (1ull << len) - 1;
   return r;
@@ -620,10 +623,12 @@ struct DeferredLine {
   uint32_t tb, eb;
 };
 
-// pass 2: line starts, kinds, touches, edges of every line starting in the tile.  The tile's
-// line starts are compacted into an LDS list (in windows of kTileLines), then lanes take
-// consecutive lines and parse them from the staged bytes.
-constexpr uint32_t kTileLines = 4096;
+// pass 2: line starts, kinds, touches, edges of every line starting in the tile.
+//  (1) one block scan over the 2048 chunks' start counts ranks every line start of the tile;
+//  (2) per window of kTileLines starts: the starts go to an LDS list, threads classify 8
+//      consecutive lines each and one block scan gives each line its S / edge line prefix;
+//  (3) lanes take consecutive lines and parse them from the staged bytes (no barriers).
+constexpr uint32_t kTileLines = 2048;
 
 __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__ in, uint64_t len,
                                                      const TileCnt* __restrict__ base, uint32_t tps, uint32_t tpe,
@@ -632,8 +637,10 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
                                                      uint64_t* __restrict__ worklist,
                                                      DeferredLine* __restrict__ deferred) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
-  __shared__ uint16_t starts[kTileLines];
-  __shared__ unsigned long long red[kTPB / 64];
+  __shared__ __attribute__((aligned(16))) uint16_t starts[kTileLines];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[kTileChunks];  // chunk ranks, then line prefixes
+  __shared__ uint8_t lkind[kTileLines];
+  __shared__ uint32_t red[kTPB / 64];
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
   stage_tile<kTileHalo>(in, len, t0, buf);
   const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
@@ -642,19 +649,51 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   const Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
   const TileCnt b = base[blockIdx.x];
   const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
+  // (1) start masks of this thread's chunks (kept), counts -> ranks
+  uint32_t stm[kChunkIters / 2];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunkIters; j++) {
+    const uint32_t c = j * kTPB + threadIdx.x;
+    uint32_t m, st;
+    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
+    if (j & 1) stm[j >> 1] |= st << 16;
+    else stm[j >> 1] = st;
+    pre[c] = __popc(st);
+  }
+  __syncthreads();
+  uint32_t n_starts;
+  {
+    uint4 v0 = *(const uint4*)(pre + 8 * threadIdx.x), v1 = *(const uint4*)(pre + 8 * threadIdx.x + 4);
+    uint32_t q[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) sum += q[k];
+    uint32_t ex;
+    n_starts = block_excl_scan_u32(sum, &ex, red);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t t = q[k];
+      q[k] = ex;
+      ex += t;
+    }
+    *(uint4*)(pre + 8 * threadIdx.x) = make_uint4(q[0], q[1], q[2], q[3]);
+    *(uint4*)(pre + 8 * threadIdx.x + 4) = make_uint4(q[4], q[5], q[6], q[7]);
+  }
+  __syncthreads();
+  uint32_t rank[kChunkIters];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = pre[j * kTPB + threadIdx.x];
   uint64_t t_run = b.touches, e_run = b.edges;
   unsigned long long unk = ~0ull;
-  for (uint32_t w0 = 0;; w0 += kTileLines) {
-    // compact the starts ranked [w0, w0 + kTileLines) into `starts`
-    uint32_t run = 0;
-#pragma unroll 1
+  for (uint32_t w0 = 0; w0 < n_starts; w0 += kTileLines) {
+    const uint32_t n_win = n_starts - w0 < kTileLines ? n_starts - w0 : kTileLines;
+    __syncthreads();  // `pre` (ranks, or the last window's prefixes) is no longer read
+    // (2) the window's starts, in order
+#pragma unroll
     for (uint32_t j = 0; j < kChunkIters; j++) {
+      uint32_t st = (stm[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+      uint32_t r = rank[j];
       const uint32_t c = j * kTPB + threadIdx.x;
-      uint32_t m, st;
-      chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
-      unsigned long long tot;
-      uint32_t r = run + (uint32_t)block_excl_scan_u64(__popc(st), &tot, red);
-      run += (uint32_t)tot;
       while (st) {
         const uint32_t o = 16 * c + __builtin_ctz(st);
         st &= st - 1;
@@ -663,43 +702,56 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       }
     }
     __syncthreads();
-    const uint32_t n_win = run - w0 < kTileLines ? run - w0 : kTileLines;
-    const bool last_win = w0 + n_win >= run;
-#pragma unroll 1
-    for (uint32_t k0 = 0; k0 < n_win; k0 += kTPB) {
-      const uint32_t j = k0 + threadIdx.x;
+    // kinds of 8 consecutive lines per thread; prefix counts of S and edge lines
+    uint32_t cs = 0, ce = 0;
+    uint8_t kk[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t j = 8 * threadIdx.x + q;
       uint8_t k = kSkip;
-      uint32_t o = 0;
       if (j < n_win) {
-        o = starts[j];
+        const uint32_t o = starts[j];
         k = kind_at(buf, o, t0 + o, len);
+        lkind[j] = k;
       }
-      const unsigned long long cnt = k == kS ? (unsigned long long)tps << 20
-                                    : k == kEdge ? ((unsigned long long)tpe << 20) | 1ull : 0ull;
-      unsigned long long tot;
-      const unsigned long long ex = block_excl_scan_u64(cnt, &tot, red);
-      if (j < n_win) {
-        const uint64_t i = idx0 + w0 + j;
-        const uint64_t p = t0 + o;
-        ls[i] = p;
-        kind[i] = k;
-        if (k == kUnknown) unk = i < unk ? i : unk;
-        if (k == kS || k == kEdge || k == kPO) {
-          const uint64_t tb = t_run + (ex >> 20), eb = e_run + (ex & 0xFFFFF);
-          // the line ends where the next one starts; the window's last line: search the staged bytes
-          const bool known = j + 1 < n_win;
-          const uint64_t bound = known ? t0 + starts[j + 1] : w1;
-          if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist)) {
-            const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
-            deferred[d] = DeferredLine{i, (uint32_t)tb, (uint32_t)eb};
-          }
+      kk[q] = k;
+      cs += k == kS;
+      ce += k == kEdge;
+    }
+    uint32_t ex;
+    const uint32_t tot = block_excl_scan_u32((cs << 16) | ce, &ex, red);
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t j = 8 * threadIdx.x + q;
+      if (j < n_win) pre[j] = ex;
+      ex += ((uint32_t)(kk[q] == kS) << 16) | (uint32_t)(kk[q] == kEdge);
+    }
+    __syncthreads();
+    // (3) parse: lane-parallel lines
+#pragma unroll 1
+    for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
+      const uint32_t o = starts[j];
+      const uint8_t k = lkind[j];
+      const uint64_t i = idx0 + w0 + j;
+      const uint64_t p = t0 + o;
+      ls[i] = p;
+      kind[i] = k;
+      if (k == kUnknown) unk = i < unk ? i : unk;
+      if (k == kS || k == kEdge || k == kPO) {
+        const uint32_t pr = pre[j];
+        const uint64_t tb = t_run + (uint64_t)(pr >> 16) * tps + (uint64_t)(pr & 0xFFFF) * tpe;
+        const uint64_t eb = e_run + (pr & 0xFFFF);
+        // the line ends where the next one starts; the window's last line: search the staged bytes
+        const bool known = j + 1 < n_win;
+        const uint64_t bound = known ? t0 + starts[j + 1] : w1;
+        if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist)) {
+          const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
+          deferred[d] = DeferredLine{i, (uint32_t)tb, (uint32_t)eb};
         }
       }
-      t_run += tot >> 20;
-      e_run += tot & 0xFFFFF;
     }
-    if (last_win) break;
-    __syncthreads();  // before the next window overwrites `starts`
+    t_run += (uint64_t)(tot >> 16) * tps + (uint64_t)(tot & 0xFFFF) * tpe;
+    e_run += tot & 0xFFFF;
   }
   unk = wave_reduce_min(unk);
   if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
