@@ -188,6 +188,11 @@ def main():
                      "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "per_unit": unit_desc,
                      "ms_per_launch": round(avg[dom], 3)},
     }
+    if dom in ("insert_claim", "insert_lookup"):
+        tps = 2 if mode.get("bidirected") else 1
+        tpe = 4 if (mode.get("bidirected") and not mode.get("keep_directed_bidir")) else 2
+        probes = n_s * tps if dom == "insert_claim" else n_edges * tpe
+        line["roofline"]["random_access"] = random_ceiling(probes, avg[dom])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
     if rank == 0:
@@ -202,10 +207,10 @@ def main():
         dist.destroy_process_group()
 
 
-KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
-    "parse": "g2n::k_parse",
-    "insert_claim": "g2n::k_insert_round<true>",
-    "insert_lookup": "g2n::k_insert_round<false>",
+KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build (S-first dictionary path)
+    "parse": "g2n::k_tile_parse",
+    "insert_claim": "g2n::k_insert_round<0>",
+    "insert_lookup": "g2n::k_insert_round<2>",
     "triplets": "g2n::k_triplets<double>",
 }
 
@@ -219,19 +224,37 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
     n_t = n_s * tps + n_edges * tpe
     d_o = 12 if bidir else 0  # orientation descriptor (u64 off + u32 len) per touch
     avg_key = names_bytes / max(n_nodes, 1)
-    if phase == "parse":  # every input byte, ls pair, kind, pack; per touch / edge descriptors out
+    if phase == "parse":  # every input byte once; line start + kind per line; descriptors per touch / edge
         per_t, per_e = 13 + d_o, 12
-        return (in_bytes + 17 * n_lines + per_t * n_t + per_e * n_edges,
-                f"B_in + 17 B/line + {per_t} B/touch + {per_e} B/edge")
+        return (in_bytes + 9 * n_lines + per_t * n_t + per_e * n_edges,
+                f"B_in + 9 B/line + {per_t} B/touch + {per_e} B/edge")
     if phase in ("insert_claim", "insert_lookup"):
         k = n_s * tps if phase == "insert_claim" else n_edges * tpe
-        per = 1 + 1 + 12 + d_o + avg_key + 32 + 4  # state r/w, descriptor, key bytes, 32-B entry, slot
+        per = 1 + 12 + d_o + avg_key + 32 + 4  # state, descriptor, key bytes, 32-B entry, slot / node id
         return (int(n_t * 1 + k * (per - 1)), f"1 B/touch + {per - 1:.1f} B per processed touch ({k} touches)")
     if phase == "triplets":
         k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
-        per = 4 + 8 + tpe * (4 + 8) + k_trip * (4 + 4 + w_dtype)  # tb, w, slot+entry per touch, COO out
+        per = 4 + 8 + tpe * 4 + k_trip * (4 + 4 + w_dtype)  # tb, w, node id per touch, COO out
         return n_edges * per, f"{per} B/edge"
     return in_bytes, "B_in"
+
+
+def random_ceiling(records: int, ms: float):
+    """The dictionary probe is one random 32-B record read per touch: its ceiling is the
+    MI355X's random-record rate, measured by tools/microbench/randread.hip on a 4 GiB table
+    (profiles/r01/randread_ceiling.jsonl), not the streaming HBM peak."""
+    p = ROOT / "profiles" / "r01" / "randread_ceiling.jsonl"
+    try:
+        rows = [json.loads(x) for x in p.read_text().splitlines() if x.strip()]
+    except (OSError, ValueError):
+        return None
+    rate = next((r["Grec_per_s"] for r in rows if r.get("shape") == "random 32B records" and r["table_GB"] > 1), None)
+    if not rate:
+        return None
+    floor_ms = records / (rate * 1e9) * 1e3
+    return {"records": records, "ceiling_Grec_per_s": rate, "floor_ms": round(floor_ms, 3),
+            "achieved_Grec_per_s": round(records / (ms / 1e3) / 1e9, 2), "frac": round(floor_ms / ms, 3),
+            "source": "profiles/r01/randread_ceiling.jsonl"}
 
 
 def measured_traffic(kernel: str):
