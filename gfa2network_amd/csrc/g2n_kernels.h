@@ -116,6 +116,10 @@ __global__ void k_insert_round(const uint8_t* in, uint64_t in_len, TouchIn T, ui
                                int bidir, Ctl* ctl, uint8_t* first, const uint32_t* nid, uint32_t n_first,
                                const uint32_t* inv, uint32_t* tid);
 __global__ void k_key_len(TouchIn T, uint64_t n, int bidir, uint32_t* klen);
+template <int kBatch>
+__global__ void k_lookup_fast(const uint8_t* in, uint64_t in_len, TouchIn T, uint64_t n_t, const DictEntry* table,
+                              uint64_t mask, uint64_t max_probes, const uint8_t* tstate, int bidir, Ctl* ctl,
+                              const uint32_t* nid, uint32_t n_first, const uint32_t* inv, uint32_t* tid);
 __global__ void k_assign_first(DictEntry* table, TouchIn T, uint64_t n_t, int bidir, const uint8_t* first,
                                const uint32_t* slot, const uint32_t* nid, uint32_t* inv, uint32_t* klen);
 __global__ void k_mark_first(const DictEntry* table, uint64_t cap, uint8_t* first);

@@ -1076,6 +1076,105 @@ __device__ inline uint32_t touch_key_len(const TouchIn& T, uint64_t t, int bidir
   return T.nlen[t] + (bidir ? 1 + T.olen[t] : 0);  // name [+ ":" + orientation]
 }
 
+// The S-first lookup round (kModeFast of k_insert_round) with kBatch touches per thread: each
+// stage's loads (touch descriptors, key bytes, first probed entry) are issued for the whole
+// batch before any is used, so a thread keeps kBatch dependent chains in flight instead of one.
+// Touches t = block base + k * kTPB + lane: every stage stays coalesced across the wave.
+template <int kBatch>
+__global__ void __launch_bounds__(kTPB) k_lookup_fast(const uint8_t* __restrict__ in, uint64_t in_len, TouchIn T,
+                                                      uint64_t n_t, const DictEntry* __restrict__ table,
+                                                      uint64_t mask, uint64_t max_probes,
+                                                      const uint8_t* __restrict__ tstate, int bidir, Ctl* ctl,
+                                                      const uint32_t* __restrict__ nid, uint32_t n_first,
+                                                      const uint32_t* __restrict__ inv, uint32_t* __restrict__ tid) {
+  const uint64_t base = (uint64_t)blockIdx.x * (kTPB * kBatch) + threadIdx.x;
+  bool act[kBatch];
+  uint64_t no[kBatch], oo[kBatch];
+  uint32_t nl[kBatch], ol[kBatch];
+#pragma unroll
+  for (int k = 0; k < kBatch; k++) {
+    const uint64_t t = base + (uint64_t)k * kTPB;
+    act[k] = t < n_t && tstate[t] != 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kBatch; k++) {
+    const uint64_t t = base + (uint64_t)k * kTPB;
+    if (act[k]) {
+      no[k] = T.noff[t];
+      nl[k] = T.nlen[t];
+      oo[k] = bidir ? T.ooff[t] : 0;
+      ol[k] = bidir ? T.olen[t] : 0;
+    }
+  }
+  KeyHead kh[kBatch];
+#pragma unroll
+  for (int k = 0; k < kBatch; k++)
+    if (act[k]) kh[k] = key_head(in, in_len, no[k], nl[k], oo[k], ol[k], bidir != 0);
+  uint64_t h[kBatch];
+  uint4 lo[kBatch], hi[kBatch];
+#pragma unroll
+  for (int k = 0; k < kBatch; k++) {
+    if (act[k]) {
+      h[k] = key_hash(in, kh[k], no[k], nl[k], oo[k]);
+      const DictEntry* e = table + (h[k] & mask);
+      lo[k] = ((const uint4*)e)[0];
+      hi[k] = ((const uint4*)e)[1];
+    }
+  }
+  bool general = false;
+#pragma unroll
+  for (int k = 0; k < kBatch; k++) {
+    if (!act[k]) continue;
+    const uint64_t t = base + (uint64_t)k * kTPB;
+    const uint32_t tag = (uint32_t)(h[k] >> 32);
+    const uint64_t k0 = (uint64_t)kh[k].k, k1 = (uint64_t)(kh[k].k >> 64);
+    uint64_t idx = h[k] & mask;
+    uint4 a = lo[k], b = hi[k];
+    bool done = false;
+    for (uint64_t probe = 0; probe < max_probes; probe++) {
+      if (probe) {
+        const DictEntry* e = table + idx;
+        a = ((const uint4*)e)[0];
+        b = ((const uint4*)e)[1];
+      }
+      const unsigned long long cur = ((unsigned long long)a.y << 32) | a.x;
+      const unsigned long long meta = ((unsigned long long)a.w << 32) | a.z;
+      const uint64_t e0 = ((uint64_t)b.y << 32) | b.x, e1 = ((uint64_t)b.w << 32) | b.z;
+      if (cur == kEmptySlot) {  // a key no S line defined: a new node
+        general = true;
+        done = true;
+        break;
+      }
+      if ((uint32_t)(cur >> 32) == tag) {
+        if ((meta >> 32) >= 2) {  // claimed after round 1: cannot happen on this path
+          general = true;
+          done = true;
+          break;
+        }
+        if ((uint32_t)meta == kh[k].len && e0 == k0 && e1 == k1 &&
+            (kh[k].len <= 16 || tail_eq(in, T, t, inv ? inv[(uint32_t)cur] : (uint32_t)cur, bidir != 0,
+                                        kh[k].len))) {
+          const uint32_t id = (uint32_t)cur;  // rank of the key's S touch among the firsts
+          if (id >= (nid ? nid[t] : n_first)) general = true;  // this touch precedes it
+          tid[t] = id;
+          done = true;
+          break;
+        }
+      }
+      idx = (idx + 1) & mask;
+    }
+    if (!done) ctl->table_overflow = 1;
+  }
+  if (__ballot(general) && (threadIdx.x & 63) == 0) ctl->dict_general = 1;
+}
+
+template __global__ void k_lookup_fast<2>(const uint8_t*, uint64_t, TouchIn, uint64_t, const DictEntry*, uint64_t,
+                                          uint64_t, const uint8_t*, int, Ctl*, const uint32_t*, uint32_t,
+                                          const uint32_t*, uint32_t*);
+template __global__ void k_lookup_fast<4>(const uint8_t*, uint64_t, TouchIn, uint64_t, const DictEntry*, uint64_t,
+                                          uint64_t, const uint8_t*, int, Ctl*, const uint32_t*, uint32_t,
+                                          const uint32_t*, uint32_t*);
+
 // S-prefix dictionary (every S touch precedes every edge touch, no S key repeated): the node id
 // of an S touch is its touch index; klen[id] for the names blob.
 __global__ void __launch_bounds__(kTPB) k_key_len(TouchIn T, uint64_t n, int bidir, uint32_t* __restrict__ klen) {

@@ -114,6 +114,11 @@ static void excl_scan(g2n_context* c, const T* in, T* out, uint64_t n) {
   G2N_HIP(rocprim::exclusive_scan(tmp, tb, in, out, T(0), (size_t)n, rocprim::plus<T>(), c->stream));
 }
 
+static int lookup_batch() {  // touches per thread in the S-first lookup (G2N_LOOKUP_BATCH=2|4)
+  const char* v = std::getenv("G2N_LOOKUP_BATCH");
+  return (v && v[0] == '4') ? 4 : 2;
+}
+
 static int bits_for(uint64_t n) {  // bits to hold values 0..n-1 (>= 1)
   int b = 1;
   while (b < 63 && (1ull << b) < n) b++;
@@ -462,9 +467,16 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     else if (mode == kModeLookup)
       hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
                          max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
-    else
-      hipLaunchKernelGGL(k_insert_round<kModeFast>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
+    else {
+      const int kb = lookup_batch();
+      const dim3 gb(grid_for(n_t, kTPB * kb));
+      if (kb == 4)
+        hipLaunchKernelGGL(k_lookup_fast<4>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
+                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+      else
+        hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
+                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+    }
     phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
     sync_ctl(c);
   };
