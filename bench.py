@@ -210,7 +210,7 @@ def main():
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build (S-first dictionary path)
     "parse": "g2n::k_tile_parse",
     "insert_claim": "g2n::k_insert_round<0>",
-    "insert_lookup": "g2n::k_insert_round<2>",
+    "insert_lookup": "g2n::k_lookup_fast<2>",
     "triplets": "g2n::k_triplets<double>",
 }
 

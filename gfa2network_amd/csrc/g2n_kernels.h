@@ -5,11 +5,11 @@
 //   tiles[len / 32 KiB]          per-tile counts (lines, touches, edges, ...) and their scan
 //   ls[n_lines + 1]   u64        line start offsets (ls[n_lines] = len)
 //   kind[n_lines]     u8         kSkip / kUnknown / kS / kEdge / kPO
-//   touches (n_t):   noff u64, nlen u32 [, ooff u64, olen u32 when bidirected], slot u32
+//   touches (n_t):   noff u64, nlen u32, tkind u8 [, ooff u64, olen u32 when bidirected]
 //   edges   (n_e):   w f64 (weight before the dtype cast), tb u32 (first touch)
-//   table[cap]        u64        (hash tag << 32 | first touch), cap = pow2 >= 2 n_t
-//   first u8, nid/tid u32 per touch; inv/klen u32 per node id; names blob + offsets
-//   rows/cols i32, data T per triplet; sort keys u64 + stream positions u32
+//   table[cap]        32-B DictEntry (see k_insert_round), cap = pow2 >= 1.5 x expected keys
+//   first u8, nid/tid/slot u32 per touch; inv/klen u32 per node id; names blob + offsets
+//   rows/cols i32, data T per triplet; row-bucket sort keys u32 + payloads; per-row SoA sums
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -6,12 +6,13 @@
 //   K2 tile_parse            split(b"\t") + _parse_link/_edge/... parser.py:133-361,
 //                            tag weight (fast grammar)            parser.py:179-204, builders.py:205-209
 //   K2b weights_slow         exact CPython int()/float() for the rest (pylit.h)
-//   K4 insert                node2idx dict (first-touch ids)      builders.py:190-198, 218-221
-//   K5 first/names           dict insertion order, node_list      builders.py:284-288
+//   K4 insert_round / lookup_fast   node2idx dict (first-touch ids)   builders.py:190-198, 218-221
+//   K5 names                 dict insertion order, node_list      builders.py:284-288
 //   K6 triplets              add_mat_edge + dtype cast            builders.py:222-234, 280-281
-//   K7-K9 (sort, group_sum, emulate_rows, maxsym)  coo.tocsr / A.maximum(A.T)
-//                            (scipy sparsetools coo_tocsr, csr_sort_indices,
-//                             csr_sum_duplicates, csr_maximum_csr)  builders.py:281-283, utils.py:55
+//   K7-K9 (row-bucket sort, row_bounds, row_sum, row_emulate, row_max, row_compact)
+//                            coo.tocsr / A.maximum(A.T) (scipy sparsetools coo_tocsr,
+//                            csr_sort_indices, csr_sum_duplicates, csr_maximum_csr)
+//                            builders.py:281-283, utils.py:55
 // Integer / byte work only; every kernel is HBM- or latency-bound (no MFMA).
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -4,7 +4,7 @@
 MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports
 exactly 1/2 of the bytes of a wide coalesced streaming read, so the prescribed figure is
 traffic = 2 x FETCH_SIZE + WRITE_SIZE.  We check that calibration on this pipeline's own
-pure-streaming kernel (k_nl_count reads the input once: FETCH_SIZE x 2 must equal the input
+pure-streaming kernel (k_tile_count reads the input once: FETCH_SIZE x 2 must equal the input
 size) and record it.  Kernels that mix streaming and random 32-64 B accesses are
 uncalibrated: the raw FETCH_SIZE (random 64-B requests counted once) is kept beside the
 corrected figure.
@@ -37,12 +37,12 @@ def main():
         fa, wa = sum(f) / len(f), sum(w) / len(w)
         kernels[k] = {"launches": len(f), "fetch_size_bytes_raw": round(fa), "write_size_bytes": round(wa),
                       "traffic_bytes_per_launch": round(2 * fa + wa)}
-    cal = kernels.get("g2n::k_nl_count", {})
+    cal = kernels.get("g2n::k_tile_count", {})
     doc = {
         "source": str(d),
         "correction": "traffic = 2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE = 1/2 of "
                       "wide streaming reads)",
-        "calibration": {"kernel": "g2n::k_nl_count (reads the input once, coalesced 16 B/lane)",
+        "calibration": {"kernel": "g2n::k_tile_count (reads the input once + a 16-B halo per 32 KiB tile, coalesced 16 B/lane)",
                         "input_bytes": in_bytes, "fetch_size_x2": 2 * cal.get("fetch_size_bytes_raw", 0),
                         "ratio": round(2 * cal.get("fetch_size_bytes_raw", 0) / max(in_bytes, 1), 4)},
         "kernels": kernels,
