@@ -27,7 +27,7 @@ E_ARG, E_IO, E_GZIP, E_DEVICE, E_NOMEM, E_UNSUPPORTED = 13, 14, 15, 16, 17, 18
 
 DTYPE_CODES = {"bool": 0, "int8": 1, "int32": 2, "float32": 3, "float64": 4}
 CODE_DTYPES = {v: np.dtype(k) for k, v in DTYPE_CODES.items()}
-OUT_PARSE, OUT_CSR = 0, 1
+OUT_PARSE, OUT_CSR, OUT_COO = 0, 1, 2
 FMT_COO, FMT_CSR = 0, 1
 
 # every symbol include/g2n.h declares (tests check the library exports all of them)
@@ -35,7 +35,7 @@ EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
-    "g2n_build_device",
+    "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
 ]
 
 
@@ -89,7 +89,7 @@ class Result(ctypes.Structure):
         ("n_cast_overflow", ctypes.c_int64),
         ("input_bytes", ctypes.c_uint64),
         ("n_phases", ctypes.c_int32),
-        ("pad_", ctypes.c_int32),
+        ("sum_t_sorted", ctypes.c_int32),
         ("phase_ms", ctypes.c_double * MAX_PHASES),
         ("phase_names", ctypes.c_char_p * MAX_PHASES),
         ("host_ms_read", ctypes.c_double),
@@ -149,6 +149,14 @@ def load() -> ctypes.CDLL:
     lib.g2n_build_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(Options), ctypes.POINTER(Result)]
     lib.g2n_build_device.restype = ctypes.c_int
+    P, U64, I32, U32, I64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64
+    lib.g2n_partition_keys.argtypes = [P, P, U64, P, U64, U32, P, P, P, P]
+    lib.g2n_dedup_keys.argtypes = [P, P, U64, P, U64, P, P, ctypes.POINTER(U64)]
+    lib.g2n_route_triplets.argtypes = [P, P, P, P, U64, I32, P, U64, U32, I32, P, P, P, P]
+    lib.g2n_csr_from_coo_pair.argtypes = [P, P, P, P, U64, P, P, P, U64, I32, I64, U64, U64, I32, I32, I32,
+                                          ctypes.POINTER(Result)]
+    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair"):
+        getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:
         raise NativeUnavailable("libg2n.so ABI version mismatch; rebuild it")
     _lib = lib

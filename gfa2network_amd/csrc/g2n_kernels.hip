@@ -1438,12 +1438,12 @@ __device__ inline double sum_copies<double>(double one, uint64_t k) {  // one ==
 template <class T, bool kUniform>
 __global__ void __launch_bounds__(kTPB) k_pack(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
                                                const T* __restrict__ data, uint64_t n, int transposed,
-                                               uint32_t* __restrict__ key, PV<T>* __restrict__ pv,
+                                               int64_t base, uint32_t* __restrict__ key, PV<T>* __restrict__ pv,
                                                uint32_t* __restrict__ pc) {
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n) return;
   const uint32_t r = (uint32_t)rows[i], c = (uint32_t)cols[i];
-  key[i] = transposed ? c : r;
+  key[i] = (uint32_t)((int64_t)(transposed ? c : r) - base);  // row within the slice
   if (kUniform) {
     pc[i] = transposed ? r : c;
   } else {
@@ -2006,6 +2006,96 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
   }
 }
 
+// ====================================================== sharded build helpers ======
+// keys of a blob as S-kind touches (g2n_dedup_keys)
+__global__ void __launch_bounds__(kTPB) k_keys_to_touches(const int64_t* __restrict__ offs, uint64_t n,
+                                                          uint64_t* __restrict__ noff, uint32_t* __restrict__ nlen,
+                                                          uint8_t* __restrict__ tkind) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t >= n) return;
+  noff[t] = (uint64_t)offs[t];
+  nlen[t] = (uint32_t)(offs[t + 1] - offs[t]);
+  tkind[t] = 1;
+}
+
+// node id of every touch, whichever dictionary path ran: the claimers and (general path) every
+// touch through its table slot, the other touches of the S-first paths through tid
+__global__ void __launch_bounds__(kTPB) k_touch_ids(uint64_t n, const uint8_t* __restrict__ first,
+                                                    const uint32_t* __restrict__ slot,
+                                                    const DictEntry* __restrict__ table,
+                                                    const uint32_t* __restrict__ tid, int general,
+                                                    uint32_t* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t >= n) return;
+  out[t] = (general || first[t]) ? (uint32_t)table[slot[t]].hdr : tid[t];
+}
+
+__global__ void __launch_bounds__(kTPB) k_first_of(uint64_t n_nodes, const uint32_t* __restrict__ inv,
+                                                   uint32_t* __restrict__ out) {
+  const uint64_t d = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (d < n_nodes) out[d] = inv ? inv[d] : (uint32_t)d;
+}
+
+// owner rank of a key: FNV-1a of its bytes mod n_ranks (any fixed function of the bytes works:
+// equal keys must meet on one rank)
+__global__ void __launch_bounds__(kTPB) k_key_owner(const uint8_t* __restrict__ blob,
+                                                    const int64_t* __restrict__ offs, uint64_t n, uint32_t n_ranks,
+                                                    uint32_t* __restrict__ owner, uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (int64_t p = offs[i]; p < offs[i + 1]; p++) h = (h ^ blob[p]) * 0x100000001b3ull;
+  owner[i] = (uint32_t)(fmix64(h) % n_ranks);
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(kTPB) k_key_lens(const int64_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ perm, uint64_t n,
+                                                   int64_t* __restrict__ lens) {
+  const uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (j < n) lens[j] = offs[perm[j] + 1] - offs[perm[j]];
+}
+
+__global__ void __launch_bounds__(kTPB) k_copy_keys(const uint8_t* __restrict__ blob, const int64_t* __restrict__ offs,
+                                                    const uint32_t* __restrict__ perm, uint64_t n,
+                                                    const int64_t* __restrict__ ooffs, uint8_t* __restrict__ oblob) {
+  const uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (j >= n) return;
+  const int64_t s = offs[perm[j]], l = offs[perm[j] + 1] - s, o = ooffs[j];
+  for (int64_t b = 0; b < l; b++) oblob[o + b] = blob[s + b];
+}
+
+// owner rank of each triplet's (remapped) row; the sort payload is the triplet index
+__global__ void __launch_bounds__(kTPB) k_route_keys(const int32_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ cols, uint64_t n,
+                                                     const uint32_t* __restrict__ map, uint64_t n_global,
+                                                     uint32_t n_ranks, int transposed, uint32_t* __restrict__ owner,
+                                                     uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t key = map[transposed ? cols[i] : rows[i]];
+  owner[i] = (uint32_t)(key * n_ranks / n_global);
+  idx[i] = (uint32_t)i;
+}
+
+template <int kW>  // element size of data
+__global__ void __launch_bounds__(kTPB) k_route_gather(const int32_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ cols,
+                                                       const uint8_t* __restrict__ data,
+                                                       const uint32_t* __restrict__ perm, uint64_t n,
+                                                       const uint32_t* __restrict__ map, int transposed,
+                                                       int32_t* __restrict__ orows, int32_t* __restrict__ ocols,
+                                                       uint8_t* __restrict__ odata) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = perm[i];
+  const int32_t r = (int32_t)map[rows[j]], c = (int32_t)map[cols[j]];
+  orows[i] = transposed ? c : r;
+  ocols[i] = transposed ? r : c;
+#pragma unroll
+  for (int b = 0; b < kW; b++) odata[i * kW + b] = data[(uint64_t)j * kW + b];
+}
+
 __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, uint64_t n,
                              unsigned long long* out) {
   *out = n ? (unsigned long long)off[n - 1] + cnt[n - 1] : 0ull;
@@ -2013,8 +2103,8 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
 
 // ----------------------------------------------------------- explicit instances --
 #define G2N_INST_U(T, U)                                                                                         \
-  template __global__ void k_pack<T, U>(const int32_t*, const int32_t*, const T*, uint64_t, int, uint32_t*, PV<T>*, \
-                                        uint32_t*);                                                              \
+  template __global__ void k_pack<T, U>(const int32_t*, const int32_t*, const T*, uint64_t, int, int64_t, uint32_t*, \
+                                        PV<T>*, uint32_t*);                                                      \
   template __global__ void k_row_sum<T, U>(const uint32_t*, uint64_t, const PV<T>*, const uint32_t*, uint32_t*,   \
                                            RowVal<T, U>::type*, void*, void*, uint32_t*, uint8_t*, Ctl*, int);   \
   template __global__ void k_row_compact<T, U>(const uint32_t*, const uint32_t*, const uint32_t*, uint64_t,      \

@@ -34,7 +34,7 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_NSLOTS
+  S_INV, S_DEFER, S_FOFF64, S_NSLOTS
 };
 
 struct DevBuf {
@@ -141,7 +141,7 @@ struct RowSide {  // one orientation's per-row sums: row r's unique entries at [
   uint32_t* ucnt;
   uint32_t* ocol;
   V* oval;
-  bool unsorted, flagged;
+  bool unsorted, flagged, local_unsorted;
 };
 
 // Stable LSD radix sort of (u32 key < 2^bits, V) pairs.  Onesweep with 9-bit digits whenever that
@@ -172,10 +172,14 @@ static void sort_pairs_u32(g2n_context* c, const uint32_t* kin, uint32_t* kout, 
 }
 
 // coo.tocsr() of one orientation (transposed: of A.T), up to the per-row sorted unique entries.
+// side: which set of per-row buffers (0: A, 1: A.T); transposed: key on the column;
+// base: first row of the slice; force_unsorted: -1 = this matrix decides scipy's global
+// has_sorted_indices, else the caller's verdict (sharded builds: the OR over all slices).
 template <class T, bool kU>
 static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n,
-                               uint64_t n_rows, int transposed) {
-  const int w = transposed;
+                               uint64_t n_rows, int side, int transposed, int64_t base = 0,
+                               int force_unsorted = -1) {
+  const int w = side;
   using V = typename RowVal<T, kU>::type;
   RowSide<T, kU> S{};
   auto* key_in = dget<uint32_t>(c, S_KEYS0, n);
@@ -194,16 +198,16 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
     if (kU) {
       auto* pc_in = dget<uint32_t>(c, S_VALS0, n);
       pc_out = dget<uint32_t>(c, S_VALS1, n);
-      hipLaunchKernelGGL((k_pack<T, true>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n, w,
-                         key_in, (PV<T>*)nullptr, pc_in);
+      hipLaunchKernelGGL((k_pack<T, true>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n,
+                         transposed, base, key_in, (PV<T>*)nullptr, pc_in);
       sort_pairs_u32<uint32_t>(c, key_in, key_out, pc_in, pc_out, n, bits);
       scr_a = key_in;
       scr_b = pc_in;
     } else {
       auto* pv_in = dget<PV<T>>(c, S_VALS0, n);
       pv_out = dget<PV<T>>(c, S_VALS1, n);
-      hipLaunchKernelGGL((k_pack<T, false>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n, w,
-                         key_in, pv_in, (uint32_t*)nullptr);
+      hipLaunchKernelGGL((k_pack<T, false>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n,
+                         transposed, base, key_in, pv_in, (uint32_t*)nullptr);
       sort_pairs_u32<PV<T>>(c, key_in, key_out, pv_in, pv_out, n, bits);
       scr_a = pv_in;
       scr_b = dget<PV<T>>(c, S_RSCR, n);
@@ -218,7 +222,8 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
     hipLaunchKernelGGL((k_row_sum<T, kU>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, S.start, n_rows, pv_out,
                        pc_out, S.ocol, S.oval, scr_a, scr_b, S.ucnt, rowflag, c->ctl, w);
   sync_ctl(c);
-  S.unsorted = c->h_ctl->unsorted[w] != 0;
+  S.local_unsorted = c->h_ctl->unsorted[w] != 0;
+  S.unsorted = force_unsorted >= 0 ? force_unsorted != 0 : S.local_unsorted;
   S.flagged = c->h_ctl->flagged[w] != 0;
   if constexpr (!kU) {
     if (n && S.unsorted && S.flagged) {  // scipy std::sort-ed these rows: redo them exactly
@@ -235,7 +240,7 @@ template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   const T one = (T)1;
-  RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0);
+  RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0);
   R->sum_sorted = A.unsorted ? 0 : 1;
   phase(c, "sum");
   auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
@@ -259,12 +264,68 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
     return;
   }
   // A.maximum(A.T): B = SUM(A) above, BT = SUM(A.T) with A.T's own scatter order
-  RowSide<T, kU> B = row_sums<T, kU>(c, rows, cols, data, n_trip, n_cols, 1);
+  RowSide<T, kU> B = row_sums<T, kU>(c, rows, cols, data, n_trip, n_cols, 1, 1);
   phase(c, "sum_t");
   auto* mcnt = dget<uint32_t>(c, S_MCNT, n_rows);
   auto* moff = dget<uint32_t>(c, S_MOFF, n_rows);
   auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_trip);
   T* odata = dget<T>(c, S_ODATA, 2 * n_trip);
+  if (n_rows) {
+    hipLaunchKernelGGL((k_row_max<T, kU, false>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                       A.ocol, A.oval, B.start, B.ucnt, B.ocol, B.oval, one, n_rows, mcnt, (const uint32_t*)nullptr,
+                       (int32_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
+    excl_scan<uint32_t>(c, mcnt, moff, n_rows);
+    hipLaunchKernelGGL((k_row_max<T, kU, true>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                       A.ocol, A.oval, B.start, B.ucnt, B.ocol, B.oval, one, n_rows, mcnt, moff, indptr, indices,
+                       odata);
+    hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, mcnt, moff, n_rows, &c->ctl->n_keep);
+  }
+  R->nnz = n_rows ? (int64_t)read_dev(c, &c->ctl->n_keep) : 0;
+  R->indices = indices;
+  R->data = odata;
+  phase(c, "maxsym");
+}
+
+// The CSR row slice [base, base + n_rows) of a sharded build from its routed triplet streams:
+// A's triplets with rows in the slice and (MAX-SYM) A.T's, i.e. (col, row, value) of A's
+// triplets whose column is in the slice; both in global stream order.
+template <class T, bool kU>
+static void assemble_pair_t(g2n_context* c, const int32_t* ar, const int32_t* ac, const T* ad, uint64_t an,
+                            const int32_t* tr, const int32_t* tc, const T* td, uint64_t tn, bool maxsym, int64_t base,
+                            uint64_t n_rows, int force_unsorted, g2n_result* R) {
+  const T one = (T)1;
+  RowSide<T, kU> A = row_sums<T, kU>(c, ar, ac, ad, an, n_rows, 0, 0, base,
+                                     force_unsorted < 0 ? -1 : (force_unsorted & 1));
+  R->sum_sorted = A.local_unsorted ? 0 : 1;
+  phase(c, "sum");
+  auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
+  if (n_rows == 0) G2N_HIP(hipMemsetAsync(indptr, 0, sizeof(int32_t), c->stream));
+  R->format = G2N_FMT_CSR;
+  R->indptr = indptr;
+  if (!maxsym) {
+    auto* uoff = dget<uint32_t>(c, S_UOFF, n_rows);
+    excl_scan<uint32_t>(c, A.ucnt, uoff, n_rows);
+    auto* indices = dget<int32_t>(c, S_INDICES, an);
+    T* odata = dget<T>(c, S_ODATA, an);
+    if (n_rows) {
+      hipLaunchKernelGGL((k_row_compact<T, kU>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
+                         uoff, n_rows, A.ocol, A.oval, one, indptr, indices, odata);
+      hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, A.ucnt, uoff, n_rows, &c->ctl->n_keep);
+    }
+    R->nnz = n_rows ? (int64_t)read_dev(c, &c->ctl->n_keep) : 0;
+    R->indices = indices;
+    R->data = odata;
+    phase(c, "csr");
+    return;
+  }
+  RowSide<T, kU> B = row_sums<T, kU>(c, tr, tc, td, tn, n_rows, 1, 0, base,
+                                     force_unsorted < 0 ? -1 : ((force_unsorted >> 1) & 1));
+  R->sum_t_sorted = B.local_unsorted ? 0 : 1;
+  phase(c, "sum_t");
+  auto* mcnt = dget<uint32_t>(c, S_MCNT, n_rows);
+  auto* moff = dget<uint32_t>(c, S_MOFF, n_rows);
+  auto* indices = dget<int32_t>(c, S_INDICES, an + tn);
+  T* odata = dget<T>(c, S_ODATA, an + tn);
   if (n_rows) {
     hipLaunchKernelGGL((k_row_max<T, kU, false>), dim3(grid_for(n_rows)), dim3(kTPB), 0, c->stream, A.start, A.ucnt,
                        A.ocol, A.oval, B.start, B.ucnt, B.ocol, B.oval, one, n_rows, mcnt, (const uint32_t*)nullptr,
@@ -317,6 +378,155 @@ static void finish_timings(g2n_context* c, g2n_result* R) {
 }
 
 // The pipeline.  R's pointers are device pointers into the context's arena.
+// ---- dictionary (K4): first-touch node ids of the n_t touches (the first n_st are the S-line
+// touches of the claim round).  est: expected distinct keys (sizes the first table).
+struct DictOut {
+  DictEntry* table;
+  uint32_t* slot;
+  uint32_t* tid;        // node id per touch (S-first paths; claimers excluded), else null
+  const uint32_t* inv;  // node id -> touch with its key bytes (null: the identity)
+  uint32_t* klen;       // node id -> key length
+  uint8_t* first;       // first-touch flags
+  bool general;         // ids came from the general insert rounds (every touch has a slot)
+  uint64_t n_nodes;
+};
+
+static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len, const TouchOut& T, uint64_t n_t,
+                                uint64_t n_st, uint64_t est, bool bidir) {
+  TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
+  // Table sized for the expected number of distinct keys; a bounded probe sequence flags
+  // overflow and the insert is redone with a table sized for every touch (load <= 1/2,
+  // unbounded probes).
+  uint64_t full_cap = 1024;
+  while (full_cap < 2 * n_t) full_cap <<= 1;
+  uint64_t cap = 1024;
+  while (cap < est + est / 2) cap <<= 1;
+  if (cap > full_cap) cap = full_cap;
+  auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
+  auto* first = dget<uint8_t>(c, S_FIRST, n_t);
+  auto* nid = dget<uint32_t>(c, S_NID, n_t);
+  auto* inv = dget<uint32_t>(c, S_INV, n_t);    // node id -> touch holding its key bytes
+  auto* klen = dget<uint32_t>(c, S_FLEN, n_t);  // node id -> key length
+  DictEntry* table = nullptr;
+  uint32_t* tid = nullptr;  // node id per touch when the S-first fast path holds
+  auto* tstate = dget<uint8_t>(c, S_TSTATE, n_t);
+  const uint32_t* nid_in = nid;  // fast lookup: firsts before each touch (null: n_first for every touch)
+  const uint32_t* inv_in = inv;
+  uint32_t n_first = 0;
+  auto insert = [&](int mode, uint32_t round, uint64_t max_probes, uint32_t* tid_out) {
+    G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
+    phase(c, "_prep");
+    const dim3 g(grid_for(n_t)), b(kTPB);
+    if (mode == kModeClaim)
+      hipLaunchKernelGGL(k_insert_round<kModeClaim>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
+    else if (mode == kModeLookup)
+      hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
+    else {
+      const int kb = lookup_batch();
+      const dim3 gb(grid_for(n_t, kTPB * kb));
+      if (kb == 4)
+        hipLaunchKernelGGL(k_lookup_fast<4>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
+                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+      else
+        hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
+                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+    }
+    phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
+    sync_ctl(c);
+  };
+  auto init_table = [&]() {
+    table = dget<DictEntry>(c, S_TABLE, cap);
+    G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
+    G2N_HIP(hipMemcpyAsync(tstate, T.tkind, n_t, hipMemcpyDeviceToDevice, c->stream));
+    phase(c, "table_init");
+  };
+  auto rank_firsts = [&]() {  // nid[t] = first touches before t; n_nodes
+    size_t tb = 0;
+    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
+                                    c->stream));
+    void* tmp = dbuf(c, S_TEMP, tb);
+    G2N_HIP(rocprim::exclusive_scan(tmp, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
+                                    c->stream));
+    hipLaunchKernelGGL(k_node_count, dim3(1), dim3(1), 0, c->stream, first, nid, n_t, c->ctl);
+  };
+  if (n_t) {
+    // S-first fast path (a GFA whose S lines define every key before any other line uses it):
+    // round 1 claims the S keys, their ranks are the node ids, one lookup round resolves every
+    // other touch to its id.  Anything else is redone by the general rounds below.
+    bool fast = !std::getenv("G2N_DICT_GENERAL");
+    if (fast) {
+      init_table();
+      n_first = (uint32_t)n_st;  // claim round: flags S touches past the first n_st
+      insert(kModeClaim, 1, cap >= full_cap ? cap : 4096, nullptr);
+      fast = !c->h_ctl->table_overflow;
+    }
+    bool sprefix = false;  // ids are touch indices: no ranking pass
+    if (fast) {
+      sprefix = c->h_ctl->deferred == 0 && !c->h_ctl->s_late;
+      if (sprefix) {
+        nid_in = nullptr;
+        inv_in = nullptr;
+        n_first = (uint32_t)n_st;
+        hipLaunchKernelGGL(k_key_len, dim3(grid_for(n_st)), dim3(kTPB), 0, c->stream, TI, n_st, (int)bidir, klen);
+        c->h_ctl->n_nodes = n_st;
+        G2N_HIP(hipMemcpyAsync(&c->ctl->n_nodes, &c->h_ctl->n_nodes, sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, c->stream));
+      } else {
+        rank_firsts();
+        hipLaunchKernelGGL(k_assign_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, table, TI, n_t,
+                           (int)bidir, first, slot, nid, inv, klen);
+      }
+      phase(c, "ids_fast");
+      tid = dget<uint32_t>(c, S_TID, n_t);
+      insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
+      fast = !c->h_ctl->dict_general && !c->h_ctl->table_overflow && c->h_ctl->deferred == 0;
+      if (!fast) {
+        tid = nullptr;
+        sprefix = false;
+        nid_in = nid;
+        inv_in = inv;
+        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
+      }
+    }
+    if (!fast) {
+      while (true) {
+        init_table();
+        const uint64_t max_probes = cap >= full_cap ? cap : 4096;
+        bool overflow = false;
+        for (uint32_t round = 1;; round++) {  // round 1: S touches; then every unresolved touch
+          insert(round == 1 ? kModeClaim : kModeLookup, round, max_probes, nullptr);
+          if (c->h_ctl->table_overflow) { overflow = true; break; }
+          if (round > 1 && c->h_ctl->deferred == 0) break;
+          if (round > 100000) throw Failure(G2N_E_DEVICE, "dictionary insert did not converge");
+        }
+        if (!overflow) break;
+        if (cap >= full_cap) throw Failure(G2N_E_DEVICE, "node table overflow");
+        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
+        cap = full_cap;
+      }
+      G2N_HIP(hipMemsetAsync(first, 0, n_t, c->stream));
+      hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, first);
+      rank_firsts();
+      hipLaunchKernelGGL(k_assign_ids, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, nid, inv, klen);
+      phase(c, "ids_general");
+    }
+  }
+  sync_ctl(c);
+  if (c->h_ctl->table_overflow) throw Failure(G2N_E_DEVICE, "node table overflow");
+  DictOut D{};
+  D.table = table;
+  D.slot = slot;
+  D.tid = tid;
+  D.inv = inv_in;
+  D.klen = klen;
+  D.first = first;
+  D.general = n_t && tid == nullptr;
+  D.n_nodes = n_t ? c->h_ctl->n_nodes : 0;
+  return D;
+}
+
 static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   R->input_bytes = len;
@@ -402,7 +612,10 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   uint64_t err_key = c->h_ctl->err_key;
   uint64_t err_line = err_key == ~0ull ? ~0ull : (err_key >> 5);
   int err_code = err_key == ~0ull ? 0 : (int)(err_key & 31);
-  const uint64_t warn_line = c->h_ctl->warn_line;
+  // options.reserved[0] != 0: an earlier shard of a sharded build already met an unsupported
+  // record, so later ones are skipped silently (parser.py:125-131 warns once per parser)
+  const uint64_t warn_line = o->reserved[0] ? ~0ull : c->h_ctl->warn_line;
+  if (warn_line != ~0ull) R->warn_line = (int64_t)warn_line;  // first unsupported line, warned or not
   if (warn_line != ~0ull && warn_line < err_line) {
     uint64_t off = read_dev(c, ls + warn_line);
     uint8_t b = read_dev(c, in + off);
@@ -435,132 +648,10 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   }
   R->n_records_before_error = R->n_records;
 
-  // ---- dictionary: first-touch node ids (K4, K5)
-  // Table sized for the expected number of distinct keys (S names + a fraction of the edge
-  // touches); a bounded probe sequence flags overflow and the insert is redone with a table
-  // sized for every touch (load <= 1/2, unbounded probes).
-  const uint64_t est = n_s * tps + (n_e * tpe) / 16 + 1024;
-  uint64_t full_cap = 1024;
-  while (full_cap < 2 * n_t) full_cap <<= 1;
-  uint64_t cap = 1024;
-  while (cap < est + est / 2) cap <<= 1;
-  if (cap > full_cap) cap = full_cap;
-  auto* slot = dget<uint32_t>(c, S_SLOT, n_t);
-  auto* first = dget<uint8_t>(c, S_FIRST, n_t);
-  auto* nid = dget<uint32_t>(c, S_NID, n_t);
-  auto* inv = dget<uint32_t>(c, S_INV, n_t);    // node id -> touch holding its key bytes
-  auto* klen = dget<uint32_t>(c, S_FLEN, n_t);  // node id -> key length
+  // ---- dictionary: first-touch node ids (K4)
+  const DictOut D = build_dictionary(c, in, len, T, n_t, n_s * tps, n_s * tps + (n_e * tpe) / 16 + 1024, bidir);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
-  DictEntry* table = nullptr;
-  uint32_t* tid = nullptr;  // node id per touch when the S-first fast path holds
-  auto* tstate = dget<uint8_t>(c, S_TSTATE, n_t);
-  const uint32_t* nid_in = nid;  // fast lookup: firsts before each touch (null: n_first for every touch)
-  const uint32_t* inv_in = inv;
-  uint32_t n_first = 0;
-  auto insert = [&](int mode, uint32_t round, uint64_t max_probes, uint32_t* tid_out) {
-    G2N_HIP(hipMemsetAsync(&c->ctl->deferred, 0, sizeof(unsigned long long), c->stream));
-    phase(c, "_prep");
-    const dim3 g(grid_for(n_t)), b(kTPB);
-    if (mode == kModeClaim)
-      hipLaunchKernelGGL(k_insert_round<kModeClaim>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
-    else if (mode == kModeLookup)
-      hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
-                         max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
-    else {
-      const int kb = lookup_batch();
-      const dim3 gb(grid_for(n_t, kTPB * kb));
-      if (kb == 4)
-        hipLaunchKernelGGL(k_lookup_fast<4>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
-                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
-      else
-        hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
-                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
-    }
-    phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
-    sync_ctl(c);
-  };
-  auto init_table = [&]() {
-    table = dget<DictEntry>(c, S_TABLE, cap);
-    G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
-    G2N_HIP(hipMemcpyAsync(tstate, T.tkind, n_t, hipMemcpyDeviceToDevice, c->stream));
-    phase(c, "table_init");
-  };
-  auto rank_firsts = [&]() {  // nid[t] = first touches before t; n_nodes
-    size_t tb = 0;
-    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
-                                    c->stream));
-    void* tmp = dbuf(c, S_TEMP, tb);
-    G2N_HIP(rocprim::exclusive_scan(tmp, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
-                                    c->stream));
-    hipLaunchKernelGGL(k_node_count, dim3(1), dim3(1), 0, c->stream, first, nid, n_t, c->ctl);
-  };
-  if (n_t) {
-    // S-first fast path (a GFA whose S lines define every key before any other line uses it):
-    // round 1 claims the S keys, their ranks are the node ids, one lookup round resolves every
-    // other touch to its id.  Anything else is redone by the general rounds below.
-    bool fast = !std::getenv("G2N_DICT_GENERAL");
-    if (fast) {
-      init_table();
-      n_first = (uint32_t)(n_s * tps);  // claim round: flags S touches past the first n_s * tps
-      insert(kModeClaim, 1, cap >= full_cap ? cap : 4096, nullptr);
-      fast = !c->h_ctl->table_overflow;
-    }
-    bool sprefix = false;  // ids are touch indices: no ranking pass
-    if (fast) {
-      const uint64_t n_st = n_s * tps;  // S touches
-      sprefix = c->h_ctl->deferred == 0 && !c->h_ctl->s_late;
-      if (sprefix) {
-        nid_in = nullptr;
-        inv_in = nullptr;
-        n_first = (uint32_t)n_st;
-        hipLaunchKernelGGL(k_key_len, dim3(grid_for(n_st)), dim3(kTPB), 0, c->stream, TI, n_st, (int)bidir, klen);
-        c->h_ctl->n_nodes = n_st;
-        G2N_HIP(hipMemcpyAsync(&c->ctl->n_nodes, &c->h_ctl->n_nodes, sizeof(unsigned long long),
-                               hipMemcpyHostToDevice, c->stream));
-      } else {
-        rank_firsts();
-        hipLaunchKernelGGL(k_assign_first, dim3(grid_for(n_t)), dim3(kTPB), 0, c->stream, table, TI, n_t,
-                           (int)bidir, first, slot, nid, inv, klen);
-      }
-      phase(c, "ids_fast");
-      tid = dget<uint32_t>(c, S_TID, n_t);
-      insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
-      fast = !c->h_ctl->dict_general && !c->h_ctl->table_overflow && c->h_ctl->deferred == 0;
-      if (!fast) {
-        tid = nullptr;
-        sprefix = false;
-        nid_in = nid;
-        inv_in = inv;
-        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
-      }
-    }
-    if (!fast) {
-      while (true) {
-        init_table();
-        const uint64_t max_probes = cap >= full_cap ? cap : 4096;
-        bool overflow = false;
-        for (uint32_t round = 1;; round++) {  // round 1: S touches; then every unresolved touch
-          insert(round == 1 ? kModeClaim : kModeLookup, round, max_probes, nullptr);
-          if (c->h_ctl->table_overflow) { overflow = true; break; }
-          if (round > 1 && c->h_ctl->deferred == 0) break;
-          if (round > 100000) throw Failure(G2N_E_DEVICE, "dictionary insert did not converge");
-        }
-        if (!overflow) break;
-        if (cap >= full_cap) throw Failure(G2N_E_DEVICE, "node table overflow");
-        G2N_HIP(hipMemsetAsync(&c->ctl->table_overflow, 0, sizeof(unsigned long long), c->stream));
-        cap = full_cap;
-      }
-      G2N_HIP(hipMemsetAsync(first, 0, n_t, c->stream));
-      hipLaunchKernelGGL(k_mark_first, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, first);
-      rank_firsts();
-      hipLaunchKernelGGL(k_assign_ids, dim3(grid_for(cap)), dim3(kTPB), 0, c->stream, table, cap, nid, inv, klen);
-      phase(c, "ids_general");
-    }
-  }
-  sync_ctl(c);
-  if (c->h_ctl->table_overflow) throw Failure(G2N_E_DEVICE, "node table overflow");
-  const uint64_t n_nodes = n_t ? c->h_ctl->n_nodes : 0;
+  const uint64_t n_nodes = D.n_nodes;
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");
@@ -569,18 +660,18 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     {
       size_t tb = 0;
       if (n_nodes) {
-        G2N_HIP(rocprim::exclusive_scan(nullptr, tb, klen, offs, (int64_t)0, (size_t)n_nodes,
+        G2N_HIP(rocprim::exclusive_scan(nullptr, tb, D.klen, offs, (int64_t)0, (size_t)n_nodes,
                                         rocprim::plus<int64_t>(), c->stream));
         void* tmp = dbuf(c, S_TEMP, tb);
-        G2N_HIP(rocprim::exclusive_scan(tmp, tb, klen, offs, (int64_t)0, (size_t)n_nodes, rocprim::plus<int64_t>(),
+        G2N_HIP(rocprim::exclusive_scan(tmp, tb, D.klen, offs, (int64_t)0, (size_t)n_nodes, rocprim::plus<int64_t>(),
                                         c->stream));
       }
-      hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, klen, n_nodes, offs, c->ctl);
+      hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, D.klen, n_nodes, offs, c->ctl);
     }
     const uint64_t names_len = read_dev(c, &c->ctl->names_len);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
     if (n_nodes)
-      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, inv_in,
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, D.inv,
                          offs, (int)bidir, blob);
     R->names_bytes = names_len;
     R->names_blob = blob;
@@ -598,11 +689,11 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
   switch (dt) {
-    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
-    default: run_triplets<double>(c, EI, n_e, slot, table, tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+    default: run_triplets<double>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
   }
   phase(c, "triplets");
   sync_ctl(c);
@@ -616,7 +707,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     return R->status;
   }
   const bool uni = !op.has_wt;  // no weight tag: every entry is dtype(1.0)
-  if (o->output == G2N_OUT_PARSE && !maxsym) {  // builders.py:281: the COO itself
+  if ((o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO) {  // builders.py:281: the COO itself
     R->format = G2N_FMT_COO;
     R->nnz = (int64_t)n_trip;
     R->rows = rows;
@@ -803,6 +894,121 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   return G2N_OK;
 }
 
+// --------------------------------------------------------- sharded build steps ------
+static void begin_call(g2n_context* c) {
+  c->n_ev = 0;
+  G2N_HIP(hipEventRecord(c->ev[0], c->stream));
+  reset_ctl(c);
+}
+
+uint64_t dedup_keys(g2n_context* c, const uint8_t* blob, uint64_t blob_len, const int64_t* offs, uint64_t n,
+                    uint32_t* ids, uint32_t* first_of) {
+  begin_call(c);
+  if (n >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 keys");
+  if (n == 0) return 0;
+  TouchOut T{dget<uint64_t>(c, S_NOFF, n), dget<uint32_t>(c, S_NLEN, n), nullptr, nullptr,
+             dget<uint8_t>(c, S_TKIND, n)};
+  hipLaunchKernelGGL(k_keys_to_touches, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, offs, n, T.noff, T.nlen, T.tkind);
+  const DictOut D = build_dictionary(c, blob, blob_len, T, n, n, n, false);
+  hipLaunchKernelGGL(k_touch_ids, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, n, D.first, D.slot, D.table, D.tid,
+                     (int)D.general, ids);
+  if (D.n_nodes)
+    hipLaunchKernelGGL(k_first_of, dim3(grid_for(D.n_nodes)), dim3(kTPB), 0, c->stream, D.n_nodes, D.inv, first_of);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  return D.n_nodes;
+}
+
+void partition_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, uint64_t n, uint32_t n_ranks,
+                    uint8_t* oblob, int64_t* ooffs, uint32_t* oindex, uint32_t* starts) {
+  begin_call(c);
+  if (n_ranks == 0 || n_ranks > 4096) throw Failure(G2N_E_ARG, "n_ranks out of range");
+  if (n >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 keys");
+  auto* owner = dget<uint32_t>(c, S_KEYS0, n);
+  auto* owner_s = dget<uint32_t>(c, S_KEYS1, n);
+  auto* idx = dget<uint32_t>(c, S_VALS0, n);
+  auto* lens = dget<int64_t>(c, S_FOFF64, n + 1);
+  if (n) {
+    hipLaunchKernelGGL(k_key_owner, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, blob, offs, n, n_ranks, owner, idx);
+    sort_pairs_u32<uint32_t>(c, owner, owner_s, idx, oindex, n, bits_for(n_ranks));
+    hipLaunchKernelGGL(k_key_lens, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, offs, oindex, n, lens);
+  }
+  G2N_HIP(hipMemsetAsync(lens + n, 0, sizeof(int64_t), c->stream));
+  excl_scan<int64_t>(c, lens, ooffs, n + 1);  // ooffs[n] = total bytes
+  if (n)
+    hipLaunchKernelGGL(k_copy_keys, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, blob, offs, oindex, n, ooffs, oblob);
+  G2N_HIP(hipMemsetAsync(&c->ctl->row_gap, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(k_row_bounds, dim3(grid_for(n + 1)), dim3(kTPB), 0, c->stream, owner_s, n, (uint64_t)n_ranks,
+                     starts, c->ctl);
+  hipLaunchKernelGGL(k_row_start, dim3(grid_for((uint64_t)n_ranks + 1)), dim3(kTPB), 0, c->stream, owner_s, n,
+                     (uint64_t)n_ranks, starts, (const Ctl*)c->ctl);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, const void* data, uint64_t nnz,
+                    int dtype, const uint32_t* map, uint64_t n_global, uint32_t n_ranks, int transposed,
+                    int32_t* orows, int32_t* ocols, void* odata, uint32_t* starts) {
+  begin_call(c);
+  if (n_ranks == 0 || n_ranks > 4096) throw Failure(G2N_E_ARG, "n_ranks out of range");
+  if (nnz >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 triplets");
+  auto* owner = dget<uint32_t>(c, S_KEYS0, nnz);
+  auto* owner_s = dget<uint32_t>(c, S_KEYS1, nnz);
+  auto* idx = dget<uint32_t>(c, S_VALS0, nnz);
+  auto* perm = dget<uint32_t>(c, S_VALS1, nnz);
+  if (nnz) {
+    hipLaunchKernelGGL(k_route_keys, dim3(grid_for(nnz)), dim3(kTPB), 0, c->stream, rows, cols, nnz, map, n_global,
+                       n_ranks, transposed, owner, idx);
+    sort_pairs_u32<uint32_t>(c, owner, owner_s, idx, perm, nnz, bits_for(n_ranks));
+    const size_t w = dtype_size(dtype);
+    const dim3 g(grid_for(nnz)), b(kTPB);
+    if (w == 1)
+      hipLaunchKernelGGL(k_route_gather<1>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
+                         transposed, orows, ocols, (uint8_t*)odata);
+    else if (w == 4)
+      hipLaunchKernelGGL(k_route_gather<4>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
+                         transposed, orows, ocols, (uint8_t*)odata);
+    else
+      hipLaunchKernelGGL(k_route_gather<8>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
+                         transposed, orows, ocols, (uint8_t*)odata);
+  }
+  // rank starts from the sorted owners (the row-start kernels, n_ranks "rows")
+  G2N_HIP(hipMemsetAsync(&c->ctl->row_gap, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(k_row_bounds, dim3(grid_for(nnz + 1)), dim3(kTPB), 0, c->stream, owner_s, nnz, (uint64_t)n_ranks,
+                     starts, c->ctl);
+  hipLaunchKernelGGL(k_row_start, dim3(grid_for((uint64_t)n_ranks + 1)), dim3(kTPB), 0, c->stream, owner_s, nnz,
+                     (uint64_t)n_ranks, starts, (const Ctl*)c->ctl);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+void csr_from_coo_pair(g2n_context* c, const int32_t* ar, const int32_t* ac, const void* ad, uint64_t an,
+                       const int32_t* tr, const int32_t* tc, const void* td, uint64_t tn, int maxsym, int64_t base,
+                       uint64_t n_rows, uint64_t n_cols, int dtype, int uniform, int force_unsorted, g2n_result* R) {
+  fill_defaults(R);
+  begin_call(c);
+  if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) throw Failure(G2N_E_ARG, "unsupported dtype");
+  if (an + tn >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 entries");
+  R->dtype = dtype;
+  R->index_width = 4;
+  R->n_nodes = (int64_t)n_rows;
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    if (uniform)
+      assemble_pair_t<T, true>(c, ar, ac, (const T*)ad, an, tr, tc, (const T*)td, tn, maxsym != 0, base, n_rows,
+                               force_unsorted, R);
+    else
+      assemble_pair_t<T, false>(c, ar, ac, (const T*)ad, an, tr, tc, (const T*)td, tn, maxsym != 0, base, n_rows,
+                                force_unsorted, R);
+  };
+  switch (dtype) {
+    case G2N_BOOL: go(uint8_t{}); break;
+    case G2N_INT8: go(int8_t{}); break;
+    case G2N_INT32: go(int32_t{}); break;
+    case G2N_FLOAT32: go(float{}); break;
+    default: go(double{}); break;
+  }
+  (void)n_cols;
+  finish_timings(c, R);
+}
+
 }  // namespace g2n
 
 // ------------------------------------------------------------------ C ABI --------
@@ -856,6 +1062,65 @@ int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t
     g2n::set_last_error(e.what());
     return G2N_E_DEVICE;
   }
+}
+
+#define G2N_CTX_CALL(ctx, body)                          \
+  do {                                                   \
+    if (!(ctx)) {                                        \
+      g2n::set_last_error("null context");               \
+      return G2N_E_ARG;                                  \
+    }                                                    \
+    try {                                                \
+      std::lock_guard<std::mutex> lk((ctx)->mu);         \
+      G2N_HIP(hipSetDevice((ctx)->device));              \
+      body;                                              \
+    } catch (const g2n::Failure& f) {                    \
+      g2n::set_last_error(f.what());                     \
+      return f.status;                                   \
+    } catch (const std::exception& e) {                  \
+      g2n::set_last_error(e.what());                     \
+      return G2N_E_DEVICE;                               \
+    }                                                    \
+  } while (0)
+
+int g2n_dedup_keys(g2n_context* ctx, const uint8_t* d_blob, uint64_t blob_len, const int64_t* d_offsets, uint64_t n,
+                   uint32_t* d_ids, uint32_t* d_first, uint64_t* n_distinct) {
+  if (!n_distinct || (n && (!d_offsets || !d_ids || !d_first))) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, *n_distinct = g2n::dedup_keys(ctx, d_blob, blob_len, d_offsets, n, d_ids, d_first));
+  return G2N_OK;
+}
+
+int g2n_partition_keys(g2n_context* ctx, const uint8_t* d_blob, uint64_t blob_len, const int64_t* d_offsets,
+                       uint64_t n, uint32_t n_ranks, uint8_t* d_out_blob, int64_t* d_out_offsets,
+                       uint32_t* d_out_index, uint32_t* d_starts) {
+  if (!d_starts || !d_out_offsets || !d_offsets || (n && (!d_out_index || (blob_len && (!d_blob || !d_out_blob)))))
+    return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::partition_keys(ctx, d_blob, d_offsets, n, n_ranks, d_out_blob, d_out_offsets, d_out_index,
+                                        d_starts));
+  return G2N_OK;
+}
+
+int g2n_route_triplets(g2n_context* ctx, const int32_t* d_rows, const int32_t* d_cols, const void* d_data,
+                       uint64_t nnz, int32_t dtype, const uint32_t* d_map, uint64_t n_global, uint32_t n_ranks,
+                       int32_t transposed, int32_t* d_out_rows, int32_t* d_out_cols, void* d_out_data,
+                       uint32_t* d_starts) {
+  if (!d_starts || (nnz && (!d_rows || !d_cols || !d_data || !d_map || !d_out_rows || !d_out_cols || !d_out_data)))
+    return G2N_E_ARG;
+  if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::route_triplets(ctx, d_rows, d_cols, d_data, nnz, dtype, d_map, n_global, n_ranks, transposed,
+                                        d_out_rows, d_out_cols, d_out_data, d_starts));
+  return G2N_OK;
+}
+
+int g2n_csr_from_coo_pair(g2n_context* ctx, const int32_t* a_rows, const int32_t* a_cols, const void* a_data,
+                          uint64_t a_nnz, const int32_t* t_rows, const int32_t* t_cols, const void* t_data,
+                          uint64_t t_nnz, int32_t maxsym, int64_t row_base, uint64_t n_rows, uint64_t n_cols,
+                          int32_t dtype, int32_t uniform, int32_t force_unsorted, g2n_result* out) {
+  if (!out) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::csr_from_coo_pair(ctx, a_rows, a_cols, a_data, a_nnz, t_rows, t_cols, t_data,
+                                           maxsym ? t_nnz : 0, maxsym, row_base, n_rows, n_cols, dtype, uniform,
+                                           force_unsorted, out));
+  return G2N_OK;
 }
 
 int g2n_device_count(void) {

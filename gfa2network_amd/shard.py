@@ -1,0 +1,499 @@
+"""Sharded build of ONE GFA file over the ranks of a torch.distributed group.
+
+The reference parses one file on one core (`parser.py:114` line loop, `builders.py:190-234`
+dict minting and triplets); its node ids are the order of first touch over the whole file.
+Here each rank takes a contiguous, line-aligned byte range and the ranks reconcile:
+
+1. local build (HIP, `g2n_build_device`, output COO): the range as a file of its own — a
+   stream-order COO over LOCAL ids (first touch inside the range) and the local names;
+2. names to owners (`g2n_partition_keys`, hash of the bytes mod G; all-to-all-v): an owner
+   receives each key from every rank that has it, concatenated in rank order, each rank's keys
+   in local-id order — i.e. in GLOBAL first-touch order, because ranges are contiguous;
+3. owner dedup (`g2n_dedup_keys`, exact bytes, the GPU dictionary): the first occurrence of
+   a key carries its order key (source rank, local id);
+4. global ids: the owners' distinct order keys are all-gathered; a key's id is the number of
+   distinct keys, over all owners, with a smaller order key (the reference's dict insertion
+   order); ids go back to the source ranks (all-to-all-v) → local → global id map;
+5. triplets to row owners (`g2n_route_triplets`, all-to-all-v; rank k owns rows
+   [ceil(k n / G), ceil((k+1) n / G))), plus the A.T stream for MAX-SYM; arrivals are in global
+   stream order, so scipy's duplicate-summation order is kept;
+6. the rank's CSR row slice (`g2n_csr_from_coo_pair`): coo.tocsr() or A.maximum(A.T).
+
+Errors and the one-shot unsupported-record warning are resolved across ranks in stream
+order (the earliest parse error wins; cast errors only when no rank has a parse error).
+
+The exchange runs on torch tensors: device tensors with the nccl (RCCL) backend, host tensors
+with gloo.  The per-rank compute goes through an engine: `HipEngine` (the product: libg2n.so
+on this rank's GPU); tests drive the same protocol with a CPU engine built on the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as nat
+
+TORCH_DTYPES = {"bool": "uint8", "int8": "int8", "int32": "int32", "float32": "float32", "float64": "float64"}
+CAST_ERRORS = (10, 11, 12)  # G2N_E_CAST_*: raised by np.array(data, dtype) after the whole parse
+
+
+@dataclass
+class LocalShard:
+    """One rank's range built on its own (local ids)."""
+
+    status: int
+    err_line: int
+    err_index: int
+    err_value: float
+    err_detail: bytes
+    warn_line: int  # first unsupported-record line of the range, -1 if none
+    has_warning: bool
+    warn_byte: int
+    n_lines: int
+    n_records: int
+    n_records_before_error: int
+    n_edges: int
+    n_local_nodes: int
+    rows: object = None  # torch int32, stream order
+    cols: object = None
+    data: object = None  # torch dtype per TORCH_DTYPES
+    names_blob: object = None  # torch uint8
+    names_offsets: object = None  # torch int64, n_local_nodes + 1
+    n_cast_overflow: int = 0
+
+
+@dataclass
+class ShardResult:
+    """This rank's slice of the global result (rows [row_lo, row_hi) of an n_nodes^2 CSR)."""
+
+    status: int
+    err_line: int = -1
+    err_index: int = -1
+    err_value: float = 0.0
+    err_detail: bytes = b""
+    has_warning: bool = False
+    warn_byte: int = 0
+    warn_line: int = -1
+    n_lines: int = 0
+    n_records: int = 0
+    n_records_before_error: int = 0
+    n_edges: int = 0
+    n_nodes: int = 0
+    row_lo: int = 0
+    row_hi: int = 0
+    indptr: object = None
+    indices: object = None
+    data: object = None
+    names: list | None = None  # node keys in id order, when gather_names
+    n_cast_overflow: int = 0
+    timings_ms: dict = field(default_factory=dict)
+
+
+def line_ranges(data: bytes | np.ndarray, n_ranks: int) -> list[tuple[int, int]]:
+    """Contiguous line-aligned byte ranges: range r starts at the first line start at or after
+    r * len / G (the line holding that offset belongs to the range holding its first byte)."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    n = len(buf)
+    starts = [0]
+    for r in range(1, n_ranks):
+        nominal = r * n // n_ranks
+        s = nominal
+        if 0 < s < n and buf[s - 1] != 0x0A:
+            nl = np.flatnonzero(buf[s:] == 0x0A)
+            s = n if len(nl) == 0 else s + int(nl[0]) + 1
+        starts.append(max(s, starts[-1]))
+    return [(starts[r], starts[r + 1] if r + 1 < n_ranks else n) for r in range(n_ranks)]
+
+
+# ------------------------------------------------------------------------ engines --
+class HipEngine:
+    """The product engine: libg2n.so on one GPU; buffers are torch device tensors."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        self.torch = torch
+        self.lib = nat.load()
+        self.device_index = device
+        self.device = torch.device("cuda", device)
+        self.ctx = self.lib.g2n_context_create(device)
+        if not self.ctx:
+            raise nat.NativeUnavailable(nat.last_error())
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+
+    def close(self):
+        if self.ctx:
+            self.lib.g2n_context_destroy(self.ctx)
+            self.ctx = None
+
+    def _sync(self):
+        self.torch.cuda.current_stream(self.device).synchronize()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {nat.status_name(rc)}: {nat.last_error()}")
+
+    def _copy_out(self, ptr, n, dtype):
+        t = self.torch.empty(n, dtype=dtype, device=self.device)
+        nbytes = n * t.element_size()
+        if nbytes:
+            if self._hip.hipMemcpy(t.data_ptr(), ptr, nbytes, 3) != 0:  # device to device
+                raise RuntimeError("hipMemcpy failed")
+        return t
+
+    def empty(self, n, dtype):
+        return self.torch.empty(n, dtype=getattr(self.torch, dtype) if isinstance(dtype, str) else dtype,
+                                device=self.device)
+
+    def local_build(self, buf, opts: dict, unknown_warned: bool = False) -> LocalShard:
+        torch = self.torch
+        o = nat.make_options(output=nat.OUT_COO, want_node_names=True, device=self.device_index, **opts)
+        o.reserved[0] = int(unknown_warned)
+        res = nat.Result()
+        self._sync()
+        rc = self.lib.g2n_build_device(self.ctx, buf.data_ptr() if buf.numel() else None, buf.numel(),
+                                       ctypes.byref(o), ctypes.byref(res))
+        if rc not in (0,) and not (1 <= rc <= 12):
+            self._check(rc, "g2n_build_device")
+        sh = LocalShard(status=rc, err_line=res.err_line, err_index=res.err_index, err_value=res.err_value,
+                        err_detail=b"", warn_line=res.warn_line, has_warning=bool(res.has_warning),
+                        warn_byte=res.warn_byte, n_lines=res.n_lines, n_records=res.n_records,
+                        n_records_before_error=res.n_records_before_error, n_edges=res.n_edges,
+                        n_local_nodes=res.n_nodes, n_cast_overflow=res.n_cast_overflow)
+        if rc == 8 and res.err_detail_len:  # the bytes whose decode raises, for the message
+            sh.err_detail = bytes(self._copy_out(res.err_detail, res.err_detail_len, torch.uint8).cpu().numpy())
+        if rc != 0:
+            return sh
+        n = res.nnz
+        sh.rows = self._copy_out(res.rows, n, torch.int32)
+        sh.cols = self._copy_out(res.cols, n, torch.int32)
+        sh.data = self._copy_out(res.data, n, getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")]))
+        sh.names_offsets = self._copy_out(res.names_offsets, res.n_nodes + 1, torch.int64)
+        sh.names_blob = self._copy_out(res.names_blob, int(res.names_bytes), torch.uint8)
+        return sh
+
+    def partition_keys(self, blob, offsets, n_ranks: int):
+        torch = self.torch
+        n = offsets.numel() - 1
+        oblob = torch.empty_like(blob)
+        ooffs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        oidx = torch.empty(n, dtype=torch.int32, device=self.device)
+        starts = torch.empty(n_ranks + 1, dtype=torch.int32, device=self.device)
+        self._sync()
+        self._check(self.lib.g2n_partition_keys(self.ctx, blob.data_ptr() if blob.numel() else None, blob.numel(),
+                                                offsets.data_ptr(), n, n_ranks,
+                                                oblob.data_ptr() if blob.numel() else None, ooffs.data_ptr(),
+                                                oidx.data_ptr() if n else None, starts.data_ptr()),
+                    "g2n_partition_keys")
+        return oblob, ooffs, oidx, starts
+
+    def dedup_keys(self, blob, offsets):
+        torch = self.torch
+        n = offsets.numel() - 1
+        ids = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        first = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        nd = ctypes.c_uint64(0)
+        self._sync()
+        self._check(self.lib.g2n_dedup_keys(self.ctx, blob.data_ptr() if blob.numel() else None, blob.numel(),
+                                            offsets.data_ptr(), n, ids.data_ptr(), first.data_ptr(),
+                                            ctypes.byref(nd)), "g2n_dedup_keys")
+        return ids[:n], first[:nd.value], nd.value
+
+    def route_triplets(self, rows, cols, data, dtype: str, gmap, n_global: int, n_ranks: int, transposed: bool):
+        torch = self.torch
+        n = rows.numel()
+        orows = torch.empty(n, dtype=torch.int32, device=self.device)
+        ocols = torch.empty(n, dtype=torch.int32, device=self.device)
+        odata = torch.empty_like(data)
+        starts = torch.empty(n_ranks + 1, dtype=torch.int32, device=self.device)
+        self._sync()
+        nz = n > 0
+        self._check(self.lib.g2n_route_triplets(
+            self.ctx, rows.data_ptr() if nz else None, cols.data_ptr() if nz else None,
+            data.data_ptr() if nz else None, n, nat.DTYPE_CODES[dtype], gmap.data_ptr() if gmap.numel() else None,
+            n_global, n_ranks, int(transposed), orows.data_ptr() if nz else None, ocols.data_ptr() if nz else None,
+            odata.data_ptr() if nz else None, starts.data_ptr()), "g2n_route_triplets")
+        return orows, ocols, odata, starts
+
+    def csr_pair(self, a, t, maxsym: bool, row_base: int, n_rows: int, n_cols: int, dtype: str, uniform: bool,
+                 force_unsorted: int):
+        torch = self.torch
+        res = nat.Result()
+        t = t if t is not None else (a[0][:0], a[1][:0], a[2][:0])
+
+        def p(x):
+            return x.data_ptr() if x.numel() else None
+
+        self._sync()
+        self._check(self.lib.g2n_csr_from_coo_pair(self.ctx, p(a[0]), p(a[1]), p(a[2]), a[0].numel(), p(t[0]),
+                                                   p(t[1]), p(t[2]), t[0].numel(), int(maxsym), row_base, n_rows,
+                                                   n_cols, nat.DTYPE_CODES[dtype], int(uniform), force_unsorted,
+                                                   ctypes.byref(res)), "g2n_csr_from_coo_pair")
+        indptr = self._copy_out(res.indptr, n_rows + 1, torch.int32)
+        indices = self._copy_out(res.indices, res.nnz, torch.int32)
+        vals = self._copy_out(res.data, res.nnz, getattr(torch, TORCH_DTYPES[dtype]))
+        return indptr, indices, vals, not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted
+
+
+# ---------------------------------------------------------------------- protocol --
+class Comm:
+    """The collectives the protocol needs, on tensors of any device: with gloo they go through
+    host memory, with nccl (RCCL over xGMI) they stay on the GPU."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.host = dist.get_backend(group) == "gloo"
+
+    def _c(self, x):
+        return x.cpu() if self.host and x.is_cuda else x
+
+    def a2av(self, x, send_counts):
+        """all-to-all-v: send_counts[k] elements of x to rank k; returns (received, counts)."""
+        torch = self.torch
+        if self.world == 1:
+            return x.clone(), list(send_counts)
+        dev = x.device
+        xc = self._c(x.contiguous())
+        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=xc.device)
+        rc = torch.empty(self.world, dtype=torch.int64, device=xc.device)
+        self.dist.all_to_all_single(rc, sc, group=self.group)
+        recv = [int(v) for v in rc.tolist()]
+        out = torch.empty(sum(recv), dtype=xc.dtype, device=xc.device)
+        self.dist.all_to_all_single(out, xc, output_split_sizes=recv, input_split_sizes=list(send_counts),
+                                    group=self.group)
+        return out.to(dev), recv
+
+    def allgather_v(self, x):
+        """every rank's (variable-length) tensor, in rank order"""
+        torch = self.torch
+        if self.world == 1:
+            return [x]
+        dev = x.device
+        xc = self._c(x)
+        n = torch.tensor([xc.numel()], dtype=torch.int64, device=xc.device)
+        ns = [torch.empty_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        ns = [int(v.item()) for v in ns]
+        m = max(ns)
+        pad = torch.zeros(m, dtype=xc.dtype, device=xc.device)
+        pad[:xc.numel()] = xc
+        outs = [torch.empty(m, dtype=xc.dtype, device=xc.device) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad, group=self.group)
+        return [o[:k].to(dev) for o, k in zip(outs, ns)]
+
+    def allgather_list(self, vals):
+        """every rank's list of numbers (float64-exact up to 2^53)"""
+        torch = self.torch
+        if self.world == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.float64)
+        if not self.host:
+            t = t.cuda()
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return [[int(v) if float(v).is_integer() else v for v in o.tolist()] for o in outs]
+
+    def bcast(self, x, src):
+        if self.world == 1:
+            return x
+        dev = x.device
+        xc = self._c(x)
+        self.dist.broadcast(xc, src=src, group=self.group)
+        return xc.to(dev)
+
+    def allreduce_max(self, x):
+        if self.world == 1:
+            return x
+        dev = x.device
+        xc = self._c(x)
+        self.dist.all_reduce(xc, op=self.dist.ReduceOp.MAX, group=self.group)
+        return xc.to(dev)
+
+
+def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, keep_directed_bidir=False,
+                  asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None,
+                  gather_names=False) -> ShardResult:
+    """Build this rank's byte range `buf` (uint8 tensor on the engine's device) as part of one
+    file split over `group` in rank order; returns this rank's CSR row slice."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    C = Comm(group)
+    world, rank = C.world, C.rank
+    dev = engine.device
+    opts = dict(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dtype, weight_tag=weight_tag)
+    gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
+    maxsym = gd and not asymmetric                               # builders.py:282
+    tpe = 4 if (bidirected and not keep_directed_bidir) else 2
+    ktrip = 4 if tpe == 4 else (1 if gd else 2)
+    tm = {}
+    t0 = time.perf_counter()
+
+    # 1. local build; 2. stream-order resolution of errors and the one-shot warning
+    local = engine.local_build(buf, opts)
+
+    def stats(sh):
+        return [sh.status, sh.err_line, sh.warn_line, sh.n_lines, sh.n_records, sh.n_records_before_error,
+                sh.n_edges, sh.n_cast_overflow]
+
+    allst = C.allgather_list(stats(local))
+    first_unk = next((k for k in range(world) if allst[k][2] >= 0), None)
+    if first_unk is not None and rank > first_unk and local.warn_line >= 0:
+        # an earlier range already warned: this range's unsupported records are silent
+        if local.status == 8 and local.err_line == local.warn_line:
+            local = engine.local_build(buf, opts, unknown_warned=True)
+        local.has_warning = False
+    allst = C.allgather_list(stats(local))
+    line_base = np.concatenate([[0], np.cumsum([int(s[3]) for s in allst])])
+    out = ShardResult(status=0, n_lines=int(line_base[-1]), n_records=int(sum(s[4] for s in allst)),
+                      n_edges=int(sum(s[6] for s in allst)))
+    parse_err = [k for k in range(world) if allst[k][0] != 0 and allst[k][0] not in CAST_ERRORS]
+    cast_err = [k for k in range(world) if allst[k][0] in CAST_ERRORS]
+    bad = parse_err[0] if parse_err else (cast_err[0] if cast_err else None)
+    if first_unk is not None:
+        gw = int(line_base[first_unk] + allst[first_unk][2])
+        if bad is None or gw < int(line_base[bad] + allst[bad][1]) or allst[bad][0] in CAST_ERRORS:
+            if not (bad == first_unk and allst[bad][0] == 8 and allst[bad][1] == allst[bad][2]):
+                out.has_warning, out.warn_line = True, gw
+                wb = torch.tensor([local.warn_byte if rank == first_unk else 0], dtype=torch.int64, device=dev)
+                out.warn_byte = int(C.bcast(wb, first_unk).item())
+    if bad is not None:
+        out.status = int(allst[bad][0])
+        if out.status in CAST_ERRORS:  # index in the global triplet stream
+            trip_base = sum(int(allst[k][6]) * ktrip for k in range(bad))
+            idx = torch.tensor([local.err_index if rank == bad else 0], dtype=torch.int64, device=dev)
+            val = torch.tensor([local.err_value if rank == bad else 0.0], dtype=torch.float64, device=dev)
+            out.err_index = trip_base + int(C.bcast(idx, bad).item())
+            out.err_value = float(C.bcast(val, bad).item())
+        else:
+            out.err_line = int(line_base[bad] + allst[bad][1])
+            out.n_records_before_error = int(sum(allst[k][4] for k in range(bad)) + allst[bad][5])
+            det = torch.zeros(64, dtype=torch.uint8, device=dev)
+            if rank == bad and local.err_detail:
+                d = np.frombuffer(local.err_detail[:63], dtype=np.uint8)
+                det[0] = len(d)
+                det[1:1 + len(d)] = torch.from_numpy(d.copy()).to(dev)
+            det = C.bcast(det, bad)
+            k = int(det[0].item())
+            out.err_detail = bytes(det[1:1 + k].cpu().numpy())
+        return out
+    out.n_records_before_error = out.n_records
+    out.n_cast_overflow = int(sum(s[7] for s in allst))
+    tm["local_build"] = (time.perf_counter() - t0) * 1e3
+
+    # 3. names to owners, owner dedup in arrival (= global first-touch) order
+    t1 = time.perf_counter()
+    pb, po, pidx, pst = engine.partition_keys(local.names_blob, local.names_offsets, world)
+    pst_l = [int(v) for v in pst.tolist()]
+    po_l = po[torch.tensor(pst_l, dtype=torch.int64, device=dev)].tolist() if local.n_local_nodes else [0] * (world + 1)
+    key_counts = [pst_l[k + 1] - pst_l[k] for k in range(world)]
+    byte_counts = [int(po_l[k + 1] - po_l[k]) for k in range(world)]
+    lens = (po[1:] - po[:-1]) if local.n_local_nodes else torch.zeros(0, dtype=torch.int64, device=dev)
+    r_blob, _ = C.a2av(pb[:int(po_l[-1])] if local.n_local_nodes else pb[:0], byte_counts)
+    r_lens, r_kc = C.a2av(lens, key_counts)
+    r_idx, _ = C.a2av(pidx.to(torch.int64), key_counts)
+    r_src = torch.repeat_interleave(torch.arange(world, dtype=torch.int64, device=dev),
+                                    torch.tensor(r_kc, dtype=torch.int64, device=dev))
+    r_off = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
+    if r_lens.numel():
+        r_off[1:] = torch.cumsum(r_lens, 0)
+    ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
+    okey = (r_src << 32) | r_idx  # (source rank, local id): global first-touch order
+    dkey = okey[first_of.to(torch.int64)] if nd else okey[:0]
+    tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
+
+    # 4. global ids: rank of each distinct key's order key among all owners'
+    t2 = time.perf_counter()
+    all_dkey = C.allgather_v(dkey)
+    n_global = int(sum(x.numel() for x in all_dkey))
+    gid = torch.arange(nd, dtype=torch.int64, device=dev)
+    for o, other in enumerate(all_dkey):
+        if o != rank and other.numel() and nd:
+            gid += torch.searchsorted(other, dkey)
+    back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
+    gmap = torch.empty(local.n_local_nodes, dtype=torch.int32, device=dev)
+    if local.n_local_nodes:
+        gmap[pidx.to(torch.int64)] = back
+    tm["global_ids"] = (time.perf_counter() - t2) * 1e3
+    out.n_nodes = n_global
+    if gather_names:
+        names_d = [bytes(r_blob[int(r_off[i]):int(r_off[i + 1])].cpu().numpy()) for i in first_of.tolist()]
+        all_gid = C.allgather_v(gid)
+        blob = b"\n".join(names_d)
+        bt = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(dev)
+        all_blob = C.allgather_v(bt)
+        names = [None] * n_global
+        for g, b in zip(all_gid, all_blob):
+            parts = bytes(b.cpu().numpy()).split(b"\n") if g.numel() else []
+            for k, nm in zip(g.tolist(), parts):
+                names[k] = nm
+        out.names = names
+
+    # 5. triplets to row owners (and the A.T stream for MAX-SYM)
+    t3 = time.perf_counter()
+    u32map = gmap.view(torch.int32)
+
+    def route(transposed):
+        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, local.data, dtype, u32map, n_global, world,
+                                               transposed)
+        st_l = [int(v) for v in st.tolist()]
+        cnt = [st_l[k + 1] - st_l[k] for k in range(world)]
+        return C.a2av(rr, cnt)[0], C.a2av(cc, cnt)[0], C.a2av(dd, cnt)[0]
+
+    a = route(False)
+    tstream = route(True) if maxsym else None
+    tm["route"] = (time.perf_counter() - t3) * 1e3
+
+    # 6. this rank's CSR row slice
+    t4 = time.perf_counter()
+    row_lo = (rank * n_global + world - 1) // world
+    row_hi = ((rank + 1) * n_global + world - 1) // world
+    uniform = not weight_tag
+    force = -1
+    if not uniform and dtype in ("float32", "float64") and world > 1:
+        # scipy's has_sorted_indices is a property of the whole matrix: OR over the slices
+        _, _, _, ua, ut = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype, uniform, -1)
+        flags = C.allreduce_max(torch.tensor([int(ua), int(ut)], dtype=torch.int64, device=dev))
+        force = int(flags[0].item()) | (int(flags[1].item()) << 1)
+    indptr, indices, vals, _, _ = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype,
+                                                  uniform, force)
+    tm["csr"] = (time.perf_counter() - t4) * 1e3
+    out.row_lo, out.row_hi = row_lo, row_hi
+    out.indptr, out.indices, out.data = indptr, indices, vals
+    out.timings_ms = tm
+    return out
+
+
+def gather_csr(res: ShardResult, group=None):
+    """Every rank's slice concatenated into the full CSR (numpy), on every rank."""
+    import torch
+
+    C = Comm(group)
+    parts_p = C.allgather_v(res.indptr.to(torch.int64))
+    parts_i = C.allgather_v(res.indices.to(torch.int64))
+    dt = res.data.dtype
+    raw = res.data.contiguous()
+    raw = raw.view(torch.uint8) if raw.numel() and dt != torch.uint8 else raw.reshape(-1).to(torch.uint8)
+    parts_d = C.allgather_v(raw)
+    indptr = [np.zeros(1, dtype=np.int64)]
+    base = 0
+    for p in parts_p:
+        p = p.cpu().numpy()
+        indptr.append(p[1:] + base)
+        base += int(p[-1]) if len(p) else 0
+    indices = np.concatenate([x.cpu().numpy() for x in parts_i])
+    npdt = {torch.uint8: np.uint8, torch.int8: np.int8, torch.int32: np.int32, torch.float32: np.float32,
+            torch.float64: np.float64}[dt]
+    data = np.concatenate([x.cpu().numpy().view(npdt) if dt != torch.uint8 else x.cpu().numpy() for x in parts_d])
+    return np.concatenate(indptr), indices, data

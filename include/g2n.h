@@ -64,7 +64,7 @@ enum {
 /* ---- matrix dtypes (cli.py:92-97 --dtype choices) ------------------------------------ */
 enum { G2N_BOOL = 0, G2N_INT8 = 1, G2N_INT32 = 2, G2N_FLOAT32 = 3, G2N_FLOAT64 = 4 };
 
-enum { G2N_OUT_PARSE = 0, G2N_OUT_CSR = 1 };
+enum { G2N_OUT_PARSE = 0, G2N_OUT_CSR = 1, G2N_OUT_COO = 2 };
 enum { G2N_FMT_COO = 0, G2N_FMT_CSR = 1 };
 
 /* Mirrors parse_gfa's keyword arguments that affect the matrix (builders.py:30-50). */
@@ -76,11 +76,13 @@ typedef struct g2n_options {
   int32_t asymmetric;          /* default 0 */
   int32_t strip_orientation;   /* default 0 */
   int32_t dtype;               /* G2N_* dtype, default G2N_FLOAT64 */
-  int32_t output;              /* G2N_OUT_PARSE (default) | G2N_OUT_CSR */
+  int32_t output;              /* G2N_OUT_PARSE (default) | G2N_OUT_CSR | G2N_OUT_COO (the
+                                  stream-order COO in every mode: one shard of a sharded build) */
   const char *weight_tag;      /* UTF-8, NUL-terminated; NULL or "" = no weights */
   int32_t want_node_names;     /* 1 (default): produce the names blob in id order */
   int32_t device;              /* HIP device ordinal, default 0 */
-  int32_t reserved[6];
+  int32_t reserved[6];         /* [0]: unsupported records skipped silently (an earlier shard of a
+                                  sharded build warned already); others 0 */
 } g2n_options;
 
 #define G2N_MAX_PHASES 40
@@ -98,7 +100,7 @@ typedef struct g2n_result {
   int64_t err_detail_len;
   int32_t has_warning;         /* RuntimeWarning("Skipping unsupported record: <c>") */
   int32_t warn_byte;           /* <c> (first byte of the first unsupported line) */
-  int64_t warn_line;
+  int64_t warn_line;           /* first unsupported-record line (-1: none), warned or not */
   int64_t n_lines;             /* lines seen (Python binary line iteration) */
   int64_t n_records;           /* records the parser yielded (S/L/E/C/P/O) */
   int64_t n_records_before_error;
@@ -121,7 +123,7 @@ typedef struct g2n_result {
                                   RuntimeWarning("overflow encountered in cast") once each */
   uint64_t input_bytes;        /* uncompressed GFA bytes parsed */
   int32_t n_phases;            /* device phase timings (hipEvent, pipeline stream) */
-  int32_t pad_;
+  int32_t sum_t_sorted;        /* MAX-SYM: has_sorted_indices of A.T's scattered COO (diagnostic) */
   double phase_ms[G2N_MAX_PHASES];
   const char *phase_names[G2N_MAX_PHASES];
   double host_ms_read;         /* host ingest (read / inflate) */
@@ -161,6 +163,51 @@ void *g2n_context_stream(g2n_context *ctx);    /* the hipStream_t the pipeline r
  * stream has drained (counts must be read back); phase timings are hipEvent-based. */
 int g2n_build_device(g2n_context *ctx, const void *d_input, size_t len, const g2n_options *opts,
                      g2n_result *out);
+
+/* ---- sharded build: device-side steps of one file split over ranks --------
+ * Each rank builds its byte range with output = G2N_OUT_COO (local ids = first-touch order
+ * inside the range, local names blob).  The protocol (gfa2network_amd/shard.py) routes names
+ * to owner ranks, where g2n_dedup_keys keeps the first occurrence of each key in arrival
+ * order (arrivals are concatenated in rank order, so that is the global first-touch order);
+ * global ids go back to the ranks, g2n_route_triplets remaps and partitions the COO by the
+ * owner of each row (and, for MAX-SYM, of each column: the A.T stream), and
+ * g2n_csr_from_coo_pair builds the rank's CSR row slice.  All pointers are DEVICE pointers
+ * on ctx's device; calls return after the stream drained. */
+
+/* keys i in [0, n): bytes d_blob[d_offsets[i] .. d_offsets[i+1]).  d_ids[i] = index of key i's
+ * distinct key, numbered in order of first occurrence; d_first[k] = first occurrence of
+ * distinct key k (k < *n_distinct; d_first sized n).  Exact byte comparison. */
+int g2n_dedup_keys(g2n_context *ctx, const uint8_t *d_blob, uint64_t blob_len, const int64_t *d_offsets,
+                   uint64_t n, uint32_t *d_ids, uint32_t *d_first, uint64_t *n_distinct);
+
+/* Key i of the names blob goes to rank (FNV-1a of its bytes) mod n_ranks: the keys, grouped
+ * by rank (order kept within a rank), to d_out_blob / d_out_offsets (n + 1); d_out_index[j] =
+ * the input index of output key j; d_starts[r] = first output key of rank r. */
+int g2n_partition_keys(g2n_context *ctx, const uint8_t *d_blob, uint64_t blob_len, const int64_t *d_offsets,
+                       uint64_t n, uint32_t n_ranks, uint8_t *d_out_blob, int64_t *d_out_offsets,
+                       uint32_t *d_out_index, uint32_t *d_starts);
+
+/* Triplet i = (d_map[d_rows[i]], d_map[d_cols[i]], d_data[i]) (transposed: row and column
+ * swapped) goes to rank floor(row * n_ranks / n_global); the output holds them grouped by
+ * rank, stream order kept within a rank; d_starts[r] = first output of rank r
+ * (d_starts[n_ranks] = nnz).  Outputs sized nnz (data: nnz elements of dtype). */
+int g2n_route_triplets(g2n_context *ctx, const int32_t *d_rows, const int32_t *d_cols, const void *d_data,
+                       uint64_t nnz, int32_t dtype, const uint32_t *d_map, uint64_t n_global, uint32_t n_ranks,
+                       int32_t transposed, int32_t *d_out_rows, int32_t *d_out_cols, void *d_out_data,
+                       uint32_t *d_starts);
+
+/* CSR of rows [row_base, row_base + n_rows) from the stream-order triplets of A whose rows
+ * fall there (global row ids) and, for MAX-SYM, those of A.T (rows = A's columns):
+ * maxsym = 0: coo.tocsr() of A's slice; 1: A.maximum(A.T)'s slice.  uniform: every value is
+ * dtype(1) (no weight tag).  force_unsorted: -1 = this slice decides scipy's
+ * has_sorted_indices; else the caller's global verdicts (the OR over all slices), bit 0 for
+ * A, bit 1 for A.T (only weighted float rows of > 16 entries depend on them).  The result's
+ * sum_sorted / sum_t_sorted report this slice's own verdicts.  Result pointers are device pointers
+ * owned by ctx (format CSR, n_nodes = n_rows). */
+int g2n_csr_from_coo_pair(g2n_context *ctx, const int32_t *a_rows, const int32_t *a_cols, const void *a_data,
+                          uint64_t a_nnz, const int32_t *t_rows, const int32_t *t_cols, const void *t_data,
+                          uint64_t t_nnz, int32_t maxsym, int64_t row_base, uint64_t n_rows, uint64_t n_cols,
+                          int32_t dtype, int32_t uniform, int32_t force_unsorted, g2n_result *out);
 
 #ifdef __cplusplus
 }

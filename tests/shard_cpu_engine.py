@@ -1,0 +1,100 @@
+"""CPU engine for the sharded-build protocol (gfa2network_amd/shard.py) — TEST INFRASTRUCTURE.
+
+Drives the product's exchange protocol on gloo without a GPU: each step the HIP engine does on
+the device is done here by the oracle (per-range build) and numpy/scipy (key partition, dedup,
+routing, per-slice coo.tocsr() / maximum).  Only tests import it.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from gfa2network_amd.shard import TORCH_DTYPES, LocalShard
+
+NP = {"bool": np.uint8, "int8": np.int8, "int32": np.int32, "float32": np.float32, "float64": np.float64}
+
+
+class CpuEngine:
+    device = torch.device("cpu")
+
+    def __init__(self, oracle_mod):
+        self.oracle = oracle_mod
+
+    def local_build(self, buf, opts, unknown_warned=False):
+        o = self.oracle.run(bytes(buf.numpy()), **opts)
+        if unknown_warned and o.status == 8:
+            raise NotImplementedError("the oracle has no silent-unknown-record mode")
+        sh = LocalShard(status=o.status, err_line=o.err_line, err_index=o.err_index, err_value=o.err_value,
+                        err_detail=o.err_detail, warn_line=o.warn_line if o.has_warning else -1,
+                        has_warning=o.has_warning, warn_byte=o.warn_byte, n_lines=o.n_lines,
+                        n_records=o.n_records, n_records_before_error=o.n_records_before_error,
+                        n_edges=0, n_local_nodes=o.n_nodes,
+                        n_cast_overflow=o.n_cast_overflow)
+        if o.status != 0:
+            return sh
+        bidir, keep = opts.get("bidirected", False), opts.get("keep_directed_bidir", False)
+        gd = keep or (not bidir and opts.get("directed", True))
+        ktrip = 4 if (bidir and not keep) else (1 if gd else 2)
+        sh.n_edges = len(o.rows) // ktrip
+        dt = opts.get("dtype", "float64")
+        sh.rows = torch.from_numpy(o.rows.astype(np.int32))
+        sh.cols = torch.from_numpy(o.cols.astype(np.int32))
+        sh.data = torch.from_numpy(np.ascontiguousarray(o.data).view(NP[dt]).copy())
+        sh.names_blob = torch.from_numpy(o.names_blob.copy())
+        sh.names_offsets = torch.from_numpy(o.names_offsets.astype(np.int64))
+        return sh
+
+    def partition_keys(self, blob, offsets, n_ranks):
+        b, off = blob.numpy().tobytes(), offsets.numpy()
+        n = len(off) - 1
+        keys = [b[off[i]:off[i + 1]] for i in range(n)]
+        owner = np.array([zlib.crc32(k) % n_ranks for k in keys], dtype=np.int64)
+        order = np.argsort(owner, kind="stable")
+        oblob = b"".join(keys[i] for i in order)
+        ooff = np.zeros(n + 1, dtype=np.int64)
+        ooff[1:] = np.cumsum([len(keys[i]) for i in order])
+        starts = np.searchsorted(owner[order], np.arange(n_ranks + 1)).astype(np.int32)
+        return (torch.from_numpy(np.frombuffer(oblob, dtype=np.uint8).copy()), torch.from_numpy(ooff),
+                torch.from_numpy(order.astype(np.int32)), torch.from_numpy(starts))
+
+    def dedup_keys(self, blob, offsets):
+        b, off = blob.numpy().tobytes(), offsets.numpy()
+        seen, ids, first = {}, [], []
+        for i in range(len(off) - 1):
+            k = b[off[i]:off[i + 1]]
+            if k not in seen:
+                seen[k] = len(first)
+                first.append(i)
+            ids.append(seen[k])
+        return (torch.tensor(ids, dtype=torch.int32), torch.tensor(first, dtype=torch.int32), len(first))
+
+    def route_triplets(self, rows, cols, data, dtype, gmap, n_global, n_ranks, transposed):
+        m = gmap.numpy().astype(np.int64)
+        r, c = m[rows.numpy()], m[cols.numpy()]
+        if transposed:
+            r, c = c, r
+        owner = r * n_ranks // max(n_global, 1)
+        order = np.argsort(owner, kind="stable")
+        starts = np.searchsorted(owner[order], np.arange(n_ranks + 1)).astype(np.int32)
+        d = data.numpy()[order]
+        return (torch.from_numpy(r[order].astype(np.int32)), torch.from_numpy(c[order].astype(np.int32)),
+                torch.from_numpy(d.copy()), torch.from_numpy(starts))
+
+    def csr_pair(self, a, t, maxsym, row_base, n_rows, n_cols, dtype, uniform, force_unsorted):
+        npdt = np.bool_ if dtype == "bool" else NP[dtype]
+
+        def csr(x):
+            rows = x[0].numpy().astype(np.int64) - row_base
+            return sp.coo_matrix((x[2].numpy().view(NP[dtype]).astype(npdt), (rows, x[1].numpy().astype(np.int64))),
+                                 shape=(n_rows, n_cols)).tocsr()
+
+        M = csr(a)
+        if maxsym:
+            M = M.maximum(csr(t))
+        data = M.data.astype(NP[dtype]) if dtype != "bool" else M.data.astype(np.uint8)
+        tdt = getattr(torch, TORCH_DTYPES[dtype])
+        return (torch.from_numpy(M.indptr.astype(np.int32)), torch.from_numpy(M.indices.astype(np.int32)),
+                torch.from_numpy(data).to(tdt), False, False)

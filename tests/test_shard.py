@@ -1,0 +1,115 @@
+"""Sharded build of one file over world_size 2 / 3 gloo ranks on the CPU.
+
+The product's protocol (gfa2network_amd/shard.py: names to owners, owner dedup, global ids,
+triplet routing, per-rank CSR slices, stream-order error / warning resolution) driven by the
+oracle-backed CPU engine (tests/shard_cpu_engine.py); the gathered result must equal the
+oracle's single-file build: node names in id order, and the CSR parse_gfa / convert_format
+returns (MAX-SYM or SUM).
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.timeout(600)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gfa(seed, n_s, n_l, shuffle, extra=()):
+    r = random.Random(seed)
+    names = [f"s{k}" if k % 4 else f"node_{k:06d}_" + "q" * r.randint(0, 20) for k in range(n_s)]
+    lines = [f"S\t{n}\t*\n" for n in names]
+    for _ in range(n_l):
+        a, b = r.choice(names), r.choice(names + ["ghost1", "ghost2"])
+        lines.append(f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t*\tRC:i:{r.randint(0, 7)}\n")
+    if shuffle:
+        r.shuffle(lines)
+        lines += [lines[3]] if lines[3].startswith("S") else []
+    lines[len(lines) // 2:len(lines) // 2] = list(extra)
+    return "".join(lines).encode()
+
+
+CASES = {
+    "s_first": (_gfa(1, 300, 1500, False), {}),
+    "shuffled": (_gfa(2, 300, 1500, True), {}),
+    "undirected": (_gfa(3, 200, 1000, True), {"directed": False}),
+    "bidirected": (_gfa(4, 200, 1000, True), {"bidirected": True}),
+    "keep": (_gfa(5, 200, 1000, True), {"bidirected": True, "keep_directed_bidir": True}),
+    "asym_weighted_int32": (_gfa(6, 200, 1000, True), {"asymmetric": True, "weight_tag": "RC", "dtype": "int32"}),
+    "weighted_int8": (_gfa(7, 150, 900, True), {"weight_tag": "RC", "dtype": "int8"}),
+    "bool": (_gfa(8, 150, 900, True), {"dtype": "bool"}),
+    "warning": (_gfa(9, 200, 1000, False, extra=["W\tsample\t1\tchr1\t0\t10\t>s1\n"]), {}),
+    "error": (_gfa(10, 200, 1000, False, extra=["L\tbad\t+\n"]), {}),
+    "tiny": (b"S\ta\t*\nL\ta\t+\tb\t-\t*\n", {}),
+}
+
+
+def _worker(rank, world, port, name, outdir):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        from gfa2network_amd.shard import build_sharded, gather_csr, line_ranges
+        from oracle import oracle as orc
+        from shard_cpu_engine import CpuEngine
+
+        data, mode = CASES[name]
+        lo, hi = line_ranges(data, world)[rank]
+        buf = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy())
+        res = build_sharded(buf, engine=CpuEngine(orc), gather_names=True, **mode)
+        full = orc.run(data, **mode)
+        if full.status:
+            assert res.status == full.status, (res.status, full.status)
+            if full.status not in (10, 11, 12):
+                assert res.err_line == full.err_line, (res.err_line, full.err_line)
+            np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+            return
+        assert res.status == 0, res.status
+        assert res.has_warning == full.has_warning and (not full.has_warning or res.warn_line == full.warn_line)
+        indptr, indices, vals = gather_csr(res)
+        want_names = [bytes(full.names_blob[full.names_offsets[i]:full.names_offsets[i + 1]])
+                      for i in range(full.n_nodes)]
+        assert res.n_nodes == full.n_nodes and res.names == want_names
+        if full.maxsym:
+            wp, wi, wd = full.ms_indptr, full.ms_indices, full.ms_data
+        else:
+            wp, wi, wd = full.sum_indptr, full.sum_indices, full.sum_data
+        assert np.array_equal(indptr, wp) and np.array_equal(indices, wi), name
+        assert np.asarray(vals).view(np.uint8).tobytes() == np.ascontiguousarray(wd).view(np.uint8).tobytes(), name
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", list(CASES))
+def test_sharded_build_equals_single_file(oracle_lib, tmp_path, world, name):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def test_line_ranges_are_line_aligned_and_cover():
+    from gfa2network_amd.shard import line_ranges
+
+    data = _gfa(3, 50, 200, True)
+    for g in (1, 2, 3, 5, 8):
+        rs = line_ranges(data, g)
+        assert rs[0][0] == 0 and rs[-1][1] == len(data)
+        for (a, b), (c, _) in zip(rs, rs[1:]):
+            assert b == c and (a == b or data[b - 1:b] == b"\n")
