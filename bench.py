@@ -38,14 +38,21 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-links", type=int, default=12_000_000)
     ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
+    ap.add_argument("--shard", action="store_true",
+                    help="one file over the ranks (gfa2network_amd/shard.py): rank r's byte range is its own "
+                         "workload-sized chunk; node names are shared across chunks (default: replicas)")
     return ap.parse_args()
 
 
-def _dist_setup(n_gpus: int):
+def _dist_setup(n_gpus: int, always: bool = False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or always:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         import torch
         import torch.distributed as dist
 
@@ -207,6 +214,65 @@ def main():
         dist.destroy_process_group()
 
 
+class _DevBytes:
+    """A device input as the protocol's byte-range argument (data_ptr / numel)."""
+
+    def __init__(self, ptr, n):
+        self.ptr, self.n = ptr, n
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.n
+
+
+def main_shard(args):
+    """One file split over the ranks, each range built and reconciled."""
+    world, rank, local = _dist_setup(args.gpus, always=True)
+    import torch.distributed as dist
+
+    from gfa2network_amd import synth
+    from gfa2network_amd.shard import HipEngine, build_sharded
+
+    wl = synth.WORKLOADS[args.workload]
+    n_s = max(1, int(wl.n_segments * args.scale))
+    n_l = max(1, int(wl.n_links * args.scale))
+    dev_in = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local)
+    eng = HipEngine(local)
+    mode = dict(wl.mode)
+    kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+              weight_tag=mode.get("weight_tag"), dtype="float64")
+    buf = _DevBytes(dev_in.ptr, dev_in.len)
+    for _ in range(args.warmup):
+        build_sharded(buf, engine=eng, **kw)
+    dist.barrier()
+    t0 = time.perf_counter()
+    tms = []
+    for _ in range(args.steps):
+        res = build_sharded(buf, engine=eng, **kw)
+        tms.append(res.timings_ms)
+    dist.barrier()
+    elapsed = _max_over_ranks(world, time.perf_counter() - t0)
+    edges_total = res.n_edges * args.steps
+    line = {
+        "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
+        "value": round(edges_total / elapsed / 1e6, 2), "unit": "M edge records/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8/int64 (float64 weights)",
+        "data": "synthetic (deterministic generator), one chunk per rank generated in HBM",
+        "config": {"workload": f"{wl.name} chunk per rank, one file over {world} ranks", "n_nodes": res.n_nodes,
+                   "edges": res.n_edges, "output": "csr row slices", "parallelism": f"shard x{world}"},
+        "gb_per_s_ingested": round(dev_in.len * world * args.steps / elapsed / 1e9, 2),
+        "host_ms_per_stage_rank0": {k: round(sum(t[k] for t in tms) / len(tms), 2) for k in tms[0]},
+    }
+    if rank == 0:
+        print(json.dumps(line))
+    eng.close()
+    dev_in.free()
+    dist.destroy_process_group()
+
+
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build (S-first dictionary path)
     "parse": "g2n::k_tile_parse",
     "insert_claim": "g2n::k_insert_round<0>",
@@ -270,4 +336,7 @@ def measured_traffic(kernel: str):
 
 
 if __name__ == "__main__":
-    main()
+    if "--shard" in sys.argv:
+        main_shard(_args())
+    else:
+        main()
