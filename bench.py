@@ -38,6 +38,9 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-links", type=int, default=12_000_000)
     ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end leg (file on the page cache -> scipy CSR + node list in host memory)")
+    ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
     ap.add_argument("--shard", action="store_true",
                     help="one file over the ranks (gfa2network_amd/shard.py): rank r's byte range is its own "
                          "workload-sized chunk; node names are shared across chunks (default: replicas)")
@@ -103,8 +106,100 @@ def cpu_baseline(workload, links: int) -> dict:
                       f"oracle/g2n_oracle.cpp single thread, {dt:.1f} s"}
 
 
+def write_gz_members(data, path: str, member_bytes: int = 64 << 20, level: int = 6, threads: int = 16) -> int:
+    """Multi-member gzip (64 MiB-uncompressed members, level 6), members
+    deflated in parallel (zlib releases the GIL).  Returns the compressed size."""
+    import struct
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+
+    mv = memoryview(data)
+
+    def one(off):
+        chunk = mv[off:off + member_bytes]
+        co = zlib.compressobj(level, zlib.DEFLATED, -zlib.MAX_WBITS)
+        body = co.compress(chunk) + co.flush()
+        return (b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\xff" + body
+                + struct.pack("<II", zlib.crc32(chunk), len(chunk) & 0xFFFFFFFF))
+
+    total = 0
+    with open(path, "wb") as fh, ThreadPoolExecutor(threads) as ex:
+        for m in ex.map(one, range(0, len(data), member_bytes)):
+            fh.write(m)
+            total += len(m)
+    return total
+
+
+def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
+    """a GFA file on the warm page cache -> parse_gfa(..., return_node_list=True)
+    + convert_format(A, "csr") in host memory, through the product's path (g2n_build_from_path:
+    parallel member inflate, pinned staged H2D, GPU pipeline, D2H, scipy/list objects).  Plain
+    and multi-member gzip inputs; one warm-up, then one timed run each."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+    from gfa2network_amd.api import convert_format, finalize
+
+    threads = int(os.environ.get("G2N_HOST_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    data = synth.host_bytes(n_s, n_l, seed=0, rc_tag=wl.rc_tag, threads=threads)
+    tmp = tempfile.mkdtemp(prefix="g2n_e2e_", dir=os.environ.get("TMPDIR") or "/tmp")
+    out = {"host_threads": threads, "input_bytes": len(data)}
+    try:
+        plain = os.path.join(tmp, "c.gfa")
+        with open(plain, "wb") as fh:
+            fh.write(data)
+        gz = os.path.join(tmp, "c.gfa.gz")
+        out["gz_bytes"] = write_gz_members(data, gz, threads=threads)
+        out["prep_s"] = round(time.perf_counter() - t0, 1)
+        del data
+        mode = dict(wl.mode)
+        dt = np.dtype("float64")
+        opts = nat.make_options(dtype="float64", output=nat.OUT_PARSE, want_node_names=True, device=device,
+                                directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+                                weight_tag=mode.get("weight_tag"))
+        for name, path in (("plain", plain), ("gzip_64MiB_members", gz)):
+            for it in range(2):
+                t0 = time.perf_counter()
+                raw = nat.build_from_path(path, opts)
+                t1 = time.perf_counter()
+                A, nodes = finalize(raw, dtype=dt, return_node_list=True, raw_bytes_id=False, verbose=False)
+                C = convert_format(A, "csr")
+                t2 = time.perf_counter()
+            assert C.format == "csr" and len(nodes) == raw.n_nodes
+            dev_ms = sum(v for k, v in raw.phase_ms.items() if not k.startswith("_"))
+            wall = t2 - t0
+            out[name] = {
+                "wall_s": round(wall, 3), "m_edges_per_s": round(raw.n_edges / wall / 1e6, 2),
+                "gb_per_s_ingested": round(raw.input_bytes / wall / 1e9, 2),
+                "stages_ms": {"read_inflate": round(raw.host_ms["read"], 1), "staged_h2d": round(raw.host_ms["h2d"], 1),
+                              "device": round(dev_ms, 1), "d2h": round(raw.host_ms["d2h"], 1),
+                              "native_total": round((t1 - t0) * 1e3, 1),
+                              "python_objects": round((t2 - t1) * 1e3, 1)},
+                "nnz": int(C.nnz), "n_nodes": len(nodes)}
+            del A, C, nodes, raw
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    ref = {"C4": 1295.5}.get(wl.name)  # BASELINE.md §2: reference parse_gfa+convert_format, gzip C4, 1 core
+    if ref:
+        out["reference_cpu_s"] = ref
+        out["speedup_vs_reference_gzip"] = round(ref / out["gzip_64MiB_members"]["wall_s"], 1)
+    return out
+
+
 def main():
     args = _args()
+    if args.e2e_only:
+        from gfa2network_amd import synth
+
+        wl = synth.WORKLOADS[args.workload]
+        print(json.dumps(end_to_end(wl, max(1, int(wl.n_segments * args.scale)),
+                                    max(1, int(wl.n_links * args.scale)), 0)))
+        return
     world, rank, local = _dist_setup(args.gpus)
     from gfa2network_amd import _native as nat
     from gfa2network_amd import synth
@@ -200,14 +295,16 @@ def main():
         tpe = 4 if (mode.get("bidirected") and not mode.get("keep_directed_bidir")) else 2
         probes = n_s * tps if dom == "insert_claim" else n_edges * tpe
         line["roofline"]["random_access"] = random_ceiling(probes, avg[dom])
+    lib.g2n_context_destroy(ctx)
+    dev_in.free()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
+    if rank == 0 and world == 1 and not args.no_e2e:
+        line["end_to_end"] = end_to_end(wl, n_s, n_l, local)
     if rank == 0:
         if args.phases:
             print(json.dumps(avg, indent=1), file=sys.stderr)
         print(json.dumps(line))
-    lib.g2n_context_destroy(ctx)
-    dev_in.free()
     if world > 1:
         import torch.distributed as dist
 

@@ -36,6 +36,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    "g2n_gunzip", "g2n_free", "g2n_join_names",
 ]
 
 
@@ -155,6 +156,12 @@ def load() -> ctypes.CDLL:
     lib.g2n_route_triplets.argtypes = [P, P, P, P, U64, I32, P, U64, U32, I32, P, P, P, P]
     lib.g2n_csr_from_coo_pair.argtypes = [P, P, P, P, U64, P, P, P, U64, I32, I64, U64, U64, I32, I32, I32,
                                           ctypes.POINTER(Result)]
+    lib.g2n_gunzip.argtypes = [P, ctypes.c_size_t, I32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
+                               ctypes.POINTER(I32), ctypes.POINTER(I32)]
+    lib.g2n_gunzip.restype = ctypes.c_int
+    lib.g2n_free.argtypes = [P]
+    lib.g2n_join_names.argtypes = [P, P, U64, ctypes.c_uint8, P]
+    lib.g2n_join_names.restype = ctypes.c_int
     for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair"):
         getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:
@@ -241,6 +248,7 @@ class RawResult:
     data: np.ndarray | None = None
     sum_sorted: bool = True
     n_cast_overflow: int = 0
+    input_bytes: int = 0
     phase_ms: dict = field(default_factory=dict)
     host_ms: dict = field(default_factory=dict)
 
@@ -260,6 +268,7 @@ def _from_result(ptr, rc: int) -> RawResult:
     out.dtype = CODE_DTYPES.get(r.dtype, np.dtype("float64"))
     out.sum_sorted = bool(r.sum_sorted)
     out.n_cast_overflow = int(r.n_cast_overflow)
+    out.input_bytes = int(r.input_bytes)
     if r.status == OK:
         idx = np.int32 if r.index_width == 4 else np.int64
         if r.names_offsets:
@@ -316,6 +325,53 @@ def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int
     out = _from_result(res, rc)
     if out.status != OK:
         raise RuntimeError(f"{status_name(out.status)}: {out.message}")
+    return out
+
+
+def host_bytes_at(addr: int, n: int) -> bytes:
+    """bytes copy of n bytes at addr (ctypes.string_at truncates its size to a C int)."""
+    if not n:
+        return b""
+    return (ctypes.c_char * n).from_address(addr).raw
+
+
+class GzipFailure(Exception):
+    """g2n_gunzip failed: ``sub`` = gzip.py's exception kind, ``message`` its text."""
+
+    def __init__(self, sub: int, message: str):
+        super().__init__(sub, message)
+        self.sub, self.message = sub, message
+
+
+def gunzip(data: bytes, parallel: bool = True) -> tuple[bytes, int]:
+    """The library's gzip.open(...).read() (host threads); returns (bytes, member count)."""
+    lib = load()
+    arr = np.frombuffer(data, dtype=np.uint8)
+    out, n, members, sub = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_int32(), ctypes.c_int32()
+    rc = lib.g2n_gunzip(arr.ctypes.data if arr.size else None, arr.size, int(parallel), ctypes.byref(out),
+                        ctypes.byref(n), ctypes.byref(members), ctypes.byref(sub))
+    if rc == E_GZIP:
+        raise GzipFailure(int(sub.value), last_error())
+    if rc != OK:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    try:
+        return host_bytes_at(out.value, n.value), int(members.value)
+    finally:
+        lib.g2n_free(out)
+
+
+def join_names(blob: np.ndarray, offsets: np.ndarray, sep: int = 0x0A) -> bytearray:
+    """Names blob + offsets -> one bytearray, names separated by `sep` (host threads)."""
+    n = len(offsets) - 1
+    if n <= 0:
+        return bytearray()
+    out = bytearray(int(offsets[-1] - offsets[0]) + n - 1)
+    if len(out):
+        buf = (ctypes.c_uint8 * len(out)).from_buffer(out)
+        rc = load().g2n_join_names(blob.ctypes.data, offsets.ctypes.data, n, sep, ctypes.addressof(buf))
+        del buf
+        if rc != OK:
+            raise RuntimeError(f"{status_name(rc)}: {last_error()}")
     return out
 
 

@@ -79,16 +79,9 @@ def _node_list(raw: RawResult, raw_bytes_id: bool) -> list:
         return []
     blob = raw.names_blob
     # names never contain b"\n" (lines are split on it): join with "\n" and split once
-    total = int(offs[-1])
-    joined = np.empty(total + n - 1, dtype=np.uint8)
-    lens = np.diff(offs)
-    dest = np.arange(total, dtype=np.int64) + np.repeat(np.arange(n, dtype=np.int64), lens)
-    joined[dest] = blob[:total]
-    if n > 1:
-        joined[offs[1:-1] + np.arange(n - 1, dtype=np.int64)] = 0x0A
-    jb = joined.tobytes()
+    jb = nat.join_names(blob, offs)
     if raw_bytes_id:
-        return jb.split(b"\n")
+        return bytes(jb).split(b"\n")
     try:
         return jb.decode().split("\n")
     except UnicodeDecodeError:

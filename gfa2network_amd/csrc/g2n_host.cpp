@@ -10,6 +10,8 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <functional>
+#include <new>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -53,17 +55,25 @@ static int io_failure(int err, const std::string& what, g2n_result** out) {
   return G2N_E_IO;
 }
 
-static int read_fd(int fd, std::vector<uint8_t>& buf) {
+static int read_fd(int fd, HostBuf& buf, size_t* len) {
   struct stat st;
+  size_t cap = (size_t)1 << 24;
   if (fstat(fd, &st) == 0) {
     if (S_ISDIR(st.st_mode)) return EISDIR;
-    if (S_ISREG(st.st_mode) && st.st_size > 0) buf.reserve((size_t)st.st_size);
+    if (S_ISREG(st.st_mode) && st.st_size > 0) cap = (size_t)st.st_size + 1;
   }
-  const size_t chunk = 1 << 24;
+  HostBuf cur;
+  cur.alloc(cap);
   size_t n = 0;
   while (true) {
-    if (buf.size() < n + chunk) buf.resize(n + chunk);
-    ssize_t r = ::read(fd, buf.data() + n, chunk);
+    if (n == cap) {  // grow (pipes, files that grew since fstat)
+      HostBuf bigger;
+      bigger.alloc(cap * 2);
+      std::memcpy(bigger.p, cur.p, n);
+      cur = std::move(bigger);
+      cap *= 2;
+    }
+    ssize_t r = ::read(fd, cur.p + n, cap - n);
     if (r < 0) {
       if (errno == EINTR) continue;
       return errno;
@@ -71,70 +81,39 @@ static int read_fd(int fd, std::vector<uint8_t>& buf) {
     if (r == 0) break;
     n += (size_t)r;
   }
-  buf.resize(n);
+  buf = std::move(cur);
+  *len = n;
   return 0;
 }
 
-// gzip.open semantics: members back to back, zero padding between/after members skipped
-// (Lib/gzip.py _GzipReader._read_eof); any other trailing bytes must start a new member.
-// Sub-codes (err_index): 1 bad magic (BadGzipFile), 2 truncated (EOFError),
-// 3 corrupt deflate data (zlib.error), 4 CRC / length mismatch (BadGzipFile).
-static int gunzip(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, int* sub, std::string* msg) {
-  size_t pos = 0;
-  out.clear();
-  out.reserve(in.size() * 3 + 1024);
-  std::vector<uint8_t> chunk((size_t)1 << 22);
-  while (true) {
-    while (pos < in.size() && in[pos] == 0) pos++;
-    if (pos >= in.size()) return 0;
-    if (in.size() - pos < 2 || in[pos] != 0x1F || in[pos + 1] != 0x8B) {
-      *sub = 1;
-      *msg = "Not a gzipped file";
-      return -1;
+// Input bytes for the staged upload, read straight from the inflated members.
+static FillFn fill_from(const Inflated& z) {
+  return [&z](size_t off, uint8_t* dst, size_t len) {
+    size_t k = (size_t)(std::upper_bound(z.start.begin(), z.start.end(), off) - z.start.begin()) - 1;
+    while (len) {
+      const size_t in_part = off - z.start[k];
+      const size_t take = std::min(len, z.parts[k].n - in_part);
+      std::memcpy(dst, z.parts[k].p + in_part, take);
+      dst += take;
+      off += take;
+      len -= take;
+      k++;
     }
-    z_stream zs;
-    std::memset(&zs, 0, sizeof(zs));
-    if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) {
-      *sub = 3;
-      *msg = "inflateInit2 failed";
-      return -1;
-    }
-    size_t fed = pos;  // bytes of `in` handed to zlib so far
-    int rc;
-    while (true) {
-      if (zs.avail_in == 0 && fed < in.size()) {
-        size_t take = std::min<size_t>(in.size() - fed, (size_t)1 << 30);
-        zs.next_in = const_cast<Bytef*>(in.data() + fed);
-        zs.avail_in = (uInt)take;
-        fed += take;
-      }
-      zs.next_out = chunk.data();
-      zs.avail_out = (uInt)chunk.size();
-      rc = inflate(&zs, Z_NO_FLUSH);
-      size_t produced = chunk.size() - zs.avail_out;
-      out.insert(out.end(), chunk.data(), chunk.data() + produced);
-      if (rc == Z_STREAM_END) break;
-      if (rc == Z_OK) continue;
-      if (rc == Z_BUF_ERROR && zs.avail_in == 0 && fed >= in.size()) {
-        inflateEnd(&zs);
-        *sub = 2;
-        *msg = "Compressed file ended before the end-of-stream marker was reached";
-        return -1;
-      }
-      if (rc == Z_BUF_ERROR) continue;
-      std::string m = zs.msg ? zs.msg : "invalid data";
-      inflateEnd(&zs);
-      if (m.find("incorrect data check") != std::string::npos || m.find("incorrect length check") != std::string::npos) {
-        *sub = 4;
-        *msg = "CRC check failed";
-      } else {
-        *sub = 3;
-        *msg = "Error -3 while decompressing data: " + m;
-      }
-      return -1;
-    }
-    pos = (size_t)(zs.next_in - in.data());
-    inflateEnd(&zs);
+  };
+}
+
+static int guarded(const std::function<int()>& f) {
+  try {
+    return f();
+  } catch (const Failure& e) {
+    set_last_error(e.what());
+    return e.status;
+  } catch (const std::bad_alloc&) {
+    set_last_error("host allocation failed");
+    return G2N_E_NOMEM;
+  } catch (const std::exception& e) {
+    set_last_error(e.what());
+    return G2N_E_DEVICE;
   }
 }
 
@@ -203,15 +182,7 @@ int g2n_build_from_buffer(const void* buf, size_t len, const g2n_options* opts, 
   int rc = check_opts(opts);
   if (rc) return rc;
   if (len && !buf) return G2N_E_ARG;
-  try {
-    return g2n::build_host(buf, len, opts, out, 0.0);
-  } catch (const g2n::Failure& f) {
-    g2n::set_last_error(f.what());
-    return f.status;
-  } catch (const std::exception& e) {
-    g2n::set_last_error(e.what());
-    return G2N_E_DEVICE;
-  }
+  return g2n::guarded([&] { return g2n::build_host(buf, len, opts, out, 0.0); });
 }
 
 int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** out) {
@@ -219,23 +190,52 @@ int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** 
   *out = nullptr;
   int rc = check_opts(opts);
   if (rc) return rc;
-  double t0 = g2n::now_ms();
-  std::vector<uint8_t> raw;
-  std::string p(path);
-  if (p == "-") {
-    int err = g2n::read_fd(0, raw);
-    if (err) return g2n::io_failure(err, "<stdin>", out);
-  } else {
-    int fd = ::open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return g2n::io_failure(errno, p, out);
-    int err = g2n::read_fd(fd, raw);
-    ::close(fd);
-    if (err) return g2n::io_failure(err, p, out);
-    if (p.size() >= 3 && p.compare(p.size() - 3, 3, ".gz") == 0) {
-      std::vector<uint8_t> inflated;
+  return g2n::guarded([&]() -> int {
+    const double t0 = g2n::now_ms();
+    std::string p(path);
+    const bool gz = p != "-" && p.size() >= 3 && p.compare(p.size() - 3, 3, ".gz") == 0;
+    int fd = 0;
+    if (p != "-") {
+      fd = ::open(path, O_RDONLY | O_CLOEXEC);
+      if (fd < 0) return g2n::io_failure(errno, p, out);
+    }
+    struct FdCloser {
+      int fd;
+      ~FdCloser() {
+        if (fd > 0) ::close(fd);
+      }
+    } closer{fd};
+    struct stat st;
+    const bool regular = fd > 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
+    if (fd > 0 && fstat(fd, &st) == 0 && S_ISDIR(st.st_mode)) return g2n::io_failure(EISDIR, p, out);
+    if (regular && !gz) {
+      // plain file: pread straight into the pinned staging slots (page cache -> HBM)
+      const size_t len = (size_t)st.st_size;
+      const int rfd = fd;
+      g2n::FillFn fill = [rfd, &p](size_t off, uint8_t* dst, size_t n) {
+        size_t got = 0;
+        while (got < n) {
+          ssize_t r = ::pread(rfd, dst + got, n - got, (off_t)(off + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) throw g2n::Failure(G2N_E_IO, p + ": " + std::strerror(r < 0 ? errno : EIO));
+          got += (size_t)r;
+        }
+      };
+      return g2n::build_host_fill(len, fill, opts, out, 0.0);
+    }
+    g2n::HostBuf raw;
+    size_t rlen = 0;
+    int err = g2n::read_fd(fd, raw, &rlen);
+    if (err) return g2n::io_failure(err, p == "-" ? "<stdin>" : p, out);
+    if (!gz) {
+      const double t1 = g2n::now_ms();
+      return g2n::build_host(raw.p, rlen, opts, out, t1 - t0);
+    }
+    g2n::Inflated z;
+    if (!g2n::gunzip_parallel(raw.p, rlen, z)) {
       int sub = 0;
       std::string msg;
-      if (g2n::gunzip(raw, inflated, &sub, &msg) != 0) {
+      if (!g2n::gunzip_exact(raw.p, rlen, z, &sub, &msg)) {
         g2n::HostResult* h = g2n::new_host_result();
         h->r.status = G2N_E_GZIP;
         h->r.err_index = sub;
@@ -243,19 +243,65 @@ int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** 
         *out = &h->r;
         return G2N_E_GZIP;
       }
-      raw.swap(inflated);
     }
-  }
-  double t1 = g2n::now_ms();
-  try {
-    return g2n::build_host(raw.data(), raw.size(), opts, out, t1 - t0);
-  } catch (const g2n::Failure& f) {
-    g2n::set_last_error(f.what());
-    return f.status;
-  } catch (const std::exception& e) {
-    g2n::set_last_error(e.what());
-    return G2N_E_DEVICE;
-  }
+    {
+      std::vector<g2n::HostBuf> done;
+      done.push_back(std::move(raw));
+      g2n::free_later(std::move(done));
+    }
+    const double t1 = g2n::now_ms();
+    const int rc2 = g2n::build_host_fill(z.total, g2n::fill_from(z), opts, out, t1 - t0);
+    g2n::free_later(std::move(z.parts));
+    return rc2;
+  });
+}
+
+int g2n_gunzip(const void* buf, size_t len, int32_t parallel, void** out, size_t* out_len, int32_t* members,
+               int32_t* sub) {
+  if (!out || !out_len || (len && !buf)) return G2N_E_ARG;
+  *out = nullptr;
+  *out_len = 0;
+  return g2n::guarded([&]() -> int {
+    g2n::Inflated z;
+    const uint8_t* in = (const uint8_t*)buf;
+    if (!(parallel && g2n::gunzip_parallel(in, len, z))) {
+      int s = 0;
+      std::string msg;
+      if (!g2n::gunzip_exact(in, len, z, &s, &msg)) {
+        if (sub) *sub = s;
+        g2n::set_last_error(msg);
+        return G2N_E_GZIP;
+      }
+    }
+    auto* o = (uint8_t*)std::malloc(z.total ? z.total : 1);
+    if (!o) return G2N_E_NOMEM;
+    for (size_t k = 0; k < z.parts.size(); k++) std::memcpy(o + z.start[k], z.parts[k].p, z.parts[k].n);
+    *out = o;
+    *out_len = z.total;
+    if (members) *members = z.members;
+    if (sub) *sub = 0;
+    return G2N_OK;
+  });
+}
+
+void g2n_free(void* p) { std::free(p); }
+
+int g2n_join_names(const uint8_t* blob, const int64_t* offsets, uint64_t n_names, uint8_t sep, uint8_t* out) {
+  if (n_names == 0) return G2N_OK;
+  if (!blob || !offsets || !out) return G2N_E_ARG;
+  return g2n::guarded([&]() -> int {
+    const uint64_t chunk = 1 << 16;
+    g2n::parallel_for((n_names + chunk - 1) / chunk, g2n::host_threads(), [&](size_t c) {
+      const uint64_t lo = c * chunk, hi = std::min<uint64_t>(n_names, lo + chunk);
+      for (uint64_t i = lo; i < hi; i++) {
+        uint8_t* d = out + offsets[i] - offsets[0] + i;
+        const size_t len = (size_t)(offsets[i + 1] - offsets[i]);
+        std::memcpy(d, blob + offsets[i], len);
+        if (i + 1 < n_names) d[len] = sep;
+      }
+    });
+    return G2N_OK;
+  });
 }
 
 void g2n_result_free(g2n_result* r) {

@@ -777,9 +777,8 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-template <class V>
-static const void* download(g2n_context* c, V& dst, const void* src, size_t bytes) {
-  dst.resize(bytes / sizeof(typename V::value_type) + 1);
+static const void* download(g2n_context* c, HostBuf& dst, const void* src, size_t bytes) {
+  dst.alloc(bytes);
   if (bytes) G2N_HIP(hipMemcpyAsync(dst.data(), src, bytes, hipMemcpyDeviceToHost, c->stream));
   return dst.data();
 }
@@ -795,13 +794,12 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
   if (D.err_detail) R.err_detail = (const uint8_t*)download(c, H->detail, D.err_detail, (size_t)D.err_detail_len);
   if (D.status == G2N_OK) {
     if (D.names_blob) {
-      H->offs.resize((size_t)D.n_nodes + 1);
-      G2N_HIP(hipMemcpyAsync(H->offs.data(), D.names_offsets, (size_t)(D.n_nodes + 1) * sizeof(int64_t),
-                             hipMemcpyDeviceToHost, c->stream));
+      const int64_t* offs =
+          (const int64_t*)download(c, H->offs, D.names_offsets, (size_t)(D.n_nodes + 1) * sizeof(int64_t));
       G2N_HIP(hipStreamSynchronize(c->stream));
-      const size_t blen = (size_t)H->offs[(size_t)D.n_nodes];
+      const size_t blen = (size_t)offs[(size_t)D.n_nodes];
       R.names_blob = (const uint8_t*)download(c, H->blob, D.names_blob, blen);
-      R.names_offsets = H->offs.data();
+      R.names_offsets = offs;
     }
     const size_t w = dtype_size(D.dtype);
     if (D.format == G2N_FMT_COO) {
@@ -816,14 +814,14 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
   G2N_HIP(hipStreamSynchronize(c->stream));
 }
 
-int build_host(const void* buf, size_t len, const g2n_options* opts, g2n_result** out, double read_ms) {
+int build_host_fill(size_t len, const FillFn& fill, const g2n_options* opts, g2n_result** out, double read_ms) {
   g2n_context* c = shared_context(opts->device);
   std::lock_guard<std::mutex> lk(c->mu);
   G2N_HIP(hipSetDevice(c->device));
   double t0 = now_ms();
   auto* din = dget<uint8_t>(c, S_IN, len + 16);
-  if (len) G2N_HIP(hipMemcpyAsync(din, buf, len, hipMemcpyHostToDevice, c->stream));
-  G2N_HIP(hipStreamSynchronize(c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));  // the slot may still be read by an earlier build
+  staged_upload(c->device, din, len, fill);
   double t1 = now_ms();
   g2n_result D;
   run_pipeline(c, din, len, opts, &D);
@@ -840,6 +838,12 @@ int build_host(const void* buf, size_t len, const g2n_options* opts, g2n_result*
   H->r.host_ms_d2h = now_ms() - t2;
   *out = &H->r;
   return H->r.status;
+}
+
+int build_host(const void* buf, size_t len, const g2n_options* opts, g2n_result** out, double read_ms) {
+  const uint8_t* src = (const uint8_t*)buf;
+  return build_host_fill(
+      len, [src](size_t off, uint8_t* dst, size_t n) { std::memcpy(dst, src + off, n); }, opts, out, read_ms);
 }
 
 // --------------------------------------------------------- convert_format ------

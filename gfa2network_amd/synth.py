@@ -66,7 +66,7 @@ def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = Fals
     if rc:
         raise RuntimeError(f"g2n_synth_host failed ({rc})")
     try:
-        return ctypes.string_at(ptr.value, n.value) if n.value else b""
+        return _native.host_bytes_at(ptr.value, n.value)
     finally:
         lib.g2n_synth_free_host(ptr)
 

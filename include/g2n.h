@@ -147,6 +147,22 @@ int g2n_build_from_path(const char *path, const g2n_options *opts, g2n_result **
 int g2n_build_from_buffer(const void *buf, size_t len, const g2n_options *opts, g2n_result **out);
 void g2n_result_free(g2n_result *res);
 
+/* gzip.open(...).read() of an in-memory .gz file (parser.py:108-109): the reader that
+ * g2n_build_from_path uses for ".gz" names.  parallel = 1: members are inflated concurrently
+ * on host threads (G2N_HOST_THREADS) when the file is a clean member chain, else serially;
+ * parallel = 0: always the serial reader.  On success *out (free with g2n_free) holds *out_len
+ * bytes and *members the member count.  On failure returns G2N_E_GZIP, *sub = the exception
+ * gzip.py raises (1 BadGzipFile, 2 EOFError, 3 zlib.error, 4 BadGzipFile CRC/length) and
+ * g2n_last_error() its message. */
+int g2n_gunzip(const void *buf, size_t len, int32_t parallel, void **out, size_t *out_len, int32_t *members,
+               int32_t *sub);
+void g2n_free(void *p);
+
+/* The node list's bytes joined by `sep` (builders.py:284-288 node_list, built in one pass by
+ * the Python shim): out (n_names ? blob_len + n_names - 1 : 0 bytes) = name 0, sep, name 1, ...
+ * with name i = blob[offsets[i] .. offsets[i+1]).  Host memory, parallel over host threads. */
+int g2n_join_names(const uint8_t *blob, const int64_t *offsets, uint64_t n_names, uint8_t sep, uint8_t *out);
+
 /* convert_format(A, "csr") for a COO matrix (utils.py:40-63 -> scipy coo.tocsr):
  * sums duplicates in dtype with scipy's summation order, keeps explicit zeros.
  * rows/cols have index_width bytes per element, data has dtype elements; n_rows x n_cols. */

@@ -75,7 +75,7 @@ def _arr(addr, count, dtype):
     dtype = np.dtype(dtype)
     if not addr or count == 0:
         return np.zeros(0, dtype=dtype)
-    return np.frombuffer(ctypes.string_at(addr, count * dtype.itemsize), dtype=dtype).copy()
+    return np.frombuffer((ctypes.c_char * (count * dtype.itemsize)).from_address(addr), dtype=dtype).copy() if count else np.empty(0, dtype)
 
 
 @dataclass

@@ -72,3 +72,21 @@ def test_out_of_scope_options_raise(tmp_path):
         parse_gfa(p, build_graph=False, build_matrix=False, return_node_list=True)
     with pytest.raises(NotImplementedError):
         parse_gfa(p, build_graph=False, build_matrix=True, dtype="float16")
+
+
+def test_join_names_matches_python():
+    """g2n_join_names (the node list's one-pass join, api._node_list) == b"\\n".join(names)."""
+    import random
+
+    import numpy as np
+
+    from gfa2network_amd import _native
+
+    r = random.Random(3)
+    for n in (1, 2, 7, 70_000, 200_001):
+        names = [bytes(r.randrange(256) for _ in range(r.choice([0, 1, 3, 9]))).replace(b"\n", b"x")
+                 for _ in range(n)]
+        offs = np.zeros(n + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(x) for x in names])
+        blob = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8)
+        assert bytes(_native.join_names(blob, offs)) == b"\n".join(names)

@@ -1,0 +1,134 @@
+"""CPU: the library's gzip reader (g2n_gunzip — what g2n_build_from_path runs for ".gz" names,
+parser.py:108-109 gzip.open) against CPython's gzip module on the same bytes: identical output,
+or the identical exception type and message.  Both the parallel member path and the serial
+reader are checked; no GPU is needed (inflate is host work)."""
+from __future__ import annotations
+
+import gzip
+import io
+import random
+import struct
+import zlib
+
+import pytest
+
+from gfa2network_amd import _native
+
+EXC = {1: gzip.BadGzipFile, 2: EOFError, 3: zlib.error, 4: gzip.BadGzipFile}
+
+
+def member(data: bytes, level: int = 6, flags: int = 0, extra: bytes = b"", name: bytes = b"",
+           comment: bytes = b"", hcrc: int | None = None, method: int = 8) -> bytes:
+    """One gzip member with the requested optional header fields (RFC 1952)."""
+    hdr = bytearray(b"\x1f\x8b" + bytes([method, flags]) + struct.pack("<I", 0) + b"\x00\xff")
+    if flags & 4:
+        hdr += struct.pack("<H", len(extra)) + extra
+    if flags & 8:
+        hdr += name + b"\x00"
+    if flags & 16:
+        hdr += comment + b"\x00"
+    if flags & 2:
+        hdr += struct.pack("<H", (zlib.crc32(hdr) & 0xFFFF) if hcrc is None else hcrc)
+    co = zlib.compressobj(level, zlib.DEFLATED, -zlib.MAX_WBITS)
+    body = co.compress(data) + co.flush()
+    return bytes(hdr) + body + struct.pack("<II", zlib.crc32(data), len(data) & 0xFFFFFFFF)
+
+
+def gfa_text(n: int, seed: int) -> bytes:
+    r = random.Random(seed)
+    lines = [f"S\t{i}\t{''.join(r.choice('ACGT') for _ in range(r.randint(0, 30)))}" for i in range(1, n + 1)]
+    lines += [f"L\t{r.randint(1, n)}\t+\t{r.randint(1, n)}\t-\t0M" for _ in range(2 * n)]
+    return ("\n".join(lines) + "\n").encode()
+
+
+def python_read(blob: bytes):
+    try:
+        return gzip.GzipFile(fileobj=io.BytesIO(blob)).read(), None
+    except (gzip.BadGzipFile, EOFError, zlib.error) as e:
+        return None, e
+
+
+def check(blob: bytes, members: int | None = None):
+    want, exc = python_read(blob)
+    for parallel in (True, False):
+        if exc is None:
+            got, m = _native.gunzip(blob, parallel=parallel)
+            assert got == want
+            if members is not None:
+                assert m == members
+        else:
+            with pytest.raises(_native.GzipFailure) as ei:
+                _native.gunzip(blob, parallel=parallel)
+            f = ei.value
+            assert EXC[f.sub] is type(exc), (f.sub, f.message, exc)
+            assert f.message == str(exc)
+
+
+T = gfa_text(3000, 1)
+PARTS = [T[: len(T) // 3], T[len(T) // 3: 2 * len(T) // 3], T[2 * len(T) // 3:]]
+
+
+def test_empty_and_single():
+    check(b"", 0)
+    check(member(b""), 1)
+    check(member(T), 1)
+    check(member(T, level=0), 1)
+    check(member(T, level=9), 1)
+
+
+def test_multi_member_and_padding():
+    check(b"".join(member(p) for p in PARTS), 3)
+    check(member(PARTS[0]) + b"\x00" * 7 + member(PARTS[1]) + b"\x00" * 3, 2)
+    check(b"".join(member(T[i:i + 997]) for i in range(0, len(T), 997)))
+
+
+def test_header_fields():
+    check(member(T, flags=4, extra=b"BC\x02\x00\x00\x00"), 1)
+    check(member(T, flags=8, name=b"x.gfa") + member(T, flags=16, comment=b"hello"), 2)
+    check(member(T, flags=2 | 4 | 8 | 16, extra=b"ab", name=b"n", comment=b"c"), 1)
+    check(member(T, flags=2, hcrc=0x1234))  # wrong header CRC: gzip.py never checks it
+    check(member(T, flags=0x20))  # reserved flag bit: gzip.py ignores it, zlib would not
+
+
+def test_errors_match_gzip_module():
+    good = member(T)
+    check(b"\x00\x00" + good)  # leading zeros are not padding
+    check(good + b"xy")  # trailing garbage
+    check(good + b"x")  # a single trailing byte
+    check(good + b"\x00\x00x\x00")  # garbage after padding
+    check(b"\x1f")
+    check(b"ab")
+    check(good[:5])  # truncated header
+    check(good[: len(good) // 2])  # truncated deflate data
+    check(good[:-3])  # truncated trailer
+    check(member(T, method=7))
+    bad = bytearray(good)
+    bad[len(bad) // 2] ^= 0xFF
+    check(bytes(bad))  # corrupt deflate data (or a CRC error, whichever zlib meets)
+    crc = bytearray(good)
+    crc[-8] ^= 1
+    check(bytes(crc))
+    ln = bytearray(good)
+    ln[-1] ^= 1
+    check(bytes(ln))
+    check(member(T, flags=4, extra=b"abc")[:12])
+
+
+def test_embedded_gzip_is_not_a_member():
+    # a stored (level 0) member whose payload is itself a gzip file: its inner header is a member
+    # candidate that inflates cleanly, yet it is not on the member chain
+    inner = member(T) + member(PARTS[0])
+    check(member(inner, level=0) + member(PARTS[1]), 2)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_member_chains(seed):
+    r = random.Random(seed)
+    text = gfa_text(r.randint(100, 2000), seed) + bytes(r.randrange(256) for _ in range(200))
+    cuts = sorted(r.sample(range(1, len(text)), r.randint(0, 12)))
+    pieces = [text[a:b] for a, b in zip([0] + cuts, cuts + [len(text)])]
+    blob = b"".join(member(p, level=r.choice([0, 1, 6, 9])) + b"\x00" * r.choice([0, 0, 1, 5]) for p in pieces)
+    check(blob, len(pieces))
+    if r.random() < 0.5:
+        cut = r.randrange(len(blob))
+        check(blob[:cut])
