@@ -70,13 +70,18 @@ struct Ctl {
   unsigned long long s_late;          // an S-line touch follows an edge touch (claim round)
   unsigned long long row_gap;         // k_row_bounds met a run of empty rows too long to fill
   unsigned long long n_deferred;      // lines parsed from global memory after k_tile_parse
-  unsigned long long pad[1];
+  unsigned long long int_fail;        // the decimal-id dictionary (k_int_ids) does not apply
 };
 
 struct ParseOpts {
   int bidir, keep, strip, has_wt;
   uint32_t wt_len;
   const uint8_t* wt;  // device copy of the weight tag bytes
+  // decimal-id dictionary fused into the parse (see k_int_ids): when tid is set, every touch's
+  // node id is computed from its own bytes while the line is staged; n_st = S touches,
+  // n_seg = S lines.  A premise failure sets ctl->int_fail (the hash dictionary then runs).
+  uint32_t* tid;
+  uint64_t n_st, n_seg;
 };
 
 struct TouchOut {

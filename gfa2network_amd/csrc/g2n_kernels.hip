@@ -535,8 +535,68 @@ __device__ inline uint64_t rev_ori(const Src& in, uint64_t oo, uint32_t ol) {
   return kConstFlag | (plus ? '-' : '+');
 }
 
+// Decimal-id dictionary, fused into the parse (ParseOpts.tid).  When the GFA's S lines come
+// first and name their segments "1", "2", ..., "N" in order (the layout of vg / odgi / PGGB
+// graphs with compacted ids, and of the C4 generator), node ids need no table: Python's dict
+// gives S touch t the id t (the S-prefix dictionary), and an edge key equals an S key iff its
+// bytes are the canonical decimal of some v in [1, N] (no sign, no leading zero: str(v) is the
+// only spelling), plus ":+" / ":-" when bidirected (builders.py:194-198, 211-212).  So each
+// edge touch's id is arithmetic on bytes the parse already holds in LDS: v - 1 (bidirected:
+// 2(v - 1) + [ori == "-"]).  Any touch that breaks the premise — an S name that is not
+// str(k + 1) for its line k, an S touch after an edge touch, an edge key that is no S key (a
+// new node: first-touch order matters) — sets ctl->int_fail and the host runs the hash
+// dictionary instead.
+//
+// src_dec: the canonical decimal value of the name [o, o + l) of the source, false when the
+// bytes are not one.
+__device__ inline bool src_dec(const Src& in, uint64_t o, uint32_t l, uint64_t* v) {
+  if (l == 0 || l > 10) return false;
+  if (l <= 8) {  // SWAR: two aligned 8-byte reads, digit check and value in registers
+    const uint64_t a = o & ~7ull;
+    const uint32_t sh = (uint32_t)(o - a) * 8;
+    uint64_t w = in.word8_z(a) >> sh;
+    if (sh && (o - a) + l > 8) w |= in.word8_z(a + 8) << (64 - sh);
+    const uint64_t keep = l == 8 ? ~0ull : ((1ull << (8 * l)) - 1);
+    w &= keep;
+    const uint64_t zeros = 0x3030303030303030ull & keep;
+    if ((w & 0xF0F0F0F0F0F0F0F0ull & keep) != zeros ||
+        (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) != 0 ||
+        (w & 0xFF) == '0')
+      return false;
+    uint64_t d = (w - zeros) << (8 * (8 - l));  // digits, most significant first, left-padded with 0s
+    d = (d * 10 + (d >> 8)) & 0x00FF00FF00FF00FFull;
+    d = (d * 100 + (d >> 16)) & 0x0000FFFF0000FFFFull;
+    *v = (d * 10000 + (d >> 32)) & 0xFFFFFFFFull;
+    return true;
+  }
+  uint64_t x = 0;
+  for (uint32_t j = 0; j < l; j++) {
+    const uint32_t c = in[o + j];
+    if (c - '0' > 9u || (j == 0 && c == '0')) return false;
+    x = x * 10 + (c - '0');
+  }
+  *v = x;
+  return true;
+}
+
+// edge touch t: its id from its bytes, or false (no S key: the premise fails)
+__device__ inline bool int_edge_touch(const Src& in, const ParseOpts& op, uint64_t t, uint64_t no, uint32_t nl,
+                                      uint64_t oo, uint32_t ol) {
+  uint64_t v;
+  if (!src_dec(in, no, nl, &v) || v < 1 || v > op.n_seg) return false;
+  uint32_t id = (uint32_t)(v - 1);
+  if (op.bidir) {
+    const uint32_t oc = (oo & kConstFlag) ? (uint32_t)(oo & 0xFF) : (ol ? (uint32_t)in[oo] : 0u);
+    if (ol != 1 || (oc != '+' && oc != '-')) return false;
+    id = 2 * id + (oc == '-');
+  }
+  op.tid[t] = id;
+  return true;
+}
+
 // S line i, name = [ns, ne): parser.py:163, builders.py:190-198
-__device__ inline void put_segment(const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t ns, uint64_t ne) {
+__device__ inline void put_segment(const Src& in, const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t ns,
+                                   uint64_t ne, uint32_t& ifail) {
   const uint32_t nl = (uint32_t)(ne - ns);
   if (!op.bidir) {
     put_touch(T, tb, ns, nl, 0, 0, false, 1);
@@ -544,12 +604,18 @@ __device__ inline void put_segment(const ParseOpts& op, const TouchOut& T, uint6
     put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
     put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true, 1);
   }
+  if (op.tid && !ifail) {  // S touch tb is node tb: its name must be str(line + 1), line = tb / tps
+    uint64_t v;
+    const uint64_t line = op.bidir ? tb >> 1 : tb;
+    if (tb + (op.bidir ? 1 : 0) >= op.n_st || (op.bidir && (tb & 1)) || !src_dec(in, ns, nl, &v) || v != line + 1)
+      ifail = 1;
+  }
 }
 
 // L / E / C line i = [s, e) ('\n' stripped), its touches from tb, its edge eb
 __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_t e, uint64_t tb, uint64_t eb,
                                   const ParseOpts& op, const TouchOut& T, const EdgeOut& E, Ctl* ctl,
-                                  uint64_t* __restrict__ worklist) {
+                                  uint64_t* __restrict__ worklist, uint32_t& ifail) {
   EdgeLayout L = edge_layout(in, s, e);
   if (L.err) {
     record_error(ctl, i, L.err);
@@ -581,6 +647,14 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
       put_touch(T, tb + 3, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, true);
     }
   }
+  if (op.tid && !ifail) {
+    bool ok = int_edge_touch(in, op, tb, L.uo, L.ul, L.ouo, L.oul) &&
+              int_edge_touch(in, op, tb + 1, L.vo, L.vl, L.ovo, L.ovl);
+    if (ok && op.bidir && !op.keep)
+      ok = int_edge_touch(in, op, tb + 2, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1) &&
+           int_edge_touch(in, op, tb + 3, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1);
+    if (!ok) ifail = 1;
+  }
 }
 
 // Line i of kind k starting at s.  The source holds the bytes [.., bound); when nl_at_bound
@@ -588,7 +662,8 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
 // run past bound < len: the line is deferred.
 __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, bool nl_at_bound, uint64_t i,
                                   uint8_t k, uint64_t s, uint64_t tb, uint64_t eb, const ParseOpts& op,
-                                  const TouchOut& T, const EdgeOut& E, Ctl* ctl, uint64_t* __restrict__ worklist) {
+                                  const TouchOut& T, const EdgeOut& E, Ctl* ctl, uint64_t* __restrict__ worklist,
+                                  uint32_t& ifail) {
   const bool cut = bound < len;
   if (k == kS || k == kPO) {  // the first two (S) / three (P, O) fields
     uint64_t t1, t2;
@@ -607,7 +682,7 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
     }
     if (t2 == bound && cut) return false;
     if (k == kS) {
-      put_segment(op, T, tb, t1 + 1, t2);
+      put_segment(in, op, T, tb, t1 + 1, t2, ifail);
     } else if (t2 == bound || in[t2] == '\n') {
       record_error(ctl, i, in[s] == 'P' ? kErrMalformedP : kErrMalformedO);
     }
@@ -615,7 +690,7 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
   }
   const uint64_t e = nl_at_bound ? bound - 1 : next_nl(in, s, bound);
   if (e == bound && cut) return false;
-  parse_edge(in, i, s, e, tb, eb, op, T, E, ctl, worklist);
+  parse_edge(in, i, s, e, tb, eb, op, T, E, ctl, worklist, ifail);
   return true;
 }
 
@@ -686,6 +761,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = pre[j * kTPB + threadIdx.x];
   uint64_t t_run = b.touches, e_run = b.edges;
   unsigned long long unk = ~0ull;
+  uint32_t ifail = 0;
   for (uint32_t w0 = 0; w0 < n_starts; w0 += kTileLines) {
     const uint32_t n_win = n_starts - w0 < kTileLines ? n_starts - w0 : kTileLines;
     __syncthreads();  // `pre` (ranks, or the last window's prefixes) is no longer read
@@ -745,7 +821,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
         // the line ends where the next one starts; the window's last line: search the staged bytes
         const bool known = j + 1 < n_win;
         const uint64_t bound = known ? t0 + starts[j + 1] : w1;
-        if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist)) {
+        if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, ifail)) {
           const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
           deferred[d] = DeferredLine{i, (uint32_t)tb, (uint32_t)eb};
         }
@@ -756,6 +832,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   }
   unk = wave_reduce_min(unk);
   if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
+  if (__ballot(ifail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
 }
 
 // Lines whose fields run past their tile's staged window: parsed from global memory.
@@ -769,7 +846,9 @@ __global__ void __launch_bounds__(64) k_parse_deferred(const uint8_t* __restrict
   if (j >= n) return;
   const DeferredLine d = deferred[j];
   const Src G{in, 0, len};
-  parse_line(G, len, len, false, d.line, kind[d.line], ls[d.line], d.tb, d.eb, op, T, E, ctl, worklist);
+  uint32_t ifail = 0;
+  parse_line(G, len, len, false, d.line, kind[d.line], ls[d.line], d.tb, d.eb, op, T, E, ctl, worklist, ifail);
+  if (ifail) ctl->int_fail = 1;
 }
 
 // Exact weights (CPython int()/float() semantics) for the edges the fast grammar deferred.

@@ -391,8 +391,11 @@ struct DictOut {
   uint64_t n_nodes;
 };
 
+// decimal-id dictionary (ParseOpts.tid): done by the parse (tid final), or not applicable
+enum IntIds { kIntDone, kIntFailed };
+
 static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len, const TouchOut& T, uint64_t n_t,
-                                uint64_t n_st, uint64_t est, bool bidir) {
+                                uint64_t n_st, uint64_t est, bool bidir, IntIds int_ids) {
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
   // Table sized for the expected number of distinct keys; a bounded probe sequence flags
   // overflow and the insert is redone with a table sized for every touch (load <= 1/2,
@@ -456,6 +459,20 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
     // round 1 claims the S keys, their ranks are the node ids, one lookup round resolves every
     // other touch to its id.  Anything else is redone by the general rounds below.
     bool fast = !std::getenv("G2N_DICT_GENERAL");
+    if (int_ids == kIntDone) {  // decimal-id dictionary: the parse wrote every edge touch's id
+      hipLaunchKernelGGL(k_key_len, dim3(grid_for(n_st)), dim3(kTPB), 0, c->stream, TI, n_st, (int)bidir, klen);
+      phase(c, "ids_fast");
+      c->h_ctl->n_nodes = n_st;
+      G2N_HIP(hipMemcpyAsync(&c->ctl->n_nodes, &c->h_ctl->n_nodes, sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, c->stream));
+      DictOut D{};
+      D.slot = slot;
+      D.tid = dget<uint32_t>(c, S_TID, n_t);
+      D.klen = klen;
+      D.first = first;
+      D.n_nodes = n_st;
+      return D;
+    }
     if (fast) {
       init_table();
       n_first = (uint32_t)n_st;  // claim round: flags S touches past the first n_st
@@ -586,6 +603,12 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
              bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr,
              dget<uint8_t>(c, S_TKIND, n_t)};
   EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
+  const bool int_ids = !std::getenv("G2N_DICT_GENERAL") && !std::getenv("G2N_DICT_HASH");
+  if (int_ids && n_t) {  // decimal-id dictionary, computed by the parse itself
+    op.tid = dget<uint32_t>(c, S_TID, n_t);
+    op.n_st = n_s * tps;
+    op.n_seg = n_s;
+  }
   auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
   auto* deferred = dget<DeferredLine>(c, S_DEFER, n_lines);
   G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
@@ -649,7 +672,8 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   R->n_records_before_error = R->n_records;
 
   // ---- dictionary: first-touch node ids (K4)
-  const DictOut D = build_dictionary(c, in, len, T, n_t, n_s * tps, n_s * tps + (n_e * tpe) / 16 + 1024, bidir);
+  const DictOut D = build_dictionary(c, in, len, T, n_t, n_s * tps, n_s * tps + (n_e * tpe) / 16 + 1024, bidir,
+                                     op.tid && !c->h_ctl->int_fail ? kIntDone : kIntFailed);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
   const uint64_t n_nodes = D.n_nodes;
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
@@ -913,7 +937,7 @@ uint64_t dedup_keys(g2n_context* c, const uint8_t* blob, uint64_t blob_len, cons
   TouchOut T{dget<uint64_t>(c, S_NOFF, n), dget<uint32_t>(c, S_NLEN, n), nullptr, nullptr,
              dget<uint8_t>(c, S_TKIND, n)};
   hipLaunchKernelGGL(k_keys_to_touches, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, offs, n, T.noff, T.nlen, T.tkind);
-  const DictOut D = build_dictionary(c, blob, blob_len, T, n, n, n, false);
+  const DictOut D = build_dictionary(c, blob, blob_len, T, n, n, n, false, kIntFailed);
   hipLaunchKernelGGL(k_touch_ids, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, n, D.first, D.slot, D.table, D.tid,
                      (int)D.general, ids);
   if (D.n_nodes)

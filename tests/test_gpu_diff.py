@@ -317,3 +317,64 @@ def test_field_boundaries_near_mask_span_and_tiles(gpu, oracle_lib):
             a = outcome(gpu_run(data, mode, "float64", wt))
             b = outcome(oracle_run(oracle_lib, data, mode, "float64", wt))
             assert a == b, (mode, wt)
+
+
+def _decimal_gfa(seed: int, n_s: int, n_l: int) -> list[str]:
+    import random
+
+    r = random.Random(seed)
+    lines = ["H\tVN:Z:1.0\n"] + [f"S\t{k}\t{'ACGT'[k % 4] * (k % 5)}\n" for k in range(1, n_s + 1)]
+    lines += [f"L\t{r.randint(1, n_s)}\t{r.choice('+-')}\t{r.randint(1, n_s)}\t{r.choice('+-')}\t0M"
+              f"\tRC:i:{r.randint(1, 9)}\n" for _ in range(n_l)]
+    return lines
+
+
+DECIMAL_CASES = {
+    "canonical": lambda L: L,
+    "s_leading_zero": lambda L: L[:5] + ["S\t05\t*\n"] + L[6:],  # line 5 named "05", not "5"
+    "s_out_of_order": lambda L: L[:3] + [L[4], L[3]] + L[5:],
+    "s_after_l": lambda L: [x for x in L if not x.startswith("S\t9")] + [x for x in L if x.startswith("S\t9")],
+    "s_duplicate": lambda L: L + ["S\t1\t*\n"],
+    "edge_new_node": lambda L: L[:700] + ["L\t99999\t+\t1\t-\t0M\n"] + L[700:],
+    "edge_leading_zero": lambda L: L[:700] + ["L\t007\t+\t1\t-\t0M\n"] + L[700:],
+    "edge_zero": lambda L: L[:700] + ["L\t0\t+\t1\t-\t0M\n"] + L[700:],
+    "edge_eleven_digits": lambda L: L[:700] + ["L\t12345678901\t+\t1\t-\t0M\n"] + L[700:],
+    "edge_odd_orientation": lambda L: L[:700] + ["L\t3\t*\t4\t-\t0M\n"] + L[700:],
+    "edge_plus_sign": lambda L: L[:700] + ["L\t+3\t+\t4\t-\t0M\n"] + L[700:],
+    "edge_embedded_orientation": lambda L: L[:700] + ["L\t3+\t4-\t0M\t*\n"] + L[700:],
+    "s_name_hex": lambda L: L[:2] + ["S\t0x2\t*\n"] + L[3:],
+}
+
+
+@pytest.mark.parametrize("case", sorted(DECIMAL_CASES))
+def test_decimal_id_dictionary(gpu, oracle_lib, case):
+    """S lines naming "1".."N" in order give ids by arithmetic in the parse; every input that breaks
+    the premise falls back to the hash dictionary.  Either way the result is the oracle's."""
+    data = "".join(DECIMAL_CASES[case](_decimal_gfa(4, 400, 2400))).encode()
+    for mode in MODES:
+        st, ph = _phases(data, **mode)
+        assert st == 0
+        took = "table_init" not in ph and "ids_general" not in ph
+        if case == "canonical":
+            assert took, (mode, sorted(ph))
+        elif case not in ("edge_odd_orientation", "edge_embedded_orientation"):
+            assert not took, (case, mode, sorted(ph))
+        for dtype, wt in (("float64", "RC"), ("int32", None)):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
+            assert a == b, (case, mode, dtype, wt)
+
+
+def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
+    """The decimal-id path and the hash dictionary (G2N_DICT_HASH=1) agree bit for bit at 10^7 edges."""
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(2_000_000, 8_000_000, seed=3, rc_tag=True)
+    for mode in ({}, {"directed": False}, {"bidirected": True}):
+        a = outcome(gpu_run(data, mode, "float64", "RC"))
+        monkeypatch.setenv("G2N_DICT_HASH", "1")
+        st, ph = _phases(data, **mode)
+        assert "insert_lookup" in ph
+        b = outcome(gpu_run(data, mode, "float64", "RC"))
+        monkeypatch.delenv("G2N_DICT_HASH")
+        assert a == b, mode
