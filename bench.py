@@ -41,6 +41,7 @@ def _args():
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end leg (file on the page cache -> scipy CSR + node list in host memory)")
     ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
+    ap.add_argument("--no-alt", action="store_true", help="skip the hash-dictionary comparison build")
     ap.add_argument("--shard", action="store_true",
                     help="one file over the ranks (gfa2network_amd/shard.py): rank r's byte range is its own "
                          "workload-sized chunk; node names are shared across chunks (default: replicas)")
@@ -242,6 +243,15 @@ def main():
     elapsed = _max_over_ranks(world, elapsed)
 
     n_edges, n_nodes, nnz, in_bytes = int(res.n_edges), int(res.n_nodes), int(res.nnz), int(res.input_bytes)
+    # the same build through the hash dictionary (what inputs without decimal segment ids take)
+    t_h, hash_ph = None, None
+    if not args.no_alt:
+        os.environ["G2N_DICT_HASH"] = "1"
+        step()
+        t_h = time.perf_counter()
+        hash_ph = step()
+        t_h = time.perf_counter() - t_h
+        del os.environ["G2N_DICT_HASH"]
     w_dtype = 8
     ms_step = elapsed / args.steps * 1e3
     edges_total = n_edges * args.steps * world
@@ -256,7 +266,8 @@ def main():
                   names_bytes=int(res.names_bytes), bidir=bool(mode.get("bidirected")),
                   keep=bool(mode.get("keep_directed_bidir")), n_s=n_s, w_dtype=w_dtype,
                   directed_csr=bool(mode.get("keep_directed_bidir")) or (not mode.get("bidirected")
-                                                                        and mode.get("directed", True)))
+                                                                        and mode.get("directed", True)),
+                  lean="values" in phases[0], weighted=bool(mode.get("weight_tag")))
     cand = {ph: avg[ph] for ph in KERNEL_OF_PHASE if ph in avg}
     dom = max(cand, key=cand.get)
     dom_bytes, unit_desc = kernel_bytes(dom, **counts)
@@ -290,6 +301,12 @@ def main():
                      "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "per_unit": unit_desc,
                      "ms_per_launch": round(avg[dom], 3)},
     }
+    if t_h is not None:
+        line["alt_paths"] = {"hash_dictionary": {
+            "ms_per_step": round(t_h * 1e3, 3), "m_edges_per_s": round(n_edges / t_h / 1e6, 2),
+            "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
+            "note": "G2N_DICT_HASH=1: segment names resolved through the GPU hash table (inputs whose S lines "
+                    "are not named 1..N in order)"}}
     if dom in ("insert_claim", "insert_lookup"):
         tps = 2 if mode.get("bidirected") else 1
         tpe = 4 if (mode.get("bidirected") and not mode.get("keep_directed_bidir")) else 2
@@ -379,7 +396,7 @@ KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build (S-f
 
 
 def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bidir, keep, n_s, w_dtype,
-                 directed_csr=True):
+                 directed_csr=True, lean=False, weighted=False):
     """Algorithmic bytes one launch must move (inputs read once, outputs written once) and the
     per-unit figure it is built from."""
     tps = 2 if bidir else 1
@@ -387,6 +404,11 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
     n_t = n_s * tps + n_edges * tpe
     d_o = 12 if bidir else 0  # orientation descriptor (u64 off + u32 len) per touch
     avg_key = names_bytes / max(n_nodes, 1)
+    k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
+    if phase == "parse" and lean:  # decimal ids: S touch descriptors, COO coordinates (+ weights) per edge
+        per_s, per_e = 13 + d_o, 8 * k_trip + (8 if weighted else 0)
+        return (in_bytes + 9 * n_lines + per_s * n_s * tps + per_e * n_edges,
+                f"B_in + 9 B/line + {per_s} B/S touch + {per_e} B/edge (lean decimal-id parse)")
     if phase == "parse":  # every input byte once; line start + kind per line; descriptors per touch / edge
         per_t, per_e = 13 + d_o, 12
         return (in_bytes + 9 * n_lines + per_t * n_t + per_e * n_edges,
@@ -396,7 +418,6 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
         per = 1 + 12 + d_o + avg_key + 32 + 4  # state, descriptor, key bytes, 32-B entry, slot / node id
         return (int(n_t * 1 + k * (per - 1)), f"1 B/touch + {per - 1:.1f} B per processed touch ({k} touches)")
     if phase == "triplets":
-        k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
         per = 4 + 8 + tpe * 4 + k_trip * (4 + 4 + w_dtype)  # tb, w, node id per touch, COO out
         return n_edges * per, f"{per} B/edge"
     return in_bytes, "B_in"

@@ -82,6 +82,12 @@ struct ParseOpts {
   // n_seg = S lines.  A premise failure sets ctl->int_fail (the hash dictionary then runs).
   uint32_t* tid;
   uint64_t n_st, n_seg;
+  // lean mode (decimal ids only): the parse writes the stream-order COO coordinates itself —
+  // rows / cols of edge e at e * ktrip (the triplet layout of k_triplets) — and skips the edge
+  // touch descriptors, E.tb and (unweighted) E.w; a premise failure re-runs a full parse
+  int32_t* rows;
+  int32_t* cols;
+  uint32_t ktrip;
 };
 
 struct TouchOut {

@@ -470,6 +470,52 @@ __device__ inline EdgeLayout edge_layout(const Src& in, uint64_t s, uint64_t e) 
   return L;
 }
 
+// bits 0..3: which bytes of w are '\t' (tab) or '\t' / '\n' (with_nl)
+__device__ inline uint32_t delim_bits4(uint32_t w, bool with_nl) {
+  uint32_t m = byte_match_mask(w, 0x09090909u);
+  if (with_nl) m |= byte_match_mask(w, 0x0A0A0A0Au);
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+
+// The common L line, "L\tu\t[+-]\tv\t[+-]\t<overlap>[\t<tags>]" of at most 60 bytes, in 32-bit
+// arithmetic: its tab mask from aligned 4-byte words, then the fields.  Returns false for any
+// other shape (the general edge_layout then decides, errors included); when it returns true the
+// layout is exactly the one edge_layout gives (parser.py:206-227, the fields[2] in {+,-} branch).
+__device__ inline bool link_fast(const Src& in, uint64_t s, uint64_t e, EdgeLayout& L) {
+  const uint32_t n = (uint32_t)(e - s);
+  const uint64_t a = s & ~3ull;
+  const uint32_t sh = (uint32_t)(s - a);
+  const uint32_t nw = (sh + n + 3) >> 2;
+  if (n > 60 || a + 4ull * nw > in.lim) return false;
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < nw; j++) m |= (uint64_t)delim_bits4(in.word(a + 4ull * j), false) << (4 * j);
+  m >>= sh;
+  m &= (1ull << n) - 1;
+  if (__popcll(m) < 5) return false;
+  uint32_t p[6];
+  uint64_t r = m;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    p[k] = r ? (uint32_t)__builtin_ctzll(r) : n;
+    r &= r - 1;
+  }
+  if (p[2] - p[1] != 2 || p[4] - p[3] != 2) return false;
+  const uint32_t c2 = in[s + p[1] + 1], c4 = in[s + p[3] + 1];
+  if ((c2 != '+' && c2 != '-') || (c4 != '+' && c4 != '-')) return false;
+  L.err = 0;
+  L.uo = s + p[0] + 1;
+  L.ul = p[1] - p[0] - 1;
+  L.ouo = kConstFlag | c2;
+  L.oul = 1;
+  L.vo = s + p[2] + 1;
+  L.vl = p[3] - p[2] - 1;
+  L.ovo = s + p[3] + 1;
+  L.ovl = 1;
+  L.has_tags = p[5] < n;  // fields[6:]
+  L.tag_start = L.has_tags ? s + p[5] + 1 : e;
+  return true;
+}
+
 __device__ inline bool span_eq(const Src& in, uint64_t off, uint64_t len, const uint8_t* __restrict__ w,
                                uint32_t wl) {
   if (len != wl) return false;
@@ -579,18 +625,17 @@ __device__ inline bool src_dec(const Src& in, uint64_t o, uint32_t l, uint64_t* 
   return true;
 }
 
-// edge touch t: its id from its bytes, or false (no S key: the premise fails)
-__device__ inline bool int_edge_touch(const Src& in, const ParseOpts& op, uint64_t t, uint64_t no, uint32_t nl,
-                                      uint64_t oo, uint32_t ol) {
+// an edge touch's node id from its bytes, or false (no S key: the premise fails)
+__device__ inline bool int_edge_id(const Src& in, const ParseOpts& op, uint64_t no, uint32_t nl, uint64_t oo,
+                                   uint32_t ol, uint32_t* id) {
   uint64_t v;
   if (!src_dec(in, no, nl, &v) || v < 1 || v > op.n_seg) return false;
-  uint32_t id = (uint32_t)(v - 1);
+  *id = (uint32_t)(v - 1);
   if (op.bidir) {
     const uint32_t oc = (oo & kConstFlag) ? (uint32_t)(oo & 0xFF) : (ol ? (uint32_t)in[oo] : 0u);
     if (ol != 1 || (oc != '+' && oc != '-')) return false;
-    id = 2 * id + (oc == '-');
+    *id = 2 * *id + (oc == '-');
   }
-  op.tid[t] = id;
   return true;
 }
 
@@ -616,7 +661,8 @@ __device__ inline void put_segment(const Src& in, const ParseOpts& op, const Tou
 __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_t e, uint64_t tb, uint64_t eb,
                                   const ParseOpts& op, const TouchOut& T, const EdgeOut& E, Ctl* ctl,
                                   uint64_t* __restrict__ worklist, uint32_t& ifail) {
-  EdgeLayout L = edge_layout(in, s, e);
+  EdgeLayout L;
+  if (!link_fast(in, s, e, L)) L = edge_layout(in, s, e);
   if (L.err) {
     record_error(ctl, i, L.err);
     return;
@@ -634,6 +680,33 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
       w = 0.0;
     }
   }
+  if (op.rows) {  // lean: ids straight into the COO coordinates (k_triplets' layout)
+    if (op.has_wt) E.w[eb] = w;
+    if (ifail) return;
+    uint32_t a, b, c = 0, d = 0;
+    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b);
+    if (ok && op.ktrip == 4)
+      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c) &&
+           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d);
+    if (!ok) {
+      ifail = 1;
+      return;
+    }
+    const uint64_t o = eb * op.ktrip;
+    op.rows[o] = (int32_t)a;
+    op.cols[o] = (int32_t)b;
+    if (op.ktrip >= 2) {
+      op.rows[o + 1] = (int32_t)b;
+      op.cols[o + 1] = (int32_t)a;
+    }
+    if (op.ktrip == 4) {
+      op.rows[o + 2] = (int32_t)c;
+      op.cols[o + 2] = (int32_t)d;
+      op.rows[o + 3] = (int32_t)d;
+      op.cols[o + 3] = (int32_t)c;
+    }
+    return;
+  }
   E.w[eb] = w;
   E.tb[eb] = (uint32_t)tb;
   if (!op.bidir) {
@@ -648,12 +721,21 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
     }
   }
   if (op.tid && !ifail) {
-    bool ok = int_edge_touch(in, op, tb, L.uo, L.ul, L.ouo, L.oul) &&
-              int_edge_touch(in, op, tb + 1, L.vo, L.vl, L.ovo, L.ovl);
+    uint32_t a, b, c = 0, d = 0;
+    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b);
     if (ok && op.bidir && !op.keep)
-      ok = int_edge_touch(in, op, tb + 2, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1) &&
-           int_edge_touch(in, op, tb + 3, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1);
-    if (!ok) ifail = 1;
+      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c) &&
+           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d);
+    if (!ok) {
+      ifail = 1;
+    } else {
+      op.tid[tb] = a;
+      op.tid[tb + 1] = b;
+      if (op.bidir && !op.keep) {
+        op.tid[tb + 2] = c;
+        op.tid[tb + 3] = d;
+      }
+    }
   }
 }
 
@@ -666,12 +748,24 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
                                   uint32_t& ifail) {
   const bool cut = bound < len;
   if (k == kS || k == kPO) {  // the first two (S) / three (P, O) fields
-    uint64_t t1, t2;
-    const uint64_t m = delim_mask(in, s, bound - s, true);
-    if (__popcll(m) >= 2) {  // both delimiters among the first 64 bytes
-      t1 = s + __builtin_ctzll(m);
-      t2 = s + __builtin_ctzll(m & (m - 1));
-    } else {
+    uint64_t t1 = bound, t2 = bound;
+    {  // the first two delimiters, 4-byte words at a time (stops at the second, or after 64 bytes)
+      const uint64_t lim = (bound < s + kMaskSpan ? bound : s + kMaskSpan);
+      uint32_t found = 0;
+      for (uint64_t a = s & ~3ull; a < lim && found < 2 && a + 4 <= in.lim; a += 4) {
+        uint32_t b = delim_bits4(in.word(a), true);
+        if (a < s) b &= 0xFu << (uint32_t)(s - a);
+        if (a + 4 > lim) b &= (1u << (uint32_t)(lim - a)) - 1u;
+        while (b && found < 2) {
+          const uint64_t q = a + (uint64_t)__builtin_ctz(b);
+          b &= b - 1;
+          if (found++ == 0) t1 = q;
+          else t2 = q;
+        }
+      }
+      if (found < 2) t1 = t2 = bound;
+    }
+    if (t2 == bound) {  // not both delimiters among the first 64 bytes
       t1 = next_delim(in, s, bound);
       if (t1 == bound && cut) return false;
       t2 = t1 < bound ? next_delim(in, t1 + 1, bound) : bound;
@@ -1421,6 +1515,27 @@ __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const
     cols[o + 3] = c;
     data[o + 3] = v;
   }
+}
+
+// Lean decimal-id builds: the parse wrote rows / cols; this writes the values (k_triplets'
+// cast, errors and float32-overflow count) when an output needs them.  uniform: no weight tag,
+// every value is dtype(1.0) (no cast can fail).
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_values(const double* __restrict__ w, uint64_t n_e, int ktrip, int uniform,
+                                                 T* __restrict__ data, Ctl* ctl) {
+  const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (e >= n_e) return;
+  const double wv = uniform ? 1.0 : w[e];
+  T v;
+  const uint32_t err = Cast<T>::go(wv, &v);
+  if (std::is_same<T, float>::value && !__builtin_isinf(wv) && wv == wv && __builtin_isinf((double)v))
+    atomicAdd(&ctl->n_f32_overflow, 1ull);
+  const uint64_t o = e * (uint64_t)ktrip;
+  if (err) {
+    atomicMin(&ctl->cast_key, (unsigned long long)((o << 4) | err));
+    return;
+  }
+  for (int j = 0; j < ktrip; j++) data[o + j] = v;
 }
 
 // ======================================================= K7-K9: COO -> CSR ========
@@ -2198,6 +2313,7 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
                                                  const uint32_t*, const RowVal<T, U>::type*, T, uint64_t,        \
                                                  uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);
 #define G2N_INST(T)                                                                                              \
+  template __global__ void k_values<T>(const double*, uint64_t, int, int, T*, Ctl*);                             \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
   template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, uint32_t*,    \

@@ -198,9 +198,15 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
     if (kU) {
       auto* pc_in = dget<uint32_t>(c, S_VALS0, n);
       pc_out = dget<uint32_t>(c, S_VALS1, n);
-      hipLaunchKernelGGL((k_pack<T, true>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n,
-                         transposed, base, key_in, (PV<T>*)nullptr, pc_in);
-      sort_pairs_u32<uint32_t>(c, key_in, key_out, pc_in, pc_out, n, bits);
+      if (base == 0) {  // the coordinates are the sort's input as they are (rocPRIM leaves inputs intact)
+        const uint32_t* r = (const uint32_t*)rows;
+        const uint32_t* q = (const uint32_t*)cols;
+        sort_pairs_u32<uint32_t>(c, transposed ? q : r, key_out, transposed ? r : q, pc_out, n, bits);
+      } else {
+        hipLaunchKernelGGL((k_pack<T, true>), dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, data, n,
+                           transposed, base, key_in, (PV<T>*)nullptr, pc_in);
+        sort_pairs_u32<uint32_t>(c, key_in, key_out, pc_in, pc_out, n, bits);
+      }
       scr_a = key_in;
       scr_b = pc_in;
     } else {
@@ -544,6 +550,23 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
   return D;
 }
 
+// Does the first S line (within the first 64 KiB) name segment "1"?  Chooses whether the parse
+// tries the decimal-id dictionary; a wrong guess only costs a second parse.
+static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len) {
+  const size_t n = (size_t)std::min<uint64_t>(len, 1 << 16);
+  if (n == 0) return false;
+  std::vector<uint8_t> h(n);
+  G2N_HIP(hipMemcpyAsync(h.data(), in, n, hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  for (size_t p = 0; p + 3 < n;) {
+    if (h[p] == 'S' && h[p + 1] == '\t') return h[p + 2] == '1' && (h[p + 3] == '\t' || h[p + 3] == '\n');
+    const void* q = std::memchr(h.data() + p, '\n', n - p);
+    if (!q) break;
+    p = (size_t)((const uint8_t*)q - h.data()) + 1;
+  }
+  return true;  // no S line seen yet (long header lines): try
+}
+
 static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   R->input_bytes = len;
@@ -603,8 +626,17 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
              bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr,
              dget<uint8_t>(c, S_TKIND, n_t)};
   EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
-  const bool int_ids = !std::getenv("G2N_DICT_GENERAL") && !std::getenv("G2N_DICT_HASH");
-  if (int_ids && n_t) {  // decimal-id dictionary, computed by the parse itself
+  const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
+  const uint64_t n_trip = n_e * (uint64_t)ktrip;
+  if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 matrix entries");
+  auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
+  auto* cols = dget<int32_t>(c, S_COLS, n_trip);
+  // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
+  // the first S line names "1" (a cheap guess: a wrong one costs one extra parse)
+  const bool int_ids = n_t && !std::getenv("G2N_DICT_GENERAL") && !std::getenv("G2N_DICT_HASH") &&
+                       first_segment_is_one(c, in, len);
+  const bool lean = int_ids && !std::getenv("G2N_NO_LEAN");
+  if (int_ids) {
     op.tid = dget<uint32_t>(c, S_TID, n_t);
     op.n_st = n_s * tps;
     op.n_seg = n_s;
@@ -613,16 +645,38 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   auto* deferred = dget<DeferredLine>(c, S_DEFER, n_lines);
   G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   phase(c, "_prep");
-  if (n_tiles)
-    hipLaunchKernelGGL(k_tile_parse, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe, op,
-                       ls, kind, T, E, c->ctl, wl, deferred);
-  sync_ctl(c);
-  const uint64_t n_def = c->h_ctl->n_deferred;
-  if (n_def)
-    hipLaunchKernelGGL(k_parse_deferred, dim3(grid_for(n_def, 64)), dim3(64), 0, c->stream, in, len, ls, kind,
-                       deferred, n_def, op, T, E, c->ctl, wl);
-  phase(c, "parse");
-  sync_ctl(c);
+  auto parse = [&](const ParseOpts& po) {
+    if (n_tiles)
+      hipLaunchKernelGGL(k_tile_parse, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe,
+                         po, ls, kind, T, E, c->ctl, wl, deferred);
+    sync_ctl(c);
+    const uint64_t n_def = c->h_ctl->n_deferred;
+    if (n_def)
+      hipLaunchKernelGGL(k_parse_deferred, dim3(grid_for(n_def, 64)), dim3(64), 0, c->stream, in, len, ls, kind,
+                         deferred, n_def, po, T, E, c->ctl, wl);
+    phase(c, "parse");
+    sync_ctl(c);
+  };
+  bool lean_done = false;
+  if (lean) {
+    ParseOpts lo = op;
+    lo.rows = rows;
+    lo.cols = cols;
+    lo.ktrip = (uint32_t)ktrip;
+    parse(lo);
+    lean_done = !c->h_ctl->int_fail || c->h_ctl->err_key != ~0ull;
+    if (!lean_done) {  // not decimal ids after all: a full parse for the hash dictionary
+      c->h_ctl->wl_count = c->h_ctl->n_deferred = c->h_ctl->int_fail = 0;
+      G2N_HIP(hipMemcpyAsync(&c->ctl->wl_count, &c->h_ctl->wl_count, sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, c->stream));
+      G2N_HIP(hipMemcpyAsync(&c->ctl->n_deferred, &c->h_ctl->n_deferred, sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, c->stream));
+      G2N_HIP(hipMemcpyAsync(&c->ctl->int_fail, &c->h_ctl->int_fail, sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, c->stream));
+      op.tid = nullptr;
+    }
+  }
+  if (!lean_done) parse(op);
   const uint64_t n_work = c->h_ctl->wl_count;
   if (n_work) {
     hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, len, ls, wl, n_work, op, E,
@@ -674,6 +728,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   // ---- dictionary: first-touch node ids (K4)
   const DictOut D = build_dictionary(c, in, len, T, n_t, n_s * tps, n_s * tps + (n_e * tpe) / 16 + 1024, bidir,
                                      op.tid && !c->h_ctl->int_fail ? kIntDone : kIntFailed);
+  const bool coords_done = lean_done;  // the parse wrote rows / cols
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
   const uint64_t n_nodes = D.n_nodes;
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
@@ -704,22 +759,35 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   }
 
   // ---- triplets (K6): stream-order COO with the dtype cast
-  const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
-  const uint64_t n_trip = n_e * (uint64_t)ktrip;
-  if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 matrix entries");
-  auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
-  auto* cols = dget<int32_t>(c, S_COLS, n_trip);
   void* data = dbuf(c, S_DATA, n_trip * dtype_size(dt));
+  const bool uni = !op.has_wt;  // no weight tag: every entry is dtype(1.0)
+  const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
-  switch (dt) {
-    case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
-    case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
-    default: run_triplets<double>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+  if (coords_done) {  // values only, and only when the output or the sums read them
+    if (n_e && (coo_out || !uni)) {
+#define G2N_VALUES(T) \
+  hipLaunchKernelGGL(k_values<T>, dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E.w, n_e, ktrip, (int)uni, (T*)data, c->ctl)
+      switch (dt) {
+        case G2N_BOOL: G2N_VALUES(uint8_t); break;
+        case G2N_INT8: G2N_VALUES(int8_t); break;
+        case G2N_INT32: G2N_VALUES(int32_t); break;
+        case G2N_FLOAT32: G2N_VALUES(float); break;
+        default: G2N_VALUES(double); break;
+      }
+#undef G2N_VALUES
+    }
+    phase(c, "values");
+  } else {
+    switch (dt) {
+      case G2N_BOOL: run_triplets<uint8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+      case G2N_INT8: run_triplets<int8_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+      case G2N_INT32: run_triplets<int32_t>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+      case G2N_FLOAT32: run_triplets<float>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+      default: run_triplets<double>(c, EI, n_e, D.slot, D.table, D.tid, (int)tpe, gd, rows, cols, data); break;
+    }
+    phase(c, "triplets");
   }
-  phase(c, "triplets");
   sync_ctl(c);
   const uint64_t cast_key = c->h_ctl->cast_key;
   R->n_cast_overflow = (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip);
@@ -730,8 +798,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     finish_timings(c, R);
     return R->status;
   }
-  const bool uni = !op.has_wt;  // no weight tag: every entry is dtype(1.0)
-  if ((o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO) {  // builders.py:281: the COO itself
+  if (coo_out) {  // builders.py:281: the COO itself
     R->format = G2N_FMT_COO;
     R->nnz = (int64_t)n_trip;
     R->rows = rows;

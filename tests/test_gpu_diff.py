@@ -366,15 +366,21 @@ def test_decimal_id_dictionary(gpu, oracle_lib, case):
 
 
 def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
-    """The decimal-id path and the hash dictionary (G2N_DICT_HASH=1) agree bit for bit at 10^7 edges."""
+    """The lean decimal-id parse (coordinates written by the parse), the non-lean one (G2N_NO_LEAN:
+    ids per touch, then k_triplets) and the hash dictionary (G2N_DICT_HASH) agree bit for bit at
+    10^7 edges, weighted and not, COO and CSR outputs."""
     from gfa2network_amd import synth
 
     data = synth.host_bytes(2_000_000, 8_000_000, seed=3, rc_tag=True)
-    for mode in ({}, {"directed": False}, {"bidirected": True}):
-        a = outcome(gpu_run(data, mode, "float64", "RC"))
-        monkeypatch.setenv("G2N_DICT_HASH", "1")
-        st, ph = _phases(data, **mode)
-        assert "insert_lookup" in ph
-        b = outcome(gpu_run(data, mode, "float64", "RC"))
-        monkeypatch.delenv("G2N_DICT_HASH")
-        assert a == b, mode
+    for mode in ({}, {"directed": False}, {"bidirected": True}, {"bidirected": True, "keep_directed_bidir": True}):
+        for wt in ("RC", None):
+            st, ph = _phases(data, **mode)
+            assert "values" in ph and "triplets" not in ph and "table_init" not in ph, sorted(ph)
+            a = outcome(gpu_run(data, mode, "float64", wt))
+            for env in ("G2N_NO_LEAN", "G2N_DICT_HASH"):
+                monkeypatch.setenv(env, "1")
+                st, ph = _phases(data, **mode)
+                assert "triplets" in ph and (("insert_lookup" in ph) == (env == "G2N_DICT_HASH")), (env, sorted(ph))
+                b = outcome(gpu_run(data, mode, "float64", wt))
+                monkeypatch.delenv(env)
+                assert a == b, (mode, wt, env)

@@ -13,6 +13,6 @@ P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR S
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --kernel-include-regex "$RE" --output-format csv -d $R/gpurun_out/$NAME/p$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > $R/gpurun_out/$NAME/p$i.log 2>&1 || { tail -20 $R/gpurun_out/$NAME/p$i.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --kernel-include-regex "$RE" --output-format csv -d $R/gpurun_out/$NAME/p$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-alt > $R/gpurun_out/$NAME/p$i.log 2>&1 || { tail -20 $R/gpurun_out/$NAME/p$i.log; exit 1; }
 done
 ls $R/gpurun_out/$NAME/*/
