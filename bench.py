@@ -183,6 +183,25 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
                               "python_objects": round((t2 - t1) * 1e3, 1)},
                 "nnz": int(C.nnz), "n_nodes": len(nodes)}
             del A, C, nodes, raw
+        # the convert CLI end to end (cli.py:193-250): gzip file -> .npz + .nodes.tsv on disk
+        from gfa2network_amd.cli import main as cli_main
+
+        npz = os.path.join(tmp, "c.npz")
+        argv = ["convert", gz, "--matrix", npz] + (["--undirected"] if not mode.get("directed", True) else []) + \
+            (["--bidirected"] if mode.get("bidirected") else []) + \
+            (["--weight-tag", mode["weight_tag"]] if mode.get("weight_tag") else [])
+        import contextlib
+        import io
+
+        with contextlib.redirect_stdout(io.StringIO()):
+            t0 = time.perf_counter()
+            cli_main(argv)
+            wall = time.perf_counter() - t0
+        out["cli_convert_gzip"] = {
+            "argv": "convert c.gfa.gz --matrix c.npz" + ("".join(" " + a for a in argv[4:])),
+            "wall_s": round(wall, 3), "m_edges_per_s": round(n_l / wall / 1e6, 2),
+            "npz_bytes": os.path.getsize(npz), "nodes_tsv_bytes": os.path.getsize(npz + ".nodes.tsv"),
+            "writers": "native (g2n_write_npz / g2n_write_node_map, host threads)"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     ref = {"C4": 1295.5}.get(wl.name)  # reference parse_gfa+convert_format, gzip C4, 1 core

@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
-    "g2n_gunzip", "g2n_free", "g2n_join_names",
+    "g2n_gunzip", "g2n_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
 
@@ -162,6 +162,12 @@ def load() -> ctypes.CDLL:
     lib.g2n_free.argtypes = [P]
     lib.g2n_join_names.argtypes = [P, P, U64, ctypes.c_uint8, P]
     lib.g2n_join_names.restype = ctypes.c_int
+    lib.g2n_write_npz.argtypes = [ctypes.c_char_p, I32, P, P, P, P, P, I32]
+    lib.g2n_write_npz.restype = ctypes.c_int
+    lib.g2n_write_node_map.argtypes = [ctypes.c_char_p, P, P, U64, I32, ctypes.POINTER(I64)]
+    lib.g2n_write_node_map.restype = ctypes.c_int
+    lib.g2n_first_bad_utf8.argtypes = [P, P, U64]
+    lib.g2n_first_bad_utf8.restype = I64
     for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair"):
         getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:
@@ -373,6 +379,47 @@ def join_names(blob: np.ndarray, offsets: np.ndarray, sep: int = 0x0A) -> bytear
         if rc != OK:
             raise RuntimeError(f"{status_name(rc)}: {last_error()}")
     return out
+
+
+def _io_error(rc: int, path: str):
+    return OSError(last_error()) if rc == E_IO else RuntimeError(f"{status_name(rc)}: {last_error()}")
+
+
+def write_npz(path: str, members: list[tuple[str, bytes, np.ndarray]], level: int = -1) -> None:
+    """numpy savez_compressed's zip64 layout, members deflated on host threads (g2n_write_npz).
+    members: (name, .npy header bytes, C-contiguous array whose raw bytes follow the header)."""
+    lib = load()
+    n = len(members)
+    names = (ctypes.c_char_p * n)(*[m[0].encode() for m in members])
+    heads_b = [m[1] for m in members]
+    heads = (ctypes.c_char_p * n)(*heads_b)
+    hl = (ctypes.c_uint64 * n)(*[len(h) for h in heads_b])
+    arrs = [np.ascontiguousarray(m[2]) for m in members]
+    datas = (ctypes.c_void_p * n)(*[a.ctypes.data if a.nbytes else None for a in arrs])
+    dl = (ctypes.c_uint64 * n)(*[a.nbytes for a in arrs])
+    rc = lib.g2n_write_npz(os.fsencode(path), n, names, heads, hl, datas, dl, level)
+    if rc != OK:
+        raise _io_error(rc, path)
+
+
+def write_node_map(path: str, blob: np.ndarray, offsets: np.ndarray, check_utf8: bool) -> int:
+    """save_node_map from the names blob (g2n_write_node_map); returns the first id whose name is
+    not UTF-8 (only the lines before it were written), or -1."""
+    lib = load()
+    n = len(offsets) - 1
+    bad = ctypes.c_int64(-1)
+    rc = lib.g2n_write_node_map(os.fsencode(path), blob.ctypes.data if blob.size else None,
+                                offsets.ctypes.data, max(n, 0), int(check_utf8), ctypes.byref(bad))
+    if rc != OK:
+        raise _io_error(rc, path)
+    return int(bad.value)
+
+
+def first_bad_utf8(blob: np.ndarray, offsets: np.ndarray) -> int:
+    n = len(offsets) - 1
+    if n <= 0:
+        return -1
+    return int(load().g2n_first_bad_utf8(blob.ctypes.data if blob.size else None, offsets.ctypes.data, n))
 
 
 def device_count() -> int:

@@ -28,7 +28,7 @@ import scipy.sparse as sp
 from . import _native as nat
 from ._native import RawResult
 
-__all__ = ["parse_gfa", "convert_format", "finalize", "raise_for_status"]
+__all__ = ["parse_gfa", "parse_gfa_names", "convert_format", "finalize", "raise_for_status", "save_npz"]
 
 _MALFORMED = {
     nat.E_MALFORMED_L: "L", nat.E_MALFORMED_E: "E", nat.E_MALFORMED_C: "C",
@@ -180,6 +180,39 @@ def parse_gfa(
                     verbose=verbose, build_matrix=build_matrix, path=path)
 
 
+def parse_gfa_names(path, *, raw_bytes_id: bool = False, **kw):
+    """``parse_gfa(path, build_graph=False, build_matrix=True, return_node_list=True, ...)`` for
+    writers that never need the Python list (the convert CLI): returns ``(A, blob, offsets)``, the
+    node names as the library's blob + offsets in id order.  A name that is not UTF-8 raises
+    here unless raw_bytes_id, exactly where building the list would (builders.py:284-288)."""
+    if kw.get("backend", "networkx") == "igraph":
+        raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
+    if kw.pop("split_on_alignment", False):
+        raise NotImplementedError("split_on_alignment is outside the GPU GFA->CSR path")
+    if kw.pop("build_graph", False):
+        raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
+    for k in ("store_seq", "store_tags", "max_tag_mb", "backend"):
+        kw.pop(k, None)
+    verbose = kw.pop("verbose", False)
+    device = kw.pop("device", 0)
+    dt = _dtype_of(kw.pop("dtype", "float64"))
+    wt = kw.pop("weight_tag", None)
+    opts = nat.make_options(dtype=dt.name, weight_tag=wt or None, output=nat.OUT_PARSE, want_node_names=True,
+                            device=device, **kw)
+    raw = _run(path, opts)
+    A = finalize(raw, dtype=dt, return_node_list=False, raw_bytes_id=raw_bytes_id, verbose=verbose, path=path)
+    blob, offs = raw.names_blob, raw.names_offsets
+    if offs is None:
+        offs = np.zeros(1, dtype=np.int64)
+        blob = np.zeros(0, dtype=np.uint8)
+    if not raw_bytes_id:
+        bad = nat.first_bad_utf8(blob, offs)
+        if bad >= 0:
+            bytes(blob[offs[bad]:offs[bad + 1]]).decode()
+            raise AssertionError("decode of the reported name unexpectedly succeeded")
+    return A, blob, offs
+
+
 def _run(path, opts) -> RawResult:
     """GFAParser's source rules (parser.py:95-112): file object, '-' = stdin, else a path."""
     if hasattr(path, "read"):
@@ -241,7 +274,7 @@ def save_matrix(A, dest: Path, *, verbose: bool = False, max_dense_gb: float = 5
         start = time.perf_counter()
         print(f"[save] {dest.suffix[1:]} → {dest}", "...", end="", file=sys.stderr, flush=True)
     if dest.suffix == ".npz":
-        sp.save_npz(dest, A)
+        save_npz(dest, A)
     elif dest.suffix == ".npy":
         np.save(dest, A.toarray() if sp.issparse(A) else A)
     elif dest.suffix == ".csv":
@@ -250,6 +283,61 @@ def save_matrix(A, dest: Path, *, verbose: bool = False, max_dense_gb: float = 5
         raise ValueError("matrix path must end with .npz, .npy, or .csv")
     if verbose:
         print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
+
+
+def _npy_header(val: np.ndarray) -> bytes:
+    """The .npy header numpy.lib.format.write_array puts before val's bytes."""
+    import io
+
+    from numpy.lib import format as npf
+
+    bio = io.BytesIO()
+    npf._write_array_header(bio, npf.header_data_from_array_1_0(val), None)
+    return bio.getvalue()
+
+
+def save_npz(file, matrix, compressed: bool = True) -> None:
+    """scipy.sparse.save_npz (scipy 1.15 _matrix_io.py, members in its order) with the zip written
+    natively: members deflated on host threads (g2n_write_npz), numpy's zip64 layout; loads with
+    scipy.sparse.load_npz / numpy.load.  Uncompressed or unsupported formats fall back to scipy."""
+    fmt = matrix.format
+    if not compressed or fmt not in ("csr", "csc", "bsr", "coo") or fmt == "bsr":
+        sp.save_npz(file, matrix, compressed=compressed)
+        return
+    path = os.fspath(file)
+    if not path.endswith(".npz"):  # numpy _savez
+        path = path + ".npz"
+    members = {}
+    if fmt in ("csr", "csc"):
+        members.update(indices=matrix.indices, indptr=matrix.indptr)
+    else:
+        members.update(row=matrix.row, col=matrix.col)
+    members.update(format=fmt.encode("ascii"), shape=matrix.shape, data=matrix.data)
+    if isinstance(matrix, sp.sparray):
+        members.update(_is_array=True)
+    out = []
+    for key, val in members.items():
+        val = np.asanyarray(val)
+        if val.dtype.hasobject:
+            sp.save_npz(file, matrix, compressed=compressed)
+            return
+        arr = val if val.flags.c_contiguous else np.ascontiguousarray(val)
+        out.append((key + ".npy", _npy_header(val), arr.reshape(-1).view(np.uint8) if arr.size else arr))
+    with open(path, "wb"):  # the reference's zipfile.ZipFile(path, "w") open: same OSError cases
+        pass
+    nat.write_npz(path, out, int(os.environ.get("G2N_NPZ_LEVEL", "-1")))
+
+
+def save_node_map_native(blob: np.ndarray, offsets: np.ndarray, dest: Path, raw_bytes_id: bool) -> None:
+    """save_node_map (utils.py:108-114) from the names blob, written on host threads.  raw_bytes_id:
+    names are decoded while writing, so the first non-UTF-8 name raises after the lines before it
+    were written, as in the reference."""
+    with open(dest, "w"):  # the reference's open(dest, "w"): same OSError cases
+        pass
+    bad = nat.write_node_map(str(dest), blob, offsets, check_utf8=raw_bytes_id)
+    if bad >= 0:
+        bytes(blob[offsets[bad]:offsets[bad + 1]]).decode()
+        raise AssertionError("decode of the reported name unexpectedly succeeded")
 
 
 def save_node_map(nodes, dest: Path) -> None:

@@ -13,7 +13,7 @@ import sys
 from pathlib import Path
 
 from . import __version__
-from .api import convert_format, parse_gfa, save_matrix, save_node_map
+from .api import convert_format, parse_gfa, parse_gfa_names, save_matrix, save_node_map_native
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -65,10 +65,7 @@ def main(argv: list[str] | None = None) -> None:
         parser.error("--graph (NetworkX / igraph objects) is outside the GPU GFA->CSR path")
     print(f"Using backend: {args.backend}")
     want_nodes = not args.no_node_map
-    result = parse_gfa(
-        args.gfa,
-        build_graph=False,
-        build_matrix=True,
+    kw = dict(
         directed=args.directed,
         weight_tag=args.weight_tag,
         store_seq=args.store_seq,
@@ -81,19 +78,21 @@ def main(argv: list[str] | None = None) -> None:
         dtype=args.dtype,
         asymmetric=args.asymmetric,
         raw_bytes_id=args.raw_bytes_id,
-        return_node_list=want_nodes,
         max_tag_mb=args.max_tag_mb,
         split_on_alignment=args.split_on_alignment,
         device=args.device,
     )
-    A, nodes = result if want_nodes else (result, None)
+    if want_nodes:  # names stay a blob: the sidecar is written natively (no Python list)
+        A, blob, offs = parse_gfa_names(args.gfa, **kw)
+    else:
+        A = parse_gfa(args.gfa, build_graph=False, build_matrix=True, return_node_list=False, **kw)
     A = convert_format(A, args.matrix_format, verbose=args.verbose)
     try:
         save_matrix(A, Path(args.matrix), verbose=args.verbose, max_dense_gb=args.max_dense_gb)
     except MemoryError as exc:
         raise SystemExit(str(exc)) from exc
     if want_nodes:
-        save_node_map(nodes, Path(str(args.matrix) + ".nodes.tsv"))
+        save_node_map_native(blob, offs, Path(str(args.matrix) + ".nodes.tsv"), args.raw_bytes_id)
 
 
 if __name__ == "__main__":  # pragma: no cover

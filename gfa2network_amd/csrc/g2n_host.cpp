@@ -304,6 +304,40 @@ int g2n_join_names(const uint8_t* blob, const int64_t* offsets, uint64_t n_names
   });
 }
 
+int g2n_write_npz(const char* path, int32_t n_members, const char* const* names, const uint8_t* const* heads,
+                  const uint64_t* head_lens, const void* const* datas, const uint64_t* data_lens, int32_t level) {
+  if (!path || n_members < 0 || (n_members && (!names || !heads || !head_lens || !datas || !data_lens)))
+    return G2N_E_ARG;
+  return g2n::guarded(
+      [&] { return g2n::write_npz(path, n_members, names, heads, head_lens, datas, data_lens, level); });
+}
+
+int g2n_write_node_map(const char* path, const uint8_t* blob, const int64_t* offsets, uint64_t n_names,
+                       int32_t check_utf8, int64_t* bad_index) {
+  if (!path || (n_names && (!blob || !offsets))) return G2N_E_ARG;
+  if (bad_index) *bad_index = -1;
+  return g2n::guarded([&]() -> int {
+    uint64_t n = n_names;
+    if (check_utf8) {
+      const int64_t bad = g2n::first_bad_utf8(blob, offsets, n_names);
+      if (bad >= 0) {
+        n = (uint64_t)bad;
+        if (bad_index) *bad_index = bad;
+      }
+    }
+    return g2n::write_node_map(path, blob, offsets, n);
+  });
+}
+
+int64_t g2n_first_bad_utf8(const uint8_t* blob, const int64_t* offsets, uint64_t n_names) {
+  if (!n_names || !blob || !offsets) return -1;
+  try {
+    return g2n::first_bad_utf8(blob, offsets, n_names);
+  } catch (...) {
+    return -1;
+  }
+}
+
 void g2n_result_free(g2n_result* r) {
   if (!r) return;
   delete static_cast<g2n::HostResult*>(r->priv_);

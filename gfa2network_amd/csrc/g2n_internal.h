@@ -94,4 +94,10 @@ bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out);
 // 2 EOFError, 3 zlib.error, 4 BadGzipFile (CRC / length) and *msg = the exception's message.
 bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::string* msg);
 
+// convert CLI writers (g2n_writers.cpp)
+int write_npz(const std::string& path, int n, const char* const* names, const uint8_t* const* heads,
+              const uint64_t* head_lens, const void* const* datas, const uint64_t* data_lens, int level);
+int write_node_map(const std::string& path, const uint8_t* blob, const int64_t* offs, uint64_t n);
+int64_t first_bad_utf8(const uint8_t* blob, const int64_t* offs, uint64_t n);
+
 }  // namespace g2n

@@ -163,6 +163,24 @@ void g2n_free(void *p);
  * with name i = blob[offsets[i] .. offsets[i+1]).  Host memory, parallel over host threads. */
 int g2n_join_names(const uint8_t *blob, const int64_t *offsets, uint64_t n_names, uint8_t sep, uint8_t *out);
 
+/* ---- convert CLI writers (host threads) -------------------------------------------------
+ * scipy.sparse.save_npz(path, A) as `convert --matrix x.npz` calls it (utils.py:85-86): a
+ * zip64 archive of deflated members (numpy savez_compressed's layout).  Member i is named
+ * names[i] and holds heads[i] (its .npy header, head_lens[i] bytes, built by numpy's format
+ * code) followed by datas[i] (data_lens[i] bytes).  level: zlib level (-1 = zlib's default, as
+ * numpy).  Returns G2N_E_IO (errno text in g2n_last_error) when the file cannot be written. */
+int g2n_write_npz(const char *path, int32_t n_members, const char *const *names, const uint8_t *const *heads,
+                  const uint64_t *head_lens, const void *const *datas, const uint64_t *data_lens, int32_t level);
+
+/* save_node_map (utils.py:108-114): "i\tname\n" for the names blob/offsets in id order.
+ * check_utf8 = 1 (raw_bytes_id names, decoded while writing): only the names before the first
+ * one that is not valid UTF-8 are written and *bad_index is its id (-1: all valid). */
+int g2n_write_node_map(const char *path, const uint8_t *blob, const int64_t *offsets, uint64_t n_names,
+                       int32_t check_utf8, int64_t *bad_index);
+
+/* Index of the first name that is not valid UTF-8 (Python's strict decoder), or -1. */
+int64_t g2n_first_bad_utf8(const uint8_t *blob, const int64_t *offsets, uint64_t n_names);
+
 /* convert_format(A, "csr") for a COO matrix (utils.py:40-63 -> scipy coo.tocsr):
  * sums duplicates in dtype with scipy's summation order, keeps explicit zeros.
  * rows/cols have index_width bytes per element, data has dtype elements; n_rows x n_cols. */
