@@ -20,7 +20,7 @@ namespace g2n {
 
 constexpr int kTPB = 256;
 constexpr uint64_t kTile = 32768;     // input bytes per front-end block (K1, K2)
-constexpr uint32_t kTileHalo = 4096;  // bytes staged past the tile for lines that end beyond it
+constexpr uint32_t kTileHalo = 2048;  // bytes staged past the tile for lines that end beyond it
 
 enum : uint8_t { kSkip = 0, kUnknown = 1, kS = 2, kEdge = 3, kPO = 4 };
 
@@ -71,6 +71,7 @@ struct Ctl {
   unsigned long long row_gap;         // k_row_bounds met a run of empty rows too long to fill
   unsigned long long n_deferred;      // lines parsed from global memory after k_tile_parse
   unsigned long long int_fail;        // the decimal-id dictionary (k_int_ids) does not apply
+  unsigned long long bucket_overflow; // k_maxsym_bucket met a bucket over its LDS capacity
 };
 
 struct ParseOpts {
@@ -88,6 +89,7 @@ struct ParseOpts {
   int32_t* rows;
   int32_t* cols;
   uint32_t ktrip;
+  uint32_t dbg;  // G2N_PARSE_DBG (profiling experiments only; 0 in every real build)
 };
 
 struct TouchOut {

@@ -39,6 +39,9 @@ struct Src {
   const uint8_t* p;
   uint64_t o;
   uint64_t lim;  // word8_z(i) reads memory only below lim
+  // LDS-staged tiles: bit b of tm[k] = byte o + 16 k + b is '\t', for bytes below tm_lim
+  const uint16_t* tm = nullptr;
+  uint64_t tm_lim = 0;
   __device__ uint8_t operator[](uint64_t i) const { return p[i - o]; }
   __device__ const uint8_t* ptr(uint64_t i) const { return p + (i - o); }
   __device__ uint32_t word(uint64_t i) const { return *(const uint32_t*)(p + (i - o)); }  // i, o % 4 == 0
@@ -477,21 +480,34 @@ __device__ inline uint32_t delim_bits4(uint32_t w, bool with_nl) {
   return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
 }
 
-// The common L line, "L\tu\t[+-]\tv\t[+-]\t<overlap>[\t<tags>]" of at most 60 bytes, in 32-bit
+// Tab bits of bytes [s, s + n), n <= 48: from the tile's tab bitmap when the source has one,
+// else from aligned 4-byte words (false when those would read past in.lim).
+__device__ inline bool tab_bits(const Src& in, uint64_t s, uint32_t n, uint64_t* out) {
+  if (in.tm && s + n <= in.tm_lim) {
+    const uint32_t l = (uint32_t)(s - in.o), k = l >> 4, sh = l & 15;
+    const uint64_t w = (uint64_t)in.tm[k] | ((uint64_t)in.tm[k + 1] << 16) | ((uint64_t)in.tm[k + 2] << 32) |
+                       ((uint64_t)in.tm[k + 3] << 48);
+    *out = (w >> sh) & ((1ull << n) - 1);
+    return true;
+  }
+  const uint64_t a = s & ~3ull;
+  const uint32_t sh = (uint32_t)(s - a);
+  const uint32_t nw = (sh + n + 3) >> 2;
+  if (a + 4ull * nw > in.lim) return false;
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < nw; j++) m |= (uint64_t)delim_bits4(in.word(a + 4ull * j), false) << (4 * j);
+  *out = (m >> sh) & ((1ull << n) - 1);
+  return true;
+}
+
+// The common L line, "L\tu\t[+-]\tv\t[+-]\t<overlap>[\t<tags>]" of at most 48 bytes, in 32-bit
 // arithmetic: its tab mask from aligned 4-byte words, then the fields.  Returns false for any
 // other shape (the general edge_layout then decides, errors included); when it returns true the
 // layout is exactly the one edge_layout gives (parser.py:206-227, the fields[2] in {+,-} branch).
 __device__ inline bool link_fast(const Src& in, uint64_t s, uint64_t e, EdgeLayout& L) {
   const uint32_t n = (uint32_t)(e - s);
-  const uint64_t a = s & ~3ull;
-  const uint32_t sh = (uint32_t)(s - a);
-  const uint32_t nw = (sh + n + 3) >> 2;
-  if (n > 60 || a + 4ull * nw > in.lim) return false;
-  uint64_t m = 0;
-  for (uint32_t j = 0; j < nw; j++) m |= (uint64_t)delim_bits4(in.word(a + 4ull * j), false) << (4 * j);
-  m >>= sh;
-  m &= (1ull << n) - 1;
-  if (__popcll(m) < 5) return false;
+  uint64_t m;
+  if (n > 48 || !tab_bits(in, s, n, &m) || __popcll(m) < 5) return false;
   uint32_t p[6];
   uint64_t r = m;
 #pragma unroll
@@ -609,10 +625,12 @@ __device__ inline bool src_dec(const Src& in, uint64_t o, uint32_t l, uint64_t* 
         (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) != 0 ||
         (w & 0xFF) == '0')
       return false;
-    uint64_t d = (w - zeros) << (8 * (8 - l));  // digits, most significant first, left-padded with 0s
-    d = (d * 10 + (d >> 8)) & 0x00FF00FF00FF00FFull;
-    d = (d * 100 + (d >> 16)) & 0x0000FFFF0000FFFFull;
-    *v = (d * 10000 + (d >> 32)) & 0xFFFFFFFFull;
+    const uint64_t d = (w - zeros) << (8 * (8 - l));  // digits, most significant first, left-padded with 0s
+    auto four = [](uint32_t x) {  // 4 digit bytes (most significant lowest) -> their value; shifts, no multiplies
+      x = ((x << 3) + (x << 1) + (x >> 8)) & 0x00FF00FFu;
+      return ((x << 6) + (x << 5) + (x << 2) + (x >> 16)) & 0xFFFFu;
+    };
+    *v = (uint64_t)(four((uint32_t)d) * 10000u + four((uint32_t)(d >> 32)));
     return true;
   }
   uint64_t x = 0;
@@ -661,6 +679,7 @@ __device__ inline void put_segment(const Src& in, const ParseOpts& op, const Tou
 __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_t e, uint64_t tb, uint64_t eb,
                                   const ParseOpts& op, const TouchOut& T, const EdgeOut& E, Ctl* ctl,
                                   uint64_t* __restrict__ worklist, uint32_t& ifail) {
+  if (op.dbg & 8) return;
   EdgeLayout L;
   if (!link_fast(in, s, e, L)) L = edge_layout(in, s, e);
   if (L.err) {
@@ -682,7 +701,7 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
   }
   if (op.rows) {  // lean: ids straight into the COO coordinates (k_triplets' layout)
     if (op.has_wt) E.w[eb] = w;
-    if (ifail) return;
+    if (ifail || (op.dbg & 2)) return;
     uint32_t a, b, c = 0, d = 0;
     bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b);
     if (ok && op.ktrip == 4)
@@ -749,7 +768,14 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
   const bool cut = bound < len;
   if (k == kS || k == kPO) {  // the first two (S) / three (P, O) fields
     uint64_t t1 = bound, t2 = bound;
-    {  // the first two delimiters, 4-byte words at a time (stops at the second, or after 64 bytes)
+    uint64_t tb_m;
+    if (nl_at_bound && bound - 1 - s <= 48 && tab_bits(in, s, (uint32_t)(bound - 1 - s), &tb_m)) {
+      // the whole line's tabs from the tile bitmap; its '\n' (byte bound - 1) ends the fields
+      const uint64_t nl = bound - 1;
+      t1 = tb_m ? s + __builtin_ctzll(tb_m) : nl;
+      tb_m &= tb_m - 1;
+      t2 = t1 == nl ? bound : (tb_m ? s + __builtin_ctzll(tb_m) : nl);
+    } else {  // the first two delimiters, 4-byte words at a time (stops at the second, or after 64 bytes)
       const uint64_t lim = (bound < s + kMaskSpan ? bound : s + kMaskSpan);
       uint32_t found = 0;
       for (uint64_t a = s & ~3ull; a < lim && found < 2 && a + 4 <= in.lim; a += 4) {
@@ -788,9 +814,11 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
   return true;
 }
 
-struct DeferredLine {
+struct DeferredLine {  // at most one per tile: the line holding the tile window's last byte
   unsigned long long line;
+  unsigned long long start;
   uint32_t tb, eb;
+  uint32_t kind, pad_;
 };
 
 // pass 2: line starts, kinds, touches, edges of every line starting in the tile.
@@ -811,12 +839,25 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   __shared__ __attribute__((aligned(16))) uint32_t pre[kTileChunks];  // chunk ranks, then line prefixes
   __shared__ uint8_t lkind[kTileLines];
   __shared__ uint32_t red[kTPB / 64];
+  constexpr uint32_t kMaskChunks = (uint32_t)((kTile + kTileHalo) / 16) + 4;  // + 4: tab_bits reads 4 ahead
+  __shared__ __attribute__((aligned(16))) uint16_t tabm[kMaskChunks];
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
   stage_tile<kTileHalo>(in, len, t0, buf);
   const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
   __syncthreads();
+  for (uint32_t c = threadIdx.x; c < kMaskChunks; c += kTPB) {  // the tile's tab bitmap (bytes past len: 0)
+    uint32_t m = 0;
+    if (16 * c + 16 <= kTile + kTileHalo + 16) {
+      const uint4 v = *(const uint4*)(buf + 16 * c);
+      m = delim_bits4(v.x, false) | (delim_bits4(v.y, false) << 4) | (delim_bits4(v.z, false) << 8) |
+          (delim_bits4(v.w, false) << 12);
+    }
+    tabm[c] = (uint16_t)m;
+  }
   const uint64_t w1 = t0 + kTile + kTileHalo < len ? t0 + kTile + kTileHalo : len;
-  const Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
+  Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
+  L.tm = tabm;
+  L.tm_lim = t0 + kTile + kTileHalo;
   const TileCnt b = base[blockIdx.x];
   const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
   // (1) start masks of this thread's chunks (kept), counts -> ranks
@@ -905,10 +946,12 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       const uint8_t k = lkind[j];
       const uint64_t i = idx0 + w0 + j;
       const uint64_t p = t0 + o;
-      ls[i] = p;
-      kind[i] = k;
+      if (!op.rows) {  // the lean parse skips them: only error / warning / slow-weight paths read them
+        ls[i] = p;
+        kind[i] = k;
+      }
       if (k == kUnknown) unk = i < unk ? i : unk;
-      if (k == kS || k == kEdge || k == kPO) {
+      if ((k == kS || k == kEdge || k == kPO) && !(op.dbg & 1) && !((op.dbg & 4) && k == kS)) {
         const uint32_t pr = pre[j];
         const uint64_t tb = t_run + (uint64_t)(pr >> 16) * tps + (uint64_t)(pr & 0xFFFF) * tpe;
         const uint64_t eb = e_run + (pr & 0xFFFF);
@@ -917,7 +960,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
         const uint64_t bound = known ? t0 + starts[j + 1] : w1;
         if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, ifail)) {
           const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
-          deferred[d] = DeferredLine{i, (uint32_t)tb, (uint32_t)eb};
+          if (d < gridDim.x) deferred[d] = DeferredLine{i, p, (uint32_t)tb, (uint32_t)eb, k, 0};
         }
       }
     }
@@ -941,7 +984,7 @@ __global__ void __launch_bounds__(64) k_parse_deferred(const uint8_t* __restrict
   const DeferredLine d = deferred[j];
   const Src G{in, 0, len};
   uint32_t ifail = 0;
-  parse_line(G, len, len, false, d.line, kind[d.line], ls[d.line], d.tb, d.eb, op, T, E, ctl, worklist, ifail);
+  parse_line(G, len, len, false, d.line, (uint8_t)d.kind, d.start, d.tb, d.eb, op, T, E, ctl, worklist, ifail);
   if (ifail) ctl->int_fail = 1;
 }
 
@@ -2200,6 +2243,151 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
   }
 }
 
+// ============================================ K7-K9 fused: unweighted A.maximum(A.T) ====
+// The default mode's CSR without the last radix pass, the per-row sums and the K9 merge: both
+// streams (A: key = row, value = column; A.T: key = column, value = row) are radix-sorted on the
+// key bits above kLow only, so a "bucket" of 2^kLow consecutive rows is one contiguous range of
+// each stream.  One block per bucket: both ranges are staged in LDS, scattered by row (LDS
+// counters), each row's columns sorted (registers for <= kRegRow entries, an in-place merge sort
+// in LDS otherwise), duplicates counted, and the two sides merged with std::max — exactly
+// k_row_sum + k_row_max on uniform values (every entry dtype(1); the order of equal entries
+// cannot matter).  kWrite = false: row counts; true: the CSR at moff.  A bucket with more than
+// kBucketCap entries on a side sets ctl->bucket_overflow (host: the classic path).
+constexpr uint32_t kBucketCap = 2048;
+
+__global__ void __launch_bounds__(kTPB) k_bucket_starts(const uint32_t* __restrict__ key, uint64_t n, uint32_t shift,
+                                                        uint64_t n_buckets, uint32_t* __restrict__ starts) {
+  const uint64_t b = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (b > n_buckets) return;
+  uint64_t lo = 0, hi = n;  // first position whose key >> shift >= b
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)(key[mid] >> shift) < b) lo = mid + 1;
+    else hi = mid;
+  }
+  starts[b] = (uint32_t)lo;
+}
+
+// sorts the n columns at seg (LDS) ascending, scr: n words of LDS scratch
+__device__ inline void lds_sort_cols(uint32_t* seg, uint32_t* scr, uint32_t n) {
+  if (n <= 1) return;
+  if (n <= kRegRow) {
+    uint32_t k[kRegRow];
+#pragma unroll
+    for (uint32_t q = 0; q < kRegRow; q++) k[q] = q < n ? seg[q] : 0xFFFFFFFFu;
+    if (n <= 8) net_sort<8>(k);
+    else net_sort<16>(k);
+#pragma unroll
+    for (uint32_t q = 0; q < kRegRow; q++)
+      if (q < n) seg[q] = k[q];
+    return;
+  }
+  uint32_t *a = seg, *b = scr;
+  for (uint32_t width = 1; width < n; width <<= 1) {
+    for (uint32_t lo = 0; lo < n; lo += 2 * width) {
+      const uint32_t mid = lo + width < n ? lo + width : n;
+      const uint32_t hi = lo + 2 * width < n ? lo + 2 * width : n;
+      uint32_t x = lo, y = mid, w = lo;
+      while (x < mid && y < hi) b[w++] = (a[y] < a[x]) ? a[y++] : a[x++];
+      while (x < mid) b[w++] = a[x++];
+      while (y < hi) b[w++] = a[y++];
+    }
+    uint32_t* t = a;
+    a = b;
+    b = t;
+  }
+  if (a != seg)
+    for (uint32_t q = 0; q < n; q++) seg[q] = a[q];
+}
+
+template <class T, bool kWrite>
+__global__ void __launch_bounds__(kTPB) k_maxsym_bucket(const uint32_t* __restrict__ ka, const uint32_t* __restrict__ va,
+                                                        const uint32_t* __restrict__ ba,
+                                                        const uint32_t* __restrict__ kt, const uint32_t* __restrict__ vt,
+                                                        const uint32_t* __restrict__ bt, uint32_t low, uint64_t n_rows,
+                                                        T one, uint32_t* __restrict__ mcnt,
+                                                        const uint32_t* __restrict__ moff, int32_t* __restrict__ indptr,
+                                                        int32_t* __restrict__ indices, T* __restrict__ data, Ctl* ctl) {
+  __shared__ uint32_t raw_a[kBucketCap], raw_t[kBucketCap];  // staged values, then sort scratch
+  __shared__ uint32_t seg_a[kBucketCap], seg_t[kBucketCap];  // values grouped by row
+  __shared__ uint8_t rl_a[kBucketCap], rl_t[kBucketCap];     // row within the bucket
+  __shared__ uint32_t cnt_a[kTPB], cnt_t[kTPB], off_a[kTPB], off_t[kTPB];
+  __shared__ uint32_t red[kTPB / 64];
+  const uint64_t b = blockIdx.x;
+  const uint32_t a0 = ba[b], na = ba[b + 1] - a0, t0 = bt[b], nt = bt[b + 1] - t0;
+  if (na > kBucketCap || nt > kBucketCap) {  // block-uniform
+    if (threadIdx.x == 0) ctl->bucket_overflow = 1;
+    return;
+  }
+  const uint32_t rmask = (1u << low) - 1u;
+  cnt_a[threadIdx.x] = 0;
+  cnt_t[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < na; i += kTPB) {
+    const uint32_t r = ka[a0 + i] & rmask;
+    raw_a[i] = va[a0 + i];
+    rl_a[i] = (uint8_t)r;
+    atomicAdd(&cnt_a[r], 1u);
+  }
+  for (uint32_t i = threadIdx.x; i < nt; i += kTPB) {
+    const uint32_t r = kt[t0 + i] & rmask;
+    raw_t[i] = vt[t0 + i];
+    rl_t[i] = (uint8_t)r;
+    atomicAdd(&cnt_t[r], 1u);
+  }
+  __syncthreads();
+  const uint32_t my_a = cnt_a[threadIdx.x], my_t = cnt_t[threadIdx.x];
+  uint32_t ex_a, ex_t;
+  const uint32_t both = block_excl_scan_u32((my_a << 16) | my_t, &ex_a, red);  // na, nt <= 2048: 16 bits each
+  (void)both;
+  ex_t = ex_a & 0xFFFFu;
+  ex_a >>= 16;
+  off_a[threadIdx.x] = ex_a;
+  off_t[threadIdx.x] = ex_t;
+  cnt_a[threadIdx.x] = ex_a;  // scatter cursors
+  cnt_t[threadIdx.x] = ex_t;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < na; i += kTPB) seg_a[atomicAdd(&cnt_a[rl_a[i]], 1u)] = raw_a[i];
+  for (uint32_t i = threadIdx.x; i < nt; i += kTPB) seg_t[atomicAdd(&cnt_t[rl_t[i]], 1u)] = raw_t[i];
+  __syncthreads();
+  const uint64_t row = (b << low) + threadIdx.x;
+  if (threadIdx.x > rmask || row >= n_rows) return;
+  uint32_t* sa = seg_a + ex_a;
+  uint32_t* st = seg_t + ex_t;
+  lds_sort_cols(sa, raw_a + ex_a, my_a);
+  lds_sort_cols(st, raw_t + ex_t, my_t);
+  // merge the two sorted multisets: per column, max(sum of A copies, sum of A.T copies); zeros dropped
+  const uint64_t base = kWrite ? moff[row] : 0;
+  if (kWrite) {
+    indptr[row] = (int32_t)base;
+    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(base + mcnt[row]);
+  }
+  uint32_t i = 0, j = 0, m = 0;
+  while (i < my_a || j < my_t) {
+    const uint32_t ca = i < my_a ? sa[i] : 0xFFFFFFFFu, ct = j < my_t ? st[j] : 0xFFFFFFFFu;
+    const uint32_t c = ca < ct ? ca : ct;
+    uint32_t ka_n = 0, kt_n = 0;
+    while (i < my_a && sa[i] == c) {
+      i++;
+      ka_n++;
+    }
+    while (j < my_t && st[j] == c) {
+      j++;
+      kt_n++;
+    }
+    const T x = ka_n ? sum_copies<T>(one, ka_n) : (T)0, y = kt_n ? sum_copies<T>(one, kt_n) : (T)0;
+    const T v = (x < y) ? y : x;
+    if (v != (T)0) {
+      if (kWrite) {
+        indices[base + m] = (int32_t)c;
+        data[base + m] = v;
+      }
+      m++;
+    }
+  }
+  if (!kWrite) mcnt[row] = m;
+}
+
 // ====================================================== sharded build helpers ======
 // keys of a blob as S-kind touches (g2n_dedup_keys)
 __global__ void __launch_bounds__(kTPB) k_keys_to_touches(const int64_t* __restrict__ offs, uint64_t n,
@@ -2314,6 +2502,14 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
                                                  uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);
 #define G2N_INST(T)                                                                                              \
   template __global__ void k_values<T>(const double*, uint64_t, int, int, T*, Ctl*);                             \
+  template __global__ void k_maxsym_bucket<T, false>(const uint32_t*, const uint32_t*, const uint32_t*,           \
+                                                     const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, \
+                                                     uint64_t, T, uint32_t*, const uint32_t*, int32_t*, int32_t*, \
+                                                     T*, Ctl*);                                                   \
+  template __global__ void k_maxsym_bucket<T, true>(const uint32_t*, const uint32_t*, const uint32_t*,            \
+                                                    const uint32_t*, const uint32_t*, const uint32_t*, uint32_t,  \
+                                                    uint64_t, T, uint32_t*, const uint32_t*, int32_t*, int32_t*,  \
+                                                    T*, Ctl*);                                                    \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
   template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, uint32_t*,    \

@@ -155,20 +155,23 @@ using SortCfg = rocprim::radix_sort_config<
 
 template <class Cfg, class V>
 static void sort_pairs_cfg(g2n_context* c, const uint32_t* kin, uint32_t* kout, const V* vin, V* vout, uint64_t n,
-                           int bits) {
+                           int bits, int begin) {
   size_t tb = 0;
-  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
-                                         c->stream));
+  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(nullptr, tb, kin, kout, vin, vout, (size_t)n, (unsigned)begin,
+                                         (unsigned)bits, c->stream));
   void* tmp = dbuf(c, S_TEMP, tb);
-  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(tmp, tb, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, c->stream));
+  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(tmp, tb, kin, kout, vin, vout, (size_t)n, (unsigned)begin, (unsigned)bits,
+                                         c->stream));
 }
 
+// stable sort on key bits [begin, bits)
 template <class V>
 static void sort_pairs_u32(g2n_context* c, const uint32_t* kin, uint32_t* kout, const V* vin, V* vout, uint64_t n,
-                           int bits) {
+                           int bits, int begin = 0) {
   if (n == 0) return;
-  if ((bits + 8) / 9 < (bits + 7) / 8) sort_pairs_cfg<SortCfg<9>>(c, kin, kout, vin, vout, n, bits);
-  else sort_pairs_cfg<SortCfg<8>>(c, kin, kout, vin, vout, n, bits);
+  const int w = bits - begin;
+  if ((w + 8) / 9 < (w + 7) / 8) sort_pairs_cfg<SortCfg<9>>(c, kin, kout, vin, vout, n, bits, begin);
+  else sort_pairs_cfg<SortCfg<8>>(c, kin, kout, vin, vout, n, bits, begin);
 }
 
 // coo.tocsr() of one orientation (transposed: of A.T), up to the per-row sorted unique entries.
@@ -242,9 +245,73 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
 }
 
 // SUM CSR, or MAX-SYM CSR when maxsym, from device COO triplets.
+// Unweighted A.maximum(A.T) through k_maxsym_bucket (see there); false when a bucket overflowed
+// its LDS capacity (nothing was written to the result: the caller runs the classic path).
+template <class T>
+static bool maxsym_buckets(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip, uint64_t n_rows,
+                           g2n_result* R) {
+  const int bits = bits_for(n_rows);
+  const double per_row = 2.0 * (double)n_trip / (double)(n_rows ? n_rows : 1);
+  int low = 8;  // rows per bucket 2^low: about 3072 entries per bucket over both sides
+  while (low > 1 && (double)(1u << low) * per_row > 3072.0) low--;
+  if (low > bits) low = bits;
+  const uint64_t n_buckets = (n_rows + (1ull << low) - 1) >> low;
+  const uint32_t *ka = (const uint32_t*)rows, *va = (const uint32_t*)cols;
+  const uint32_t *kt = (const uint32_t*)cols, *vt = (const uint32_t*)rows;
+  if (bits > low) {
+    auto* ka_s = dget<uint32_t>(c, S_KEYS1, n_trip);
+    auto* va_s = dget<uint32_t>(c, S_VALS1, n_trip);
+    auto* kt_s = dget<uint32_t>(c, S_KEYS0, n_trip);
+    auto* vt_s = dget<uint32_t>(c, S_VALS0, n_trip);
+    sort_pairs_u32<uint32_t>(c, ka, ka_s, va, va_s, n_trip, bits, low);
+    sort_pairs_u32<uint32_t>(c, kt, kt_s, vt, vt_s, n_trip, bits, low);
+    ka = ka_s;
+    va = va_s;
+    kt = kt_s;
+    vt = vt_s;
+  }
+  auto* ba = dget<uint32_t>(c, S_RSTART0, n_buckets + 1);
+  auto* bt = dget<uint32_t>(c, S_RSTART1, n_buckets + 1);
+  hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream, ka, n_trip,
+                     (uint32_t)low, n_buckets, ba);
+  hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream, kt, n_trip,
+                     (uint32_t)low, n_buckets, bt);
+  phase(c, "sum");
+  auto* mcnt = dget<uint32_t>(c, S_MCNT, n_rows);
+  auto* moff = dget<uint32_t>(c, S_MOFF, n_rows);
+  auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
+  auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_trip);
+  T* odata = dget<T>(c, S_ODATA, 2 * n_trip);
+  const T one = (T)1;
+  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL((k_maxsym_bucket<T, false>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt,
+                     vt, bt, (uint32_t)low, n_rows, one, mcnt, (const uint32_t*)nullptr, (int32_t*)nullptr,
+                     (int32_t*)nullptr, (T*)nullptr, c->ctl);
+  sync_ctl(c);
+  if (c->h_ctl->bucket_overflow) return false;
+  excl_scan<uint32_t>(c, mcnt, moff, n_rows);
+  hipLaunchKernelGGL((k_maxsym_bucket<T, true>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt,
+                     vt, bt, (uint32_t)low, n_rows, one, mcnt, moff, indptr, indices, odata, c->ctl);
+  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, mcnt, moff, n_rows, &c->ctl->n_keep);
+  R->format = G2N_FMT_CSR;
+  R->indptr = indptr;
+  R->nnz = (int64_t)read_dev(c, &c->ctl->n_keep);
+  R->indices = indices;
+  R->data = odata;
+  R->sum_sorted = -1;  // not computed: unweighted sums cannot depend on scipy's order
+  R->sum_t_sorted = -1;
+  phase(c, "maxsym");
+  return true;
+}
+
 template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
+  if constexpr (kU) {
+    if (maxsym && n_trip && n_rows && n_rows == n_cols && !std::getenv("G2N_NO_BUCKETS") &&
+        maxsym_buckets<T>(c, rows, cols, n_trip, n_rows, R))
+      return;
+  }
   const T one = (T)1;
   RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0);
   R->sum_sorted = A.unsorted ? 0 : 1;
@@ -614,6 +681,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   op.bidir = bidir;
   op.keep = keep;
   op.strip = o->strip_orientation != 0;
+  op.dbg = std::getenv("G2N_PARSE_DBG") ? (uint32_t)std::atoi(std::getenv("G2N_PARSE_DBG")) : 0u;
   const size_t wtl = o->weight_tag ? std::strlen(o->weight_tag) : 0;
   op.has_wt = wtl > 0;
   op.wt_len = (uint32_t)wtl;
@@ -642,7 +710,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     op.n_seg = n_s;
   }
   auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
-  auto* deferred = dget<DeferredLine>(c, S_DEFER, n_lines);
+  auto* deferred = dget<DeferredLine>(c, S_DEFER, n_tiles + 1);
   G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   phase(c, "_prep");
   auto parse = [&](const ParseOpts& po) {
@@ -651,6 +719,7 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
                          po, ls, kind, T, E, c->ctl, wl, deferred);
     sync_ctl(c);
     const uint64_t n_def = c->h_ctl->n_deferred;
+    if (n_def > n_tiles) throw Failure(G2N_E_DEVICE, "internal: more deferred lines than tiles");
     if (n_def)
       hipLaunchKernelGGL(k_parse_deferred, dim3(grid_for(n_def, 64)), dim3(64), 0, c->stream, in, len, ls, kind,
                          deferred, n_def, po, T, E, c->ctl, wl);
@@ -664,8 +733,12 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
     lo.cols = cols;
     lo.ktrip = (uint32_t)ktrip;
     parse(lo);
-    lean_done = !c->h_ctl->int_fail || c->h_ctl->err_key != ~0ull;
-    if (!lean_done) {  // not decimal ids after all: a full parse for the hash dictionary
+    // the lean parse wrote no line starts / kinds: errors, the unsupported-record warning and
+    // slow weights need a full parse (decimal ids kept unless they failed)
+    lean_done = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && c->h_ctl->warn_line == ~0ull &&
+                c->h_ctl->wl_count == 0;
+    if (!lean_done) {
+      const bool int_ok = !c->h_ctl->int_fail;
       c->h_ctl->wl_count = c->h_ctl->n_deferred = c->h_ctl->int_fail = 0;
       G2N_HIP(hipMemcpyAsync(&c->ctl->wl_count, &c->h_ctl->wl_count, sizeof(unsigned long long),
                              hipMemcpyHostToDevice, c->stream));
@@ -673,10 +746,14 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
                              hipMemcpyHostToDevice, c->stream));
       G2N_HIP(hipMemcpyAsync(&c->ctl->int_fail, &c->h_ctl->int_fail, sizeof(unsigned long long),
                              hipMemcpyHostToDevice, c->stream));
-      op.tid = nullptr;
+      if (!int_ok) op.tid = nullptr;  // not decimal ids after all: the hash dictionary
     }
   }
   if (!lean_done) parse(op);
+  if (op.dbg) {  // profiling experiment: the parse alone (its outputs are incomplete)
+    finish_timings(c, R);
+    return G2N_OK;
+  }
   const uint64_t n_work = c->h_ctl->wl_count;
   if (n_work) {
     hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, len, ls, wl, n_work, op, E,

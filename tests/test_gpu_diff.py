@@ -384,3 +384,49 @@ def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
                 b = outcome(gpu_run(data, mode, "float64", wt))
                 monkeypatch.delenv(env)
                 assert a == b, (mode, wt, env)
+
+
+def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
+    """The fused bucket A.maximum(A.T) (k_maxsym_bucket) equals the oracle and the classic
+    row-sum + merge path: hubs that overflow a bucket (classic fallback), heavy duplicate runs
+    (int8 wrap-around to 0 and -128, bool), self loops, every CLI dtype."""
+    import random
+
+    r = random.Random(12)
+    lines = [f"S\t{k}\t*\n" for k in range(1, 6001)]
+    lines += [f"L\t{r.randint(1, 6000)}\t+\t{r.randint(1, 6000)}\t-\t0M\n" for _ in range(30000)]
+    lines += ["L\t7\t+\t9\t+\t0M\n"] * 256 + ["L\t9\t+\t7\t+\t0M\n"] * 128 + ["L\t11\t+\t11\t+\t0M\n"] * 300
+    hub = [f"L\t5000\t+\t{k}\t+\t0M\n" for k in range(1, 6001)]  # > one bucket's capacity
+    for extra in ([], hub):
+        data = "".join(lines + extra).encode()
+        for dtype in ("bool", "int8", "int32", "float32", "float64"):
+            a = outcome(gpu_run(data, {}, dtype, None))
+            b = outcome(oracle_run(oracle_lib, data, {}, dtype, None))
+            assert a == b, (dtype, bool(extra))
+            monkeypatch.setenv("G2N_NO_BUCKETS", "1")
+            c = outcome(gpu_run(data, {}, dtype, None))
+            monkeypatch.delenv("G2N_NO_BUCKETS")
+            assert a == c, (dtype, bool(extra))
+
+
+def test_maxsym_buckets_large(gpu, monkeypatch):
+    """Bucket path == classic path at 10^7 edges (several radix passes skipped)."""
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(2_000_000, 8_000_000, seed=21)
+    a = outcome(gpu_run(data, {}, "float64", None))
+    monkeypatch.setenv("G2N_NO_BUCKETS", "1")
+    b = outcome(gpu_run(data, {}, "float64", None))
+    assert a == b
+
+
+def test_builds_are_deterministic(gpu):
+    """Atomics decide table slots, scatter positions and bucket cursors: two builds of the same
+    input still give identical bytes, on every dictionary tier."""
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(300_000, 1_200_000, seed=4, rc_tag=True)
+    hashed = data.replace(b"S\t1\t", b"S\tx1\t", 1)  # first S not "1": the hash tiers
+    for d in (data, hashed):
+        for mode, wt in (({}, None), ({"directed": False}, "RC"), ({"bidirected": True}, "RC")):
+            assert outcome(gpu_run(d, mode, "float64", wt)) == outcome(gpu_run(d, mode, "float64", wt))
