@@ -34,7 +34,7 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_FOFF64, S_NSLOTS
+  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_NSLOTS
 };
 
 struct DevBuf {
@@ -283,15 +283,17 @@ static bool maxsym_buckets(g2n_context* c, const int32_t* rows, const int32_t* c
   auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_trip);
   T* odata = dget<T>(c, S_ODATA, 2 * n_trip);
   const T one = (T)1;
+  auto* tmp_c = dget<int32_t>(c, S_BTC, 2 * n_trip);
+  T* tmp_v = dget<T>(c, S_BTV, 2 * n_trip);
+  auto* btot = dget<uint32_t>(c, S_BTOT, n_buckets);
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL((k_maxsym_bucket<T, false>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt,
-                     vt, bt, (uint32_t)low, n_rows, one, mcnt, (const uint32_t*)nullptr, (int32_t*)nullptr,
-                     (int32_t*)nullptr, (T*)nullptr, c->ctl);
+  hipLaunchKernelGGL((k_maxsym_bucket<T>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt, vt, bt,
+                     (uint32_t)low, n_rows, one, mcnt, btot, tmp_c, tmp_v, c->ctl);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
   excl_scan<uint32_t>(c, mcnt, moff, n_rows);
-  hipLaunchKernelGGL((k_maxsym_bucket<T, true>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt,
-                     vt, bt, (uint32_t)low, n_rows, one, mcnt, moff, indptr, indices, odata, c->ctl);
+  hipLaunchKernelGGL((k_bucket_compact<T>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ba, bt, btot, mcnt,
+                     moff, (uint32_t)low, n_rows, tmp_c, tmp_v, indptr, indices, odata);
   hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, mcnt, moff, n_rows, &c->ctl->n_keep);
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
