@@ -27,8 +27,8 @@ E_ARG, E_IO, E_GZIP, E_DEVICE, E_NOMEM, E_UNSUPPORTED = 13, 14, 15, 16, 17, 18
 
 DTYPE_CODES = {"bool": 0, "int8": 1, "int32": 2, "float32": 3, "float64": 4}
 CODE_DTYPES = {v: np.dtype(k) for k, v in DTYPE_CODES.items()}
-OUT_PARSE, OUT_CSR, OUT_COO = 0, 1, 2
-FMT_COO, FMT_CSR = 0, 1
+OUT_PARSE, OUT_CSR, OUT_COO, OUT_EDGE_LIST = 0, 1, 2, 3
+FMT_COO, FMT_CSR, FMT_TEXT = 0, 1, 2
 
 # every symbol include/g2n.h declares (tests check the library exports all of them)
 EXPORTED = [
@@ -275,7 +275,10 @@ def _from_result(ptr, rc: int) -> RawResult:
     out.sum_sorted = bool(r.sum_sorted)
     out.n_cast_overflow = int(r.n_cast_overflow)
     out.input_bytes = int(r.input_bytes)
-    if r.status == OK:
+    if r.format == FMT_TEXT and (r.status == OK or (r.status == E_UNICODE and r.err_line < 0)):
+        out.format = "text"  # export --format edge-list: the rendered lines (before an undecodable key)
+        out.data = _view(r.data, r.nnz, np.uint8, owner)
+    elif r.status == OK:
         idx = np.int32 if r.index_width == 4 else np.int64
         if r.names_offsets:
             out.names_offsets = _view(r.names_offsets, r.n_nodes + 1, np.int64, owner)

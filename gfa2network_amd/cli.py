@@ -3,8 +3,9 @@
 Same global flags (they precede the subcommand) and ``convert`` flags as
 gfa2network/cli.py:22-135, same handler order (cli.py:193-250): print the backend, parse,
 ``convert_format``, ``save_matrix`` (dense guard -> SystemExit), then the
-``<matrix>.nodes.tsv`` sidecar.  Graph outputs and the other subcommands
-(export / stats / distance / distance-matrix) are outside the GPU GFA->CSR path.
+``<matrix>.nodes.tsv`` sidecar.  ``export --format edge-list`` (cli.py:264-281) renders its
+lines on the GPU from the same parse.  Graph outputs (``--graph``, export graphml / gexf /
+json) and stats / distance / distance-matrix are outside the GPU GFA->CSR path.
 """
 from __future__ import annotations
 
@@ -13,7 +14,7 @@ import sys
 from pathlib import Path
 
 from . import __version__
-from .api import convert_format, parse_gfa, parse_gfa_names, save_matrix, save_node_map_native
+from .api import convert_format, export_edge_list, parse_gfa, parse_gfa_names, save_matrix, save_node_map_native
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -48,7 +49,14 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--keep-directed-bidir", action="store_true", help="Keep original directed bidirected behaviour")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("-o", "--output", metavar="PATH", help="Write graph pickle to PATH (not supported)")
-    for name in ("export", "stats", "distance", "distance-matrix"):
+    p_exp = sub.add_parser("export", help="Stream edges in simple formats")  # cli.py:137-149
+    p_exp.add_argument("gfa")
+    p_exp.add_argument("--format", default="edge-list", choices=["edge-list", "graphml", "gexf", "json"])
+    p_exp.add_argument("--bidirected", action="store_true")
+    p_exp.add_argument("--keep-directed-bidir", action="store_true",
+                       help="Keep original directed bidirected behaviour")
+    p_exp.add_argument("--output", help="Output path", default="-")
+    for name in ("stats", "distance", "distance-matrix"):
         sp_ = sub.add_parser(name, help="(outside the GPU GFA->CSR path)")
         sp_.add_argument("rest", nargs=argparse.REMAINDER)
     return parser
@@ -57,6 +65,11 @@ def _parser() -> argparse.ArgumentParser:
 def main(argv: list[str] | None = None) -> None:
     parser = _parser()
     args = parser.parse_args(argv)
+    if args.cmd == "export":
+        if args.format != "edge-list":
+            parser.error(f"export --format {args.format} builds a NetworkX graph, outside the GPU GFA->CSR path")
+        export_edge_list(args.gfa, args.output, bidirected=args.bidirected, device=args.device)
+        return
     if args.cmd != "convert":
         parser.error(f"'{args.cmd}' is outside the GPU GFA->CSR path; use the reference gfa2network for it")
     if not args.graph and not args.matrix:

@@ -169,7 +169,7 @@ static int check_opts(const g2n_options* o) {
     g2n::set_last_error("g2n_options: unsupported dtype");
     return G2N_E_ARG;
   }
-  if (o->output != G2N_OUT_PARSE && o->output != G2N_OUT_CSR && o->output != G2N_OUT_COO) {
+  if (o->output < G2N_OUT_PARSE || o->output > G2N_OUT_EDGE_LIST) {
     g2n::set_last_error("g2n_options: unknown output");
     return G2N_E_ARG;
   }

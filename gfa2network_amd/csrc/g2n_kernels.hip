@@ -2527,6 +2527,54 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
   *out = n ? (unsigned long long)off[n - 1] + cnt[n - 1] : 0ull;
 }
 
+// ====================================================== export --format edge-list ======
+// cli.py:264-281: one "u\tv\n" line per L/E/C record in stream order, u/v the record's
+// endpoint keys (bidirected: "u:ori"), which are the names of the stream-order COO's row/col
+// ids.  Bytes per edge: 8 B ids + |u| + |v| + 2 written, names read from the (L2-resident
+// for local graphs) blob.
+
+// per-name flag: the key's bytes are not strict UTF-8 (the export's u.decode() raises)
+__global__ void __launch_bounds__(kTPB) k_name_bad_utf8(const uint8_t* __restrict__ blob,
+                                                        const int64_t* __restrict__ offs, uint64_t n_names,
+                                                        uint8_t* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n_names) return;
+  const int64_t o = offs[i], n = offs[i + 1] - o;
+  bad[i] = utf8_valid(blob + o, (uint64_t)n) ? 0 : 1;
+}
+
+// per-edge line length; the first edge (stream order) with an undecodable endpoint
+__global__ void __launch_bounds__(kTPB) k_edge_text_len(const int32_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ cols, uint64_t n,
+                                                        const int64_t* __restrict__ offs,
+                                                        const uint8_t* __restrict__ bad, uint64_t* __restrict__ len,
+                                                        unsigned long long* first_bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  const int32_t r = rows[i], c = cols[i];
+  len[i] = (uint64_t)(offs[r + 1] - offs[r]) + (uint64_t)(offs[c + 1] - offs[c]) + 2u;
+  if (bad[r] | bad[c]) atomicMin(first_bad, (unsigned long long)i);
+}
+
+// renders the lines at their scanned positions: a wavefront per 64 edges, lanes copy the
+// bytes of one line each (lines are short; stores of neighbouring lanes land in the same
+// cache lines)
+__global__ void __launch_bounds__(kTPB) k_edge_text(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                                    uint64_t n, const int64_t* __restrict__ offs,
+                                                    const uint8_t* __restrict__ blob, const uint64_t* __restrict__ pos,
+                                                    uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (i >= n) return;
+  const int32_t r = rows[i], c = cols[i];
+  uint8_t* d = out + pos[i];
+  const int64_t ur = offs[r], ul = offs[r + 1] - ur, vr = offs[c], vl = offs[c + 1] - vr;
+  for (int64_t k = 0; k < ul; k++) d[k] = blob[ur + k];
+  d[ul] = '\t';
+  d += ul + 1;
+  for (int64_t k = 0; k < vl; k++) d[k] = blob[vr + k];
+  d[vl] = '\n';
+}
+
 // ----------------------------------------------------------- explicit instances --
 #define G2N_INST_U(T, U)                                                                                         \
   template __global__ void k_pack<T, U>(const int32_t*, const int32_t*, const T*, uint64_t, int, int64_t, uint32_t*, \

@@ -34,7 +34,7 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_NSLOTS
+  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_NSLOTS
 };
 
 struct DevBuf {
@@ -636,7 +636,7 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
   return true;  // no S line seen yet (long header lines): try
 }
 
-static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
+static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   R->input_bytes = len;
   c->n_ev = 0;
@@ -897,6 +897,75 @@ static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g
   return G2N_OK;
 }
 
+// export --format edge-list (cli.py:264-281).  The lines come from the same parse: the
+// stream-order COO of a directed, keep-orientation build (one entry per L/E/C record, ids of
+// the record's endpoint keys, builders.py:199-228 with keep_directed_bidir) and its names blob;
+// the text is rendered in HBM.  Result: format G2N_FMT_TEXT, data = text, nnz = its bytes.
+// An endpoint key that is not UTF-8: status G2N_E_UNICODE, err_line -1, err_index = the edge,
+// err_detail = the key, and the text holds the lines before it (what the reference wrote).
+static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
+  g2n_options b = *o;
+  b.directed = 1;
+  b.keep_directed_bidir = 1;
+  b.asymmetric = 1;
+  b.strip_orientation = 0;
+  b.weight_tag = nullptr;
+  b.dtype = G2N_BOOL;
+  b.output = G2N_OUT_COO;
+  b.want_node_names = 1;
+  const int rc = run_build(c, in, len, &b, R);
+  if (rc != G2N_OK) return rc;
+  const uint64_t n = (uint64_t)R->nnz, n_names = (uint64_t)R->n_nodes;
+  const auto* rows = (const int32_t*)R->rows;
+  const auto* cols = (const int32_t*)R->cols;
+  const int64_t* offs = R->names_offsets;
+  const uint8_t* blob = R->names_blob;
+  auto* bad = dget<uint8_t>(c, S_EBAD, n_names + 1);
+  auto* elen = dget<uint64_t>(c, S_ELEN, n + 1);
+  auto* epos = dget<uint64_t>(c, S_EPOS, n + 1);
+  auto* first = dget<unsigned long long>(c, S_EFIRST, 1);
+  G2N_HIP(hipMemsetAsync(first, 0xFF, sizeof(unsigned long long), c->stream));
+  if (n_names)
+    hipLaunchKernelGGL(k_name_bad_utf8, dim3(grid_for(n_names)), dim3(kTPB), 0, c->stream, blob, offs, n_names, bad);
+  if (n)
+    hipLaunchKernelGGL(k_edge_text_len, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, offs, bad, elen,
+                       first);
+  G2N_HIP(hipMemsetAsync(elen + n, 0, sizeof(uint64_t), c->stream));
+  excl_scan<uint64_t>(c, elen, epos, n + 1);
+  const uint64_t total = read_dev(c, epos + n);
+  const unsigned long long fb = read_dev(c, first);
+  auto* text = dget<uint8_t>(c, S_ETEXT, total + 1);
+  if (n)
+    hipLaunchKernelGGL(k_edge_text, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, offs, blob, epos,
+                       text);
+  phase(c, "edge_text");
+  R->format = G2N_FMT_TEXT;
+  R->rows = R->cols = nullptr;
+  R->data = text;
+  R->nnz = (int64_t)total;
+  R->names_blob = nullptr;  // the names are in the text
+  R->names_offsets = nullptr;
+  R->names_bytes = 0;
+  if (fb != ~0ull) {  // f"{u.decode()}\t{v.decode()}\n": u is decoded first
+    const int32_t r = read_dev(c, rows + fb), cc = read_dev(c, cols + fb);
+    const int32_t who = read_dev(c, bad + r) ? r : cc;
+    const int64_t o0 = read_dev(c, offs + who), o1 = read_dev(c, offs + who + 1);
+    R->nnz = (int64_t)read_dev(c, epos + fb);
+    R->status = G2N_E_UNICODE;
+    R->err_line = -1;
+    R->err_index = (int64_t)fb;
+    R->err_detail = blob + o0;
+    R->err_detail_len = o1 - o0;
+  }
+  finish_timings(c, R);
+  return R->status;
+}
+
+static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
+  if (o->output == G2N_OUT_EDGE_LIST) return run_edge_list(c, in, len, o, R);
+  return run_build(c, in, len, o, R);
+}
+
 // --------------------------------------------------------------- contexts ----------
 static g2n_context* context_create(int device) {
   int n = 0;
@@ -962,7 +1031,7 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
   R.names_offsets = nullptr;
   R.rows = R.cols = R.indptr = R.indices = R.data = nullptr;
   if (D.err_detail) R.err_detail = (const uint8_t*)download(c, H->detail, D.err_detail, (size_t)D.err_detail_len);
-  if (D.status == G2N_OK) {
+  if (D.status == G2N_OK || (D.format == G2N_FMT_TEXT && D.status == G2N_E_UNICODE)) {
     if (D.names_blob) {
       const int64_t* offs =
           (const int64_t*)download(c, H->offs, D.names_offsets, (size_t)(D.n_nodes + 1) * sizeof(int64_t));
@@ -972,14 +1041,16 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
       R.names_offsets = offs;
     }
     const size_t w = dtype_size(D.dtype);
-    if (D.format == G2N_FMT_COO) {
+    if (D.format == G2N_FMT_TEXT) {
+      R.data = download(c, H->data, D.data, (size_t)D.nnz);
+    } else if (D.format == G2N_FMT_COO) {
       R.rows = download(c, H->rows, D.rows, (size_t)D.nnz * 4);
       R.cols = download(c, H->cols, D.cols, (size_t)D.nnz * 4);
     } else {
       R.indptr = download(c, H->indptr, D.indptr, (size_t)(D.n_nodes + 1) * 4);
       R.indices = download(c, H->indices, D.indices, (size_t)D.nnz * 4);
     }
-    R.data = download(c, H->data, D.data, (size_t)D.nnz * w);
+    if (D.format != G2N_FMT_TEXT) R.data = download(c, H->data, D.data, (size_t)D.nnz * w);
   }
   G2N_HIP(hipStreamSynchronize(c->stream));
 }

@@ -20,6 +20,15 @@
  *                  CSR when graph_directed and not asymmetric (builders.py:282-283),
  *                  otherwise the stream-order, unsummed COO (builders.py:281).
  *   G2N_OUT_CSR    what convert_format(parse_gfa(...), "csr") returns (cli.py:239).
+ *   G2N_OUT_EDGE_LIST  the bytes `gfa2network export --format edge-list [--bidirected]`
+ *                  writes (cli.py:264-281): "u\tv\n" per L/E/C record in stream order
+ *                  (bidirected: "u:ori\tv:ori\n").  Only `bidirected` is read from the
+ *                  options.  Result format G2N_FMT_TEXT: data = the text, nnz = its length.
+ *                  An endpoint key that is not UTF-8 (the export's u.decode() raises):
+ *                  status G2N_E_UNICODE with err_line = -1, err_index = the edge record,
+ *                  err_detail = the key, and the text holds the lines written before it.
+ *                  Parse errors (err_line >= 0) carry no text: the caller renders the
+ *                  input's prefix [0, start of err_line) to reproduce the partial output.
  *
  * Errors: a non-zero status is one of G2N_E_*; each maps 1:1 to the exception the
  * reference raises for the same input (type + message; the Python shim re-raises it).
@@ -64,8 +73,8 @@ enum {
 /* ---- matrix dtypes (cli.py:92-97 --dtype choices) ------------------------------------ */
 enum { G2N_BOOL = 0, G2N_INT8 = 1, G2N_INT32 = 2, G2N_FLOAT32 = 3, G2N_FLOAT64 = 4 };
 
-enum { G2N_OUT_PARSE = 0, G2N_OUT_CSR = 1, G2N_OUT_COO = 2 };
-enum { G2N_FMT_COO = 0, G2N_FMT_CSR = 1 };
+enum { G2N_OUT_PARSE = 0, G2N_OUT_CSR = 1, G2N_OUT_COO = 2, G2N_OUT_EDGE_LIST = 3 };
+enum { G2N_FMT_COO = 0, G2N_FMT_CSR = 1, G2N_FMT_TEXT = 2 };
 
 /* Mirrors parse_gfa's keyword arguments that affect the matrix (builders.py:30-50). */
 typedef struct g2n_options {

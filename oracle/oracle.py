@@ -179,3 +179,40 @@ def to_raw(o: OracleResult, output: str = "parse"):
         raw.indices = o.sum_indices.astype(np.int32)
         raw.data = o.sum_data
     return raw
+
+
+def export_edge_list(data: bytes, *, bidirected: bool = False):
+    """CPU restatement of ``export --format edge-list`` (cli.py:264-281) for the tests.
+
+    The reference's loop writes ``f"{u.decode()}\\t{v.decode()}\\n"`` for every L/E/C record the
+    parser yields; u / v are the record keys that the directed, keep-orientation matrix build
+    mints for the same record (builders.py:199-228, bidirected ``u:ori``), so the lines are
+    the stream-order COO's row / col names.  Returns ``(text, error, first)``: error = None or
+    ``(kind, payload)``: ("status", the failing OracleResult) for a parse failure (text = the
+    lines before the failing line), ("decode", key bytes) for a key that is not UTF-8; first =
+    the full-input OracleResult (its warning flags).
+    """
+    o = run(data, directed=True, bidirected=bidirected, keep_directed_bidir=True, asymmetric=True, dtype="bool")
+    err = None
+    first = o
+    if o.status != 0:
+        if o.err_line < 0:
+            return b"", ("status", o), first
+        err = ("status", o)
+        arr = np.frombuffer(bytes(data), dtype=np.uint8)
+        nl = np.flatnonzero(arr == 0x0A)
+        end = 0 if o.err_line == 0 else int(nl[o.err_line - 1]) + 1
+        o = run(arr[:end].tobytes(), directed=True, bidirected=bidirected, keep_directed_bidir=True,
+                asymmetric=True, dtype="bool")
+        assert o.status == 0, "the prefix before a failing line parses"
+    blob, offs = o.names_blob.tobytes(), o.names_offsets
+    names = [blob[offs[i]:offs[i + 1]] for i in range(o.n_nodes)]
+    out = []
+    for r, c in zip(o.rows.tolist(), o.cols.tolist()):
+        for k in (r, c):
+            try:
+                names[k].decode()
+            except UnicodeDecodeError:
+                return b"".join(out), ("decode", names[k]), first
+        out.append(names[r] + b"\t" + names[c] + b"\n")
+    return b"".join(out), err, first

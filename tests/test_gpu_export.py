@@ -1,0 +1,62 @@
+"""GPU: export --format edge-list (cli.py:264-281) rendered in HBM (G2N_OUT_EDGE_LIST),
+checked byte for byte against the reference's own outputs (tests/golden/expected/export.json:
+written bytes, exception, warnings, every input x {plain, --bidirected}), the reference's
+tests/test_export_edge_list.py re-run on the GPU CLI, and the oracle's restatement on a
+synthetic 200k-edge input."""
+import subprocess
+import sys
+import warnings
+from pathlib import Path
+
+import pytest
+
+from test_export_golden import EXPECTED, INPUTS, expected
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+@pytest.mark.parametrize("key", sorted(EXPECTED))
+def test_gpu_export_matches_reference(gpu, key, tmp_path):
+    from gfa2network_amd import export_edge_list
+
+    name, bidir = key.split("|")
+    out = tmp_path / "edges.tsv"
+    exc = None
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        try:
+            export_edge_list(INPUTS / name, out, bidirected=bidir == "1")
+        except Exception as e:  # noqa: BLE001
+            exc = [type(e).__name__, str(e)]
+    want_text, want_exc, want_warn = expected(key)
+    assert out.read_bytes() == want_text
+    assert exc == want_exc
+    assert [str(x.message) for x in w if issubclass(x.category, RuntimeWarning)] == want_warn
+
+
+def test_gpu_export_cli(gpu, tmp_path):  # the reference's tests/test_export_edge_list.py
+    gfa = tmp_path / "e.gfa"
+    gfa.write_bytes(b"S\ts1\t4\nS\ts2\t4\nL\ts1\t+\ts2\t+\t0M\n")
+    out = tmp_path / "edges.tsv"
+    subprocess.run([sys.executable, "-m", "gfa2network_amd", "export", str(gfa), "--format", "edge-list",
+                    "--output", str(out)], check=True, cwd=ROOT)
+    assert out.read_text().strip() == "s1\ts2"
+    r = subprocess.run([sys.executable, "-m", "gfa2network_amd", "export", str(gfa), "--bidirected"], check=True,
+                       cwd=ROOT, capture_output=True)
+    assert r.stdout == b"s1:+\ts2:+\n"
+
+
+@pytest.mark.parametrize("bidir", [False, True])
+def test_gpu_export_synthetic_vs_oracle(gpu, oracle_lib, tmp_path, bidir):
+    from gfa2network_amd import export_edge_list, synth
+
+    data = synth.host_bytes(50_000, 200_000, seed=7)
+    src = tmp_path / "s.gfa"
+    src.write_bytes(data)
+    out = tmp_path / "edges.tsv"
+    export_edge_list(src, out, bidirected=bidir)
+    text, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
+    assert err is None
+    assert out.read_bytes() == text
+    assert text.count(b"\n") == 200_000
