@@ -238,8 +238,8 @@ def main():
                             weight_tag=mode.get("weight_tag"))
     res = nat.Result()
 
-    def step():
-        rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(opts), ctypes.byref(res))
+    def step(o=None):
+        rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o or opts), ctypes.byref(res))
         if rc != 0:
             raise RuntimeError(f"{nat.status_name(rc)}: {nat.last_error()}")
         ph = {}
@@ -271,6 +271,16 @@ def main():
         hash_ph = step()
         t_h = time.perf_counter() - t_h
         del os.environ["G2N_DICT_HASH"]
+    # export --format edge-list on the same input (the text rendered in HBM)
+    t_x, x_ph, x_bytes = None, None, 0
+    if not args.no_alt:
+        xopts = nat.make_options(output=nat.OUT_EDGE_LIST, device=local)
+        step(xopts)
+        t_x = time.perf_counter()
+        x_ph = step(xopts)
+        t_x = time.perf_counter() - t_x
+        x_bytes = int(res.nnz)
+        step()  # leaves res describing the CSR build again
     w_dtype = 8
     ms_step = elapsed / args.steps * 1e3
     edges_total = n_edges * args.steps * world
@@ -326,6 +336,15 @@ def main():
             "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
             "note": "G2N_DICT_HASH=1: segment names resolved through the GPU hash table (inputs whose S lines "
                     "are not named 1..N in order)"}}
+    if t_x is not None:
+        xt = x_ph.get("edge_text", 0.0)
+        line.setdefault("alt_paths", {})["export_edge_list"] = {
+            "ms_per_step": round(t_x * 1e3, 3), "m_edges_per_s": round(n_edges / t_x / 1e6, 2),
+            "text_bytes": x_bytes, "phase_ms": {k: round(v, 3) for k, v in x_ph.items()},
+            "edge_text_gbs": round((x_bytes + 8 * n_edges) / (xt / 1e3) / 1e9, 1) if xt else None,
+            "note": "export --format edge-list (cli.py:264-281): the same parse with a stream-order COO, "
+                    "then per-edge lengths, a scan and the rendered u\\tv lines in HBM (device-resident; "
+                    "edge_text_gbs = (text bytes + 8 B ids per edge) / edge_text phase)"}
     if dom in ("insert_claim", "insert_lookup"):
         tps = 2 if mode.get("bidirected") else 1
         tpe = 4 if (mode.get("bidirected") and not mode.get("keep_directed_bidir")) else 2
