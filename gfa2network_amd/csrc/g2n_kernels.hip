@@ -2533,46 +2533,92 @@ __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* _
 // ids.  Bytes per edge: 8 B ids + |u| + |v| + 2 written, names read from the (L2-resident
 // for local graphs) blob.
 
-// per-name flag: the key's bytes are not strict UTF-8 (the export's u.decode() raises)
-__global__ void __launch_bounds__(kTPB) k_name_bad_utf8(const uint8_t* __restrict__ blob,
-                                                        const int64_t* __restrict__ offs, uint64_t n_names,
-                                                        uint8_t* __restrict__ bad) {
+// per-name record, one 8-byte gather per edge endpoint: offset << 24 | length << 1 | bad, bad =
+// the key's bytes are not strict UTF-8 (the export's u.decode() raises); a length that does not
+// fit 23 bits is saturated and read from offs
+constexpr uint64_t kMetaLen = 0x7FFFFF;
+
+__global__ void __launch_bounds__(kTPB) k_name_meta(const uint8_t* __restrict__ blob,
+                                                    const int64_t* __restrict__ offs, uint64_t n_names,
+                                                    uint64_t* __restrict__ meta) {
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n_names) return;
-  const int64_t o = offs[i], n = offs[i + 1] - o;
-  bad[i] = utf8_valid(blob + o, (uint64_t)n) ? 0 : 1;
+  const uint64_t o = (uint64_t)offs[i], n = (uint64_t)offs[i + 1] - o;
+  meta[i] = (o << 24) | ((n < kMetaLen ? n : kMetaLen) << 1) | (utf8_valid(blob + o, n) ? 0u : 1u);
+}
+
+__device__ inline uint64_t meta_len(uint64_t m, uint32_t id, const int64_t* __restrict__ offs) {
+  const uint64_t l = (m >> 1) & kMetaLen;
+  return l == kMetaLen ? (uint64_t)(offs[id + 1] - offs[id]) : l;
 }
 
 // per-edge line length; the first edge (stream order) with an undecodable endpoint
 __global__ void __launch_bounds__(kTPB) k_edge_text_len(const int32_t* __restrict__ rows,
                                                         const int32_t* __restrict__ cols, uint64_t n,
-                                                        const int64_t* __restrict__ offs,
-                                                        const uint8_t* __restrict__ bad, uint64_t* __restrict__ len,
-                                                        unsigned long long* first_bad) {
+                                                        const uint64_t* __restrict__ meta,
+                                                        const int64_t* __restrict__ offs, uint64_t* __restrict__ len,
+                                                        ulonglong2* __restrict__ em, unsigned long long* first_bad) {
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n) return;
   const int32_t r = rows[i], c = cols[i];
-  len[i] = (uint64_t)(offs[r + 1] - offs[r]) + (uint64_t)(offs[c + 1] - offs[c]) + 2u;
-  if (bad[r] | bad[c]) atomicMin(first_bad, (unsigned long long)i);
+  uint64_t mr = meta[r], mc = meta[c];
+  const uint64_t lr = meta_len(mr, r, offs), lc = meta_len(mc, c, offs);
+  len[i] = lr + lc + 2u;
+  // the endpoints' (offset, length) for the render pass: one coalesced 16-byte read there
+  // instead of two more random gathers
+  em[i] = make_ulonglong2(((mr >> 24) << 24) | (lr < 0xFFFFFFu ? lr : 0xFFFFFFu), mc >> 24);
+  if ((mr | mc) & 1u) atomicMin(first_bad, (unsigned long long)i);
 }
 
-// renders the lines at their scanned positions: a wavefront per 64 edges, lanes copy the
-// bytes of one line each (lines are short; stores of neighbouring lanes land in the same
-// cache lines)
-__global__ void __launch_bounds__(kTPB) k_edge_text(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
-                                                    uint64_t n, const int64_t* __restrict__ offs,
-                                                    const uint8_t* __restrict__ blob, const uint64_t* __restrict__ pos,
-                                                    uint8_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (i >= n) return;
-  const int32_t r = rows[i], c = cols[i];
-  uint8_t* d = out + pos[i];
-  const int64_t ur = offs[r], ul = offs[r + 1] - ur, vr = offs[c], vl = offs[c + 1] - vr;
+// renders the lines at their scanned positions.  A block takes kTextEdges consecutive edges,
+// whose text is one contiguous range [pos[e0], pos[e1]): the lines are assembled in LDS at
+// their offset from the 16-byte-aligned start of that range, then written out with aligned
+// 16-byte stores (byte stores only for the two partial words at the range ends, whose other
+// bytes belong to the neighbouring blocks).  A range longer than the LDS stage (long names)
+// is written line by line straight to HBM.
+constexpr uint32_t kTextEdges = 1024;
+constexpr uint32_t kTextLds = 32 * 1024;
+
+__device__ inline void edge_line(uint8_t* d, int64_t ur, int64_t ul, int64_t vr, int64_t vl,
+                                 const uint8_t* __restrict__ blob) {
   for (int64_t k = 0; k < ul; k++) d[k] = blob[ur + k];
   d[ul] = '\t';
   d += ul + 1;
   for (int64_t k = 0; k < vl; k++) d[k] = blob[vr + k];
   d[vl] = '\n';
+}
+
+__global__ void __launch_bounds__(kTPB) k_edge_text(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                                    uint64_t n, const ulonglong2* __restrict__ em,
+                                                    const int64_t* __restrict__ offs, const uint8_t* __restrict__ blob, const uint64_t* __restrict__ pos,
+                                                    uint8_t* __restrict__ out) {
+  __shared__ uint4 stage4[kTextLds / 16];
+  uint8_t* stage = (uint8_t*)stage4;
+  const uint64_t e0 = (uint64_t)blockIdx.x * kTextEdges;
+  const uint64_t e1 = e0 + kTextEdges < n ? e0 + kTextEdges : n;
+  const uint64_t p0 = pos[e0], p1 = pos[e1];  // pos holds n + 1 entries
+  const uint64_t base = p0 & ~15ull;
+  const bool staged = p1 - base <= kTextLds;  // block-uniform
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kTPB) {
+    const ulonglong2 m = em[e];
+    const uint64_t pe = pos[e];
+    uint64_t ul = m.x & 0xFFFFFFu;  // |u| (saturated: from offs); |v| = line - |u| - 2
+    if (ul == 0xFFFFFFu) ul = (uint64_t)(offs[rows[e] + 1] - offs[rows[e]]);
+    const uint64_t vl = pos[e + 1] - pe - 2 - ul;
+    edge_line(staged ? stage + (pe - base) : out + pe, (int64_t)(m.x >> 24), (int64_t)ul, (int64_t)m.y, (int64_t)vl,
+              blob);
+  }
+  if (!staged) return;
+  __syncthreads();
+  const uint64_t w0 = base >> 4, w1 = (p1 + 15) >> 4;
+  for (uint64_t w = w0 + threadIdx.x; w < w1; w += kTPB) {
+    const uint64_t a = w << 4;
+    if (a >= p0 && a + 16 <= p1) {
+      *(uint4*)(out + a) = stage4[w - w0];
+    } else {
+      for (uint64_t b = a < p0 ? p0 : a; b < a + 16 && b < p1; b++) out[b] = stage[b - base];
+    }
+  }
 }
 
 // ----------------------------------------------------------- explicit instances --

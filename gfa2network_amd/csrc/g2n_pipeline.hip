@@ -34,7 +34,7 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_NSLOTS
+  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_NSLOTS
 };
 
 struct DevBuf {
@@ -920,24 +920,25 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
   const auto* cols = (const int32_t*)R->cols;
   const int64_t* offs = R->names_offsets;
   const uint8_t* blob = R->names_blob;
-  auto* bad = dget<uint8_t>(c, S_EBAD, n_names + 1);
+  auto* meta = dget<uint64_t>(c, S_EBAD, n_names + 1);
   auto* elen = dget<uint64_t>(c, S_ELEN, n + 1);
   auto* epos = dget<uint64_t>(c, S_EPOS, n + 1);
   auto* first = dget<unsigned long long>(c, S_EFIRST, 1);
+  auto* em = dget<ulonglong2>(c, S_EMETA, n + 1);
   G2N_HIP(hipMemsetAsync(first, 0xFF, sizeof(unsigned long long), c->stream));
   if (n_names)
-    hipLaunchKernelGGL(k_name_bad_utf8, dim3(grid_for(n_names)), dim3(kTPB), 0, c->stream, blob, offs, n_names, bad);
+    hipLaunchKernelGGL(k_name_meta, dim3(grid_for(n_names)), dim3(kTPB), 0, c->stream, blob, offs, n_names, meta);
   if (n)
-    hipLaunchKernelGGL(k_edge_text_len, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, offs, bad, elen,
-                       first);
+    hipLaunchKernelGGL(k_edge_text_len, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, meta, offs,
+                       elen, em, first);
   G2N_HIP(hipMemsetAsync(elen + n, 0, sizeof(uint64_t), c->stream));
   excl_scan<uint64_t>(c, elen, epos, n + 1);
   const uint64_t total = read_dev(c, epos + n);
   const unsigned long long fb = read_dev(c, first);
-  auto* text = dget<uint8_t>(c, S_ETEXT, total + 1);
+  auto* text = dget<uint8_t>(c, S_ETEXT, total + 16);
   if (n)
-    hipLaunchKernelGGL(k_edge_text, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, rows, cols, n, offs, blob, epos,
-                       text);
+    hipLaunchKernelGGL(k_edge_text, dim3((unsigned)((n + kTextEdges - 1) / kTextEdges)), dim3(kTPB), 0, c->stream,
+                       rows, cols, n, em, offs, blob, epos, text);
   phase(c, "edge_text");
   R->format = G2N_FMT_TEXT;
   R->rows = R->cols = nullptr;
@@ -948,7 +949,7 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
   R->names_bytes = 0;
   if (fb != ~0ull) {  // f"{u.decode()}\t{v.decode()}\n": u is decoded first
     const int32_t r = read_dev(c, rows + fb), cc = read_dev(c, cols + fb);
-    const int32_t who = read_dev(c, bad + r) ? r : cc;
+    const int32_t who = (read_dev(c, meta + r) & 1u) ? r : cc;
     const int64_t o0 = read_dev(c, offs + who), o1 = read_dev(c, offs + who + 1);
     R->nnz = (int64_t)read_dev(c, epos + fb);
     R->status = G2N_E_UNICODE;

@@ -60,3 +60,25 @@ def test_gpu_export_synthetic_vs_oracle(gpu, oracle_lib, tmp_path, bidir):
     assert err is None
     assert out.read_bytes() == text
     assert text.count(b"\n") == 200_000
+
+
+def test_gpu_export_long_names_vs_oracle(gpu, oracle_lib, tmp_path):
+    """Lines longer than the LDS stage holds per block (direct-to-HBM rendering), mixed with
+    short ones, ragged block ends."""
+    from gfa2network_amd import export_edge_list
+
+    rng = __import__("random").Random(3)
+    names = [("n%d_" % i + "x" * rng.choice([0, 1, 40, 300])).encode() for i in range(3000)]
+    lines = [b"S\t" + nm + b"\t*\n" for nm in names]
+    for _ in range(5003):
+        u, v = rng.choice(names), rng.choice(names)
+        lines.append(b"L\t" + u + b"\t" + rng.choice([b"+", b"-"]) + b"\t" + v + b"\t+\t0M\n")
+    data = b"".join(lines)
+    src = tmp_path / "long.gfa"
+    src.write_bytes(data)
+    for bidir in (False, True):
+        out = tmp_path / "edges.tsv"
+        export_edge_list(src, out, bidirected=bidir)
+        text, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
+        assert err is None
+        assert out.read_bytes() == text
