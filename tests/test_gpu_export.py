@@ -82,3 +82,32 @@ def test_gpu_export_long_names_vs_oracle(gpu, oracle_lib, tmp_path):
         text, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
         assert err is None
         assert out.read_bytes() == text
+
+
+@pytest.mark.parametrize("name", ["warn_then_error.gfa", "short_l.gfa", "bad_utf8_name.gfa", "sample.gfa"])
+def test_gpu_export_gzip_and_stdin(gpu, tmp_path, name):
+    """The same reference outputs through a .gz input (a parse error re-inflates the input to
+    render its prefix) and through stdin (`-`, parser.py:104-105) on the CLI."""
+    import gzip as gz
+
+    from gfa2network_amd import export_edge_list
+
+    want_text, want_exc, _ = expected(f"{name}|0")
+    src = tmp_path / (name + ".gz")
+    src.write_bytes(gz.compress((INPUTS / name).read_bytes()))
+    out = tmp_path / "edges.tsv"
+    exc = None
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        try:
+            export_edge_list(src, out)
+        except Exception as e:  # noqa: BLE001
+            exc = [type(e).__name__, str(e)]
+    assert out.read_bytes() == want_text
+    assert exc == want_exc
+    r = subprocess.run([sys.executable, "-m", "gfa2network_amd", "export", "-"], cwd=ROOT, capture_output=True,
+                       input=(INPUTS / name).read_bytes())
+    assert r.stdout == want_text
+    assert (r.returncode != 0) == (want_exc is not None)
+    if want_exc:
+        assert r.stderr.decode().rstrip().splitlines()[-1] == f"{want_exc[0]}: {want_exc[1]}"
