@@ -40,6 +40,12 @@ EXPORTED = [
 ]
 
 
+# options.reserved[1] test flags (include/g2n.h): the builds of this process take normally-rare
+# paths when a test sets them; 0 in every real use
+TEST_NO_LOOKBACK = 1   # MAX-SYM bucket finish: every bucket staged + fix-up kernel
+TEST_FLAGS = 0
+
+
 class Options(ctypes.Structure):
     _fields_ = [
         ("abi_version", ctypes.c_uint32),
@@ -186,7 +192,7 @@ def status_name(code: int) -> str:
 
 def make_options(*, directed=True, bidirected=False, keep_directed_bidir=False, asymmetric=False,
                  strip_orientation=False, dtype="float64", weight_tag=None, output=OUT_PARSE,
-                 want_node_names=True, device=0) -> Options:
+                 want_node_names=True, device=0, test_flags=None) -> Options:
     lib = load()
     o = Options()
     lib.g2n_options_init(ctypes.byref(o))
@@ -200,6 +206,8 @@ def make_options(*, directed=True, bidirected=False, keep_directed_bidir=False, 
     o.weight_tag = weight_tag.encode("utf-8") if weight_tag else None
     o.want_node_names = int(bool(want_node_names))
     o.device = int(device)
+    # tests only: force a normally rare path (same results); see include/g2n.h reserved[1]
+    o.reserved[1] = int(TEST_FLAGS if test_flags is None else test_flags)
     return o
 
 

@@ -314,7 +314,10 @@ def convert_format(A, fmt: str, *, verbose: bool = False):
     if fmt == A.format:
         out = A
     elif fmt == "dok":
-        raise NotImplementedError("dok output is outside the GPU GFA->CSR path")
+        # a Python dict of (row, col) -> value: scipy's own asformat("dok") on the GPU-built
+        # matrix (for a COO it sums duplicates in place, in stream order, as the reference's
+        # A.asformat(fmt) does, utils.py:55)
+        out = A.asformat("dok")
     else:
         coo = A if A.format == "coo" else A.tocoo()
         out = _native_tocsr(coo) if fmt == "csr" else _native_tocsc(coo)

@@ -2243,195 +2243,6 @@ __global__ void __launch_bounds__(kTPB) k_row_max(const uint32_t* __restrict__ s
   }
 }
 
-// ============================================ K7-K9 fused: unweighted A.maximum(A.T) ====
-// The default mode's CSR without the last radix pass, the per-row sums and the K9 merge: both
-// streams (A: key = row, value = column; A.T: key = column, value = row) are radix-sorted on the
-// key bits above kLow only, so a "bucket" of 2^kLow consecutive rows is one contiguous range of
-// each stream.  One block per bucket: both ranges are staged in LDS, scattered by row (LDS
-// counters), each row's columns sorted (registers for <= kRegRow entries, an in-place merge sort
-// in LDS otherwise), duplicates counted, and the two sides merged with std::max — exactly
-// k_row_sum + k_row_max on uniform values (every entry dtype(1); the order of equal entries
-// cannot matter).  kWrite = false: row counts; true: the CSR at moff.  A bucket with more than
-// kBucketCap entries on a side sets ctl->bucket_overflow (host: the classic path).
-constexpr uint32_t kBucketCap = 2048;
-
-__global__ void __launch_bounds__(kTPB) k_bucket_starts(const uint32_t* __restrict__ key, uint64_t n, uint32_t shift,
-                                                        uint64_t n_buckets, uint32_t* __restrict__ starts) {
-  const uint64_t b = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (b > n_buckets) return;
-  uint64_t lo = 0, hi = n;  // first position whose key >> shift >= b
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)(key[mid] >> shift) < b) lo = mid + 1;
-    else hi = mid;
-  }
-  starts[b] = (uint32_t)lo;
-}
-
-// sorts the n columns at seg (LDS) ascending: registers for n <= kRegRow, else an in-place Shell
-// sort (rows that long are rare; a bucket holds at most kBucketCap entries per side)
-__device__ inline void lds_sort_cols(uint32_t* seg, uint32_t n) {
-  if (n <= 1) return;
-  if (n <= kRegRow) {
-    uint32_t k[kRegRow];
-#pragma unroll
-    for (uint32_t q = 0; q < kRegRow; q++) k[q] = q < n ? seg[q] : 0xFFFFFFFFu;
-    if (n <= 8) net_sort<8>(k);
-    else net_sort<16>(k);
-#pragma unroll
-    for (uint32_t q = 0; q < kRegRow; q++)
-      if (q < n) seg[q] = k[q];
-    return;
-  }
-  constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};  // Ciura
-  for (uint32_t g : gaps) {
-    if (g >= n) continue;
-    for (uint32_t i = g; i < n; i++) {
-      const uint32_t v = seg[i];
-      uint32_t j = i;
-      while (j >= g && seg[j - g] > v) {
-        seg[j] = seg[j - g];
-        j -= g;
-      }
-      seg[j] = v;
-    }
-  }
-}
-
-// Entries are staged in registers (kBucketPer per thread and side, every load in flight at
-// once), counted per row with LDS atomics, scattered by row into LDS; LDS stays at ~17 KB so
-// many blocks per CU overlap their latency chains.
-constexpr uint32_t kBucketPer = kBucketCap / kTPB;
-
-// One pass: the rows' merged entries go to the bucket's own slice of tmp (at ba[b] + bt[b], room
-// for na + nt entries), in row order (a block scan of the rows' counts); k_bucket_compact then
-// moves every slice to its CSR position with coalesced copies.
-template <class T>
-__global__ void __launch_bounds__(kTPB) k_maxsym_bucket(const uint32_t* __restrict__ ka, const uint32_t* __restrict__ va,
-                                                        const uint32_t* __restrict__ ba,
-                                                        const uint32_t* __restrict__ kt, const uint32_t* __restrict__ vt,
-                                                        const uint32_t* __restrict__ bt, uint32_t low, uint64_t n_rows,
-                                                        T one, uint32_t* __restrict__ mcnt, uint32_t* __restrict__ btot,
-                                                        int32_t* __restrict__ tmp_c, T* __restrict__ tmp_v, Ctl* ctl) {
-  __shared__ uint32_t seg_a[kBucketCap], seg_t[kBucketCap];  // values grouped by row
-  __shared__ uint32_t cnt_a[kTPB], cnt_t[kTPB];
-  __shared__ uint32_t red[kTPB / 64];
-  const uint64_t b = blockIdx.x;
-  const uint32_t a0 = ba[b], na = ba[b + 1] - a0, t0 = bt[b], nt = bt[b + 1] - t0;
-  if (na > kBucketCap || nt > kBucketCap) {  // block-uniform
-    if (threadIdx.x == 0) ctl->bucket_overflow = 1;
-    return;
-  }
-  const uint32_t rmask = (1u << low) - 1u;
-  cnt_a[threadIdx.x] = 0;
-  cnt_t[threadIdx.x] = 0;
-  uint32_t ra[kBucketPer], xa[kBucketPer], rt[kBucketPer], xt[kBucketPer];
-#pragma unroll
-  for (uint32_t k = 0; k < kBucketPer; k++) {
-    const uint32_t i = threadIdx.x + k * kTPB;
-    if (i < na) {
-      ra[k] = ka[a0 + i] & rmask;
-      xa[k] = va[a0 + i];
-    }
-    if (i < nt) {
-      rt[k] = kt[t0 + i] & rmask;
-      xt[k] = vt[t0 + i];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t k = 0; k < kBucketPer; k++) {
-    const uint32_t i = threadIdx.x + k * kTPB;
-    if (i < na) atomicAdd(&cnt_a[ra[k]], 1u);
-    if (i < nt) atomicAdd(&cnt_t[rt[k]], 1u);
-  }
-  __syncthreads();
-  const uint32_t my_a = cnt_a[threadIdx.x], my_t = cnt_t[threadIdx.x];
-  uint32_t ex;
-  block_excl_scan_u32((my_a << 16) | my_t, &ex, red);  // na, nt <= 2048: 16 bits each
-  const uint32_t ex_a = ex >> 16, ex_t = ex & 0xFFFFu;
-  cnt_a[threadIdx.x] = ex_a;  // scatter cursors
-  cnt_t[threadIdx.x] = ex_t;
-  __syncthreads();
-#pragma unroll
-  for (uint32_t k = 0; k < kBucketPer; k++) {
-    const uint32_t i = threadIdx.x + k * kTPB;
-    if (i < na) seg_a[atomicAdd(&cnt_a[ra[k]], 1u)] = xa[k];
-    if (i < nt) seg_t[atomicAdd(&cnt_t[rt[k]], 1u)] = xt[k];
-  }
-  __syncthreads();
-  const uint64_t row = (b << low) + threadIdx.x;
-  const bool live = threadIdx.x <= rmask && row < n_rows;  // rows past the bucket have no entries
-  const uint32_t* sa = seg_a + ex_a;
-  const uint32_t* st = seg_t + ex_t;
-  if (live) {
-    lds_sort_cols(seg_a + ex_a, my_a);
-    lds_sort_cols(seg_t + ex_t, my_t);
-  }
-  // merge the two sorted multisets: per column, max(sum of A copies, sum of A.T copies); zeros
-  // dropped.  Run twice: count (for the block's row offsets), then write.
-  auto merge = [&](int32_t* oc, T* ov) -> uint32_t {
-    uint32_t i = 0, j = 0, m = 0;
-    while (i < my_a || j < my_t) {
-      const uint32_t ca = i < my_a ? sa[i] : 0xFFFFFFFFu, ct = j < my_t ? st[j] : 0xFFFFFFFFu;
-      const uint32_t c = ca < ct ? ca : ct;
-      uint32_t ka_n = 0, kt_n = 0;
-      while (i < my_a && sa[i] == c) {
-        i++;
-        ka_n++;
-      }
-      while (j < my_t && st[j] == c) {
-        j++;
-        kt_n++;
-      }
-      const T x = ka_n ? sum_copies<T>(one, ka_n) : (T)0, y = kt_n ? sum_copies<T>(one, kt_n) : (T)0;
-      const T v = (x < y) ? y : x;
-      if (v != (T)0) {
-        if (oc) {
-          oc[m] = (int32_t)c;
-          ov[m] = v;
-        }
-        m++;
-      }
-    }
-    return m;
-  };
-  const uint32_t m = live ? merge(nullptr, nullptr) : 0u;
-  uint32_t off;
-  const uint32_t tot = block_excl_scan_u32(m, &off, red);
-  if (live) {
-    mcnt[row] = m;
-    const uint64_t o = (uint64_t)a0 + t0 + off;
-    merge(tmp_c + o, tmp_v + o);
-  }
-  if (threadIdx.x == 0) btot[b] = tot;
-}
-
-// Bucket b's merged entries (tmp slice at ba[b] + bt[b], btot[b] of them) to their CSR place
-// moff[first row of b]; indptr of the bucket's rows.
-template <class T>
-__global__ void __launch_bounds__(kTPB) k_bucket_compact(const uint32_t* __restrict__ ba, const uint32_t* __restrict__ bt,
-                                                         const uint32_t* __restrict__ btot,
-                                                         const uint32_t* __restrict__ mcnt,
-                                                         const uint32_t* __restrict__ moff, uint32_t low, uint64_t n_rows,
-                                                         const int32_t* __restrict__ tmp_c, const T* __restrict__ tmp_v,
-                                                         int32_t* __restrict__ indptr, int32_t* __restrict__ indices,
-                                                         T* __restrict__ data) {
-  const uint64_t b = blockIdx.x;
-  const uint64_t r0 = b << low;
-  const uint64_t src = (uint64_t)ba[b] + bt[b], dst = moff[r0];
-  const uint32_t n = btot[b];
-  for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
-    indices[dst + i] = tmp_c[src + i];
-    data[dst + i] = tmp_v[src + i];
-  }
-  const uint64_t row = r0 + threadIdx.x;
-  if (threadIdx.x < (1u << low) && row < n_rows) {
-    indptr[row] = (int32_t)moff[row];
-    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(moff[row] + mcnt[row]);
-  }
-}
-
 // ====================================================== sharded build helpers ======
 // keys of a blob as S-kind touches (g2n_dedup_keys)
 __global__ void __launch_bounds__(kTPB) k_keys_to_touches(const int64_t* __restrict__ offs, uint64_t n,
@@ -2640,12 +2451,6 @@ __global__ void __launch_bounds__(kTPB) k_edge_text(const int32_t* __restrict__ 
                                                  uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);
 #define G2N_INST(T)                                                                                              \
   template __global__ void k_values<T>(const double*, uint64_t, int, int, T*, Ctl*);                             \
-  template __global__ void k_maxsym_bucket<T>(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,   \
-                                              const uint32_t*, const uint32_t*, uint32_t, uint64_t, T, uint32_t*,    \
-                                              uint32_t*, int32_t*, T*, Ctl*);                                        \
-  template __global__ void k_bucket_compact<T>(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,  \
-                                               const uint32_t*, uint32_t, uint64_t, const int32_t*, const T*,       \
-                                               int32_t*, int32_t*, T*);                                             \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
   template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, uint32_t*,    \

@@ -18,6 +18,8 @@
 
 #include "g2n_internal.h"
 #include "g2n_kernels.hip"
+#include "g2n_scan.hip"
+#include "g2n_sym.hip"
 
 #define G2N_HIP(call)                                                                                      \
   do {                                                                                                     \
@@ -34,8 +36,12 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_NSLOTS
+  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_LBST, S_SCANST, S_NSLOTS
 };
+
+// options.reserved[1] bits (tests only): take a path that is normally rare, same results
+constexpr uint32_t kTestNoLookback = 1;  // k_sym_finish: every bucket staged + k_sym_fixup
 
 struct DevBuf {
   void* p = nullptr;
@@ -46,6 +52,7 @@ struct DevBuf {
 
 struct g2n_context {
   int device = 0;
+  uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
   hipStream_t stream = nullptr;
   std::vector<g2n::DevBuf> bufs;
   g2n::Ctl* ctl = nullptr;    // device
@@ -104,14 +111,19 @@ static T read_dev(g2n_context* c, const T* p) {
   return v;
 }
 
-// rocPRIM wrappers (query temp size, grow the TEMP slot, run)
+// exclusive scan of n items (k_scan_excl, decoupled look-back); *total (device, optional) = sum
+template <class TIn, class TOut>
+static void scan_excl(g2n_context* c, const TIn* in, TOut* out, uint64_t n, TOut* total = nullptr) {
+  if (n == 0 && !total) return;
+  const uint64_t tiles = scan_tiles(n);
+  auto* st = dget<unsigned long long>(c, S_SCANST, tiles + 1);  // status words + the ticket
+  G2N_HIP(hipMemsetAsync(st, 0, (tiles + 1) * sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL((k_scan_excl<TIn, TOut>), dim3((unsigned)tiles), dim3(256), 0, c->stream, in, out, n, st,
+                     (uint32_t*)(st + tiles), total);
+}
 template <class T>
 static void excl_scan(g2n_context* c, const T* in, T* out, uint64_t n) {
-  if (n == 0) return;
-  size_t tb = 0;
-  G2N_HIP(rocprim::exclusive_scan(nullptr, tb, in, out, T(0), (size_t)n, rocprim::plus<T>(), c->stream));
-  void* tmp = dbuf(c, S_TEMP, tb);
-  G2N_HIP(rocprim::exclusive_scan(tmp, tb, in, out, T(0), (size_t)n, rocprim::plus<T>(), c->stream));
+  scan_excl<T, T>(c, in, out, n);
 }
 
 static int lookup_batch() {  // touches per thread in the S-first lookup (G2N_LOOKUP_BATCH=2|4)
@@ -244,60 +256,86 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
   return S;
 }
 
-// SUM CSR, or MAX-SYM CSR when maxsym, from device COO triplets.
-// Unweighted A.maximum(A.T) through k_maxsym_bucket (see there); false when a bucket overflowed
-// its LDS capacity (nothing was written to the result: the caller runs the classic path).
+// Unweighted A.maximum(A.T) through the bucket partition (g2n_sym.hip): the A entries and their
+// A.T twins are partitioned by the high bits of their row (one or two hand-written passes), then
+// one finish block per bucket writes its rows' CSR entries at their final place.  False when
+// the row ids are too wide for two passes or a bucket overflowed its LDS capacity (nothing
+// usable was written: the caller runs the general path).
 template <class T>
-static bool maxsym_buckets(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip, uint64_t n_rows,
-                           g2n_result* R) {
+static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip,
+                             uint64_t n_rows, g2n_result* R) {
   const int bits = bits_for(n_rows);
   const double per_row = 2.0 * (double)n_trip / (double)(n_rows ? n_rows : 1);
-  int low = 8;  // rows per bucket 2^low: about 3072 entries per bucket over both sides
-  while (low > 1 && (double)(1u << low) * per_row > 3072.0) low--;
+  int low = 8;  // rows per bucket 2^low: about 2048 elements per bucket on average (capacity 4096)
+  while (low > 1 && (double)(1u << low) * per_row > 2048.0) low--;
   if (low > bits) low = bits;
-  const uint64_t n_buckets = (n_rows + (1ull << low) - 1) >> low;
-  const uint32_t *ka = (const uint32_t*)rows, *va = (const uint32_t*)cols;
-  const uint32_t *kt = (const uint32_t*)cols, *vt = (const uint32_t*)rows;
-  if (bits > low) {
-    auto* ka_s = dget<uint32_t>(c, S_KEYS1, n_trip);
-    auto* va_s = dget<uint32_t>(c, S_VALS1, n_trip);
-    auto* kt_s = dget<uint32_t>(c, S_KEYS0, n_trip);
-    auto* vt_s = dget<uint32_t>(c, S_VALS0, n_trip);
-    sort_pairs_u32<uint32_t>(c, ka, ka_s, va, va_s, n_trip, bits, low);
-    sort_pairs_u32<uint32_t>(c, kt, kt_s, vt, vt_s, n_trip, bits, low);
-    ka = ka_s;
-    va = va_s;
-    kt = kt_s;
-    vt = vt_s;
+  const int hb = bits - low;  // bucket id bits
+  if (hb > 2 * (int)kMaxDigitBits) return false;
+  const int bits2 = hb > (int)kMaxDigitBits ? hb / 2 : 0, bits1 = hb - bits2;
+  const uint32_t n_dig1 = 1u << bits1, n_dig2 = 1u << bits2;
+  const uint64_t n_el = 2 * n_trip;
+  const uint64_t n_buckets = 1ull << hb;                      // ids of the partition
+  const uint64_t n_bk = (n_rows + (1ull << low) - 1) >> low;  // buckets holding rows
+  const uint32_t shift1 = (uint32_t)(low + bits2);
+  PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, nullptr, nullptr, nullptr, 0};
+  // pass 1: over the COO entries, both sides
+  const uint64_t n_blk1 = (n_el + kPartTile - 1) / kPartTile;
+  auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
+  auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
+  auto* el1 = dget<uint2>(c, S_EL0, n_el);
+  hipLaunchKernelGGL(k_part_hist<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1, cnt1,
+                     n_blk1);
+  scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+  hipLaunchKernelGGL(k_part_scatter<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                     (const uint32_t*)off1, n_blk1, el1);
+  auto* bst = dget<uint32_t>(c, S_BSTART, n_buckets + 1);
+  const uint2* el = el1;
+  if (bits2 == 0) {
+    hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                       (const uint32_t*)off1, n_blk1, (uint32_t)n_el, n_buckets, bst);
+  } else {  // pass 2 inside each pass-1 group
+    auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
+    PartSrc s2{nullptr, nullptr, 0, el1, grp, grp + n_dig1 + 1, n_dig1};
+    hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, n_blk1, n_dig1,
+                       (uint32_t)n_el, grp, grp + n_dig1 + 1);
+    const uint64_t n_blk2 = n_blk1 + n_dig1;  // >= the blocks the groups need
+    auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
+    auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
+    auto* el2 = dget<uint2>(c, S_EL1, n_el);
+    hipLaunchKernelGGL(k_part_hist<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low, n_dig2,
+                       cnt2, n_blk2);
+    scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+    hipLaunchKernelGGL(k_part_scatter<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low, n_dig2,
+                       (const uint32_t*)off2, n_blk2, el2);
+    hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                       (const uint32_t*)off2, s2, n_dig2, (uint32_t)n_el, n_buckets, bst);
+    el = el2;
   }
-  auto* ba = dget<uint32_t>(c, S_RSTART0, n_buckets + 1);
-  auto* bt = dget<uint32_t>(c, S_RSTART1, n_buckets + 1);
-  hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream, ka, n_trip,
-                     (uint32_t)low, n_buckets, ba);
-  hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream, kt, n_trip,
-                     (uint32_t)low, n_buckets, bt);
   phase(c, "sum");
-  auto* mcnt = dget<uint32_t>(c, S_MCNT, n_rows);
-  auto* moff = dget<uint32_t>(c, S_MOFF, n_rows);
   auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
-  auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_trip);
-  T* odata = dget<T>(c, S_ODATA, 2 * n_trip);
-  const T one = (T)1;
-  auto* tmp_c = dget<int32_t>(c, S_BTC, 2 * n_trip);
-  T* tmp_v = dget<T>(c, S_BTV, 2 * n_trip);
-  auto* btot = dget<uint32_t>(c, S_BTOT, n_buckets);
-  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL((k_maxsym_bucket<T>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ka, va, ba, kt, vt, bt,
-                     (uint32_t)low, n_rows, one, mcnt, btot, tmp_c, tmp_v, c->ctl);
+  auto* indices = dget<int32_t>(c, S_INDICES, n_el);
+  T* odata = dget<T>(c, S_ODATA, n_el);
+  auto* btot = dget<uint32_t>(c, S_BTOT, n_bk);
+  auto* fixq = dget<uint32_t>(c, S_MCNT, n_bk);
+  auto* status = dget<unsigned long long>(c, S_LBST, n_bk);
+  uint2* tmp = el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1;  // the pass-1 output is dead by now
+  G2N_HIP(hipMemsetAsync(status, 0, n_bk * sizeof(unsigned long long), c->stream));
+  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, 2 * sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL((k_sym_finish<T>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el, (const uint32_t*)bst,
+                     (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices, odata, c->ctl,
+                     (c->test_flags & kTestNoLookback) ? 0u : kSpinLimit);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
-  excl_scan<uint32_t>(c, mcnt, moff, n_rows);
-  hipLaunchKernelGGL((k_bucket_compact<T>), dim3((unsigned)n_buckets), dim3(kTPB), 0, c->stream, ba, bt, btot, mcnt,
-                     moff, (uint32_t)low, n_rows, tmp_c, tmp_v, indptr, indices, odata);
-  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(1), 0, c->stream, mcnt, moff, n_rows, &c->ctl->n_keep);
+  if (c->h_ctl->n_fix) {  // buckets that gave up waiting on their predecessors
+    auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
+    scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
+    hipLaunchKernelGGL((k_sym_fixup<T>), dim3((unsigned)c->h_ctl->n_fix), dim3(kTPB), 0, c->stream,
+                       (const uint32_t*)fixq, (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff,
+                       (uint32_t)low, n_rows, (T)1, (const uint2*)tmp, indptr, indices, odata);
+  }
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
-  R->nnz = (int64_t)read_dev(c, &c->ctl->n_keep);
+  R->nnz = (int64_t)read_dev(c, indptr + n_rows);
   R->indices = indices;
   R->data = odata;
   R->sum_sorted = -1;  // not computed: unweighted sums cannot depend on scipy's order
@@ -311,7 +349,7 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   if constexpr (kU) {
     if (maxsym && n_trip && n_rows && n_rows == n_cols && !std::getenv("G2N_NO_BUCKETS") &&
-        maxsym_buckets<T>(c, rows, cols, n_trip, n_rows, R))
+        maxsym_partition<T>(c, rows, cols, n_trip, n_rows, R))
       return;
   }
   const T one = (T)1;
@@ -521,12 +559,7 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
     phase(c, "table_init");
   };
   auto rank_firsts = [&]() {  // nid[t] = first touches before t; n_nodes
-    size_t tb = 0;
-    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
-                                    c->stream));
-    void* tmp = dbuf(c, S_TEMP, tb);
-    G2N_HIP(rocprim::exclusive_scan(tmp, tb, first, nid, (uint32_t)0, (size_t)n_t, rocprim::plus<uint32_t>(),
-                                    c->stream));
+    scan_excl<uint8_t, uint32_t>(c, first, nid, n_t);
     hipLaunchKernelGGL(k_node_count, dim3(1), dim3(1), 0, c->stream, first, nid, n_t, c->ctl);
   };
   if (n_t) {
@@ -638,6 +671,7 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
 
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
+  c->test_flags = (uint32_t)o->reserved[1];
   R->input_bytes = len;
   c->n_ev = 0;
   G2N_HIP(hipEventRecord(c->ev[0], c->stream));
@@ -815,17 +849,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   phase(c, "ids");
   if (o->want_node_names) {  // names blob + offsets in id order
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
-    {
-      size_t tb = 0;
-      if (n_nodes) {
-        G2N_HIP(rocprim::exclusive_scan(nullptr, tb, D.klen, offs, (int64_t)0, (size_t)n_nodes,
-                                        rocprim::plus<int64_t>(), c->stream));
-        void* tmp = dbuf(c, S_TEMP, tb);
-        G2N_HIP(rocprim::exclusive_scan(tmp, tb, D.klen, offs, (int64_t)0, (size_t)n_nodes, rocprim::plus<int64_t>(),
-                                        c->stream));
-      }
-      hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, D.klen, n_nodes, offs, c->ctl);
-    }
+    scan_excl<uint32_t, int64_t>(c, D.klen, offs, n_nodes);
+    hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, D.klen, n_nodes, offs, c->ctl);
     const uint64_t names_len = read_dev(c, &c->ctl->names_len);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
     if (n_nodes)

@@ -1,0 +1,579 @@
+// g2n_sym.hip — A.maximum(A.T) of an unweighted build on gfx950: bucket partition + bucket finish.
+//
+// Replaces scipy's `coo_matrix.maximum(A.T)` of the matrix branch (builders.py:282-283:
+// coo -> csr for A and for A.T, csr_sort_indices, csr_sum_duplicates, csr_maximum_csr) for
+// builds whose every value is dtype(1) (no weight tag).  Each entry of A (stream-order COO from
+// the parse) is one element of row a (side 0, column b) and one of row b (side 1: the A.T entry,
+// column a).  Because every value is 1, a row's result is a function of the MULTISET of its
+// (column, side) pairs: out[r, c] = max(sum of the side-0 copies, sum of the side-1 copies)
+// (dtype arithmetic, zeros dropped).  The order inside a bucket is therefore free, and the
+// partition need not be stable.
+//
+//   P1 (one or two passes, MSD): elements are partitioned by the high bits of their row into
+//      buckets of 2^low rows — per block, a 16-byte-coalesced load of 4096 elements, an LDS
+//      histogram (written to a digit-major count matrix), a device scan of that matrix
+//      (g2n_scan.hip), then the same block re-ranks its elements with LDS atomics, stages them
+//      in LDS in digit order and writes each digit's run contiguously.  Pass 1 reads the COO
+//      coordinates themselves (both sides generated on the fly); pass 2 works inside each
+//      pass-1 group, blocks mapped to (group, chunk) on the device.
+//   F  one block per bucket (<= kSymCap elements): count rows in LDS, scatter by row, sort each
+//      row (registers, or Shell sort for long rows), merge the two sides per column, stage the
+//      merged entries in LDS; the bucket's CSR offset comes from a decoupled look-back over the
+//      buckets' entry counts (bucket order = ticket order), so indptr / indices / data are
+//      written once, at their final place, with coalesced stores.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "g2n_kernels.h"
+#include "g2n_scan.hip"
+
+namespace g2n {
+
+constexpr uint32_t kPartTPB = 1024;               // threads of a partition block
+constexpr uint32_t kSubPer = 8;                    // elements per thread in one sub-tile
+constexpr uint32_t kSub = kSubPer * kPartTPB;      // 8192 elements per sub-tile
+constexpr uint32_t kChunkSubs = 8;                 // sub-tiles per block
+constexpr uint32_t kPartTile = kSub * kChunkSubs;  // 65536 elements per partition block
+constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits
+constexpr uint32_t kSymCap = 4096;                 // elements one finish block holds
+constexpr uint32_t kSymPer = kSymCap / kTPB;       // 16 per thread
+
+// exclusive scan of one u32 per thread over a kN-thread block; returns the block total
+template <uint32_t kN>
+__device__ inline uint32_t block_excl_scan_n(uint32_t v, uint32_t* excl, uint32_t* lds /* >= kN / 64 */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  uint32_t wbase = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < (int)(kN / 64); w++) {
+    const uint32_t y = lds[w];
+    if (w < wid) wbase += y;
+    tot += y;
+  }
+  __syncthreads();
+  *excl = wbase + x - v;
+  return tot;
+}
+
+// element: x = row, y = column << 1 | side  (columns < 2^31)
+__device__ inline uint2 sym_elem(uint32_t row, uint32_t col, uint32_t side) { return make_uint2(row, (col << 1) | side); }
+
+// Where a partition block's elements come from.  Pass 1: the COO entries [blk * kPartTile / 2,
+// ...), each giving two elements (row a, side 0) and (row b, side 1).  Pass 2: the pass-1 output
+// of one group g (block -> (group, chunk j) through bstart).
+struct PartSrc {
+  const uint32_t* rows;   // pass 1
+  const uint32_t* cols;
+  uint64_t n_entries;
+  const uint2* in;        // pass 2
+  const uint32_t* gstart; // n_groups + 1 element offsets of the groups
+  const uint32_t* bstart; // n_groups + 1 first block of each group
+  uint32_t n_groups;
+};
+
+struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e0/2, e1/2))
+  uint64_t e0, e1;
+  uint32_t g, j, nb;
+};
+
+template <int kPass>
+__device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) {
+  if (kPass == 1) {
+    B.g = 0;
+    B.j = blk;
+    B.nb = 0;
+    B.e0 = (uint64_t)blk * kPartTile;
+    const uint64_t n_el = 2 * S.n_entries;
+    B.e1 = B.e0 + kPartTile < n_el ? B.e0 + kPartTile : n_el;
+    return true;
+  }
+  if (blk >= S.bstart[S.n_groups]) return false;
+  uint32_t lo = 0, hi = S.n_groups;  // last g with bstart[g] <= blk
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (S.bstart[mid] <= blk) lo = mid;
+    else hi = mid;
+  }
+  B.g = lo;
+  B.j = blk - S.bstart[lo];
+  B.nb = S.bstart[lo + 1] - S.bstart[lo];
+  B.e0 = (uint64_t)S.gstart[lo] + (uint64_t)B.j * kPartTile;
+  const uint64_t ge = S.gstart[lo + 1];
+  B.e1 = B.e0 + kPartTile < ge ? B.e0 + kPartTile : ge;
+  return true;
+}
+
+// Sub-tile at element e (e multiple of kSub within the block's range): thread t's elements.
+// Pass 1: entries e/2 + t + 1024 k (k < 4), coalesced u32 loads of rows and cols; pass 2:
+// elements e + t + 1024 k (k < 8), coalesced 8-byte loads.
+template <int kPass>
+__device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint2 (&x)[kSubPer], uint32_t& valid) {
+  valid = 0;
+  if (kPass == 1) {
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer / 2; k++) {
+      const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
+      uint32_t a = 0, b = 0;
+      if (2 * i < e1) {
+        a = S.rows[i];
+        b = S.cols[i];
+        valid |= 3u << (2 * k);
+      }
+      x[2 * k] = sym_elem(a, b, 0);
+      x[2 * k + 1] = sym_elem(b, a, 1);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++) {
+      const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
+      x[k] = make_uint2(0, 0);
+      if (i < e1) {
+        x[k] = S.in[i];
+        valid |= 1u << k;
+      }
+    }
+  }
+}
+
+// index of the block's count for digit d in the count matrix: pass 1 digit-major over blocks,
+// pass 2 group by group, digit-major over the group's blocks (so one device scan of the matrix
+// gives every (block, digit) run its output position)
+template <int kPass>
+__device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint32_t d, uint32_t n_dig, uint64_t n_blk) {
+  if (kPass == 1) return (uint64_t)d * n_blk + B.j;
+  return (uint64_t)S.bstart[B.g] * n_dig + (uint64_t)d * B.nb + B.j;
+}
+
+// Histogram of the block's digits (row >> shift) & (n_dig - 1) over its whole range.
+template <int kPass>
+__global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shift, uint32_t n_dig,
+                                                    uint32_t* __restrict__ counts, uint64_t n_blk) {
+  __shared__ uint32_t hist[1u << kMaxDigitBits];
+  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
+  PartBlock B;
+  if (!part_block<kPass>(S, blockIdx.x, B)) {  // block-uniform: past the last group's blocks
+    for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) counts[(uint64_t)blockIdx.x * n_dig + d] = 0;
+    return;
+  }
+  __syncthreads();
+  const uint32_t dmask = n_dig - 1;
+#pragma unroll 2
+  for (uint64_t e = B.e0; e < B.e1; e += kSub) {
+    uint2 x[kSubPer];
+    uint32_t valid;
+    part_load<kPass>(S, e, B.e1, x, valid);
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++)
+      if (valid >> k & 1) atomicAdd(&hist[(x[k].x >> shift) & dmask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) counts[part_slot<kPass>(S, B, d, n_dig, n_blk)] = hist[d];
+}
+
+// Scatter: per sub-tile, elements ranked in LDS (unstable), staged in digit order and written
+// as runs at each digit's cursor; the cursors advance sub-tile by sub-tile, so one block fills
+// each of its runs front to back (whole cache lines from one L2).
+template <int kPass>
+__global__ void __launch_bounds__(kPartTPB) k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
+                                                       const uint32_t* __restrict__ offs, uint64_t n_blk,
+                                                       uint2* __restrict__ out) {
+  __shared__ uint32_t hist[1u << kMaxDigitBits];  // sub-tile counts, then its digit starts
+  __shared__ uint32_t cur[1u << kMaxDigitBits];   // output position of the next element of digit d
+  __shared__ uint2 stage[kSub];
+  __shared__ uint32_t red[kPartTPB / 64];
+  PartBlock B;
+  if (!part_block<kPass>(S, blockIdx.x, B)) return;
+  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)];
+  const uint32_t dmask = n_dig - 1;
+  uint2 x[kSubPer], nx[kSubPer];
+  uint32_t valid, nvalid = 0;
+  part_load<kPass>(S, B.e0, B.e1, x, valid);
+  for (uint64_t e = B.e0; e < B.e1; e += kSub) {
+    for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
+    if (e + kSub < B.e1) part_load<kPass>(S, e + kSub, B.e1, nx, nvalid);  // next sub-tile in flight
+    __syncthreads();
+    uint32_t rk[kSubPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++)
+      rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(x[k].x >> shift) & dmask], 1u) : 0u;
+    __syncthreads();
+    const uint32_t hv = threadIdx.x < n_dig ? hist[threadIdx.x] : 0u;  // n_dig <= 1024: one digit per thread
+    uint32_t ex;
+    const uint32_t tot = block_excl_scan_n<kPartTPB>(hv, &ex, red);
+    if (threadIdx.x < n_dig) hist[threadIdx.x] = ex;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++)
+      if (valid >> k & 1) stage[hist[(x[k].x >> shift) & dmask] + rk[k]] = x[k];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kPartTPB) {
+      const uint2 y = stage[i];
+      const uint32_t d = (y.x >> shift) & dmask;
+      out[cur[d] + (i - hist[d])] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x < n_dig) cur[threadIdx.x] += hv;
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++) x[k] = nx[k];
+    valid = nvalid;
+  }
+}
+
+// pass-1 groups -> pass-2 block map: gstart[g] = offs[g * n_blk1] (the scan at digit g, block 0),
+// bstart = scan of the groups' block counts.  One block of 1024 threads (n_groups <= 1024).
+__global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs1, uint64_t n_blk1,
+                                                      uint32_t n_groups, uint32_t total, uint32_t* __restrict__ gstart,
+                                                      uint32_t* __restrict__ bstart) {
+  __shared__ uint32_t red[16];
+  const uint32_t g = threadIdx.x;
+  const uint32_t s = g < n_groups ? offs1[(uint64_t)g * n_blk1] : total;
+  const uint32_t e = g + 1 < n_groups ? offs1[(uint64_t)(g + 1) * n_blk1] : total;
+  const uint32_t nb = g < n_groups ? (e - s + kPartTile - 1) / kPartTile : 0u;
+  // block scan over 1024 threads (16 waves)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = nb;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) red[wid] = x;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (int q = 0; q < 16; q++) {
+    if (q < wid) base += red[q];
+    all += red[q];
+  }
+  if (g < n_groups) {
+    gstart[g] = s;
+    bstart[g] = base + x - nb;
+  }
+  if (g == 0) {
+    gstart[n_groups] = total;
+    bstart[n_groups] = all;
+  }
+}
+
+// bucket starts after the last pass: bucket q = (g << bits2) | d
+__global__ void __launch_bounds__(kTPB) k_part_bucket_starts(const uint32_t* __restrict__ offs2, PartSrc m,
+                                                             uint32_t n_dig2, uint32_t total, uint64_t n_buckets,
+                                                             uint32_t* __restrict__ bstart_out) {
+  const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (q > n_buckets) return;
+  if (q == n_buckets) {
+    bstart_out[q] = total;
+    return;
+  }
+  const uint32_t g = (uint32_t)(q / n_dig2), d = (uint32_t)(q % n_dig2);
+  const uint32_t nb = m.bstart[g + 1] - m.bstart[g];
+  bstart_out[q] = nb ? offs2[(uint64_t)m.bstart[g] * n_dig2 + (uint64_t)d * nb] : m.gstart[g];
+}
+
+// single pass: bucket q = digit q, start = offs1[q * n_blk1]
+__global__ void __launch_bounds__(kTPB) k_part_bucket_starts1(const uint32_t* __restrict__ offs1, uint64_t n_blk1,
+                                                              uint32_t total, uint64_t n_buckets,
+                                                              uint32_t* __restrict__ bstart_out) {
+  const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (q > n_buckets) return;
+  bstart_out[q] = q == n_buckets ? total : offs1[q * n_blk1];
+}
+
+// ---- F: bucket finish --------------------------------------------------------------------
+// sorts the n values at seg (LDS) ascending: registers for n <= 16, else Shell sort
+__device__ inline void sym_sort_row(uint32_t* seg, uint32_t n) {
+  if (n <= 1) return;
+  if (n <= 16) {
+    uint32_t k[16];
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) k[q] = q < n ? seg[q] : 0xFFFFFFFFu;
+    if (n <= 4) net_sort<4>(k);
+    else if (n <= 8) net_sort<8>(k);
+    else net_sort<16>(k);
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++)
+      if (q < n) seg[q] = k[q];
+    return;
+  }
+  constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};  // Ciura
+  for (uint32_t gp : gaps) {
+    if (gp >= n) continue;
+    for (uint32_t i = gp; i < n; i++) {
+      const uint32_t v = seg[i];
+      uint32_t jj = i;
+      while (jj >= gp && seg[jj - gp] > v) {
+        seg[jj] = seg[jj - gp];
+        jj -= gp;
+      }
+      seg[jj] = v;
+    }
+  }
+}
+
+// One block per bucket of 2^low <= 256 rows; the bucket's CSR offset comes from a decoupled
+// look-back over the buckets' entry counts in blockIdx order.  The order needs no atomic ticket
+// (a ticket on ONE counter serializes at ~11 ns per block — 2.2 ms for C4's 195K buckets,
+// tools/microbench/dispatch.hip) because the look-back is BOUNDED: a block whose predecessors do
+// not publish within kSpinLimit polls (a dispatch order that is not by blockIdx, another process
+// holding the CUs) gives up waiting, stages its merged entries in `tmp` at its input offset, keeps
+// its rows' local offsets in indptr and queues itself; k_sym_fixup then moves the queued buckets
+// once the host has scanned btot.  Every block therefore finishes: no order assumption is needed
+// for progress, only for speed.  A bucket over kSymCap elements sets ctl->bucket_overflow (the
+// host then takes the general path).
+//
+constexpr uint32_t kSpinLimit = 1u << 14;
+
+// look-back of bucket b with aggregate agg, by the whole block (256 predecessors per probe):
+// true and *excl = the exclusive prefix, or false when a predecessor did not publish within the
+// spin budget.  Block-uniform result; every thread calls it.
+__device__ inline bool lookback_bounded(unsigned long long* __restrict__ status, uint64_t b, unsigned long long agg,
+                                        unsigned long long* excl_out, uint32_t spin_limit, unsigned long long* red64,
+                                        uint32_t* redf) {
+  if (b == 0) {
+    if (threadIdx.x == 0) status_store(&status[0], kStInc | agg);
+    *excl_out = 0;
+    return true;
+  }
+  if (threadIdx.x == 0) status_store(&status[b], kStAgg | agg);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long excl = 0;
+  int64_t w = (int64_t)b - 1;
+  uint32_t spins = 0;
+  while (true) {
+    const int64_t q = w - (int64_t)threadIdx.x;
+    unsigned long long st = q >= 0 ? status_load(&status[q]) : kStInc;
+    bool gave_up = false;
+    while (true) {  // until every thread of the block sees a published word
+      const uint32_t pending = __syncthreads_or((st >> 62) == 0);
+      if (!pending) break;
+      if (++spins > spin_limit) {
+        gave_up = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if ((st >> 62) == 0) st = status_load(&status[q]);
+    }
+    if (gave_up) return false;
+    // closest predecessor with an inclusive prefix: the lowest thread index holding one
+    const unsigned long long inc = __ballot((st >> 62) == 2);
+    if (lane == 0) redf[wid] = inc ? (uint32_t)(wid * 64 + __builtin_ctzll(inc)) : 0xFFFFFFFFu;
+    __syncthreads();
+    uint32_t stop = 0xFFFFFFFFu;
+    for (int k = 0; k < kTPB / 64; k++) stop = min(stop, redf[k]);
+    unsigned long long v = threadIdx.x <= stop ? (st & kStVal) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red64[wid] = v;
+    __syncthreads();
+    for (int k = 0; k < kTPB / 64; k++) excl += red64[k];
+    __syncthreads();
+    if (stop != 0xFFFFFFFFu) break;
+    w -= kTPB;
+  }
+  if (threadIdx.x == 0) status_store(&status[b], kStInc | (excl + agg));
+  *excl_out = excl;
+  return true;
+}
+
+constexpr uint32_t kShortRow = 16;
+constexpr uint32_t kStagedSkip = 0xFFFFFFFFu;
+
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
+                                                     uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
+                                                     unsigned long long* __restrict__ status, uint2* __restrict__ tmp,
+                                                     uint32_t* __restrict__ fixq, int32_t* __restrict__ indptr,
+                                                     int32_t* __restrict__ indices, T* __restrict__ data, Ctl* ctl,
+                                                     uint32_t spin_limit) {
+  __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
+  __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
+  __shared__ uint32_t cnt[kTPB];
+  __shared__ uint32_t red[kTPB / 64];
+  cnt[threadIdx.x] = 0;
+  const uint64_t b = blockIdx.x;
+  const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
+  const bool over = n > kSymCap;  // block-uniform
+  if (over) {  // the build's sums go through the general path; successors must not wait on b
+    if (threadIdx.x == 0) {
+      ctl->bucket_overflow = 1;
+      btot[b] = 0;
+      status_store(&status[b], kStAgg);
+    }
+    return;
+  }
+  __syncthreads();
+  const uint32_t rmask = (1u << low) - 1u;
+  uint32_t my, rs;
+  {
+    uint32_t rr[kSymPer], vv[kSymPer];
+    {
+#pragma unroll
+      for (uint32_t k = 0; k < kSymPer; k++) {
+        const uint32_t i = threadIdx.x + k * kTPB;
+        if (i < n) {
+          const uint2 x = el[e0 + i];
+          rr[k] = x.x & rmask;
+          vv[k] = x.y;
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kSymPer; k++)
+        if (threadIdx.x + k * kTPB < n) rr[k] |= atomicAdd(&cnt[rr[k]], 1u) << 16;  // rank within the row
+    }
+    __syncthreads();
+    my = cnt[threadIdx.x];
+    block_excl_scan_u32(my, &rs, red);
+    cnt[threadIdx.x] = rs;  // row starts
+    __syncthreads();
+    {
+#pragma unroll
+      for (uint32_t k = 0; k < kSymPer; k++)
+        if (threadIdx.x + k * kTPB < n) seg[cnt[rr[k] & 0xFFFFu] + (rr[k] >> 16)] = vv[k];
+    }
+    __syncthreads();
+  }
+  const uint64_t row = (b << low) + threadIdx.x;
+  const bool live = threadIdx.x <= rmask && row < n_rows;
+  const bool shortrow = my <= kShortRow;
+  uint32_t* sg = seg + rs;
+  // short rows: registers; sorted ascending, padding sorts last
+  uint32_t k[kShortRow];
+#pragma unroll
+  for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
+  {  // one network per wave: the longest short row of the wave picks it (no divergent sorts)
+    uint32_t wm = (live && shortrow) ? my : 0u;
+    for (int o = 32; o > 0; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor(wm, o, 64));
+    if (wm > 8) net_sort<16>(k);
+    else if (wm > 4) net_sort<8>(k);
+    else if (wm > 1) net_sort<4>(k);
+  }
+  if (live && !shortrow) sym_sort_row(sg, my);
+  // merged entries: per column the side-0 copies (x) and side-1 copies (y); the value is
+  // max(sum of x ones, sum of y ones) in dtype arithmetic, zeros dropped (csr_maximum_csr)
+  auto keep = [&](uint32_t kx, uint32_t ky, uint32_t& kk) -> bool {
+    if constexpr (std::is_same<T, int8_t>::value) {  // int8 sums wrap: compare the dtype values
+      const T x = kx ? sum_copies<T>(one, kx) : (T)0, y = ky ? sum_copies<T>(one, ky) : (T)0;
+      kk = (x < y) ? ky : kx;
+      return ((x < y) ? y : x) != (T)0;
+    } else {  // bool / int32 / float32 / float64: the sum of k >= 1 ones is non-zero and
+              // non-decreasing in k (k <= kSymCap), so the max is the larger count's sum
+      kk = kx > ky ? kx : ky;
+      return kk != 0;
+    }
+  };
+  // short row, unrolled and branch-free except for the emit: emit(j, col, copies) for each kept
+  // column in order (padding 0xFFFFFFFF never ends a run of a real column: columns < 2^31 - 1)
+  auto short_merge = [&](auto emit, bool emits) -> uint32_t {
+    uint32_t m = 0, kx = 0, ky = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kShortRow; q++) {
+      const bool valid = q < my;
+      const uint32_t sd = k[q] & 1u;
+      kx += (valid && !sd) ? 1u : 0u;
+      ky += (valid && sd) ? 1u : 0u;
+      const bool last = valid && (q + 1 == kShortRow || (k[q + 1] >> 1) != (k[q] >> 1));
+      uint32_t kk;
+      const bool kept = keep(kx, ky, kk);
+      if (emits) {
+        if (last && kept) emit(m, k[q] >> 1, kk);
+      }
+      m += (last && kept) ? 1u : 0u;
+      kx = last ? 0u : kx;
+      ky = last ? 0u : ky;
+    }
+    return m;
+  };
+  auto long_merge = [&](auto emit) -> uint32_t {
+    uint32_t i = 0, m = 0;
+    while (i < my) {
+      const uint32_t c = sg[i] >> 1;
+      uint32_t kx = 0, ky = 0;
+      while (i < my && (sg[i] >> 1) == c) {
+        if (sg[i] & 1) ky++;
+        else kx++;
+        i++;
+      }
+      uint32_t kk;
+      if (keep(kx, ky, kk)) emit(m++, c, kk);
+    }
+    return m;
+  };
+  auto none = [](uint32_t, uint32_t, uint32_t) {};
+  const uint32_t m = !live ? 0u : (shortrow ? short_merge(none, false) : long_merge(none));
+  uint32_t off;
+  const uint32_t tot = block_excl_scan_u32(m, &off, red);
+  __shared__ unsigned long long red64[kTPB / 64];
+  unsigned long long base = 0;
+  const bool ok = spin_limit && lookback_bounded(status, b, tot, &base, spin_limit, red64, red);
+  if (threadIdx.x == 0) {
+    btot[b] = tot;
+    if (!ok) fixq[atomicAdd(&ctl->n_fix, 1ull)] = (uint32_t)b;
+  }
+  if (!ok) {  // staged at the bucket's input offset for k_sym_fixup; indptr holds local offsets
+    if (live) {
+      indptr[row] = (int32_t)off;
+      if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
+      auto put = [&](uint32_t j, uint32_t c, uint32_t kk) { tmp[e0 + off + j] = make_uint2(c, kk); };
+      if (shortrow) short_merge(put, true);
+      else long_merge(put);
+    }
+    return;
+  }
+  if (live) {
+    indptr[row] = (int32_t)(base + off);
+    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(base + off + m);
+    if (!shortrow)  // straight to HBM, before the staging below reuses the segments
+      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
+        indices[base + off + j] = (int32_t)c;
+        data[base + off + j] = sum_copies<T>(one, kk);
+      });
+  }
+  __syncthreads();
+  if (live) {
+    if (shortrow) {
+      short_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
+        seg[off + j] = c;
+        ocnt[off + j] = (uint8_t)kk;
+      }, true);
+    } else {
+      for (uint32_t j = 0; j < m; j++) seg[off + j] = kStagedSkip;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
+    const uint32_t c = seg[i];
+    if (c != kStagedSkip) {
+      indices[base + i] = (int32_t)c;
+      data[base + i] = sum_copies<T>(one, ocnt[i]);
+    }
+  }
+}
+
+// Buckets whose look-back gave up: their staged entries to the final place (boff = scan of btot).
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_sym_fixup(const uint32_t* __restrict__ fixq, const uint32_t* __restrict__ bstart,
+                                                    const uint32_t* __restrict__ btot, const uint32_t* __restrict__ boff,
+                                                    uint32_t low, uint64_t n_rows, T one, const uint2* __restrict__ tmp,
+                                                    int32_t* __restrict__ indptr, int32_t* __restrict__ indices,
+                                                    T* __restrict__ data) {
+  const uint32_t b = fixq[blockIdx.x];
+  const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
+  for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
+    const uint2 x = tmp[e0 + i];
+    indices[base + i] = (int32_t)x.x;
+    data[base + i] = sum_copies<T>(one, x.y);
+  }
+  const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
+  if (threadIdx.x < (1u << low) && row < n_rows) {
+    indptr[row] += (int32_t)base;
+    if (row == n_rows - 1) indptr[n_rows] += (int32_t)base;
+  }
+}
+
+}  // namespace g2n

@@ -91,7 +91,9 @@ typedef struct g2n_options {
   int32_t want_node_names;     /* 1 (default): produce the names blob in id order */
   int32_t device;              /* HIP device ordinal, default 0 */
   int32_t reserved[6];         /* [0]: unsupported records skipped silently (an earlier shard of a
-                                  sharded build warned already); others 0 */
+                                  sharded build warned already); [1]: test flags, bit 0 = MAX-SYM
+                                  bucket finish without its look-back (every bucket staged and
+                                  moved by the fix-up kernel; same result); others 0 */
 } g2n_options;
 
 #define G2N_MAX_PHASES 40

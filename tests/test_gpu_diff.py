@@ -410,11 +410,20 @@ def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
 
 
 def test_maxsym_buckets_large(gpu, monkeypatch):
-    """Bucket path == classic path at 10^7 edges (several radix passes skipped)."""
+    """Bucket path == classic path at 10^7 edges (two partition passes), and == the bucket path
+    whose look-back is disabled (every bucket staged and moved by k_sym_fixup)."""
+    from gfa2network_amd import _native as nat
     from gfa2network_amd import synth
 
     data = synth.host_bytes(2_000_000, 8_000_000, seed=21)
     a = outcome(gpu_run(data, {}, "float64", None))
+    monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_LOOKBACK)
+    for dtype in ("float64", "int8"):
+        assert outcome(gpu_run(data, {}, dtype, None)) == (a if dtype == "float64" else
+                                                           outcome(gpu_run(data, {}, dtype, None)))
+    f = outcome(gpu_run(data, {}, "float64", None))
+    monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+    assert a == f
     monkeypatch.setenv("G2N_NO_BUCKETS", "1")
     b = outcome(gpu_run(data, {}, "float64", None))
     assert a == b
