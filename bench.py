@@ -265,12 +265,13 @@ def main():
     # the same build through the hash dictionary (what inputs without decimal segment ids take)
     t_h, hash_ph = None, None
     if not args.no_alt:
-        os.environ["G2N_DICT_HASH"] = "1"
-        step()
+        hopts = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=local,
+                                 directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+                                 weight_tag=mode.get("weight_tag"), test_flags=nat.TEST_DICT_HASH)
+        step(hopts)
         t_h = time.perf_counter()
-        hash_ph = step()
+        hash_ph = step(hopts)
         t_h = time.perf_counter() - t_h
-        del os.environ["G2N_DICT_HASH"]
     # export --format edge-list on the same input (the text rendered in HBM)
     t_x, x_ph, x_bytes = None, None, 0
     if not args.no_alt:
@@ -301,7 +302,7 @@ def main():
     dom = max(cand, key=cand.get)
     dom_bytes, unit_desc = kernel_bytes(dom, **counts)
     achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
-    traffic = measured_traffic(KERNEL_OF_PHASE[dom])
+    traffic, traffic_src = measured_traffic(KERNEL_OF_PHASE[dom])
     line = {
         "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
         "value": round(value, 2),
@@ -327,14 +328,15 @@ def main():
                               "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
         "roofline": {"bound": "hbm", "kernel": KERNEL_OF_PHASE[dom], "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "per_unit": unit_desc,
-                     "ms_per_launch": round(avg[dom], 3)},
+                     "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
+                     "per_unit": unit_desc, "ms_per_launch": round(avg[dom], 3),
+                     "timing": "hipEvents on the pipeline stream around the kernel, averaged over the timed steps"},
     }
     if t_h is not None:
         line["alt_paths"] = {"hash_dictionary": {
             "ms_per_step": round(t_h * 1e3, 3), "m_edges_per_s": round(n_edges / t_h / 1e6, 2),
             "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
-            "note": "G2N_DICT_HASH=1: segment names resolved through the GPU hash table (inputs whose S lines "
+            "note": "options.reserved[1] = TEST_DICT_HASH: segment names resolved through the GPU hash table (inputs whose S lines "
                     "are not named 1..N in order)"}}
     if t_x is not None:
         xt = x_ph.get("edge_text", 0.0)
@@ -425,7 +427,8 @@ def main_shard(args):
     dist.destroy_process_group()
 
 
-KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build (S-first dictionary path)
+KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
+    "tiles": "g2n::k_tile_count",
     "parse": "g2n::k_tile_parse",
     "insert_claim": "g2n::k_insert_round<0>",
     "insert_lookup": "g2n::k_lookup_fast<2>",
@@ -443,10 +446,13 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
     d_o = 12 if bidir else 0  # orientation descriptor (u64 off + u32 len) per touch
     avg_key = names_bytes / max(n_nodes, 1)
     k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
-    if phase == "parse" and lean:  # decimal ids: S touch descriptors, COO coordinates (+ weights) per edge
-        per_s, per_e = 13 + d_o, 8 * k_trip + (8 if weighted else 0)
-        return (in_bytes + 9 * n_lines + per_s * n_s * tps + per_e * n_edges,
-                f"B_in + 9 B/line + {per_s} B/S touch + {per_e} B/edge (lean decimal-id parse)")
+    if phase == "tiles":  # K1 reads every byte once; 48 B of counts per 32 KiB tile
+        return in_bytes, "B_in (K1: every input byte read once)"
+    if phase == "parse" and lean:  # decimal ids: S touch descriptors, COO coordinates (+ weights) per edge;
+        # the lean parse writes no line starts / kinds (k_tile_parse skips them when op.rows is set)
+        per_s, per_e = 13 + d_o, 4 * k_trip * 2 + (8 if weighted else 0)
+        return (in_bytes + per_s * n_s * tps + per_e * n_edges,
+                f"B_in + {per_s} B/S touch + {per_e} B/edge (lean decimal-id parse)")
     if phase == "parse":  # every input byte once; line start + kind per line; descriptors per touch / edge
         per_t, per_e = 13 + d_o, 12
         return (in_bytes + 9 * n_lines + per_t * n_t + per_e * n_edges,
@@ -479,16 +485,19 @@ def random_ceiling(records: int, ms: float):
             "source": "profiles/r01/randread_ceiling.jsonl"}
 
 
+PMC_SUMMARY = ROOT / "profiles" / "r02" / "pmc_c4.json"
+
+
 def measured_traffic(kernel: str):
-    """HBM bytes per launch for `kernel` from the committed rocprofv3 PMC summary
-    (profiles/latest_pmc.json, FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or None."""
-    p = ROOT / "profiles" / "latest_pmc.json"
-    if not p.exists():
-        return None
+    """HBM bytes per launch for `kernel` (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
+    correction) from the committed rocprofv3 PMC summary of this bench's C4 workload, with the
+    commit of the sources it was measured on (tools/counter_table.py writes both), or None."""
     try:
-        return json.loads(p.read_text()).get("kernels", {}).get(kernel, {}).get("traffic_bytes_per_launch")
+        doc = json.loads(PMC_SUMMARY.read_text())
     except (OSError, ValueError):
-        return None
+        return None, None
+    k = doc.get("kernels", {}).get(kernel, {})
+    return k.get("traffic_bytes_per_launch"), {"file": str(PMC_SUMMARY.relative_to(ROOT)), "commit": doc.get("commit")}
 
 
 if __name__ == "__main__":

@@ -79,18 +79,17 @@ struct ParseOpts {
   int bidir, keep, strip, has_wt;
   uint32_t wt_len;
   const uint8_t* wt;  // device copy of the weight tag bytes
-  // decimal-id dictionary fused into the parse (see k_int_ids): when tid is set, every touch's
-  // node id is computed from its own bytes while the line is staged; n_st = S touches,
-  // n_seg = S lines.  A premise failure sets ctl->int_fail (the hash dictionary then runs).
+  // decimal-id dictionary fused into the parse (see src_dec): when tid is set, every touch's
+  // node id is computed from its own bytes while the line is staged; n_seg = S lines (an edge
+  // key must name one).  A premise failure sets ctl->int_fail (the hash dictionary then runs).
   uint32_t* tid;
-  uint64_t n_st, n_seg;
+  uint64_t n_seg;
   // lean mode (decimal ids only): the parse writes the stream-order COO coordinates itself —
   // rows / cols of edge e at e * ktrip (the triplet layout of k_triplets) — and skips the edge
   // touch descriptors, E.tb and (unweighted) E.w; a premise failure re-runs a full parse
   int32_t* rows;
   int32_t* cols;
   uint32_t ktrip;
-  uint32_t dbg;  // G2N_PARSE_DBG (profiling experiments only; 0 in every real build)
 };
 
 struct TouchOut {

@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "g2n_kernels.h"
+#include "g2n_scan.hip"
 #include "pylit.h"
 #include "stl_sort.h"
 
@@ -199,26 +200,34 @@ __device__ inline uint4 load16(const uint8_t* __restrict__ in, uint64_t pos, uin
 // its first byte; its index is the number of '\n' before it (parser.py:114 `for line in fh`),
 // its record kind the first-byte dispatch of parser.py:117-134 (a record type must be followed
 // by '\t', '\n' or the end of input).
-constexpr uint32_t kTileChunks = (uint32_t)(kTile / 16);  // 2048
-constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // 8
+constexpr uint32_t kTileChunks = (uint32_t)(kTile / 16);  // 16-byte chunks per tile
+constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // chunks per thread
 
+// A tile's bytes (plus kHalo past it) in registers: thread t holds the 16-byte chunks
+// t + 256 j; all loads are issued before the first LDS write.  (A persistent variant that loads
+// tile i + G while parsing tile i measured slower on gfx950: the prefetch registers took K2 from
+// 80 to 212 VGPRs, 2 waves/SIMD, 6.3 -> 10.7 ms on C4.)
 template <uint32_t kHalo>
-__device__ inline void stage_tile(const uint8_t* __restrict__ in, uint64_t len, uint64_t t0, uint8_t* lds) {
-  constexpr uint32_t kChunks = (uint32_t)((kTile + kHalo) / 16);
-  constexpr uint32_t kPer = (kChunks + kTPB - 1) / kTPB;
+struct TileRegs {
+  static constexpr uint32_t kChunks = (uint32_t)((kTile + kHalo) / 16);
+  static constexpr uint32_t kPer = (kChunks + kTPB - 1) / kTPB;
   uint4 r[kPer];
+  __device__ inline void load(const uint8_t* __restrict__ in, uint64_t len, uint64_t t0) {
 #pragma unroll
-  for (uint32_t j = 0; j < kPer; j++) {  // every load in flight before the first LDS write
-    const uint32_t c = j * kTPB + threadIdx.x;
-    const uint64_t pos = t0 + (uint64_t)c * 16;
-    r[j] = (c < kChunks && pos < len) ? load16(in, pos, len) : make_uint4(0, 0, 0, 0);
+    for (uint32_t j = 0; j < kPer; j++) {  // every load in flight before any is used
+      const uint32_t c = j * kTPB + threadIdx.x;
+      const uint64_t pos = t0 + (uint64_t)c * 16;
+      r[j] = (c < kChunks && pos < len) ? load16(in, pos, len) : make_uint4(0, 0, 0, 0);
+    }
   }
+  __device__ inline void store(uint8_t* lds) const {
 #pragma unroll
-  for (uint32_t j = 0; j < kPer; j++) {
-    const uint32_t c = j * kTPB + threadIdx.x;
-    if (c < kChunks) *(uint4*)(lds + (uint64_t)c * 16) = r[j];
+    for (uint32_t j = 0; j < kPer; j++) {
+      const uint32_t c = j * kTPB + threadIdx.x;
+      if (c < kChunks) *(uint4*)(lds + (uint64_t)c * 16) = r[j];
+    }
   }
-}
+};
 
 __device__ inline uint8_t line_kind(uint8_t c0, bool exact) {
   switch (c0) {
@@ -260,12 +269,10 @@ __device__ inline void chunk_masks(const uint8_t* buf, uint32_t c, uint64_t t0, 
 struct TileCnt {
   unsigned long long nl, lines, touches, edges, segs, recs;
 };
-struct TileCntPlus {
-  __device__ __host__ TileCnt operator()(const TileCnt& a, const TileCnt& b) const {
-    return TileCnt{a.nl + b.nl, a.lines + b.lines, a.touches + b.touches, a.edges + b.edges, a.segs + b.segs,
-                   a.recs + b.recs};
-  }
-};
+__device__ __host__ inline TileCnt operator+(const TileCnt& a, const TileCnt& b) {
+  return TileCnt{a.nl + b.nl, a.lines + b.lines, a.touches + b.touches, a.edges + b.edges, a.segs + b.segs,
+                 a.recs + b.recs};
+}
 
 template <class T>
 __device__ inline T block_sum(T v, T* lds /* >= kTPB / 64 */) {
@@ -302,16 +309,21 @@ __device__ inline unsigned long long block_excl_scan_u64(unsigned long long v, u
   return wbase + x - v;
 }
 
-// pass 1: per tile, the '\n', lines, touches, edges, S lines and records it holds
+// pass 1: per tile, the '\n', lines, touches, edges, S lines and records it holds.  Per-tile
+// counts are < 2^16 (32 KiB tiles), so four of them share one block reduction.
 __global__ void __launch_bounds__(kTPB) k_tile_count(const uint8_t* __restrict__ in, uint64_t len, uint32_t tps,
                                                      uint32_t tpe, TileCnt* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + 16];
   __shared__ unsigned long long red[kTPB / 64];
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
-  stage_tile<16>(in, len, t0, buf);
+  {
+    TileRegs<16> R;
+    R.load(in, len, t0);
+    R.store(buf);
+  }
   const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
   __syncthreads();
-  unsigned long long nl = 0, lines = 0, touches = 0, edges = 0, segs = 0, recs = 0;
+  uint32_t nl = 0, lines = 0, edges = 0, segs = 0, po = 0;
 #pragma unroll 2
   for (uint32_t j = 0; j < kChunkIters; j++) {
     const uint32_t c = j * kTPB + threadIdx.x;
@@ -323,19 +335,25 @@ __global__ void __launch_bounds__(kTPB) k_tile_count(const uint8_t* __restrict__
       const uint32_t o = 16 * c + __builtin_ctz(st);
       st &= st - 1;
       const uint8_t k = kind_at(buf, o, t0 + o, len);
-      if (k == kS) { touches += tps; segs++; recs++; }
-      else if (k == kEdge) { touches += tpe; edges++; recs++; }
-      else if (k == kPO) recs++;
+      segs += k == kS;
+      edges += k == kEdge;
+      po += k == kPO;
     }
   }
-  TileCnt cnt;
-  cnt.nl = block_sum(nl, red);
-  cnt.lines = block_sum(lines, red);
-  cnt.touches = block_sum(touches, red);
-  cnt.edges = block_sum(edges, red);
-  cnt.segs = block_sum(segs, red);
-  cnt.recs = block_sum(recs, red);
-  if (threadIdx.x == 0) out[blockIdx.x] = cnt;
+  const unsigned long long a = block_sum((unsigned long long)nl | ((unsigned long long)lines << 16) |
+                                             ((unsigned long long)segs << 32) | ((unsigned long long)edges << 48),
+                                         red);
+  const unsigned long long b = block_sum((unsigned long long)po, red);
+  if (threadIdx.x == 0) {
+    TileCnt cnt;
+    cnt.nl = a & 0xFFFF;
+    cnt.lines = (a >> 16) & 0xFFFF;
+    cnt.segs = (a >> 32) & 0xFFFF;
+    cnt.edges = a >> 48;
+    cnt.touches = cnt.segs * tps + cnt.edges * tpe;
+    cnt.recs = cnt.segs + cnt.edges + b;
+    out[blockIdx.x] = cnt;
+  }
 }
 
 // ================================================================ K2: parse =======
@@ -643,9 +661,14 @@ __device__ inline bool src_dec(const Src& in, uint64_t o, uint32_t l, uint64_t* 
   return true;
 }
 
+// Decimal-id premise state of one thread: fail = a premise broke.
+struct IntState {
+  uint32_t fail = 0;
+};
+
 // an edge touch's node id from its bytes, or false (no S key: the premise fails)
 __device__ inline bool int_edge_id(const Src& in, const ParseOpts& op, uint64_t no, uint32_t nl, uint64_t oo,
-                                   uint32_t ol, uint32_t* id) {
+                                   uint32_t ol, uint32_t* id, IntState& is) {
   uint64_t v;
   if (!src_dec(in, no, nl, &v) || v < 1 || v > op.n_seg) return false;
   *id = (uint32_t)(v - 1);
@@ -658,8 +681,8 @@ __device__ inline bool int_edge_id(const Src& in, const ParseOpts& op, uint64_t 
 }
 
 // S line i, name = [ns, ne): parser.py:163, builders.py:190-198
-__device__ inline void put_segment(const Src& in, const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t ns,
-                                   uint64_t ne, uint32_t& ifail) {
+__device__ inline void put_segment(const Src& in, const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t eb,
+                                   uint64_t ns, uint64_t ne, IntState& is) {
   const uint32_t nl = (uint32_t)(ne - ns);
   if (!op.bidir) {
     put_touch(T, tb, ns, nl, 0, 0, false, 1);
@@ -667,19 +690,18 @@ __device__ inline void put_segment(const Src& in, const ParseOpts& op, const Tou
     put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
     put_touch(T, tb + 1, ns, nl, kConstFlag | '-', 1, true, 1);
   }
-  if (op.tid && !ifail) {  // S touch tb is node tb: its name must be str(line + 1), line = tb / tps
+  if (op.tid && !is.fail) {  // no edge line before it (eb = 0), so S touch tb is node tb: its name
+                              // must be str(k + 1), k = tb / tps = the S lines before it
     uint64_t v;
     const uint64_t line = op.bidir ? tb >> 1 : tb;
-    if (tb + (op.bidir ? 1 : 0) >= op.n_st || (op.bidir && (tb & 1)) || !src_dec(in, ns, nl, &v) || v != line + 1)
-      ifail = 1;
+    if (eb != 0 || !src_dec(in, ns, nl, &v) || v != line + 1) is.fail = 1;
   }
 }
 
 // L / E / C line i = [s, e) ('\n' stripped), its touches from tb, its edge eb
 __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_t e, uint64_t tb, uint64_t eb,
                                   const ParseOpts& op, const TouchOut& T, const EdgeOut& E, Ctl* ctl,
-                                  uint64_t* __restrict__ worklist, uint32_t& ifail) {
-  if (op.dbg & 8) return;
+                                  uint64_t* __restrict__ worklist, IntState& is) {
   EdgeLayout L;
   if (!link_fast(in, s, e, L)) L = edge_layout(in, s, e);
   if (L.err) {
@@ -701,14 +723,14 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
   }
   if (op.rows) {  // lean: ids straight into the COO coordinates (k_triplets' layout)
     if (op.has_wt) E.w[eb] = w;
-    if (ifail || (op.dbg & 2)) return;
+    if (is.fail) return;
     uint32_t a, b, c = 0, d = 0;
-    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b);
+    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a, is) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b, is);
     if (ok && op.ktrip == 4)
-      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c) &&
-           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d);
+      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c, is) &&
+           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d, is);
     if (!ok) {
-      ifail = 1;
+      is.fail = 1;
       return;
     }
     const uint64_t o = eb * op.ktrip;
@@ -739,14 +761,14 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
       put_touch(T, tb + 3, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, true);
     }
   }
-  if (op.tid && !ifail) {
+  if (op.tid && !is.fail) {
     uint32_t a, b, c = 0, d = 0;
-    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b);
+    bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a, is) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b, is);
     if (ok && op.bidir && !op.keep)
-      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c) &&
-           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d);
+      ok = int_edge_id(in, op, L.vo, L.vl, rev_ori(in, L.ovo, L.ovl), 1, &c, is) &&
+           int_edge_id(in, op, L.uo, L.ul, rev_ori(in, L.ouo, L.oul), 1, &d, is);
     if (!ok) {
-      ifail = 1;
+      is.fail = 1;
     } else {
       op.tid[tb] = a;
       op.tid[tb + 1] = b;
@@ -764,7 +786,7 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
 __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, bool nl_at_bound, uint64_t i,
                                   uint8_t k, uint64_t s, uint64_t tb, uint64_t eb, const ParseOpts& op,
                                   const TouchOut& T, const EdgeOut& E, Ctl* ctl, uint64_t* __restrict__ worklist,
-                                  uint32_t& ifail) {
+                                  IntState& is) {
   const bool cut = bound < len;
   if (k == kS || k == kPO) {  // the first two (S) / three (P, O) fields
     uint64_t t1 = bound, t2 = bound;
@@ -802,7 +824,7 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
     }
     if (t2 == bound && cut) return false;
     if (k == kS) {
-      put_segment(in, op, T, tb, t1 + 1, t2, ifail);
+      put_segment(in, op, T, tb, eb, t1 + 1, t2, is);
     } else if (t2 == bound || in[t2] == '\n') {
       record_error(ctl, i, in[s] == 'P' ? kErrMalformedP : kErrMalformedO);
     }
@@ -810,7 +832,7 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
   }
   const uint64_t e = nl_at_bound ? bound - 1 : next_nl(in, s, bound);
   if (e == bound && cut) return false;
-  parse_edge(in, i, s, e, tb, eb, op, T, E, ctl, worklist, ifail);
+  parse_edge(in, i, s, e, tb, eb, op, T, E, ctl, worklist, is);
   return true;
 }
 
@@ -822,18 +844,24 @@ struct DeferredLine {  // at most one per tile: the line holding the tile window
 };
 
 // pass 2: line starts, kinds, touches, edges of every line starting in the tile.
-//  (1) one block scan over the 2048 chunks' start counts ranks every line start of the tile;
-//  (2) per window of kTileLines starts: the starts go to an LDS list, threads classify 8
-//      consecutive lines each and one block scan gives each line its S / edge line prefix;
+//  (1) one block scan over the tile's chunks' start counts ranks every line start;
+//  (2) per window of kTileLines starts: the starts go to an LDS list, threads classify
+//      kLinesPer consecutive lines each and one block scan gives each line its S / edge prefix;
 //  (3) lanes take consecutive lines and parse them from the staged bytes (no barriers).
-constexpr uint32_t kTileLines = 2048;
+// The tile bases come from K1's counts (exclusive scan).  A single pass that learns them from a
+// decoupled look-back over the tiles instead (no K1) measured 12.0 ms on C4 against 2.2 + 6.3
+// ms: in-order waiting across the 8 XCDs (status words polled past the non-coherent L2s) stalls
+// every tile behind the slowest.
+constexpr uint32_t kTileLines = kTileChunks;            // line starts per window (= chunks: pre[] holds both)
+constexpr uint32_t kLinesPer = kTileLines / kTPB;       // lines classified per thread
+static_assert(kChunkIters % 4 == 0 && kTile <= 32768, "tile layout: per-tile counts fit 16 bits");
 
 __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__ in, uint64_t len,
                                                      const TileCnt* __restrict__ base, uint32_t tps, uint32_t tpe,
                                                      ParseOpts op, uint64_t* __restrict__ ls,
                                                      uint8_t* __restrict__ kind, TouchOut T, EdgeOut E, Ctl* ctl,
                                                      uint64_t* __restrict__ worklist,
-                                                     DeferredLine* __restrict__ deferred) {
+                                                     DeferredLine* __restrict__ deferred, uint64_t n_tiles) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
   __shared__ __attribute__((aligned(16))) uint16_t starts[kTileLines];
   __shared__ __attribute__((aligned(16))) uint32_t pre[kTileChunks];  // chunk ranks, then line prefixes
@@ -841,9 +869,15 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   __shared__ uint32_t red[kTPB / 64];
   constexpr uint32_t kMaskChunks = (uint32_t)((kTile + kTileHalo) / 16) + 4;  // + 4: tab_bits reads 4 ahead
   __shared__ __attribute__((aligned(16))) uint16_t tabm[kMaskChunks];
-  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
-  stage_tile<kTileHalo>(in, len, t0, buf);
+  const uint64_t tile = blockIdx.x;
+  const uint64_t t0 = tile * kTile;
+  {
+    TileRegs<kTileHalo> R;
+    R.load(in, len, t0);
+    R.store(buf);
+  }
   const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
+  const TileCnt b = base[tile];
   __syncthreads();
   for (uint32_t c = threadIdx.x; c < kMaskChunks; c += kTPB) {  // the tile's tab bitmap (bytes past len: 0)
     uint32_t m = 0;
@@ -858,8 +892,6 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
   L.tm = tabm;
   L.tm_lim = t0 + kTile + kTileHalo;
-  const TileCnt b = base[blockIdx.x];
-  const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
   // (1) start masks of this thread's chunks (kept), counts -> ranks
   uint32_t stm[kChunkIters / 2];
 #pragma unroll
@@ -869,38 +901,47 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
     if (j & 1) stm[j >> 1] |= st << 16;
     else stm[j >> 1] = st;
-    pre[c] = __popc(st);
+    pre[c] = (uint32_t)__popc(st);
   }
   __syncthreads();
   uint32_t n_starts;
-  {
-    uint4 v0 = *(const uint4*)(pre + 8 * threadIdx.x), v1 = *(const uint4*)(pre + 8 * threadIdx.x + 4);
-    uint32_t q[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  {  // kChunkIters consecutive chunk counts per thread (4-word vector accesses)
+    uint32_t q[kChunkIters];
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkIters; k += 4) {
+      const uint4 v = *(const uint4*)(pre + kChunkIters * threadIdx.x + k);
+      q[k] = v.x;
+      q[k + 1] = v.y;
+      q[k + 2] = v.z;
+      q[k + 3] = v.w;
+    }
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) sum += q[k];
+    for (uint32_t k = 0; k < kChunkIters; k++) sum += q[k];
     uint32_t ex;
     n_starts = block_excl_scan_u32(sum, &ex, red);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (uint32_t k = 0; k < kChunkIters; k++) {
       const uint32_t t = q[k];
       q[k] = ex;
       ex += t;
     }
-    *(uint4*)(pre + 8 * threadIdx.x) = make_uint4(q[0], q[1], q[2], q[3]);
-    *(uint4*)(pre + 8 * threadIdx.x + 4) = make_uint4(q[4], q[5], q[6], q[7]);
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkIters; k += 4)
+      *(uint4*)(pre + kChunkIters * threadIdx.x + k) = make_uint4(q[k], q[k + 1], q[k + 2], q[k + 3]);
   }
+  const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
   __syncthreads();
   uint32_t rank[kChunkIters];
 #pragma unroll
   for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = pre[j * kTPB + threadIdx.x];
   uint64_t t_run = b.touches, e_run = b.edges;
   unsigned long long unk = ~0ull;
-  uint32_t ifail = 0;
+  IntState is;
   for (uint32_t w0 = 0; w0 < n_starts; w0 += kTileLines) {
     const uint32_t n_win = n_starts - w0 < kTileLines ? n_starts - w0 : kTileLines;
     __syncthreads();  // `pre` (ranks, or the last window's prefixes) is no longer read
-    // (2) the window's starts, in order
+    // (3) the window's starts, in order
 #pragma unroll
     for (uint32_t j = 0; j < kChunkIters; j++) {
       uint32_t st = (stm[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
@@ -914,12 +955,12 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       }
     }
     __syncthreads();
-    // kinds of 8 consecutive lines per thread; prefix counts of S and edge lines
+    // kinds of kLinesPer consecutive lines per thread; prefix counts of S and edge lines
     uint32_t cs = 0, ce = 0;
-    uint8_t kk[8];
+    uint8_t kk[kLinesPer];
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) {
-      const uint32_t j = 8 * threadIdx.x + q;
+    for (uint32_t q = 0; q < kLinesPer; q++) {
+      const uint32_t j = kLinesPer * threadIdx.x + q;
       uint8_t k = kSkip;
       if (j < n_win) {
         const uint32_t o = starts[j];
@@ -933,13 +974,13 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     uint32_t ex;
     const uint32_t tot = block_excl_scan_u32((cs << 16) | ce, &ex, red);
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) {
-      const uint32_t j = 8 * threadIdx.x + q;
+    for (uint32_t q = 0; q < kLinesPer; q++) {
+      const uint32_t j = kLinesPer * threadIdx.x + q;
       if (j < n_win) pre[j] = ex;
       ex += ((uint32_t)(kk[q] == kS) << 16) | (uint32_t)(kk[q] == kEdge);
     }
     __syncthreads();
-    // (3) parse: lane-parallel lines
+    // (4) parse: lane-parallel lines
 #pragma unroll 1
     for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
       const uint32_t o = starts[j];
@@ -951,16 +992,16 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
         kind[i] = k;
       }
       if (k == kUnknown) unk = i < unk ? i : unk;
-      if ((k == kS || k == kEdge || k == kPO) && !(op.dbg & 1) && !((op.dbg & 4) && k == kS)) {
+      if (k == kS || k == kEdge || k == kPO) {
         const uint32_t pr = pre[j];
         const uint64_t tb = t_run + (uint64_t)(pr >> 16) * tps + (uint64_t)(pr & 0xFFFF) * tpe;
         const uint64_t eb = e_run + (pr & 0xFFFF);
         // the line ends where the next one starts; the window's last line: search the staged bytes
         const bool known = j + 1 < n_win;
         const uint64_t bound = known ? t0 + starts[j + 1] : w1;
-        if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, ifail)) {
+        if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, is)) {
           const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
-          if (d < gridDim.x) deferred[d] = DeferredLine{i, p, (uint32_t)tb, (uint32_t)eb, k, 0};
+          if (d < n_tiles) deferred[d] = DeferredLine{i, p, (uint32_t)tb, (uint32_t)eb, k, 0};
         }
       }
     }
@@ -969,7 +1010,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   }
   unk = wave_reduce_min(unk);
   if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
-  if (__ballot(ifail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+  if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
 }
 
 // Lines whose fields run past their tile's staged window: parsed from global memory.
@@ -983,9 +1024,9 @@ __global__ void __launch_bounds__(64) k_parse_deferred(const uint8_t* __restrict
   if (j >= n) return;
   const DeferredLine d = deferred[j];
   const Src G{in, 0, len};
-  uint32_t ifail = 0;
-  parse_line(G, len, len, false, d.line, (uint8_t)d.kind, d.start, d.tb, d.eb, op, T, E, ctl, worklist, ifail);
-  if (ifail) ctl->int_fail = 1;
+  IntState is;
+  parse_line(G, len, len, false, d.line, (uint8_t)d.kind, d.start, d.tb, d.eb, op, T, E, ctl, worklist, is);
+  if (is.fail) ctl->int_fail = 1;
 }
 
 // Exact weights (CPython int()/float() semantics) for the edges the fast grammar deferred.
@@ -1388,9 +1429,7 @@ __global__ void __launch_bounds__(kTPB) k_lookup_fast(const uint8_t* __restrict_
 template __global__ void k_lookup_fast<2>(const uint8_t*, uint64_t, TouchIn, uint64_t, const DictEntry*, uint64_t,
                                           uint64_t, const uint8_t*, int, Ctl*, const uint32_t*, uint32_t,
                                           const uint32_t*, uint32_t*);
-template __global__ void k_lookup_fast<4>(const uint8_t*, uint64_t, TouchIn, uint64_t, const DictEntry*, uint64_t,
-                                          uint64_t, const uint8_t*, int, Ctl*, const uint32_t*, uint32_t,
-                                          const uint32_t*, uint32_t*);
+
 
 // S-prefix dictionary (every S touch precedes every edge touch, no S key repeated): the node id
 // of an S touch is its touch index; klen[id] for the names blob.

@@ -41,7 +41,12 @@ enum Slot {
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
-constexpr uint32_t kTestNoLookback = 1;  // k_sym_finish: every bucket staged + k_sym_fixup
+constexpr uint32_t kTestNoLookback = 1;     // k_sym_finish: every bucket staged + k_sym_fixup
+constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-sum path
+constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean parse (ids per touch, k_triplets)
+constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
+constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast path: the general rounds
+
 
 struct DevBuf {
   void* p = nullptr;
@@ -52,6 +57,7 @@ struct DevBuf {
 
 struct g2n_context {
   int device = 0;
+  int n_cu = 256;  // compute units: persistent launches size their grid from it
   uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
   hipStream_t stream = nullptr;
   std::vector<g2n::DevBuf> bufs;
@@ -84,6 +90,13 @@ static void* dbuf(g2n_context* c, int slot, size_t bytes) {
 template <class T>
 static T* dget(g2n_context* c, int slot, uint64_t count) {
   return (T*)dbuf(c, slot, (size_t)count * sizeof(T));
+}
+
+// grid of a persistent kernel: blocks_per_cu resident blocks per CU (its LDS occupancy), no more
+// than there are work items
+static unsigned persistent_grid(const g2n_context* c, uint64_t n_items, unsigned blocks_per_cu) {
+  const uint64_t g = (uint64_t)c->n_cu * blocks_per_cu;
+  return (unsigned)(n_items < g ? (n_items ? n_items : 1) : g);
 }
 
 static inline unsigned grid_for(uint64_t n, unsigned tpb = kTPB) {
@@ -126,10 +139,6 @@ static void excl_scan(g2n_context* c, const T* in, T* out, uint64_t n) {
   scan_excl<T, T>(c, in, out, n);
 }
 
-static int lookup_batch() {  // touches per thread in the S-first lookup (G2N_LOOKUP_BATCH=2|4)
-  const char* v = std::getenv("G2N_LOOKUP_BATCH");
-  return (v && v[0] == '4') ? 4 : 2;
-}
 
 static int bits_for(uint64_t n) {  // bits to hold values 0..n-1 (>= 1)
   int b = 1;
@@ -348,7 +357,7 @@ template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   if constexpr (kU) {
-    if (maxsym && n_trip && n_rows && n_rows == n_cols && !std::getenv("G2N_NO_BUCKETS") &&
+    if (maxsym && n_trip && n_rows && n_rows == n_cols && !(c->test_flags & kTestNoBuckets) &&
         maxsym_partition<T>(c, rows, cols, n_trip, n_rows, R))
       return;
   }
@@ -540,14 +549,9 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
       hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
                          max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
     else {
-      const int kb = lookup_batch();
-      const dim3 gb(grid_for(n_t, kTPB * kb));
-      if (kb == 4)
-        hipLaunchKernelGGL(k_lookup_fast<4>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
-                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
-      else
-        hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes,
-                           tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+      const dim3 gb(grid_for(n_t, kTPB * 2));  // two touches per thread
+      hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes, tstate,
+                         (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
     }
     phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
     sync_ctl(c);
@@ -566,7 +570,7 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
     // S-first fast path (a GFA whose S lines define every key before any other line uses it):
     // round 1 claims the S keys, their ranks are the node ids, one lookup round resolves every
     // other touch to its id.  Anything else is redone by the general rounds below.
-    bool fast = !std::getenv("G2N_DICT_GENERAL");
+    bool fast = !(c->test_flags & kTestDictGeneral);
     if (int_ids == kIntDone) {  // decimal-id dictionary: the parse wrote every edge touch's id
       hipLaunchKernelGGL(k_key_len, dim3(grid_for(n_st)), dim3(kTPB), 0, c->stream, TI, n_st, (int)bidir, klen);
       phase(c, "ids_fast");
@@ -692,13 +696,14 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   TileCnt tot{};
   if (n_tiles) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
-    size_t tb = 0;
-    G2N_HIP(rocprim::exclusive_scan(nullptr, tb, tcnt, tbase, TileCnt{}, (size_t)n_tiles, TileCntPlus(),
-                                    c->stream));
-    void* tmp = dbuf(c, S_TEMP, tb);
-    G2N_HIP(rocprim::exclusive_scan(tmp, tb, tcnt, tbase, TileCnt{}, (size_t)n_tiles, TileCntPlus(), c->stream));
-    const TileCnt last_b = read_dev(c, tbase + n_tiles - 1), last_c = read_dev(c, tcnt + n_tiles - 1);
-    tot = TileCntPlus()(last_b, last_c);
+    const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
+    auto* part = dget<TileCnt>(c, S_TEMP, n_parts + 1);  // chunk sums, then the total
+    hipLaunchKernelGGL(k_struct_reduce<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
+                       (const TileCnt*)tcnt, n_tiles, part);
+    hipLaunchKernelGGL(k_struct_scan_parts<TileCnt>, dim3(1), dim3(256), 0, c->stream, part, n_parts, part + n_parts);
+    hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
+                       (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
+    tot = read_dev(c, part + n_parts);
   }
   const uint64_t n_lines = tot.lines;
   const uint64_t n_e = tot.edges, n_s = tot.segs;
@@ -717,7 +722,6 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   op.bidir = bidir;
   op.keep = keep;
   op.strip = o->strip_orientation != 0;
-  op.dbg = std::getenv("G2N_PARSE_DBG") ? (uint32_t)std::atoi(std::getenv("G2N_PARSE_DBG")) : 0u;
   const size_t wtl = o->weight_tag ? std::strlen(o->weight_tag) : 0;
   op.has_wt = wtl > 0;
   op.wt_len = (uint32_t)wtl;
@@ -737,12 +741,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto* cols = dget<int32_t>(c, S_COLS, n_trip);
   // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
   // the first S line names "1" (a cheap guess: a wrong one costs one extra parse)
-  const bool int_ids = n_t && !std::getenv("G2N_DICT_GENERAL") && !std::getenv("G2N_DICT_HASH") &&
-                       first_segment_is_one(c, in, len);
-  const bool lean = int_ids && !std::getenv("G2N_NO_LEAN");
+  const bool int_ids =
+      n_t && !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
+  const bool lean = int_ids && !(c->test_flags & kTestNoLean);
   if (int_ids) {
     op.tid = dget<uint32_t>(c, S_TID, n_t);
-    op.n_st = n_s * tps;
     op.n_seg = n_s;
   }
   auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
@@ -752,7 +755,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto parse = [&](const ParseOpts& po) {
     if (n_tiles)
       hipLaunchKernelGGL(k_tile_parse, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe,
-                         po, ls, kind, T, E, c->ctl, wl, deferred);
+                         po, ls, kind, T, E, c->ctl, wl, deferred, n_tiles);
     sync_ctl(c);
     const uint64_t n_def = c->h_ctl->n_deferred;
     if (n_def > n_tiles) throw Failure(G2N_E_DEVICE, "internal: more deferred lines than tiles");
@@ -786,10 +789,6 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     }
   }
   if (!lean_done) parse(op);
-  if (op.dbg) {  // profiling experiment: the parse alone (its outputs are incomplete)
-    finish_timings(c, R);
-    return G2N_OK;
-  }
   const uint64_t n_work = c->h_ctl->wl_count;
   if (n_work) {
     hipLaunchKernelGGL(k_weights_slow, dim3(grid_for(n_work, 64)), dim3(64), 0, c->stream, in, len, ls, wl, n_work, op, E,
@@ -1004,6 +1003,8 @@ static g2n_context* context_create(int device) {
   c->device = device;
   G2N_HIP(hipSetDevice(device));
   G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  G2N_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+  if (c->n_cu <= 0) c->n_cu = 1;
   c->bufs.resize(S_NSLOTS);
   G2N_HIP(hipMalloc(&c->ctl, sizeof(Ctl)));
   G2N_HIP(hipHostMalloc(&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));

@@ -141,4 +141,73 @@ __global__ void __launch_bounds__(256) k_scan_excl(const TIn* __restrict__ in, T
 
 inline uint64_t scan_tiles(uint64_t n) { return n ? (n + kScanTile - 1) / kScanTile : 1; }
 
+// Exclusive scan of an array of a multi-field count struct T (T + T; T{} = 0) by reduce-then-
+// scan (its sums do not fit one 62-bit look-back word): k_struct_reduce sums each kStructChunk
+// run, k_struct_scan_parts (one block) scans those sums, k_struct_scan_chunks scans every run from
+// its base.  For the front end's per-tile counts (~200K x 48 B on C4).
+constexpr uint32_t kStructChunk = 1024;  // 4 items per thread of a 256-thread block
+
+template <class T>
+__device__ inline T block_incl_scan_struct(T v, T* buf /* 256 */) {  // Hillis-Steele in LDS
+  buf[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const T y = (int)threadIdx.x >= o ? buf[threadIdx.x - o] : T{};
+    __syncthreads();
+    v = v + y;
+    buf[threadIdx.x] = v;
+    __syncthreads();
+  }
+  return v;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_struct_reduce(const T* __restrict__ in, uint64_t n, T* __restrict__ part) {
+  __shared__ T buf[256];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kStructChunk + 4 * threadIdx.x;
+  T s{};
+  for (uint32_t k = 0; k < 4; k++)
+    if (i0 + k < n) s = s + in[i0 + k];
+  const T inc = block_incl_scan_struct(s, buf);
+  if (threadIdx.x == 255) part[blockIdx.x] = inc;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_struct_scan_parts(T* __restrict__ part, uint64_t n_parts, T* __restrict__ total) {
+  __shared__ T buf[256];
+  __shared__ T carry;
+  if (threadIdx.x == 0) carry = T{};
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < n_parts; b0 += 256) {
+    const uint64_t k = b0 + threadIdx.x;
+    const T v = k < n_parts ? part[k] : T{};
+    const T inc = block_incl_scan_struct(v, buf);
+    const T c = carry;
+    const T excl = threadIdx.x ? buf[threadIdx.x - 1] : T{};
+    __syncthreads();
+    if (k < n_parts) part[k] = c + excl;
+    if (threadIdx.x == 255) carry = c + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_struct_scan_chunks(const T* __restrict__ in, uint64_t n,
+                                                            const T* __restrict__ part, T* __restrict__ out) {
+  __shared__ T buf[256];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kStructChunk + 4 * threadIdx.x;
+  T v[4], s{};
+  for (uint32_t k = 0; k < 4; k++) {
+    v[k] = i0 + k < n ? in[i0 + k] : T{};
+    s = s + v[k];
+  }
+  block_incl_scan_struct(s, buf);
+  T run = part[blockIdx.x] + (threadIdx.x ? buf[threadIdx.x - 1] : T{});
+  for (uint32_t k = 0; k < 4; k++) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run = run + v[k];
+  }
+}
+
 }  // namespace g2n

@@ -256,8 +256,10 @@ def test_s_first_fallback_to_general_dictionary(gpu, oracle_lib, case):
 
 
 def test_general_dictionary_forced(gpu, oracle_lib, monkeypatch):
-    """G2N_DICT_GENERAL=1 keeps the general insert rounds covered on canonical inputs too."""
-    monkeypatch.setenv("G2N_DICT_GENERAL", "1")
+    """TEST_DICT_GENERAL keeps the general insert rounds covered on canonical inputs too."""
+    from gfa2network_amd import _native as nat
+
+    monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_DICT_GENERAL)
     data = _canonical_gfa(11, 2000, 8000, True)
     for mode in MODES:
         st, ph = _phases(data, **mode)
@@ -366,9 +368,10 @@ def test_decimal_id_dictionary(gpu, oracle_lib, case):
 
 
 def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
-    """The lean decimal-id parse (coordinates written by the parse), the non-lean one (G2N_NO_LEAN:
-    ids per touch, then k_triplets) and the hash dictionary (G2N_DICT_HASH) agree bit for bit at
+    """The lean decimal-id parse (coordinates written by the parse), the non-lean one (TEST_NO_LEAN:
+    ids per touch, then k_triplets) and the hash dictionary (TEST_DICT_HASH) agree bit for bit at
     10^7 edges, weighted and not, COO and CSR outputs."""
+    from gfa2network_amd import _native as nat
     from gfa2network_amd import synth
 
     data = synth.host_bytes(2_000_000, 8_000_000, seed=3, rc_tag=True)
@@ -377,13 +380,14 @@ def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
             st, ph = _phases(data, **mode)
             assert "values" in ph and "triplets" not in ph and "table_init" not in ph, sorted(ph)
             a = outcome(gpu_run(data, mode, "float64", wt))
-            for env in ("G2N_NO_LEAN", "G2N_DICT_HASH"):
-                monkeypatch.setenv(env, "1")
+            for flag in (nat.TEST_NO_LEAN, nat.TEST_DICT_HASH):
+                monkeypatch.setattr(nat, "TEST_FLAGS", flag)
                 st, ph = _phases(data, **mode)
-                assert "triplets" in ph and (("insert_lookup" in ph) == (env == "G2N_DICT_HASH")), (env, sorted(ph))
+                assert "triplets" in ph and (("insert_lookup" in ph) == (flag == nat.TEST_DICT_HASH)), \
+                    (flag, sorted(ph))
                 b = outcome(gpu_run(data, mode, "float64", wt))
-                monkeypatch.delenv(env)
-                assert a == b, (mode, wt, env)
+                monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+                assert a == b, (mode, wt, flag)
 
 
 def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
@@ -391,6 +395,8 @@ def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
     row-sum + merge path: hubs that overflow a bucket (classic fallback), heavy duplicate runs
     (int8 wrap-around to 0 and -128, bool), self loops, every CLI dtype."""
     import random
+
+    from gfa2network_amd import _native as nat
 
     r = random.Random(12)
     lines = [f"S\t{k}\t*\n" for k in range(1, 6001)]
@@ -403,9 +409,9 @@ def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
             a = outcome(gpu_run(data, {}, dtype, None))
             b = outcome(oracle_run(oracle_lib, data, {}, dtype, None))
             assert a == b, (dtype, bool(extra))
-            monkeypatch.setenv("G2N_NO_BUCKETS", "1")
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_BUCKETS)
             c = outcome(gpu_run(data, {}, dtype, None))
-            monkeypatch.delenv("G2N_NO_BUCKETS")
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
             assert a == c, (dtype, bool(extra))
 
 
@@ -422,11 +428,10 @@ def test_maxsym_buckets_large(gpu, monkeypatch):
         assert outcome(gpu_run(data, {}, dtype, None)) == (a if dtype == "float64" else
                                                            outcome(gpu_run(data, {}, dtype, None)))
     f = outcome(gpu_run(data, {}, "float64", None))
-    monkeypatch.setattr(nat, "TEST_FLAGS", 0)
-    assert a == f
-    monkeypatch.setenv("G2N_NO_BUCKETS", "1")
+    monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_BUCKETS)
     b = outcome(gpu_run(data, {}, "float64", None))
-    assert a == b
+    monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+    assert a == f and a == b
 
 
 def test_builds_are_deterministic(gpu):

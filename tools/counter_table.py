@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Per-kernel table from gpu_counters.sh passes: avg duration, HBM bytes (2*FETCH_SIZE + WRITE_SIZE,
-MI355X_MICROARCH.md gfx950 correction), SQ instruction mix and wait fractions (per launch)."""
+"""Per-kernel table from gpu_counters.sh passes: median duration, HBM bytes (2*FETCH_SIZE + WRITE_SIZE,
+MI355X_MICROARCH.md gfx950 correction: FETCH_SIZE reports half of a wide streaming read), SQ
+instruction mix and wait fractions, all per launch.
+
+usage: counter_table.py <gpu_counters dir> [out.json commit]   (out.json: the summary bench.py reads)"""
 import collections
 import csv
 import json
@@ -26,7 +29,8 @@ for k, m in vals.items():
         per[cn].append(sum(v))  # summed over dimensions (XCDs / SEs) of one dispatch
     avg = {cn: sum(v) / len(v) for cn, v in per.items()}
     row = {"ms": round(sorted(dur[k])[len(dur[k]) // 2], 3) if dur[k] else None}
-    if "FETCH_SIZE" in avg:
+    if "FETCH_SIZE" in avg:  # KiB
+        row["traffic_bytes_per_launch"] = round((2 * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024)
         row["hbm_GB"] = round((2 * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024 / 1e9, 3)
         row["fetchx2_GB"] = round(2 * avg["FETCH_SIZE"] * 1024 / 1e9, 3)
         row["write_GB"] = round(avg.get("WRITE_SIZE", 0) * 1024 / 1e9, 3)
@@ -43,3 +47,9 @@ for k, m in vals.items():
 for k, r in sorted(out.items(), key=lambda kv: -(kv[1]["ms"] or 0)):
     print(k[:40], json.dumps(r))
 (d / "table.json").write_text(json.dumps(out, indent=1))
+if len(sys.argv) > 3:
+    Path(sys.argv[2]).write_text(json.dumps({
+        "commit": sys.argv[3], "source": "tools/gpu_counters.sh (rocprofv3 --pmc, one pass per counter group, "
+        "kernel-trace only) on `bench.py --steps 1 --warmup 0` (C4)",
+        "correction": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: gfx950 FETCH_SIZE = 1/2 of a "
+        "wide streaming read; WRITE_SIZE exact)", "kernels": out}, indent=1))

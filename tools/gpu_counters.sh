@@ -13,4 +13,4 @@ for P in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace --kernel-include-regex "$RE" --output-format csv -d $R/gpurun_out/$NAME/p$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-alt ${BENCH_ARGS:-} > $R/gpurun_out/$NAME/p$i.log 2>&1 || { tail -20 $R/gpurun_out/$NAME/p$i.log; exit 1; }
 done
-python3 $R/tools/counter_table.py $R/gpurun_out/$NAME
+python3 $R/tools/counter_table.py $R/gpurun_out/$NAME ${OUT_JSON:-} ${COMMIT:-}
