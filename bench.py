@@ -33,7 +33,7 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="C4", choices=["C2", "C3", "C4"])
+    ap.add_argument("--workload", default="C4", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-links", type=int, default=12_000_000)

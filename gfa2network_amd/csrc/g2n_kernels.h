@@ -84,6 +84,7 @@ struct ParseOpts {
   // key must name one).  A premise failure sets ctl->int_fail (the hash dictionary then runs).
   uint32_t* tid;
   uint64_t n_seg;
+  uint64_t s_base;  // sharded decimal build: S lines before this byte range (0 otherwise)
   // lean mode (decimal ids only): the parse writes the stream-order COO coordinates itself —
   // rows / cols of edge e at e * ktrip (the triplet layout of k_triplets) — and skips the edge
   // touch descriptors, E.tb and (unweighted) E.w; a premise failure re-runs a full parse

@@ -693,7 +693,7 @@ __device__ inline void put_segment(const Src& in, const ParseOpts& op, const Tou
   if (op.tid && !is.fail) {  // no edge line before it (eb = 0), so S touch tb is node tb: its name
                               // must be str(k + 1), k = tb / tps = the S lines before it
     uint64_t v;
-    const uint64_t line = op.bidir ? tb >> 1 : tb;
+    const uint64_t line = op.s_base + (op.bidir ? tb >> 1 : tb);  // s_base: S lines of earlier ranges
     if (eb != 0 || !src_dec(in, ns, nl, &v) || v != line + 1) is.fail = 1;
   }
 }
@@ -2349,7 +2349,8 @@ __global__ void __launch_bounds__(kTPB) k_route_keys(const int32_t* __restrict__
                                                      uint32_t* __restrict__ idx) {
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n) return;
-  const uint64_t key = map[transposed ? cols[i] : rows[i]];
+  const uint32_t x = (uint32_t)(transposed ? cols[i] : rows[i]);
+  const uint64_t key = map ? map[x] : x;  // no map: the ids are global already
   owner[i] = (uint32_t)(key * n_ranks / n_global);
   idx[i] = (uint32_t)i;
 }
@@ -2365,7 +2366,7 @@ __global__ void __launch_bounds__(kTPB) k_route_gather(const int32_t* __restrict
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n) return;
   const uint32_t j = perm[i];
-  const int32_t r = (int32_t)map[rows[j]], c = (int32_t)map[cols[j]];
+  const int32_t r = map ? (int32_t)map[rows[j]] : rows[j], c = map ? (int32_t)map[cols[j]] : cols[j];
   orows[i] = transposed ? c : r;
   ocols[i] = transposed ? r : c;
 #pragma unroll

@@ -265,16 +265,22 @@ static RowSide<T, kU> row_sums(g2n_context* c, const int32_t* rows, const int32_
   return S;
 }
 
-// Unweighted A.maximum(A.T) through the bucket partition (g2n_sym.hip): the A entries and their
-// A.T twins are partitioned by the high bits of their row (one or two hand-written passes), then
-// one finish block per bucket writes its rows' CSR entries at their final place.  False when
+// Unweighted A.maximum(A.T) (sum = false) or coo.tocsr() (sum = true) through the bucket partition
+// (g2n_sym.hip): the A entries (and, for MAX-SYM, their A.T twins) are partitioned by the high bits
+// of their row (one or two hand-written passes), then one finish block per bucket writes its rows'
+// CSR entries at their final place.  False when
 // the row ids are too wide for two passes or a bucket overflowed its LDS capacity (nothing
 // usable was written: the caller runs the general path).
+// The same for a sharded build's row slice [row_base, row_base + n_rows): t_rows / t_cols / n_t =
+// the slice's A.T entries (MAX-SYM; rows = A's columns), each one element of side 1.
 template <class T>
-static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip,
-                             uint64_t n_rows, g2n_result* R) {
+static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip, uint64_t n_rows,
+                          bool sum, g2n_result* R, const int32_t* t_rows = nullptr, const int32_t* t_cols = nullptr,
+                          uint64_t n_t = 0, int64_t row_base = 0) {
+  const bool pair = t_rows != nullptr || row_base != 0;  // one element per entry of two streams
   const int bits = bits_for(n_rows);
-  const double per_row = 2.0 * (double)n_trip / (double)(n_rows ? n_rows : 1);
+  const double per_row =
+      (double)(pair ? n_trip + n_t : (sum ? 1 : 2) * n_trip) / (double)(n_rows ? n_rows : 1);
   int low = 8;  // rows per bucket 2^low: about 2048 elements per bucket on average (capacity 4096)
   while (low > 1 && (double)(1u << low) * per_row > 2048.0) low--;
   if (low > bits) low = bits;
@@ -282,11 +288,14 @@ static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t*
   if (hb > 2 * (int)kMaxDigitBits) return false;
   const int bits2 = hb > (int)kMaxDigitBits ? hb / 2 : 0, bits1 = hb - bits2;
   const uint32_t n_dig1 = 1u << bits1, n_dig2 = 1u << bits2;
-  const uint64_t n_el = 2 * n_trip;
+  const uint64_t n_el = pair ? n_trip + n_t : (sum ? 1 : 2) * n_trip;
+  if (n_el >= 0xFFFFFFFFull) return false;
   const uint64_t n_buckets = 1ull << hb;                      // ids of the partition
   const uint64_t n_bk = (n_rows + (1ull << low) - 1) >> low;  // buckets holding rows
   const uint32_t shift1 = (uint32_t)(low + bits2);
-  PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, nullptr, nullptr, nullptr, 0};
+  PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, (sum || pair) ? 1u : 0u,
+              (const uint32_t*)t_rows, (const uint32_t*)t_cols, pair ? n_t : 0, (uint32_t)row_base,
+              nullptr, nullptr, nullptr, 0};
   // pass 1: over the COO entries, both sides
   const uint64_t n_blk1 = (n_el + kPartTile - 1) / kPartTile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
@@ -304,7 +313,7 @@ static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t*
                        (const uint32_t*)off1, n_blk1, (uint32_t)n_el, n_buckets, bst);
   } else {  // pass 2 inside each pass-1 group
     auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
-    PartSrc s2{nullptr, nullptr, 0, el1, grp, grp + n_dig1 + 1, n_dig1};
+    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1};
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, n_blk1, n_dig1,
                        (uint32_t)n_el, grp, grp + n_dig1 + 1);
     const uint64_t n_blk2 = n_blk1 + n_dig1;  // >= the blocks the groups need
@@ -330,9 +339,15 @@ static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t*
   uint2* tmp = el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1;  // the pass-1 output is dead by now
   G2N_HIP(hipMemsetAsync(status, 0, n_bk * sizeof(unsigned long long), c->stream));
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, 2 * sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL((k_sym_finish<T>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el, (const uint32_t*)bst,
-                     (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices, odata, c->ctl,
-                     (c->test_flags & kTestNoLookback) ? 0u : kSpinLimit);
+  const uint32_t spin = (c->test_flags & kTestNoLookback) ? 0u : kSpinLimit;
+  if (sum)
+    hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices,
+                       odata, c->ctl, spin);
+  else
+    hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices,
+                       odata, c->ctl, spin);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
   if (c->h_ctl->n_fix) {  // buckets that gave up waiting on their predecessors
@@ -349,7 +364,7 @@ static bool maxsym_partition(g2n_context* c, const int32_t* rows, const int32_t*
   R->data = odata;
   R->sum_sorted = -1;  // not computed: unweighted sums cannot depend on scipy's order
   R->sum_t_sorted = -1;
-  phase(c, "maxsym");
+  phase(c, sum ? "csr" : "maxsym");
   return true;
 }
 
@@ -357,8 +372,8 @@ template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   if constexpr (kU) {
-    if (maxsym && n_trip && n_rows && n_rows == n_cols && !(c->test_flags & kTestNoBuckets) &&
-        maxsym_partition<T>(c, rows, cols, n_trip, n_rows, R))
+    if (n_trip && n_rows && (n_rows == n_cols || !maxsym) && !(c->test_flags & kTestNoBuckets) &&
+        csr_partition<T>(c, rows, cols, n_trip, n_rows, !maxsym, R))
       return;
   }
   const T one = (T)1;
@@ -415,6 +430,14 @@ template <class T, bool kU>
 static void assemble_pair_t(g2n_context* c, const int32_t* ar, const int32_t* ac, const T* ad, uint64_t an,
                             const int32_t* tr, const int32_t* tc, const T* td, uint64_t tn, bool maxsym, int64_t base,
                             uint64_t n_rows, int force_unsorted, g2n_result* R) {
+  if constexpr (kU) {  // unweighted: the bucket partition (the slice's sums cannot depend on order)
+    if (an + tn && n_rows && base >= 0 && base < 0xFFFFFFFFll && !(c->test_flags & kTestNoBuckets) &&
+        csr_partition<T>(c, ar, ac, an, n_rows, !maxsym, R, maxsym ? (tr ? tr : ar) : nullptr,
+                         maxsym ? tc : nullptr, maxsym ? tn : 0, base ? base : 0)) {
+      R->sum_sorted = R->sum_t_sorted = 1;
+      return;
+    }
+  }
   const T one = (T)1;
   RowSide<T, kU> A = row_sums<T, kU>(c, ar, ac, ad, an, n_rows, 0, 0, base,
                                      force_unsorted < 0 ? -1 : (force_unsorted & 1));
@@ -741,12 +764,19 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto* cols = dget<int32_t>(c, S_COLS, n_trip);
   // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
   // the first S line names "1" (a cheap guess: a wrong one costs one extra parse)
-  const bool int_ids =
-      n_t && !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
-  const bool lean = int_ids && !(c->test_flags & kTestNoLean);
+  // options.reserved[4] bit 0: one byte range of a sharded build whose node ids are decimal and
+  // GLOBAL: reserved[2] S lines precede the range, reserved[3] S lines in the whole file (the
+  // caller checked across ranges that no edge line precedes an S line).  Lean parse or nothing.
+  const bool shard_dec = (o->reserved[4] & 1) != 0;
+  if (shard_dec && (o->output != G2N_OUT_COO || o->want_node_names || o->reserved[2] < 0 || o->reserved[3] < 0))
+    throw Failure(G2N_E_ARG, "sharded decimal-id build: output COO without names, s_base / n_seg >= 0");
+  const bool int_ids = n_t && (shard_dec || (!(c->test_flags & (kTestDictHash | kTestDictGeneral)) &&
+                                              first_segment_is_one(c, in, len)));
+  const bool lean = int_ids && (shard_dec || !(c->test_flags & kTestNoLean));
   if (int_ids) {
     op.tid = dget<uint32_t>(c, S_TID, n_t);
-    op.n_seg = n_s;
+    op.n_seg = shard_dec ? (uint64_t)o->reserved[3] : n_s;
+    op.s_base = shard_dec ? (uint64_t)o->reserved[2] : 0;
   }
   auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
   auto* deferred = dget<DeferredLine>(c, S_DEFER, n_tiles + 1);
@@ -776,6 +806,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     // slow weights need a full parse (decimal ids kept unless they failed)
     lean_done = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && c->h_ctl->warn_line == ~0ull &&
                 c->h_ctl->wl_count == 0;
+    if (!lean_done && shard_dec)  // errors, warnings, slow weights or ids that are not decimal
+      throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id build: this range needs the general protocol");
     if (!lean_done) {
       const bool int_ok = !c->h_ctl->int_fail;
       c->h_ctl->wl_count = c->h_ctl->n_deferred = c->h_ctl->int_fail = 0;
@@ -842,7 +874,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
                                      op.tid && !c->h_ctl->int_fail ? kIntDone : kIntFailed);
   const bool coords_done = lean_done;  // the parse wrote rows / cols
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
-  const uint64_t n_nodes = D.n_nodes;
+  const uint64_t n_nodes = shard_dec ? (uint64_t)o->reserved[3] : D.n_nodes;  // global ids: the file's nodes
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");

@@ -67,13 +67,18 @@ __device__ inline uint32_t block_excl_scan_n(uint32_t v, uint32_t* excl, uint32_
 // element: x = row, y = column << 1 | side  (columns < 2^31)
 __device__ inline uint2 sym_elem(uint32_t row, uint32_t col, uint32_t side) { return make_uint2(row, (col << 1) | side); }
 
-// Where a partition block's elements come from.  Pass 1: the COO entries [blk * kPartTile / 2,
-// ...), each giving two elements (row a, side 0) and (row b, side 1).  Pass 2: the pass-1 output
-// of one group g (block -> (group, chunk j) through bstart).
+// Where a partition block's elements come from.  Pass 1: the COO entries, each giving two
+// elements (row a, side 0) and (row b, side 1) for A.maximum(A.T), or one (row a, side 0) for the
+// SUM CSR (coo.tocsr).  Pass 2: the pass-1 output of one group g (block -> (group, chunk j)).
 struct PartSrc {
-  const uint32_t* rows;   // pass 1
+  const uint32_t* rows;   // pass 1: stream A
   const uint32_t* cols;
   uint64_t n_entries;
+  uint32_t one_side;      // pass 1: 1 = one element per entry (A side 0, then T side 1), 0 = two per A entry
+  const uint32_t* rows_t; // pass 1, one_side: stream T (a sharded MAX-SYM slice's A.T entries), side 1
+  const uint32_t* cols_t;
+  uint64_t n_t;
+  uint32_t row_base;      // pass 1: rows are global ids; elements carry row - row_base (a slice's rows)
   const uint2* in;        // pass 2
   const uint32_t* gstart; // n_groups + 1 element offsets of the groups
   const uint32_t* bstart; // n_groups + 1 first block of each group
@@ -92,7 +97,7 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
     B.j = blk;
     B.nb = 0;
     B.e0 = (uint64_t)blk * kPartTile;
-    const uint64_t n_el = 2 * S.n_entries;
+    const uint64_t n_el = S.one_side ? S.n_entries + S.n_t : 2 * S.n_entries;
     B.e1 = B.e0 + kPartTile < n_el ? B.e0 + kPartTile : n_el;
     return true;
   }
@@ -118,7 +123,19 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
 template <int kPass>
 __device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint2 (&x)[kSubPer], uint32_t& valid) {
   valid = 0;
-  if (kPass == 1) {
+  if (kPass == 1 && S.one_side) {
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++) {
+      const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
+      x[k] = make_uint2(0, 0);
+      if (i < e1) {
+        const bool t = i >= S.n_entries;
+        const uint64_t j = t ? i - S.n_entries : i;
+        x[k] = sym_elem((t ? S.rows_t[j] : S.rows[j]) - S.row_base, t ? S.cols_t[j] : S.cols[j], t ? 1u : 0u);
+        valid |= 1u << k;
+      }
+    }
+  } else if (kPass == 1) {
 #pragma unroll
     for (uint32_t k = 0; k < kSubPer / 2; k++) {
       const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
@@ -384,7 +401,7 @@ __device__ inline bool lookback_bounded(unsigned long long* __restrict__ status,
 constexpr uint32_t kShortRow = 16;
 constexpr uint32_t kStagedSkip = 0xFFFFFFFFu;
 
-template <class T>
+template <class T, bool kSum>
 __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
                                                      unsigned long long* __restrict__ status, uint2* __restrict__ tmp,
@@ -457,7 +474,10 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   // merged entries: per column the side-0 copies (x) and side-1 copies (y); the value is
   // max(sum of x ones, sum of y ones) in dtype arithmetic, zeros dropped (csr_maximum_csr)
   auto keep = [&](uint32_t kx, uint32_t ky, uint32_t& kk) -> bool {
-    if constexpr (std::is_same<T, int8_t>::value) {  // int8 sums wrap: compare the dtype values
+    if constexpr (kSum) {  // coo.tocsr: the run's sum, explicit zeros kept (csr_sum_duplicates)
+      kk = kx;
+      return true;
+    } else if constexpr (std::is_same<T, int8_t>::value) {  // int8 sums wrap: compare the dtype values
       const T x = kx ? sum_copies<T>(one, kx) : (T)0, y = ky ? sum_copies<T>(one, ky) : (T)0;
       kk = (x < y) ? ky : kx;
       return ((x < y) ? y : x) != (T)0;

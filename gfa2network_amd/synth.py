@@ -37,6 +37,8 @@ WORKLOADS = {
                    "1M S / 4M L + RC:i, bidirected weighted"),
     "C4": Workload("C4", 50_000_000, 200_000_000, False, {},
                    "50M S / 200M L, default (directed, MAX-SYM CSR), HBM-resident parse"),
+    "C5": Workload("C5", 125_000_000, 500_000_000, False, {"directed": False},
+                   "125M S / 500M L pangenome, undirected CSR (16 GB)"),
 }
 
 

@@ -91,9 +91,17 @@ typedef struct g2n_options {
   int32_t want_node_names;     /* 1 (default): produce the names blob in id order */
   int32_t device;              /* HIP device ordinal, default 0 */
   int32_t reserved[6];         /* [0]: unsupported records skipped silently (an earlier shard of a
-                                  sharded build warned already); [1]: test flags, bit 0 = MAX-SYM
-                                  bucket finish without its look-back (every bucket staged and
-                                  moved by the fix-up kernel; same result); others 0 */
+                                  sharded build warned already);
+                                  [1]: test flags (normally rare paths, same results): 1 = MAX-SYM
+                                  bucket finish without its look-back, 2 = MAX-SYM / SUM CSR through
+                                  the general row sums, 4 = decimal ids without the lean parse,
+                                  8 = hash dictionary, 16 = general dictionary rounds;
+                                  [2], [3], [4] bit 0: sharded decimal-id build — this byte range's
+                                  node ids are global decimals: [2] = S lines before the range,
+                                  [3] = S lines in the file (output G2N_OUT_COO, no names; returns
+                                  G2N_E_UNSUPPORTED when the range needs the general protocol:
+                                  ids that are not decimal, errors, warnings, slow weights);
+                                  [5] = 0 */
 } g2n_options;
 
 #define G2N_MAX_PHASES 40

@@ -444,3 +444,43 @@ def test_builds_are_deterministic(gpu):
     for d in (data, hashed):
         for mode, wt in (({}, None), ({"directed": False}, "RC"), ({"bidirected": True}, "RC")):
             assert outcome(gpu_run(d, mode, "float64", wt)) == outcome(gpu_run(d, mode, "float64", wt))
+
+
+def _csr_cases():
+    import random
+
+    from gfa2network_amd import synth
+
+    r = random.Random(3)
+    dup = [f"S\t{k}\t*\n" for k in range(1, 3001)]
+    dup += [f"L\t{r.randint(1, 3000)}\t+\t{r.randint(1, 3000)}\t-\t0M\tRC:i:{r.randint(-2, 3)}\n" for _ in range(20000)]
+    dup += ["L\t7\t+\t9\t+\t0M\n"] * 256 + ["L\t9\t+\t7\t+\t0M\n"] * 128 + ["L\t11\t+\t11\t+\t0M\n"] * 300
+    dup += [f"L\t2000\t+\t{k}\t+\t0M\n" for k in range(1, 3001)]  # a hub longer than a finish bucket
+    return {"dups": "".join(dup).encode(), "synth": synth.host_bytes(200_000, 800_000, seed=7, rc_tag=True)}
+
+
+@pytest.mark.parametrize("case", ["dups", "synth"])
+def test_csr_output_equals_oracle(gpu, oracle_lib, case):
+    """output = G2N_OUT_CSR (what convert_format(parse_gfa(...), "csr") returns, cli.py:239) in every
+    mode and dtype family: unweighted SUM CSRs through the bucket partition (g2n_sym.hip, sum mode:
+    int8 runs of 256 copies stay as explicit zeros), weighted ones through the row sums."""
+    from gfa2network_amd import _native as nat
+
+    data = _csr_cases()[case]
+    bad = []
+    for mode in MODES:
+        for dtype in ("float64", "int8", "bool"):
+            for wt in (None, "RC"):
+                raw = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, dtype=dtype, weight_tag=wt,
+                                                                   **mode))
+                o = oracle_lib.run(data, dtype=dtype, weight_tag=wt, **mode)
+                if raw.status != o.status:
+                    bad.append((mode, dtype, wt, raw.status, o.status))
+                    continue
+                if o.status:
+                    continue
+                R = oracle_lib.to_raw(o, "csr")
+                if not (raw.indptr.tobytes() == R.indptr.tobytes() and raw.indices.tobytes() == R.indices.tobytes()
+                        and raw.data.tobytes() == R.data.tobytes()):
+                    bad.append((mode, dtype, wt))
+    assert not bad, bad[:4]
