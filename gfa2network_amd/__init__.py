@@ -5,8 +5,8 @@ Drop-in for the reference's matrix path: ``parse_gfa(..., build_matrix=True)``,
 gfa2network/__init__.py:3-14).  The work runs in hand-written gfx950 kernels behind the
 C-ABI in include/g2n.h (libg2n.so, loaded with ctypes).
 """
-from .api import convert_format, export_edge_list, parse_gfa
+from .api import convert_format, export_edge_list, parse_gfa, parse_gfa_sharded
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"
 
-__all__ = ["parse_gfa", "convert_format", "export_edge_list", "__version__"]
+__all__ = ["parse_gfa", "parse_gfa_sharded", "convert_format", "export_edge_list", "__version__"]

@@ -178,7 +178,10 @@ def load() -> ctypes.CDLL:
     lib.g2n_write_node_map.restype = ctypes.c_int
     lib.g2n_first_bad_utf8.argtypes = [P, P, U64]
     lib.g2n_first_bad_utf8.restype = I64
-    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair"):
+    lib.g2n_upload_file_range.argtypes = [ctypes.c_char_p, U64, U64, P, I32]
+    lib.g2n_count_device.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(I64)]
+    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+              "g2n_upload_file_range", "g2n_count_device"):
         getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:
         raise NativeUnavailable("libg2n.so ABI version mismatch; rebuild it")

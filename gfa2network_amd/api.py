@@ -29,7 +29,13 @@ import scipy.sparse as sp
 from . import _native as nat
 from ._native import RawResult
 
-__all__ = ["parse_gfa", "parse_gfa_names", "convert_format", "finalize", "raise_for_status", "save_npz"]
+__all__ = ["parse_gfa", "parse_gfa_names", "parse_gfa_sharded", "convert_format", "finalize", "raise_for_status",
+           "save_npz"]
+
+# Auto-sharding (BASELINE north_star: byte-range-shard "only when it exceeds one GPU's HBM"): a
+# build's device working set is at most about this many bytes per input byte (the lean decimal-id
+# MAX-SYM build of C4 peaks near 3x; hash-dictionary, bidirected and weighted builds need more).
+WORKING_SET_PER_INPUT_BYTE = 8
 
 _MALFORMED = {
     nat.E_MALFORMED_L: "L", nat.E_MALFORMED_E: "E", nat.E_MALFORMED_C: "C",
@@ -156,11 +162,17 @@ def parse_gfa(
     max_tag_mb: float = 100.0,
     split_on_alignment: bool = False,
     device: int = 0,
+    shard: str = "auto",
 ):
     """GPU ``parse_gfa`` (gfa2network/builders.py:30-299), matrix outputs only.
 
     Returns ``A`` or ``(A, node_list)`` exactly as the reference does for
     ``build_graph=False, build_matrix=True``.
+
+    ``shard`` (extension; the reference has no such argument): with torch.distributed
+    initialized over more than one rank, ``"auto"`` splits the file over the ranks
+    (``parse_gfa_sharded``, every rank must make the same call) when its working set would not
+    fit this GPU's free HBM; ``"always"`` / ``"never"`` force the choice.
     """
     if backend == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
@@ -171,6 +183,13 @@ def parse_gfa(
     if build_graph:
         raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
     dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
+    if shard not in ("auto", "always", "never"):
+        raise ValueError("shard must be 'auto', 'always' or 'never'")
+    if build_matrix and _want_shard(path, shard, device):
+        return parse_gfa_sharded(path, directed=directed, weight_tag=weight_tag, strip_orientation=strip_orientation,
+                                 verbose=verbose, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                                 dtype=dt.name, asymmetric=asymmetric, raw_bytes_id=raw_bytes_id,
+                                 return_node_list=return_node_list)
     opts = nat.make_options(
         directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
         asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
@@ -179,6 +198,97 @@ def parse_gfa(
     raw = _run(path, opts)
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
                     verbose=verbose, build_matrix=build_matrix, path=path)
+
+
+def _dist_world() -> int:
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover - torch is in the image
+        return 1
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def _want_shard(path, shard: str, device: int) -> bool:
+    """Split the file over the process group? Only for a plain file on disk, more than one rank,
+    and ("auto") a working set beyond this GPU's free HBM."""
+    if shard == "never" or _dist_world() < 2 or hasattr(path, "read"):
+        return False
+    p = str(path)
+    if p == "-" or not os.path.isfile(p):
+        return False
+    if shard == "always":
+        return True
+    import torch
+
+    free, _ = torch.cuda.mem_get_info(device)
+    return os.path.getsize(p) * WORKING_SET_PER_INPUT_BYTE > free
+
+
+def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = None,
+                      strip_orientation: bool = False, verbose: bool = False, bidirected: bool = False,
+                      keep_directed_bidir: bool = False, dtype="float64", asymmetric: bool = False,
+                      raw_bytes_id: bool = False, return_node_list: bool = False, output: str = "parse",
+                      group=None, engine=None):
+    """``parse_gfa(path, build_graph=False, build_matrix=True, ...)`` with the file split over the
+    ranks of a torch.distributed group — a collective: every rank calls it with
+    the same path.  Each rank preads only its line-aligned byte range (``file_line_ranges``) into
+    its GPU's HBM, the ranks reconcile node ids (the decimal-id fast path or the general owner
+    protocol, gfa2network_amd/shard.py) and route triplets to row owners, and every rank returns
+    the whole result: what parse_gfa returns (the MAX-SYM CSR, or the stream-order COO) — or, with
+    ``output="csr"``, what ``convert_format(parse_gfa(...), "csr")`` returns.  Exceptions, the
+    one-shot warning and the verbose strings are the reference's (builders.py:95-299).  A ``.gz``
+    file is inflated by every rank (its byte ranges are not seekable); plain files are read per
+    range."""
+    import torch
+
+    from .shard import HipEngine, build_sharded, file_line_ranges, gather_coo, gather_csr
+
+    dt = _dtype_of(dtype)
+    if output not in ("parse", "csr"):
+        raise ValueError("output must be 'parse' or 'csr'")
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    eng = engine or HipEngine(torch.cuda.current_device())
+    p = str(path)
+    if p.endswith(".gz"):
+        with open(p, "rb") as fh:
+            data, _ = nat.gunzip(fh.read())
+        from .shard import line_ranges
+
+        lo, hi = line_ranges(data, world)[rank]
+        buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
+    else:
+        lo, hi = file_line_ranges(p, world)[rank]
+        buf = eng.read_range(p, lo, hi - lo)
+    gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
+    maxsym = gd and not asymmetric                               # builders.py:282
+    res = build_sharded(buf, engine=eng, group=group, directed=directed, bidirected=bidirected,
+                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
+                        strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
+                        gather_names=return_node_list, keep_coo=not maxsym and output == "parse")
+    raw = RawResult(status=res.status, err_line=res.err_line, err_index=res.err_index, err_value=res.err_value,
+                    err_detail=res.err_detail, has_warning=res.has_warning, warn_byte=res.warn_byte,
+                    warn_line=res.warn_line, n_lines=res.n_lines, n_records=res.n_records,
+                    n_records_before_error=res.n_records_before_error, n_nodes=res.n_nodes, dtype=dt,
+                    n_cast_overflow=res.n_cast_overflow)
+    if res.status == 0:
+        if not maxsym and output == "parse":
+            raw.format = "coo"
+            raw.rows, raw.cols, raw.data = gather_coo(res, group)
+        else:
+            raw.format = "csr"
+            raw.indptr, raw.indices, raw.data = gather_csr(res, group)
+            raw.indptr = raw.indptr.astype(np.int32)
+            raw.indices = raw.indices.astype(np.int32)
+        if return_node_list:
+            blob = b"".join(res.names)
+            offs = np.zeros(len(res.names) + 1, dtype=np.int64)
+            offs[1:] = np.cumsum([len(x) for x in res.names])
+            raw.names_blob, raw.names_offsets = np.frombuffer(blob, dtype=np.uint8), offs
+    return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=verbose,
+                    path=path)
 
 
 def parse_gfa_names(path, *, raw_bytes_id: bool = False, **kw):

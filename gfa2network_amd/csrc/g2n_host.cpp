@@ -256,6 +256,33 @@ int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** 
   });
 }
 
+int g2n_upload_file_range(const char* path, uint64_t offset, uint64_t len, void* d_dst, int32_t device) {
+  if (!path || (len && !d_dst)) return G2N_E_ARG;
+  return g2n::guarded([&]() -> int {
+    const std::string p(path);
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      g2n::set_last_error(p + ": " + std::strerror(errno));
+      return G2N_E_IO;
+    }
+    struct FdCloser {
+      int fd;
+      ~FdCloser() { ::close(fd); }
+    } closer{fd};
+    g2n::FillFn fill = [fd, offset, &p](size_t off, uint8_t* dst, size_t n) {
+      size_t got = 0;
+      while (got < n) {
+        ssize_t r = ::pread(fd, dst + got, n - got, (off_t)(offset + off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) throw g2n::Failure(G2N_E_IO, p + ": " + std::strerror(r < 0 ? errno : EIO));
+        got += (size_t)r;
+      }
+    };
+    g2n::staged_upload(device, (uint8_t*)d_dst, (size_t)len, fill);
+    return G2N_OK;
+  });
+}
+
 int g2n_gunzip(const void* buf, size_t len, int32_t parallel, void** out, size_t* out_len, int32_t* members,
                int32_t* sub) {
   if (!out || !out_len || (len && !buf)) return G2N_E_ARG;

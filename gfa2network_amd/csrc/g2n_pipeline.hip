@@ -1427,6 +1427,31 @@ int g2n_csr_from_coo_pair(g2n_context* ctx, const int32_t* a_rows, const int32_t
   return G2N_OK;
 }
 
+int g2n_count_device(g2n_context* ctx, const void* d_input, size_t len, int64_t* out4) {
+  if (!out4 || (len && !d_input)) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, {
+    const uint64_t n_tiles = (len + g2n::kTile - 1) / g2n::kTile;
+    g2n::TileCnt tot{};
+    if (n_tiles) {
+      auto* tcnt = g2n::dget<g2n::TileCnt>(ctx, g2n::S_TILE_CNT, n_tiles + 1);
+      const uint64_t n_parts = (n_tiles + g2n::kStructChunk - 1) / g2n::kStructChunk;
+      auto* part = g2n::dget<g2n::TileCnt>(ctx, g2n::S_TEMP, n_parts + 1);
+      hipLaunchKernelGGL(g2n::k_tile_count, dim3((unsigned)n_tiles), dim3(g2n::kTPB), 0, ctx->stream,
+                         (const uint8_t*)d_input, (uint64_t)len, 1u, 2u, tcnt);
+      hipLaunchKernelGGL(g2n::k_struct_reduce<g2n::TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, ctx->stream,
+                         (const g2n::TileCnt*)tcnt, n_tiles, part);
+      hipLaunchKernelGGL(g2n::k_struct_scan_parts<g2n::TileCnt>, dim3(1), dim3(256), 0, ctx->stream, part, n_parts,
+                         part + n_parts);
+      tot = g2n::read_dev(ctx, part + n_parts);
+    }
+    out4[0] = (int64_t)tot.lines;
+    out4[1] = (int64_t)tot.segs;
+    out4[2] = (int64_t)tot.edges;
+    out4[3] = (int64_t)tot.recs;
+  });
+  return G2N_OK;
+}
+
 int g2n_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {

@@ -19,6 +19,15 @@ Here each rank takes a contiguous, line-aligned byte range and the ranks reconci
    stream order, so scipy's duplicate-summation order is kept;
 6. the rank's CSR row slice (`g2n_csr_from_coo_pair`): coo.tocsr() or A.maximum(A.T).
 
+Fast path (decimal ids, the layout of vg / odgi / PGGB graphs with compacted ids and of the
+synthetic configs): when the file's S lines come first and name their segments "1".."N" in
+order, a node's global id is arithmetic on its name, so steps 2-4 collapse to an all-gather of
+the ranges' record counts (each rank learns how many S lines precede it and N) and one
+all-reduce of the ranges' verdicts ("every range's ids are global decimals"): each rank parses
+its range straight into global ids (`g2n_build_device` with options.reserved[2..4]), routes the
+triplets with an identity map and builds its slice.  Any range that breaks the premise (or
+holds an error / warning / slow weight) makes every rank take the general protocol above.
+
 Errors and the one-shot unsupported-record warning are resolved across ranks in stream
 order (the earliest parse error wins; cast errors only when no rank has a parse error).
 
@@ -29,6 +38,7 @@ on this rank's GPU); tests drive the same protocol with a CPU engine built on th
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -89,6 +99,8 @@ class ShardResult:
     names: list | None = None  # node keys in id order, when gather_names
     n_cast_overflow: int = 0
     timings_ms: dict = field(default_factory=dict)
+    fast_path: bool = False  # the decimal-id fast path built it
+    coo: tuple | None = None  # keep_coo: this range's stream-order triplets over global ids
 
 
 def line_ranges(data: bytes | np.ndarray, n_ranks: int) -> list[tuple[int, int]]:
@@ -105,6 +117,34 @@ def line_ranges(data: bytes | np.ndarray, n_ranks: int) -> list[tuple[int, int]]
             s = n if len(nl) == 0 else s + int(nl[0]) + 1
         starts.append(max(s, starts[-1]))
     return [(starts[r], starts[r + 1] if r + 1 < n_ranks else n) for r in range(n_ranks)]
+
+
+def file_line_ranges(path: str, n_ranks: int, window: int = 1 << 16) -> list[tuple[int, int]]:
+    """line_ranges() of a file on disk without reading it whole: each boundary is found with
+    os.pread windows from its nominal offset r * size / G (parser.py:114 lines, `\n` only)."""
+    import os
+
+    size = os.path.getsize(path)
+    starts = [0]
+    with open(path, "rb") as fh:
+        fd = fh.fileno()
+        for r in range(1, n_ranks):
+            nominal = r * size // n_ranks
+            s = nominal
+            if 0 < s < size and os.pread(fd, 1, s - 1) != b"\n":
+                pos = s
+                while True:
+                    chunk = os.pread(fd, window, pos)
+                    k = chunk.find(b"\n")
+                    if k >= 0:
+                        s = pos + k + 1
+                        break
+                    if len(chunk) < window:
+                        s = size
+                        break
+                    pos += len(chunk)
+            starts.append(max(s, starts[-1]))
+    return [(starts[r], starts[r + 1] if r + 1 < n_ranks else size) for r in range(n_ranks)]
 
 
 # ------------------------------------------------------------------------ engines --
@@ -175,6 +215,48 @@ class HipEngine:
         sh.names_blob = self._copy_out(res.names_blob, int(res.names_bytes), torch.uint8)
         return sh
 
+    def read_range(self, path: str, offset: int, length: int):
+        """Bytes [offset, offset + length) of the file, pread into pinned staging and copied to this
+        rank's HBM (g2n_upload_file_range): a rank never reads the other ranks' bytes."""
+        t = self.torch.empty(length, dtype=self.torch.uint8, device=self.device)
+        if length:
+            self._sync()
+            self._check(self.lib.g2n_upload_file_range(os.fsencode(path), offset, length, t.data_ptr(),
+                                                       self.device_index), "g2n_upload_file_range")
+        return t
+
+    def count(self, buf):
+        """{lines, S lines, edge records, records} of the range (g2n_count_device: K1 only)."""
+        out = (ctypes.c_int64 * 4)()
+        self._sync()
+        self._check(self.lib.g2n_count_device(self.ctx, buf.data_ptr() if buf.numel() else None, buf.numel(), out),
+                    "g2n_count_device")
+        return [int(v) for v in out]
+
+    def build_decimal(self, buf, opts: dict, s_base: int, n_seg: int):
+        """The range parsed straight into GLOBAL decimal ids (S lines s_base.. of n_seg), or None when
+        it needs the general protocol (ids that are not decimal, errors, warnings, slow weights)."""
+        torch = self.torch
+        o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
+        o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1
+        res = nat.Result()
+        self._sync()
+        rc = self.lib.g2n_build_device(self.ctx, buf.data_ptr() if buf.numel() else None, buf.numel(),
+                                       ctypes.byref(o), ctypes.byref(res))
+        if rc != 0:
+            if rc not in (nat.E_UNSUPPORTED,) and not (1 <= rc <= 12):
+                self._check(rc, "g2n_build_device")
+            return None
+        n = res.nnz
+        sh = LocalShard(status=0, err_line=-1, err_index=-1, err_value=0.0, err_detail=b"", warn_line=-1,
+                        has_warning=False, warn_byte=0, n_lines=res.n_lines, n_records=res.n_records,
+                        n_records_before_error=res.n_records, n_edges=res.n_edges, n_local_nodes=res.n_nodes,
+                        n_cast_overflow=res.n_cast_overflow)
+        sh.rows = self._copy_out(res.rows, n, torch.int32)
+        sh.cols = self._copy_out(res.cols, n, torch.int32)
+        sh.data = self._copy_out(res.data, n, getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")]))
+        return sh
+
     def partition_keys(self, blob, offsets, n_ranks: int):
         torch = self.torch
         n = offsets.numel() - 1
@@ -213,7 +295,8 @@ class HipEngine:
         nz = n > 0
         self._check(self.lib.g2n_route_triplets(
             self.ctx, rows.data_ptr() if nz else None, cols.data_ptr() if nz else None,
-            data.data_ptr() if nz else None, n, nat.DTYPE_CODES[dtype], gmap.data_ptr() if gmap.numel() else None,
+            data.data_ptr() if nz else None, n, nat.DTYPE_CODES[dtype],
+            gmap.data_ptr() if gmap is not None and gmap.numel() else None,
             n_global, n_ranks, int(transposed), orows.data_ptr() if nz else None, ocols.data_ptr() if nz else None,
             odata.data_ptr() if nz else None, starts.data_ptr()), "g2n_route_triplets")
         return orows, ocols, odata, starts
@@ -317,12 +400,121 @@ class Comm:
         self.dist.all_reduce(xc, op=self.dist.ReduceOp.MAX, group=self.group)
         return xc.to(dev)
 
+    def allreduce_min(self, x):
+        if self.world == 1:
+            return x
+        dev = x.device
+        xc = self._c(x)
+        self.dist.all_reduce(xc, op=self.dist.ReduceOp.MIN, group=self.group)
+        return xc.to(dev)
+
+
+def _decimal_names(n: int, bidirected: bool) -> list:
+    """The node keys of a decimal-id graph in id order (builders.py:190-198: "k" or "k:+", "k:-")."""
+    if not bidirected:
+        return [str(k + 1).encode() for k in range(n)]
+    return [f"{k // 2 + 1}:{'+-'[k & 1]}".encode() for k in range(n)]
+
+
+def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm):
+    """Step 6: this rank's CSR row slice (rows [row_lo, row_hi) of n_global)."""
+    import time
+
+    import torch
+
+    world, rank = C.world, C.rank
+    t4 = time.perf_counter()
+    row_lo = (rank * n_global + world - 1) // world
+    row_hi = ((rank + 1) * n_global + world - 1) // world
+    uniform = not weight_tag
+    force = -1
+    if not uniform and dtype in ("float32", "float64") and world > 1:
+        # scipy's has_sorted_indices is a property of the whole matrix: OR over the slices
+        _, _, _, ua, ut = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype, uniform, -1)
+        flags = C.allreduce_max(torch.tensor([int(ua), int(ut)], dtype=torch.int64, device=engine.device))
+        force = int(flags[0].item()) | (int(flags[1].item()) << 1)
+    indptr, indices, vals, _, _ = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype,
+                                                  uniform, force)
+    tm["csr"] = (time.perf_counter() - t4) * 1e3
+    return row_lo, row_hi, indptr, indices, vals
+
+
+def _route(engine, C, local, dtype, gmap, n_global, maxsym, tm):
+    """Step 5: triplets to the owners of their rows (and the A.T stream for MAX-SYM)."""
+    import time
+
+    t3 = time.perf_counter()
+
+    def route(transposed):
+        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, local.data, local.dtype_name, gmap, n_global,
+                                               C.world, transposed)
+        st_l = [int(v) for v in st.tolist()]
+        cnt = [st_l[k + 1] - st_l[k] for k in range(C.world)]
+        return C.a2av(rr, cnt)[0], C.a2av(cc, cnt)[0], C.a2av(dd, cnt)[0]
+
+    a = route(False)
+    tstream = route(True) if maxsym else None
+    tm["route"] = (time.perf_counter() - t3) * 1e3
+    return a, tstream
+
+
+def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo=False):
+    """The decimal-id fast path (module docstring), or None when a range breaks its premise."""
+    import time
+
+    import torch
+
+    world, rank = C.world, C.rank
+    t0 = time.perf_counter()
+    cnt = engine.count(buf)  # [lines, S lines, edges, records]
+    allc = C.allgather_list(cnt)
+    seen_edge, ok = False, True
+    for k in range(world):  # no edge line may precede an S line (ids = S order)
+        if allc[k][1] and seen_edge:
+            ok = False
+        seen_edge = seen_edge or allc[k][2] > 0
+    n_seg = int(sum(c[1] for c in allc))
+    tps = 2 if opts.get("bidirected") else 1
+    if not ok or n_seg == 0 or n_seg * tps >= 2**31 - 1:
+        return None
+    s_base = int(sum(allc[k][1] for k in range(rank)))
+    local = engine.build_decimal(buf, opts, s_base, n_seg)
+    # every range's ids are global decimals (the id map needs no exchange) — or nobody's are
+    verdict = torch.tensor([0 if local is None else 1], dtype=torch.int64, device=engine.device)
+    if int(C.allreduce_min(verdict).item()) == 0:
+        return None
+    tm["count_build"] = (time.perf_counter() - t0) * 1e3
+    n_global = n_seg * tps
+    local.dtype_name = opts.get("dtype", "float64")
+    a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, tm)
+    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
+                                                   opts.get("weight_tag"), tm)
+    casts = torch.tensor([local.n_cast_overflow], dtype=torch.int64, device=engine.device)
+    if world > 1:
+        import torch.distributed as dist
+
+        cc = C._c(casts)
+        dist.all_reduce(cc, group=C.group)
+        casts = cc
+    out = ShardResult(status=0, n_lines=int(sum(c[0] for c in allc)), n_records=int(sum(c[3] for c in allc)),
+                      n_edges=int(sum(c[2] for c in allc)), n_nodes=n_global, row_lo=row_lo, row_hi=row_hi,
+                      indptr=indptr, indices=indices, data=vals, n_cast_overflow=int(casts.item()))
+    out.n_records_before_error = out.n_records
+    if gather_names:
+        out.names = _decimal_names(n_global, bool(opts.get("bidirected")))
+    out.timings_ms = tm
+    out.fast_path = True
+    if keep_coo:
+        out.coo = (local.rows, local.cols, local.data)
+    return out
+
 
 def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, keep_directed_bidir=False,
                   asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None,
-                  gather_names=False) -> ShardResult:
+                  gather_names=False, keep_coo=False) -> ShardResult:
     """Build this rank's byte range `buf` (uint8 tensor on the engine's device) as part of one
-    file split over `group` in rank order; returns this rank's CSR row slice."""
+    file split over `group` in rank order; returns this rank's CSR row slice (and, keep_coo, the
+    range's stream-order triplets over global ids: res.coo = (rows, cols, data))."""
     import time
 
     import torch
@@ -338,6 +530,9 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     tpe = 4 if (bidirected and not keep_directed_bidir) else 2
     ktrip = 4 if tpe == 4 else (1 if gd else 2)
     tm = {}
+    fast = _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo)
+    if fast is not None:
+        return fast
     t0 = time.perf_counter()
 
     # 1. local build; 2. stream-order resolution of errors and the one-shot warning
@@ -440,39 +635,37 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
                 names[k] = nm
         out.names = names
 
-    # 5. triplets to row owners (and the A.T stream for MAX-SYM)
-    t3 = time.perf_counter()
-    u32map = gmap.view(torch.int32)
-
-    def route(transposed):
-        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, local.data, dtype, u32map, n_global, world,
-                                               transposed)
-        st_l = [int(v) for v in st.tolist()]
-        cnt = [st_l[k + 1] - st_l[k] for k in range(world)]
-        return C.a2av(rr, cnt)[0], C.a2av(cc, cnt)[0], C.a2av(dd, cnt)[0]
-
-    a = route(False)
-    tstream = route(True) if maxsym else None
-    tm["route"] = (time.perf_counter() - t3) * 1e3
-
-    # 6. this rank's CSR row slice
-    t4 = time.perf_counter()
-    row_lo = (rank * n_global + world - 1) // world
-    row_hi = ((rank + 1) * n_global + world - 1) // world
-    uniform = not weight_tag
-    force = -1
-    if not uniform and dtype in ("float32", "float64") and world > 1:
-        # scipy's has_sorted_indices is a property of the whole matrix: OR over the slices
-        _, _, _, ua, ut = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype, uniform, -1)
-        flags = C.allreduce_max(torch.tensor([int(ua), int(ut)], dtype=torch.int64, device=dev))
-        force = int(flags[0].item()) | (int(flags[1].item()) << 1)
-    indptr, indices, vals, _, _ = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype,
-                                                  uniform, force)
-    tm["csr"] = (time.perf_counter() - t4) * 1e3
+    # 5. triplets to row owners (and the A.T stream for MAX-SYM); 6. this rank's CSR row slice
+    local.dtype_name = dtype
+    if keep_coo:
+        g = gmap.to(torch.int64)
+        out.coo = (g[local.rows.to(torch.int64)].to(torch.int32), g[local.cols.to(torch.int64)].to(torch.int32),
+                   local.data)
+    a, tstream = _route(engine, C, local, dtype, gmap.view(torch.int32), n_global, maxsym, tm)
+    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm)
     out.row_lo, out.row_hi = row_lo, row_hi
     out.indptr, out.indices, out.data = indptr, indices, vals
     out.timings_ms = tm
     return out
+
+
+def gather_coo(res: ShardResult, group=None):
+    """Every rank's stream-order triplets concatenated in rank order (numpy) on every rank: the
+    file's stream-order COO (builders.py:281), since the ranges are contiguous."""
+    import torch
+
+    C = Comm(group)
+    rows, cols, data = res.coo
+    pr = C.allgather_v(rows)
+    pc = C.allgather_v(cols)
+    dt = data.dtype
+    raw = data.contiguous()
+    raw = raw.view(torch.uint8) if raw.numel() and dt != torch.uint8 else raw.reshape(-1).to(torch.uint8)
+    pd = C.allgather_v(raw)
+    npdt = {torch.uint8: np.uint8, torch.int8: np.int8, torch.int32: np.int32, torch.float32: np.float32,
+            torch.float64: np.float64}[dt]
+    return (np.concatenate([x.cpu().numpy() for x in pr]), np.concatenate([x.cpu().numpy() for x in pc]),
+            np.concatenate([x.cpu().numpy().view(npdt) if dt != torch.uint8 else x.cpu().numpy() for x in pd]))
 
 
 def gather_csr(res: ShardResult, group=None):

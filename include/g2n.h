@@ -262,6 +262,14 @@ int g2n_csr_from_coo_pair(g2n_context *ctx, const int32_t *a_rows, const int32_t
                           uint64_t t_nnz, int32_t maxsym, int64_t row_base, uint64_t n_rows, uint64_t n_cols,
                           int32_t dtype, int32_t uniform, int32_t force_unsorted, g2n_result *out);
 
+/* One rank's byte range of a file split over ranks: bytes [offset, offset + len) of path, read
+ * with pread into pinned staging slots and copied to d_dst (len bytes of `device`'s HBM). */
+int g2n_upload_file_range(const char *path, uint64_t offset, uint64_t len, void *d_dst, int32_t device);
+
+/* The record counts of a device-resident range, before any build (what the ranks of a sharded
+ * build exchange first): out4 = {lines, S lines, edge records (L/E/C), records (S/L/E/C/P/O)}. */
+int g2n_count_device(g2n_context *ctx, const void *d_input, size_t len, int64_t *out4);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,53 @@ class CpuEngine:
         sh.names_offsets = torch.from_numpy(o.names_offsets.astype(np.int64))
         return sh
 
+    def read_range(self, path, offset, length):
+        import os
+
+        with open(path, "rb") as fh:
+            return torch.from_numpy(np.frombuffer(os.pread(fh.fileno(), length, offset), dtype=np.uint8).copy())
+
+    def count(self, buf):
+        """{lines, S lines, edge records, records} of the range: first-byte dispatch as K1 does it
+        (a record type must be followed by a tab, a newline or the end of the input)."""
+        b = bytes(buf.numpy())
+        lines = b.split(b"\n")
+        if lines and lines[-1] == b"":
+            lines.pop()
+        kind = [ln[:1] if (len(ln) == 1 or ln[1:2] == b"\t") else b"" for ln in lines]
+        segs = sum(k == b"S" for k in kind)
+        edges = sum(k in (b"L", b"E", b"C") for k in kind)
+        po = sum(k in (b"P", b"O") for k in kind)
+        return [len(lines), segs, edges, segs + edges + po]
+
+    def build_decimal(self, buf, opts, s_base, n_seg):
+        """The oracle's range build with its local ids mapped to GLOBAL decimal ids, or None when a
+        key is not the canonical decimal of a segment (or the range has a warning / error)."""
+        o = self.oracle.run(bytes(buf.numpy()), **opts)
+        if o.status != 0 or o.has_warning:
+            return None
+        bidir = opts.get("bidirected", False)
+        blob, off = o.names_blob.tobytes(), o.names_offsets
+        gid = np.empty(o.n_nodes, dtype=np.int64)
+        for i in range(o.n_nodes):
+            k = blob[off[i]:off[i + 1]]
+            name, ori = (k[:-2], k[-1:]) if bidir else (k, b"")
+            if bidir and (len(k) < 3 or k[-2:-1] != b":" or ori not in (b"+", b"-")):
+                return None
+            if not name.isdigit() or name[:1] == b"0" or not (1 <= int(name) <= n_seg):
+                return None
+            gid[i] = (int(name) - 1) * (2 if bidir else 1) + (ori == b"-")
+        # S lines of this range must be named s_base + 1, s_base + 2, ... in order
+        s_names = [ln.split(b"\t")[1] for ln in bytes(buf.numpy()).split(b"\n")
+                   if ln[:2] == b"S\t" and len(ln.split(b"\t")) > 1]
+        if s_names != [str(s_base + k + 1).encode() for k in range(len(s_names))]:
+            return None
+        sh = self.local_build(buf, opts)
+        sh.rows = torch.from_numpy(gid[sh.rows.numpy()].astype(np.int32))
+        sh.cols = torch.from_numpy(gid[sh.cols.numpy()].astype(np.int32))
+        sh.n_local_nodes = n_seg * (2 if bidir else 1)
+        return sh
+
     def partition_keys(self, blob, offsets, n_ranks):
         b, off = blob.numpy().tobytes(), offsets.numpy()
         n = len(off) - 1
@@ -72,8 +119,11 @@ class CpuEngine:
         return (torch.tensor(ids, dtype=torch.int32), torch.tensor(first, dtype=torch.int32), len(first))
 
     def route_triplets(self, rows, cols, data, dtype, gmap, n_global, n_ranks, transposed):
-        m = gmap.numpy().astype(np.int64)
-        r, c = m[rows.numpy()], m[cols.numpy()]
+        if gmap is None:  # ids are global already (decimal fast path)
+            r, c = rows.numpy().astype(np.int64), cols.numpy().astype(np.int64)
+        else:
+            m = gmap.numpy().astype(np.int64)
+            r, c = m[rows.numpy()], m[cols.numpy()]
         if transposed:
             r, c = c, r
         owner = r * n_ranks // max(n_global, 1)

@@ -58,6 +58,7 @@ def _worker(rank, world, port, outdir):
             for mode in modes:
                 res = build_sharded(buf, engine=eng, gather_names=True, **mode)
                 assert res.status == 0, (name, mode, res.status)
+                assert res.fast_path == (name == "synthetic"), (name, mode)  # decimal ids: no id exchange
                 indptr, indices, vals = gather_csr(res)
                 if rank != 0:
                     continue
@@ -80,5 +81,58 @@ def test_gpu_sharded_build_equals_single_file(gpu, oracle_lib, tmp_path, world):
     import torch.multiprocessing as mp
 
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def _file_worker(rank, world, port, path, backend, outdir):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gfa2network_amd import convert_format, parse_gfa, parse_gfa_sharded
+
+        for mode in ({}, {"directed": False}, {"bidirected": True, "weight_tag": "RC"}):
+            A, nodes = parse_gfa_sharded(path, return_node_list=True, **mode)
+            B, bnodes = parse_gfa(path, build_graph=False, build_matrix=True, return_node_list=True, shard="never",
+                                  **mode)
+            assert A.format == B.format and nodes == bnodes, mode
+            if A.format == "coo":
+                assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col), mode
+            else:
+                assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices), mode
+            assert A.data.tobytes() == B.data.tobytes(), mode
+            C = parse_gfa_sharded(path, output="csr", **mode)
+            D = convert_format(B, "csr")
+            assert np.array_equal(C.indptr, D.indptr) and C.data.tobytes() == D.data.tobytes(), mode
+            # parse_gfa's own dispatch: shard="always" takes the same collective path
+            E = parse_gfa(path, build_graph=False, build_matrix=True, shard="always", **mode)
+            assert E.format == B.format and E.data.tobytes() == B.data.tobytes(), mode
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (3, "gloo"), (1, "nccl")])
+def test_gpu_parse_gfa_sharded_from_file(gpu, tmp_path, world, backend):
+    """The collective entry point on the HIP engine: each rank preads its byte range of the file
+    straight into HBM (g2n_upload_file_range); the result equals the single-GPU parse_gfa.  The
+    nccl (RCCL) case runs the exchange on device tensors (one rank: the box has one GPU, and RCCL
+    refuses two ranks on one device)."""
+    import torch.multiprocessing as mp
+
+    from gfa2network_amd import synth
+
+    path = tmp_path / "in.gfa"
+    path.write_bytes(synth.host_bytes(60_000, 240_000, seed=9, rc_tag=True))
+    mp.spawn(_file_worker, args=(world, _free_port(), str(path), backend, str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}.npy").exists()

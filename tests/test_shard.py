@@ -53,6 +53,29 @@ CASES = {
 }
 
 
+def _decimal_gfa(seed, n_s, n_l, breaks=None):
+    """S lines "1".."N" first, then L lines naming them: the decimal-id fast path; `breaks` spoils
+    its premise somewhere (the general protocol must then give the same answer)."""
+    r = random.Random(seed)
+    lines = [f"S\t{k}\t{'ACGT' * r.randint(0, 3)}\n" for k in range(1, n_s + 1)]
+    lines += [f"L\t{r.randint(1, n_s)}\t{r.choice('+-')}\t{r.randint(1, n_s)}\t{r.choice('+-')}\t0M\n"
+              for _ in range(n_l)]
+    if breaks == "late_s":  # an S line after the edges (in the last range)
+        lines.append(f"S\t{n_s + 1}\t*\n")
+    if breaks == "ghost":  # an edge key that is no segment
+        lines.insert(n_s + n_l // 2, f"L\t{n_s + 5}\t+\t1\t+\t*\n")
+    return "".join(lines).encode()
+
+
+CASES.update({
+    "decimal": (_decimal_gfa(11, 400, 2000), {}),
+    "decimal_undirected": (_decimal_gfa(12, 400, 2000), {"directed": False}),
+    "decimal_bidir": (_decimal_gfa(13, 300, 1500), {"bidirected": True}),
+    "decimal_late_s": (_decimal_gfa(14, 300, 1500, "late_s"), {}),
+    "decimal_ghost": (_decimal_gfa(15, 300, 1500, "ghost"), {"directed": False}),
+})
+
+
 def _worker(rank, world, port, name, outdir):
     import torch.distributed as dist
 
@@ -78,6 +101,8 @@ def _worker(rank, world, port, name, outdir):
             np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
             return
         assert res.status == 0, res.status
+        # the decimal-id fast path runs exactly when its premise holds over the whole file
+        assert res.fast_path == (name in ("decimal", "decimal_undirected", "decimal_bidir")), (name, res.fast_path)
         assert res.has_warning == full.has_warning and (not full.has_warning or res.warn_line == full.warn_line)
         indptr, indices, vals = gather_csr(res)
         want_names = [bytes(full.names_blob[full.names_offsets[i]:full.names_offsets[i + 1]])
@@ -113,3 +138,64 @@ def test_line_ranges_are_line_aligned_and_cover():
         assert rs[0][0] == 0 and rs[-1][1] == len(data)
         for (a, b), (c, _) in zip(rs, rs[1:]):
             assert b == c and (a == b or data[b - 1:b] == b"\n")
+
+
+def _file_worker(rank, world, port, path, mode, outdir):
+    """parse_gfa_sharded through its file entry point: each rank preads only its byte range."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+
+        from gfa2network_amd.api import finalize, parse_gfa_sharded
+        from oracle import oracle as orc
+        from shard_cpu_engine import CpuEngine
+
+        data = open(path, "rb").read()
+        full = orc.run(data, **mode)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            A, nodes = parse_gfa_sharded(path, engine=CpuEngine(orc), return_node_list=True, **mode)
+        B, bnodes = finalize(orc.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                             return_node_list=True, raw_bytes_id=False, verbose=False)
+        assert A.format == B.format and A.shape == B.shape and nodes == bnodes
+        if A.format == "coo":
+            assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+        else:
+            assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        assert A.data.tobytes() == B.data.tobytes()
+        C = parse_gfa_sharded(path, engine=CpuEngine(orc), output="csr", **mode)
+        R = orc.to_raw(full, "csr")
+        assert np.array_equal(C.indptr, R.indptr) and np.array_equal(C.indices, R.indices)
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["decimal", "decimal_undirected", "shuffled", "undirected", "warning"])
+def test_parse_gfa_sharded_from_file(oracle_lib, tmp_path, world, name):
+    """The collective entry point (per-rank pread of its line-aligned byte range, the exchange,
+    the gathered result in parse_gfa's format) equals the single-file answer."""
+    import torch.multiprocessing as mp
+
+    data, mode = CASES[name]
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    mp.spawn(_file_worker, args=(world, _free_port(), str(path), mode, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def test_file_line_ranges_match_in_memory_ranges(tmp_path):
+    from gfa2network_amd.shard import file_line_ranges, line_ranges
+
+    for seed in range(4):
+        data = _gfa(seed, 80, 300, True) + b"S\tlong\t" + b"A" * 70000 + b"\nL\ta\t+\tb\t+\t*"
+        path = tmp_path / f"f{seed}.gfa"
+        path.write_bytes(data)
+        for g in (1, 2, 3, 7, 8):
+            assert file_line_ranges(str(path), g, window=4096) == line_ranges(data, g)
