@@ -33,7 +33,8 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="C4", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--workload", default=None, choices=["C2", "C3", "C4", "C5"],
+                    help="default: C4 on one GPU (the headline config), C5 byte-range-sharded over N > 1 ranks")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-links", type=int, default=12_000_000)
@@ -43,8 +44,8 @@ def _args():
     ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
     ap.add_argument("--no-alt", action="store_true", help="skip the hash-dictionary comparison build")
     ap.add_argument("--shard", action="store_true",
-                    help="one file over the ranks (gfa2network_amd/shard.py): rank r's byte range is its own "
-                         "workload-sized chunk; node names are shared across chunks (default: replicas)")
+                    help="byte-range-shard the workload's one file over the ranks (gfa2network_amd/shard.py; "
+                         "always on for C5)")
     return ap.parse_args()
 
 
@@ -211,8 +212,121 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
     return out
 
 
+def _line_start_device(ptr: int, length: int, nominal: int) -> int:
+    """The first line start at or after `nominal` in a device-resident file (shard.line_ranges's
+    rule), from small windows copied to the host."""
+    import numpy as np
+
+    from gfa2network_amd import synth
+
+    if nominal <= 0 or nominal >= length:
+        return min(max(nominal, 0), length)
+    pos = nominal - 1
+    while pos < length:
+        n = min(1 << 16, length - pos)
+        win = np.empty(n, dtype=np.uint8)
+        synth._lib().g2n_synth_download(win.ctypes.data, ptr + pos, n)
+        k = np.flatnonzero(win == 0x0A)
+        if len(k):
+            return pos + int(k[0]) + 1
+        pos += n
+    return length
+
+
+def main_sharded(args, wl):
+    """BASELINE config 5: ONE synthetic file byte-range-sharded over the ranks.
+    Every rank holds the whole file in its HBM (the generator is deterministic: the same bytes on
+    every rank; generation is untimed) and builds only its line-aligned range through the sharded
+    protocol (gfa2network_amd/shard.py: record counts all-gather + premise all-reduce over RCCL, the
+    range parsed into global decimal ids, triplets all-to-all to their row owners, the rank's CSR row
+    slice).  Strong scaling: the total work is the one file.  Rank 0 first times the same file built
+    by one GPU alone (g2n_build_device), the scaling reference of the same line."""
+    world, rank, local = _dist_setup(args.gpus, always=True)
+    import torch
+    import torch.distributed as dist
+
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+    from gfa2network_amd.shard import HipEngine, build_sharded
+
+    n_s = max(1, int(wl.n_segments * args.scale))
+    n_l = max(1, int(wl.n_links * args.scale))
+    dev_in = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=wl.rc_tag, device=local)
+    starts = [_line_start_device(dev_in.ptr, dev_in.len, r * dev_in.len // world) for r in range(world)] + [dev_in.len]
+    lo, hi = starts[rank], starts[rank + 1]
+    mode = dict(wl.mode)
+    kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+              weight_tag=mode.get("weight_tag"), dtype="float64")
+    one = None
+    lib = nat.load()
+    if rank == 0:  # the whole file on one GPU: the scaling reference
+        ctx = lib.g2n_context_create(local)
+        o = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=local,
+                             directed=kw["directed"], bidirected=kw["bidirected"], weight_tag=kw["weight_tag"])
+        res = nat.Result()
+        for _ in range(max(1, args.warmup)):
+            assert lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res)) == 0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            assert lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res)) == 0
+        dt = (time.perf_counter() - t0) / args.steps
+        one = {"ms_per_step": round(dt * 1e3, 3), "value": round(n_l / dt / 1e6, 2), "nnz": int(res.nnz)}
+        lib.g2n_context_destroy(ctx)
+    dist.barrier()
+    eng = HipEngine(local)
+    buf = _DevBytes(dev_in.ptr + lo, hi - lo)
+    for _ in range(args.warmup):
+        build_sharded(buf, engine=eng, **kw)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    tms = []
+    for _ in range(args.steps):
+        res = build_sharded(buf, engine=eng, **kw)
+        tms.append(res.timings_ms)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = _max_over_ranks(world, time.perf_counter() - t0)
+    slice_nnz = torch.tensor([int(res.indices.numel())], dtype=torch.int64, device="cuda")
+    dist.all_reduce(slice_nnz)
+    ms = elapsed / args.steps * 1e3
+    value = res.n_edges * args.steps / elapsed / 1e6
+    line = {
+        "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
+        "value": round(value, 2), "unit": "M edge records/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8/int64 (float64 weights)",
+        "data": "synthetic (deterministic generator, gfa2network_amd/csrc/synth.h), generated in HBM on every rank",
+        "config": {"workload": f"{wl.name}: {wl.note}, one file byte-range-sharded over {world} rank(s)"
+                               + (f" x{args.scale}" if args.scale != 1 else ""),
+                   "n_segments": n_s, "n_links": n_l, "input_bytes": dev_in.len, "n_nodes": res.n_nodes,
+                   "nnz": int(slice_nnz.item()), "mode": mode or "default", "output": "csr row slice per rank",
+                   "parallelism": f"shard x{world} (RCCL: all-gather of range counts, all-reduce of the "
+                                  f"id premise, all-to-all of triplets to row owners)",
+                   "id_path": "decimal-id fast path" if res.fast_path else "general owner protocol"},
+        "gb_per_s_ingested": round(dev_in.len * args.steps / elapsed / 1e9, 2),
+        "host_ms_per_stage_rank0": {k: round(sum(t.get(k, 0.0) for t in tms) / len(tms), 2) for k in tms[0]},
+    }
+    if one is not None:
+        line["one_gpu"] = one
+        line["speedup_vs_one_gpu"] = round(value / one["value"], 3)
+    if rank == 0:
+        print(json.dumps(line))
+    eng.close()
+    dev_in.free()
+    dist.destroy_process_group()
+
+
 def main():
     args = _args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.workload is None:
+        args.workload = "C5" if max(world_env, args.gpus) > 1 else "C4"
+    if (args.workload == "C5" or args.shard) and not args.e2e_only:
+        from gfa2network_amd import synth
+
+        main_sharded(args, synth.WORKLOADS[args.workload])
+        return
     if args.e2e_only:
         from gfa2network_amd import synth
 
@@ -381,52 +495,6 @@ class _DevBytes:
         return self.n
 
 
-def main_shard(args):
-    """One file split over the ranks, each range built and reconciled."""
-    world, rank, local = _dist_setup(args.gpus, always=True)
-    import torch.distributed as dist
-
-    from gfa2network_amd import synth
-    from gfa2network_amd.shard import HipEngine, build_sharded
-
-    wl = synth.WORKLOADS[args.workload]
-    n_s = max(1, int(wl.n_segments * args.scale))
-    n_l = max(1, int(wl.n_links * args.scale))
-    dev_in = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local)
-    eng = HipEngine(local)
-    mode = dict(wl.mode)
-    kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
-              weight_tag=mode.get("weight_tag"), dtype="float64")
-    buf = _DevBytes(dev_in.ptr, dev_in.len)
-    for _ in range(args.warmup):
-        build_sharded(buf, engine=eng, **kw)
-    dist.barrier()
-    t0 = time.perf_counter()
-    tms = []
-    for _ in range(args.steps):
-        res = build_sharded(buf, engine=eng, **kw)
-        tms.append(res.timings_ms)
-    dist.barrier()
-    elapsed = _max_over_ranks(world, time.perf_counter() - t0)
-    edges_total = res.n_edges * args.steps
-    line = {
-        "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
-        "value": round(edges_total / elapsed / 1e6, 2), "unit": "M edge records/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8/int64 (float64 weights)",
-        "data": "synthetic (deterministic generator), one chunk per rank generated in HBM",
-        "config": {"workload": f"{wl.name} chunk per rank, one file over {world} ranks", "n_nodes": res.n_nodes,
-                   "edges": res.n_edges, "output": "csr row slices", "parallelism": f"shard x{world}"},
-        "gb_per_s_ingested": round(dev_in.len * world * args.steps / elapsed / 1e9, 2),
-        "host_ms_per_stage_rank0": {k: round(sum(t[k] for t in tms) / len(tms), 2) for k in tms[0]},
-    }
-    if rank == 0:
-        print(json.dumps(line))
-    eng.close()
-    dev_in.free()
-    dist.destroy_process_group()
-
-
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
     "tiles": "g2n::k_tile_count",
     "parse": "g2n::k_tile_parse",
@@ -501,7 +569,4 @@ def measured_traffic(kernel: str):
 
 
 if __name__ == "__main__":
-    if "--shard" in sys.argv:
-        main_shard(_args())
-    else:
-        main()
+    main()

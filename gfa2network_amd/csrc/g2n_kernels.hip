@@ -2355,22 +2355,21 @@ __global__ void __launch_bounds__(kTPB) k_route_keys(const int32_t* __restrict__
   idx[i] = (uint32_t)i;
 }
 
-template <int kW>  // element size of data
+template <class W>  // an unsigned type of the data's element size; data == nullptr: coordinates only
 __global__ void __launch_bounds__(kTPB) k_route_gather(const int32_t* __restrict__ rows,
                                                        const int32_t* __restrict__ cols,
-                                                       const uint8_t* __restrict__ data,
+                                                       const W* __restrict__ data,
                                                        const uint32_t* __restrict__ perm, uint64_t n,
                                                        const uint32_t* __restrict__ map, int transposed,
                                                        int32_t* __restrict__ orows, int32_t* __restrict__ ocols,
-                                                       uint8_t* __restrict__ odata) {
+                                                       W* __restrict__ odata) {
   const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (i >= n) return;
   const uint32_t j = perm[i];
   const int32_t r = map ? (int32_t)map[rows[j]] : rows[j], c = map ? (int32_t)map[cols[j]] : cols[j];
   orows[i] = transposed ? c : r;
   ocols[i] = transposed ? r : c;
-#pragma unroll
-  for (int b = 0; b < kW; b++) odata[i * kW + b] = data[(uint64_t)j * kW + b];
+  if (data) odata[i] = data[j];
 }
 
 __global__ void k_scan_total(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off, uint64_t n,

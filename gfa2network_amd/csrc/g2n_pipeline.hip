@@ -92,13 +92,6 @@ static T* dget(g2n_context* c, int slot, uint64_t count) {
   return (T*)dbuf(c, slot, (size_t)count * sizeof(T));
 }
 
-// grid of a persistent kernel: blocks_per_cu resident blocks per CU (its LDS occupancy), no more
-// than there are work items
-static unsigned persistent_grid(const g2n_context* c, uint64_t n_items, unsigned blocks_per_cu) {
-  const uint64_t g = (uint64_t)c->n_cu * blocks_per_cu;
-  return (unsigned)(n_items < g ? (n_items ? n_items : 1) : g);
-}
-
 static inline unsigned grid_for(uint64_t n, unsigned tpb = kTPB) {
   uint64_t g = (n + tpb - 1) / tpb;
   return (unsigned)(g ? g : 1);
@@ -1262,17 +1255,17 @@ void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, co
     hipLaunchKernelGGL(k_route_keys, dim3(grid_for(nnz)), dim3(kTPB), 0, c->stream, rows, cols, nnz, map, n_global,
                        n_ranks, transposed, owner, idx);
     sort_pairs_u32<uint32_t>(c, owner, owner_s, idx, perm, nnz, bits_for(n_ranks));
-    const size_t w = dtype_size(dtype);
+    const size_t w = data ? dtype_size(dtype) : 0;
     const dim3 g(grid_for(nnz)), b(kTPB);
-    if (w == 1)
-      hipLaunchKernelGGL(k_route_gather<1>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
-                         transposed, orows, ocols, (uint8_t*)odata);
+    if (w == 8)
+      hipLaunchKernelGGL(k_route_gather<uint64_t>, g, b, 0, c->stream, rows, cols, (const uint64_t*)data, perm, nnz,
+                         map, transposed, orows, ocols, (uint64_t*)odata);
     else if (w == 4)
-      hipLaunchKernelGGL(k_route_gather<4>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
-                         transposed, orows, ocols, (uint8_t*)odata);
+      hipLaunchKernelGGL(k_route_gather<uint32_t>, g, b, 0, c->stream, rows, cols, (const uint32_t*)data, perm, nnz,
+                         map, transposed, orows, ocols, (uint32_t*)odata);
     else
-      hipLaunchKernelGGL(k_route_gather<8>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz, map,
-                         transposed, orows, ocols, (uint8_t*)odata);
+      hipLaunchKernelGGL(k_route_gather<uint8_t>, g, b, 0, c->stream, rows, cols, (const uint8_t*)data, perm, nnz,
+                         map, transposed, orows, ocols, (uint8_t*)odata);
   }
   // rank starts from the sorted owners (the row-start kernels, n_ranks "rows")
   G2N_HIP(hipMemsetAsync(&c->ctl->row_gap, 0, sizeof(unsigned long long), c->stream));
@@ -1408,7 +1401,7 @@ int g2n_route_triplets(g2n_context* ctx, const int32_t* d_rows, const int32_t* d
                        uint64_t nnz, int32_t dtype, const uint32_t* d_map, uint64_t n_global, uint32_t n_ranks,
                        int32_t transposed, int32_t* d_out_rows, int32_t* d_out_cols, void* d_out_data,
                        uint32_t* d_starts) {
-  if (!d_starts || (nnz && (!d_rows || !d_cols || !d_data || !d_map || !d_out_rows || !d_out_cols || !d_out_data)))
+  if (!d_starts || (nnz && (!d_rows || !d_cols || !d_data != !d_out_data || !d_out_rows || !d_out_cols)))
     return G2N_E_ARG;
   if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) return G2N_E_ARG;
   G2N_CTX_CALL(ctx, g2n::route_triplets(ctx, d_rows, d_cols, d_data, nnz, dtype, d_map, n_global, n_ranks, transposed,

@@ -13,7 +13,7 @@
 // shift-and-round conversion (the "simple decimal conversion" of the Go strconv package's
 // decimal.go, rewritten here): exact for any digit count, used only on the slow path.
 //
-// Everything is G2N_HD so tests/test_pylit.py can compile this header with g++ and fuzz
+// Everything is G2N_HD so tests/test_host_headers.py (tests/native/hostcheck.cpp) compiles it with g++ and fuzzes
 // it against CPython's own int()/float() on the CPU; the GPU kernels include the same code.
 #pragma once
 #include <stdint.h>

@@ -14,7 +14,7 @@
 // __final_insertion_sort / __insertion_sort / __unguarded_linear_insert, and
 // bits/stl_heap.h __make_heap / __adjust_heap / __push_heap / __pop_heap /
 // __sort_heap (the __partial_sort fallback).  Checked against the real std::sort in
-// tests/test_stl_sort.py.
+// tests/test_host_headers.py (tests/native/hostcheck.cpp).
 #pragma once
 #include <stdint.h>
 

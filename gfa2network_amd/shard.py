@@ -148,6 +148,24 @@ def file_line_ranges(path: str, n_ranks: int, window: int = 1 << 16) -> list[tup
 
 
 # ------------------------------------------------------------------------ engines --
+class DevArray:
+    """A view of `n` elements of a device array owned by an engine context (no copy): valid until
+    the next build on that context.  Exposes what the engine calls read (data_ptr, numel, [a:b])."""
+
+    def __init__(self, ptr: int, n: int, itemsize: int):
+        self.ptr, self.n, self.itemsize = ptr, n, itemsize
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.n
+
+    def __getitem__(self, sl: slice):
+        a, b, _ = sl.indices(self.n)
+        return DevArray(self.ptr + a * self.itemsize, max(b - a, 0), self.itemsize)
+
+
 class HipEngine:
     """The product engine: libg2n.so on one GPU; buffers are torch device tensors."""
 
@@ -163,11 +181,13 @@ class HipEngine:
             raise nat.NativeUnavailable(nat.last_error())
         self._hip = ctypes.CDLL("libamdhip64.so")
         self._hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        self.ctx_b = None  # the fast path's build context: its COO is read in place by route / csr (on ctx)
 
     def close(self):
-        if self.ctx:
-            self.lib.g2n_context_destroy(self.ctx)
-            self.ctx = None
+        for name in ("ctx", "ctx_b"):
+            if getattr(self, name):
+                self.lib.g2n_context_destroy(getattr(self, name))
+                setattr(self, name, None)
 
     def _sync(self):
         self.torch.cuda.current_stream(self.device).synchronize()
@@ -233,15 +253,20 @@ class HipEngine:
                     "g2n_count_device")
         return [int(v) for v in out]
 
-    def build_decimal(self, buf, opts: dict, s_base: int, n_seg: int):
+    def build_decimal(self, buf, opts: dict, s_base: int, n_seg: int, view: bool = False):
         """The range parsed straight into GLOBAL decimal ids (S lines s_base.. of n_seg), or None when
-        it needs the general protocol (ids that are not decimal, errors, warnings, slow weights)."""
+        it needs the general protocol (ids that are not decimal, errors, warnings, slow weights).
+        view: the COO as DevArray views of the build context (valid until the next build_decimal)."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
         o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1
         res = nat.Result()
+        if self.ctx_b is None:
+            self.ctx_b = self.lib.g2n_context_create(self.device_index)
+            if not self.ctx_b:
+                raise nat.NativeUnavailable(nat.last_error())
         self._sync()
-        rc = self.lib.g2n_build_device(self.ctx, buf.data_ptr() if buf.numel() else None, buf.numel(),
+        rc = self.lib.g2n_build_device(self.ctx_b, buf.data_ptr() if buf.numel() else None, buf.numel(),
                                        ctypes.byref(o), ctypes.byref(res))
         if rc != 0:
             if rc not in (nat.E_UNSUPPORTED,) and not (1 <= rc <= 12):
@@ -252,9 +277,14 @@ class HipEngine:
                         has_warning=False, warn_byte=0, n_lines=res.n_lines, n_records=res.n_records,
                         n_records_before_error=res.n_records, n_edges=res.n_edges, n_local_nodes=res.n_nodes,
                         n_cast_overflow=res.n_cast_overflow)
-        sh.rows = self._copy_out(res.rows, n, torch.int32)
-        sh.cols = self._copy_out(res.cols, n, torch.int32)
-        sh.data = self._copy_out(res.data, n, getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")]))
+        tdt = getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")])
+        if view:
+            sh.rows, sh.cols = DevArray(res.rows or 0, n, 4), DevArray(res.cols or 0, n, 4)
+            sh.data = DevArray(res.data or 0, n, torch.empty(0, dtype=tdt).element_size())
+        else:
+            sh.rows = self._copy_out(res.rows, n, torch.int32)
+            sh.cols = self._copy_out(res.cols, n, torch.int32)
+            sh.data = self._copy_out(res.data, n, tdt)
         return sh
 
     def partition_keys(self, blob, offsets, n_ranks: int):
@@ -289,26 +319,27 @@ class HipEngine:
         n = rows.numel()
         orows = torch.empty(n, dtype=torch.int32, device=self.device)
         ocols = torch.empty(n, dtype=torch.int32, device=self.device)
-        odata = torch.empty_like(data)
+        # data None: uniform values (unweighted), nothing to route
+        odata = None if data is None else torch.empty(n, dtype=getattr(torch, TORCH_DTYPES[dtype]), device=self.device)
         starts = torch.empty(n_ranks + 1, dtype=torch.int32, device=self.device)
         self._sync()
         nz = n > 0
         self._check(self.lib.g2n_route_triplets(
             self.ctx, rows.data_ptr() if nz else None, cols.data_ptr() if nz else None,
-            data.data_ptr() if nz else None, n, nat.DTYPE_CODES[dtype],
+            data.data_ptr() if nz and data is not None else None, n, nat.DTYPE_CODES[dtype],
             gmap.data_ptr() if gmap is not None and gmap.numel() else None,
             n_global, n_ranks, int(transposed), orows.data_ptr() if nz else None, ocols.data_ptr() if nz else None,
-            odata.data_ptr() if nz else None, starts.data_ptr()), "g2n_route_triplets")
+            odata.data_ptr() if nz and odata is not None else None, starts.data_ptr()), "g2n_route_triplets")
         return orows, ocols, odata, starts
 
     def csr_pair(self, a, t, maxsym: bool, row_base: int, n_rows: int, n_cols: int, dtype: str, uniform: bool,
                  force_unsorted: int):
         torch = self.torch
         res = nat.Result()
-        t = t if t is not None else (a[0][:0], a[1][:0], a[2][:0])
+        t = t if t is not None else (a[0][:0], a[1][:0], None)
 
-        def p(x):
-            return x.data_ptr() if x.numel() else None
+        def p(x):  # uniform builds pass no values (None)
+            return x.data_ptr() if x is not None and x.numel() else None
 
         self._sync()
         self._check(self.lib.g2n_csr_from_coo_pair(self.ctx, p(a[0]), p(a[1]), p(a[2]), a[0].numel(), p(t[0]),
@@ -340,19 +371,33 @@ class Comm:
 
     def a2av(self, x, send_counts):
         """all-to-all-v: send_counts[k] elements of x to rank k; returns (received, counts)."""
+        outs, recv = self.a2av_multi([x], send_counts)
+        return outs[0], recv
+
+    def a2av_multi(self, xs, send_counts):
+        """a2av of several tensors with the same per-rank counts: one count exchange for all of
+        them (None entries pass through as None)."""
         torch = self.torch
         if self.world == 1:
-            return x.clone(), list(send_counts)
-        dev = x.device
-        xc = self._c(x.contiguous())
-        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=xc.device)
-        rc = torch.empty(self.world, dtype=torch.int64, device=xc.device)
+            return [None if x is None else x.clone() for x in xs], list(send_counts)
+        ref = next(x for x in xs if x is not None)
+        dev = ref.device
+        host = self._c(ref[:0]).device
+        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=host)
+        rc = torch.empty(self.world, dtype=torch.int64, device=host)
         self.dist.all_to_all_single(rc, sc, group=self.group)
         recv = [int(v) for v in rc.tolist()]
-        out = torch.empty(sum(recv), dtype=xc.dtype, device=xc.device)
-        self.dist.all_to_all_single(out, xc, output_split_sizes=recv, input_split_sizes=list(send_counts),
-                                    group=self.group)
-        return out.to(dev), recv
+        outs = []
+        for x in xs:
+            if x is None:
+                outs.append(None)
+                continue
+            xc = self._c(x.contiguous())
+            out = torch.empty(sum(recv), dtype=xc.dtype, device=xc.device)
+            self.dist.all_to_all_single(out, xc, output_split_sizes=recv, input_split_sizes=list(send_counts),
+                                        group=self.group)
+            outs.append(out.to(dev))
+        return outs, recv
 
     def allgather_v(self, x):
         """every rank's (variable-length) tensor, in rank order"""
@@ -439,18 +484,23 @@ def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm):
     return row_lo, row_hi, indptr, indices, vals
 
 
-def _route(engine, C, local, dtype, gmap, n_global, maxsym, tm):
-    """Step 5: triplets to the owners of their rows (and the A.T stream for MAX-SYM)."""
+def _route(engine, C, local, dtype, gmap, n_global, maxsym, uniform, tm):
+    """Step 5: triplets to the owners of their rows (and the A.T stream for MAX-SYM).  Uniform
+    (unweighted) values are not routed; one rank with global ids routes nothing."""
     import time
 
     t3 = time.perf_counter()
+    if C.world == 1 and gmap is None:  # every row is this rank's: the streams as they are
+        d = None if uniform else local.data
+        tm["route"] = 0.0
+        return (local.rows, local.cols, d), ((local.cols, local.rows, d) if maxsym else None)
 
     def route(transposed):
-        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, local.data, local.dtype_name, gmap, n_global,
-                                               C.world, transposed)
+        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, None if uniform else local.data,
+                                               local.dtype_name, gmap, n_global, C.world, transposed)
         st_l = [int(v) for v in st.tolist()]
         cnt = [st_l[k + 1] - st_l[k] for k in range(C.world)]
-        return C.a2av(rr, cnt)[0], C.a2av(cc, cnt)[0], C.a2av(dd, cnt)[0]
+        return tuple(C.a2av_multi([rr, cc, dd], cnt)[0])
 
     a = route(False)
     tstream = route(True) if maxsym else None
@@ -478,15 +528,16 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     if not ok or n_seg == 0 or n_seg * tps >= 2**31 - 1:
         return None
     s_base = int(sum(allc[k][1] for k in range(rank)))
-    local = engine.build_decimal(buf, opts, s_base, n_seg)
+    tm["count"] = (time.perf_counter() - t0) * 1e3
+    local = engine.build_decimal(buf, opts, s_base, n_seg, view=not keep_coo)
     # every range's ids are global decimals (the id map needs no exchange) — or nobody's are
     verdict = torch.tensor([0 if local is None else 1], dtype=torch.int64, device=engine.device)
     if int(C.allreduce_min(verdict).item()) == 0:
         return None
-    tm["count_build"] = (time.perf_counter() - t0) * 1e3
+    tm["build"] = (time.perf_counter() - t0) * 1e3 - tm["count"]
     n_global = n_seg * tps
     local.dtype_name = opts.get("dtype", "float64")
-    a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, tm)
+    a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"), tm)
     row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
                                                    opts.get("weight_tag"), tm)
     casts = torch.tensor([local.n_cast_overflow], dtype=torch.int64, device=engine.device)
@@ -641,7 +692,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         g = gmap.to(torch.int64)
         out.coo = (g[local.rows.to(torch.int64)].to(torch.int32), g[local.cols.to(torch.int64)].to(torch.int32),
                    local.data)
-    a, tstream = _route(engine, C, local, dtype, gmap.view(torch.int32), n_global, maxsym, tm)
+    a, tstream = _route(engine, C, local, dtype, gmap.view(torch.int32), n_global, maxsym, not weight_tag, tm)
     row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm)
     out.row_lo, out.row_hi = row_lo, row_hi
     out.indptr, out.indices, out.data = indptr, indices, vals

@@ -243,7 +243,9 @@ int g2n_partition_keys(g2n_context *ctx, const uint8_t *d_blob, uint64_t blob_le
 /* Triplet i = (d_map[d_rows[i]], d_map[d_cols[i]], d_data[i]) (transposed: row and column
  * swapped) goes to rank floor(row * n_ranks / n_global); the output holds them grouped by
  * rank, stream order kept within a rank; d_starts[r] = first output of rank r
- * (d_starts[n_ranks] = nnz).  Outputs sized nnz (data: nnz elements of dtype). */
+ * (d_starts[n_ranks] = nnz).  Outputs sized nnz (data: nnz elements of dtype).  d_map may be
+ * NULL: the identity map (the rows / cols already hold global ids, the decimal-id shard path).
+ * d_data and d_out_data both NULL: the coordinates only (uniform values need no routing). */
 int g2n_route_triplets(g2n_context *ctx, const int32_t *d_rows, const int32_t *d_cols, const void *d_data,
                        uint64_t nnz, int32_t dtype, const uint32_t *d_map, uint64_t n_global, uint32_t n_ranks,
                        int32_t transposed, int32_t *d_out_rows, int32_t *d_out_cols, void *d_out_data,

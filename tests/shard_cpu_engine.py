@@ -66,7 +66,7 @@ class CpuEngine:
         po = sum(k in (b"P", b"O") for k in kind)
         return [len(lines), segs, edges, segs + edges + po]
 
-    def build_decimal(self, buf, opts, s_base, n_seg):
+    def build_decimal(self, buf, opts, s_base, n_seg, view=False):
         """The oracle's range build with its local ids mapped to GLOBAL decimal ids, or None when a
         key is not the canonical decimal of a segment (or the range has a warning / error)."""
         o = self.oracle.run(bytes(buf.numpy()), **opts)
@@ -129,16 +129,18 @@ class CpuEngine:
         owner = r * n_ranks // max(n_global, 1)
         order = np.argsort(owner, kind="stable")
         starts = np.searchsorted(owner[order], np.arange(n_ranks + 1)).astype(np.int32)
-        d = data.numpy()[order]
-        return (torch.from_numpy(r[order].astype(np.int32)), torch.from_numpy(c[order].astype(np.int32)),
-                torch.from_numpy(d.copy()), torch.from_numpy(starts))
+        d = None if data is None else torch.from_numpy(data.numpy()[order].copy())  # None: uniform values
+        return (torch.from_numpy(r[order].astype(np.int32)), torch.from_numpy(c[order].astype(np.int32)), d,
+                torch.from_numpy(starts))
 
     def csr_pair(self, a, t, maxsym, row_base, n_rows, n_cols, dtype, uniform, force_unsorted):
         npdt = np.bool_ if dtype == "bool" else NP[dtype]
 
         def csr(x):
             rows = x[0].numpy().astype(np.int64) - row_base
-            return sp.coo_matrix((x[2].numpy().view(NP[dtype]).astype(npdt), (rows, x[1].numpy().astype(np.int64))),
+            vals = (np.ones(len(rows), dtype=npdt) if uniform or x[2] is None
+                    else x[2].numpy().view(NP[dtype]).astype(npdt))
+            return sp.coo_matrix((vals, (rows, x[1].numpy().astype(np.int64))),
                                  shape=(n_rows, n_cols)).tocsr()
 
         M = csr(a)
