@@ -128,6 +128,13 @@ def load() -> ctypes.CDLL:
             f"{path} not found: build it with `make -C gfa2network_amd/csrc` "
             "(or __graft_entry__.build()); the GFA->CSR path has no CPU fallback")
     try:
+        # One HIP runtime per process: torch's wheel bundles a libamdhip64.so.7 of its own (same
+        # SONAME as /opt/rocm's, which libg2n.so names), and whichever loads first serves both.
+        # torch cannot initialise the device on /opt/rocm's, so load torch's first when present.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    try:
         lib = ctypes.CDLL(path)
     except OSError as exc:  # pragma: no cover - depends on the image
         raise NativeUnavailable(f"cannot load {path}: {exc}") from exc

@@ -20,6 +20,7 @@
 #include "g2n_kernels.hip"
 #include "g2n_scan.hip"
 #include "g2n_sym.hip"
+#include "g2n_route.hip"
 
 #define G2N_HIP(call)                                                                                      \
   do {                                                                                                     \
@@ -37,7 +38,7 @@ enum Slot {
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
-  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_LBST, S_SCANST, S_NSLOTS
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_LBST, S_SCANST, S_RBOUND, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -1247,6 +1248,38 @@ void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, co
   begin_call(c);
   if (n_ranks == 0 || n_ranks > 4096) throw Failure(G2N_E_ARG, "n_ranks out of range");
   if (nnz >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 triplets");
+  if (n_ranks <= kRouteMaxRanks) {  // stable owner partition (g2n_route.hip)
+    std::vector<uint64_t> hb(n_ranks + 1);
+    for (uint32_t k = 0; k <= n_ranks; k++) hb[k] = ((uint64_t)k * n_global + n_ranks - 1) / n_ranks;
+    auto* bounds = dget<uint64_t>(c, S_RBOUND, n_ranks + 1);
+    G2N_HIP(hipMemcpyAsync(bounds, hb.data(), hb.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    const uint64_t n_blk = nnz ? (nnz + kRouteTile - 1) / kRouteTile : 0;
+    const uint32_t bits = n_ranks > 1 ? (uint32_t)bits_for(n_ranks) : 0u;
+    RouteSrc s{rows, cols, map, nnz, n_ranks, transposed, bounds};
+    if (n_blk) {
+      auto* cnt = dget<uint32_t>(c, S_PCNT, (uint64_t)n_ranks * n_blk);
+      auto* off = dget<uint32_t>(c, S_POFF, (uint64_t)n_ranks * n_blk);
+      hipLaunchKernelGGL(k_route_count, dim3((unsigned)n_blk), dim3(kRouteTPB), 0, c->stream, s, bits, n_blk, cnt);
+      scan_excl<uint32_t, uint32_t>(c, cnt, off, (uint64_t)n_ranks * n_blk);
+      const size_t w = data ? dtype_size(dtype) : 0;
+      const dim3 g((unsigned)n_blk), b(kRouteTPB);
+      if (w == 8)
+        hipLaunchKernelGGL(k_route_scatter<uint64_t>, g, b, 0, c->stream, s, bits, n_blk, (const uint32_t*)off,
+                           (const uint64_t*)data, orows, ocols, (uint64_t*)odata);
+      else if (w == 4)
+        hipLaunchKernelGGL(k_route_scatter<uint32_t>, g, b, 0, c->stream, s, bits, n_blk, (const uint32_t*)off,
+                           (const uint32_t*)data, orows, ocols, (uint32_t*)odata);
+      else
+        hipLaunchKernelGGL(k_route_scatter<uint8_t>, g, b, 0, c->stream, s, bits, n_blk, (const uint32_t*)off,
+                           (const uint8_t*)data, orows, ocols, (uint8_t*)odata);
+      hipLaunchKernelGGL(k_route_starts, dim3(grid_for(n_ranks + 1)), dim3(kTPB), 0, c->stream,
+                         (const uint32_t*)off, n_blk, n_ranks, nnz, starts);
+    } else {
+      G2N_HIP(hipMemsetAsync(starts, 0, (n_ranks + 1) * sizeof(uint32_t), c->stream));
+    }
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    return;
+  }
   auto* owner = dget<uint32_t>(c, S_KEYS0, nnz);
   auto* owner_s = dget<uint32_t>(c, S_KEYS1, nnz);
   auto* idx = dget<uint32_t>(c, S_VALS0, nnz);

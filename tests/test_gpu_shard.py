@@ -136,3 +136,49 @@ def test_gpu_parse_gfa_sharded_from_file(gpu, tmp_path, world, backend):
     mp.spawn(_file_worker, args=(world, _free_port(), str(path), backend, str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}.npy").exists()
+
+
+@pytest.mark.parametrize("n_ranks", [1, 2, 3, 8, 100, 256, 300])
+def test_gpu_route_triplets_stable_partition(gpu, n_ranks):
+    """g2n_route_triplets (the owner partition of g2n_route.hip; > 256 ranks the sort path) equals
+    numpy's stable partition by owner = floor(row * R / n_global): stream order kept per owner, with
+    and without an id map, transposed, values of 1, 4 and 8 bytes or none."""
+    import torch
+
+    from gfa2network_amd.shard import HipEngine
+
+    rng = np.random.default_rng(n_ranks)
+    n, n_global = 300_000 + n_ranks, 1_000_003
+    rows = rng.integers(0, n_global, n).astype(np.int32)
+    cols = rng.integers(0, n_global, n).astype(np.int32)
+    perm = rng.permutation(n_global).astype(np.uint32)
+    eng = HipEngine(0)
+    try:
+        for use_map in (False, True):
+            for transposed in (False, True):
+                for dt in ("float64", "int32", "int8", None):
+                    data = None if dt is None else rng.integers(-100, 100, n).astype(dt)
+                    r, c = (perm[rows].astype(np.int64), perm[cols].astype(np.int64)) if use_map else (rows, cols)
+                    if transposed:
+                        r, c = c, r
+                    owner = np.asarray(r, dtype=np.int64) * n_ranks // n_global
+                    order = np.argsort(owner, kind="stable")
+                    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(eng.device)  # noqa: E731
+                    rr, cc, dd, st = eng.route_triplets(d(rows), d(cols), None if data is None else d(data),
+                                                        dt or "float64", d(perm.view(np.int32)) if use_map else None,
+                                                        n_global, n_ranks, transposed)
+                    key = (use_map, transposed, dt)
+                    assert np.array_equal(rr.cpu().numpy(), np.asarray(r)[order]), key
+                    assert np.array_equal(cc.cpu().numpy(), np.asarray(c)[order]), key
+                    if data is not None:
+                        assert np.array_equal(dd.cpu().numpy(), data[order]), key
+                    else:
+                        assert dd is None
+                    want = np.searchsorted(owner[order], np.arange(n_ranks + 1))
+                    assert np.array_equal(st.cpu().numpy(), want), key
+        # empty input
+        e = torch.zeros(0, dtype=torch.int32, device=eng.device)
+        rr, cc, dd, st = eng.route_triplets(e, e, None, "float64", None, n_global, n_ranks, False)
+        assert rr.numel() == 0 and np.array_equal(st.cpu().numpy(), np.zeros(n_ranks + 1))
+    finally:
+        eng.close()
