@@ -297,8 +297,8 @@ def _from_result(ptr, rc: int) -> RawResult:
     out.sum_sorted = bool(r.sum_sorted)
     out.n_cast_overflow = int(r.n_cast_overflow)
     out.input_bytes = int(r.input_bytes)
-    if r.format == FMT_TEXT and (r.status == OK or (r.status == E_UNICODE and r.err_line < 0)):
-        out.format = "text"  # export --format edge-list: the rendered lines (before an undecodable key)
+    if r.format == FMT_TEXT and r.data:
+        out.format = "text"  # export --format edge-list: the rendered lines (all, or those before a failure)
         out.data = _view(r.data, r.nnz, np.uint8, owner)
     elif r.status == OK:
         idx = np.int32 if r.index_width == 4 else np.int64
@@ -367,11 +367,12 @@ def host_bytes_at(addr: int, n: int) -> bytes:
 
 
 class GzipFailure(Exception):
-    """g2n_gunzip failed: ``sub`` = gzip.py's exception kind, ``message`` its text."""
+    """g2n_gunzip failed: ``sub`` = gzip.py's exception kind, ``message`` its text, ``prefix``
+    the bytes gzip.py's reader returned before raising."""
 
-    def __init__(self, sub: int, message: str):
+    def __init__(self, sub: int, message: str, prefix: bytes = b""):
         super().__init__(sub, message)
-        self.sub, self.message = sub, message
+        self.sub, self.message, self.prefix = sub, message, prefix
 
 
 def gunzip(data: bytes, parallel: bool = True) -> tuple[bytes, int]:
@@ -382,7 +383,12 @@ def gunzip(data: bytes, parallel: bool = True) -> tuple[bytes, int]:
     rc = lib.g2n_gunzip(arr.ctypes.data if arr.size else None, arr.size, int(parallel), ctypes.byref(out),
                         ctypes.byref(n), ctypes.byref(members), ctypes.byref(sub))
     if rc == E_GZIP:
-        raise GzipFailure(int(sub.value), last_error())
+        msg = last_error()
+        try:
+            prefix = host_bytes_at(out.value, n.value) if out.value else b""
+        finally:
+            lib.g2n_free(out)
+        raise GzipFailure(int(sub.value), msg, prefix)
     if rc != OK:
         raise RuntimeError(f"{status_name(rc)}: {last_error()}")
     try:

@@ -107,7 +107,13 @@ def _progress(n_records: int) -> None:
 def finalize(raw: RawResult, *, dtype: np.dtype, return_node_list: bool, raw_bytes_id: bool,
              verbose: bool, build_matrix: bool = True, path: Any = None):
     """Turn one native result into the reference's return value / warning / exception."""
-    if raw.status in (nat.E_IO, nat.E_GZIP, nat.E_ARG, nat.E_DEVICE, nat.E_NOMEM, nat.E_UNSUPPORTED):
+    if raw.status in (nat.E_IO, nat.E_ARG, nat.E_DEVICE, nat.E_NOMEM, nat.E_UNSUPPORTED):
+        raise_for_status(raw, dtype, path)
+    if raw.status == nat.E_GZIP:  # the lines gzip returned before failing were parsed first
+        if raw.has_warning:
+            warnings.warn(f"Skipping unsupported record: {chr(raw.warn_byte)}", RuntimeWarning, stacklevel=3)
+        if verbose:
+            _progress(raw.n_records)
         raise_for_status(raw, dtype, path)
     if raw.has_warning:  # parser.py:124-130
         warnings.warn(f"Skipping unsupported record: {chr(raw.warn_byte)}", RuntimeWarning, stacklevel=3)
@@ -334,19 +340,6 @@ def _run(path, opts) -> RawResult:
     return nat.build_from_path(p, opts)
 
 
-_PARSE_ERRORS = (nat.E_INDEX_LIST, nat.E_INDEX_BYTES, nat.E_UNICODE)
-
-
-def _input_bytes(path) -> bytes:
-    """The uncompressed input, read as GFAParser would (parser.py:100-112)."""
-    p = str(path)
-    with open(p, "rb") as fh:
-        data = fh.read()
-    if p.endswith(".gz"):
-        data, _ = nat.gunzip(data)
-    return data
-
-
 def export_edge_list(gfa, output="-", *, bidirected: bool = False, device: int = 0) -> None:
     """``gfa2network export GFA --format edge-list [--bidirected] --output PATH`` (cli.py:264-281).
 
@@ -354,34 +347,25 @@ def export_edge_list(gfa, output="-", *, bidirected: bool = False, device: int =
     record keys the reference's parser yields (parser.py:206-341), rendered on the GPU from the
     same parse as the matrix path (``G2N_OUT_EDGE_LIST``).  Failure behaviour follows the
     reference's streaming loop: the output file is opened first, the lines of the records
-    before a failing one are written, then the failure is raised (a malformed record, or the
-    ``u.decode()`` / ``v.decode()`` of a key that is not UTF-8); the unsupported-record warning
-    is emitted as by ``GFAParser``.
+    before a failing one are written, then the failure is raised (a malformed record, the
+    ``u.decode()`` / ``v.decode()`` of a key that is not UTF-8, or a gzip error after the lines
+    gzip returned); the unsupported-record warning is emitted as by ``GFAParser``.
     """
     opts = nat.make_options(bidirected=bidirected, output=nat.OUT_EDGE_LIST, device=device)
     fh = open(output, "wb") if output != "-" else None  # cli.py:266-267: opened before parsing
     try:
         src = gfa
         if not hasattr(gfa, "read") and str(gfa) == "-":
-            src = io.BytesIO(sys.stdin.buffer.read())  # kept: a parse error re-renders its prefix
+            src = io.BytesIO(sys.stdin.buffer.read())  # parser.py:104: sys.stdin.buffer, not gunzipped
         if hasattr(src, "read"):
-            data = src.read()
-            raw = nat.build_from_buffer(data, opts)
+            raw = nat.build_from_buffer(src.read(), opts)
         else:
-            data = None
             raw = nat.build_from_path(str(src), opts)
         if raw.has_warning:  # parser.py:124-130
             warnings.warn(f"Skipping unsupported record: {chr(raw.warn_byte)}", RuntimeWarning, stacklevel=2)
-        first = raw
-        if raw.status in _MALFORMED or (raw.status in _PARSE_ERRORS and raw.err_line >= 0):
-            # the records before the failing line were exported: render the prefix
-            if data is None:
-                data = _input_bytes(gfa)
-            arr = np.frombuffer(data, dtype=np.uint8)
-            k = int(raw.err_line)
-            nl = np.flatnonzero(arr == 0x0A)
-            end = 0 if k == 0 else int(nl[k - 1]) + 1
-            raw = nat.build_from_buffer(arr[:end], opts)
+        # on a failure the text holds the lines the reference wrote before it: the records before
+        # a malformed line, before an undecodable key, or before the gzip error (the lines gzip
+        # returned) — rendered by the native build from the input it already holds
         text = raw.data if raw.format == "text" and raw.data is not None else np.zeros(0, np.uint8)
         if fh is not None:
             fh.write(memoryview(text))
@@ -389,9 +373,7 @@ def export_edge_list(gfa, output="-", *, bidirected: bool = False, device: int =
             sys.stdout.flush()
             sys.stdout.buffer.write(memoryview(text))
             sys.stdout.buffer.flush()
-        if raw.status != nat.OK:  # an undecodable key before the malformed line comes first
-            raise_for_status(raw, np.dtype("bool"), gfa)
-        raise_for_status(first, np.dtype("bool"), gfa)
+        raise_for_status(raw, np.dtype("bool"), gfa)
     finally:
         if fh is not None:
             fh.close()

@@ -87,6 +87,15 @@ static int read_fd(int fd, HostBuf& buf, size_t* len) {
 }
 
 // Input bytes for the staged upload, read straight from the inflated members.
+// bytes of z up to and including its last '\n' (0 if none)
+static size_t whole_lines(const Inflated& z) {
+  for (size_t k = z.parts.size(); k-- > 0;) {
+    const auto* p = (const uint8_t*)memrchr(z.parts[k].p, '\n', z.parts[k].n);
+    if (p) return z.start[k] + (size_t)(p - z.parts[k].p) + 1;
+  }
+  return 0;
+}
+
 static FillFn fill_from(const Inflated& z) {
   return [&z](size_t off, uint8_t* dst, size_t len) {
     size_t k = (size_t)(std::upper_bound(z.start.begin(), z.start.end(), off) - z.start.begin()) - 1;
@@ -236,11 +245,27 @@ int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** 
       int sub = 0;
       std::string msg;
       if (!g2n::gunzip_exact(raw.p, rlen, z, &sub, &msg)) {
-        g2n::HostResult* h = g2n::new_host_result();
-        h->r.status = G2N_E_GZIP;
-        h->r.err_index = sub;
+        // parser.py:114 iterates the lines gzip returned before it raised: those whole lines are
+        // parsed first, so their parse error wins, and their warning precedes the gzip error
+        // (a cast error comes after the loop: the gzip error is first)
+        const size_t cut = g2n::whole_lines(z);
+        g2n_result* pr = nullptr;
+        if (cut) {
+          const int rc2 = g2n::build_host_fill(cut, g2n::fill_from(z), opts, &pr, g2n::now_ms() - t0);
+          if ((rc2 >= G2N_E_MALFORMED_L && rc2 <= G2N_E_INT_TOO_LARGE) || rc2 >= G2N_E_ARG) {
+            g2n::free_later(std::move(z.parts));
+            *out = pr;
+            return rc2;
+          }
+        }
+        g2n::free_later(std::move(z.parts));
+        if (!pr) pr = &g2n::new_host_result()->r;
+        pr->status = G2N_E_GZIP;
+        pr->err_index = sub;
+        pr->err_line = -1;
+        pr->err_value = 0.0;
         g2n::set_last_error(msg);
-        *out = &h->r;
+        *out = pr;
         return G2N_E_GZIP;
       }
     }
@@ -296,6 +321,12 @@ int g2n_gunzip(const void* buf, size_t len, int32_t parallel, void** out, size_t
       std::string msg;
       if (!g2n::gunzip_exact(in, len, z, &s, &msg)) {
         if (sub) *sub = s;
+        // the bytes gzip.py's reader returned before raising
+        auto* o = (uint8_t*)std::malloc(z.total ? z.total : 1);
+        if (!o) return G2N_E_NOMEM;
+        for (size_t k = 0; k < z.parts.size(); k++) std::memcpy(o + z.start[k], z.parts[k].p, z.parts[k].n);
+        *out = o;
+        *out_len = z.total;
         g2n::set_last_error(msg);
         return G2N_E_GZIP;
       }

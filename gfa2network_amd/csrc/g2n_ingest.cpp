@@ -411,11 +411,54 @@ static std::string py_bytes_repr(const uint8_t* b, size_t n) {
   return s;
 }
 
+// Bytes gzip.py's reader has returned for one member's deflate data starting at `dstart` when
+// zlib.error is raised: _GzipReader.read(8192) (io.BufferedReader's refill size) feeds
+// decompress(self._fp.read(8192), 8192) — one inflate(Z_SYNC_FLUSH) with <= 8192 bytes of input
+// and 8192 of output room, the unconsumed tail prepended for the next call — and the output of
+// the call that fails is discarded with it (zlibmodule.c).
+static size_t delivered_before_zlib_error(const uint8_t* in, size_t n, size_t dstart) {
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) return 0;
+  uint8_t buf[8192];
+  size_t p = dstart, delivered = 0;
+  while (p < n) {
+    const size_t take = std::min<size_t>(n - p, sizeof(buf));
+    zs.next_in = const_cast<Bytef*>(in + p);
+    zs.avail_in = (uInt)take;
+    zs.next_out = buf;
+    zs.avail_out = sizeof(buf);
+    const int rc = inflate(&zs, Z_SYNC_FLUSH);
+    if (rc != Z_OK && rc != Z_BUF_ERROR && rc != Z_STREAM_END) break;
+    delivered += sizeof(buf) - zs.avail_out;
+    p += take - zs.avail_in;
+    if (rc == Z_STREAM_END || (rc == Z_BUF_ERROR && zs.avail_in == take)) break;  // no progress
+  }
+  inflateEnd(&zs);
+  return delivered;
+}
+
 bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::string* msg) {
   static const char* kEOF = "Compressed file ended before the end-of-stream marker was reached";
   out = Inflated();
   size_t pos = 0, total = 0;
-  auto fail = [&](int s, const std::string& m) {
+  Grow g;  // the current member's output
+  auto keep = [&](size_t len) {  // the member's first len bytes become a part of the output
+    out.start.push_back(total);
+    total += len;
+    HostBuf b;
+    b.p = g.p;
+    b.n = len;
+    g.p = nullptr;
+    g.n = g.cap = 0;
+    out.parts.push_back(std::move(b));
+  };
+  auto fail = [&](int s, const std::string& m, size_t member_bytes) {
+    // the prefix the reference's line loop saw before the exception: finished members plus
+    // what this member had delivered (out.total; the caller cuts it to whole lines)
+    if (member_bytes) keep(member_bytes);
+    out.start.push_back(total);
+    out.total = total;
     *sub = s;
     *msg = m;
     return false;
@@ -424,17 +467,17 @@ bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::str
     if (pos >= n) break;  // magic == b"": no further member
     const size_t ml = std::min<size_t>(2, n - pos);
     if (ml < 2 || in[pos] != 0x1F || in[pos + 1] != 0x8B)
-      return fail(1, "Not a gzipped file (" + py_bytes_repr(in + pos, ml) + ")");
+      return fail(1, "Not a gzipped file (" + py_bytes_repr(in + pos, ml) + ")", 0);
     pos += 2;
-    if (n - pos < 8) return fail(2, kEOF);
+    if (n - pos < 8) return fail(2, kEOF, 0);
     const uint8_t method = in[pos], flag = in[pos + 1];
     pos += 8;
-    if (method != 8) return fail(1, "Unknown compression method");
+    if (method != 8) return fail(1, "Unknown compression method", 0);
     if (flag & 4) {  // FEXTRA
-      if (n - pos < 2) return fail(2, kEOF);
+      if (n - pos < 2) return fail(2, kEOF, 0);
       const size_t xlen = (size_t)in[pos] | ((size_t)in[pos + 1] << 8);
       pos += 2;
-      if (n - pos < xlen) return fail(2, kEOF);
+      if (n - pos < xlen) return fail(2, kEOF, 0);
       pos += xlen;
     }
     for (int f : {8, 16}) {  // FNAME, FCOMMENT: NUL-terminated, EOF ends them silently
@@ -443,16 +486,17 @@ bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::str
         }
     }
     if (flag & 2) {  // FHCRC
-      if (n - pos < 2) return fail(2, kEOF);
+      if (n - pos < 2) return fail(2, kEOF, 0);
       pos += 2;
     }
-    Grow g;
     z_stream zs;
     memset(&zs, 0, sizeof(zs));
-    if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) return fail(3, "Error -2 while preparing to decompress data");
+    if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) return fail(3, "Error -2 while preparing to decompress data", 0);
+    const size_t dstart = pos;
     size_t fed = pos;
     uLong crc = crc32(0L, Z_NULL, 0);
     bool ended = false;
+    g.n = 0;
     g.reserve((size_t)1 << 22);
     for (;;) {
       if (zs.avail_in == 0) {
@@ -477,13 +521,14 @@ bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::str
       if (rc == Z_OK || rc == Z_BUF_ERROR) continue;
       std::string m = zs.msg ? zs.msg : (rc == Z_DATA_ERROR ? "invalid input data" : "inconsistent stream state");
       inflateEnd(&zs);
-      return fail(3, "Error " + std::to_string(rc) + " while decompressing data: " + m);
+      const size_t d = std::min(g.n, delivered_before_zlib_error(in, n, dstart));
+      return fail(3, "Error " + std::to_string(rc) + " while decompressing data: " + m, d);
     }
     const size_t used_end = (size_t)(zs.next_in - in);
     inflateEnd(&zs);
-    if (!ended) return fail(2, kEOF);
+    if (!ended) return fail(2, kEOF, g.n);  // every byte inflatable from the input was returned
     pos = used_end;
-    if (n - pos < 8) return fail(2, kEOF);
+    if (n - pos < 8) return fail(2, kEOF, g.n);  // the member's data went out before _read_eof
     const uint32_t crc_st = (uint32_t)in[pos] | ((uint32_t)in[pos + 1] << 8) | ((uint32_t)in[pos + 2] << 16) |
                             ((uint32_t)in[pos + 3] << 24);
     const uint32_t isz = (uint32_t)in[pos + 4] | ((uint32_t)in[pos + 5] << 8) | ((uint32_t)in[pos + 6] << 16) |
@@ -492,16 +537,10 @@ bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::str
     if (crc_st != (uint32_t)crc) {
       char b[64];
       snprintf(b, sizeof(b), "CRC check failed 0x%x != 0x%x", crc_st, (uint32_t)crc);
-      return fail(4, b);
+      return fail(4, b, g.n);
     }
-    if (isz != (uint32_t)(g.n & 0xFFFFFFFFu)) return fail(4, "Incorrect length of data produced");
-    out.start.push_back(total);
-    total += g.n;
-    HostBuf b;
-    b.p = g.p;
-    b.n = g.n;
-    g.p = nullptr;
-    out.parts.push_back(std::move(b));
+    if (isz != (uint32_t)(g.n & 0xFFFFFFFFu)) return fail(4, "Incorrect length of data produced", g.n);
+    keep(g.n);
     out.members++;
     while (pos < n && in[pos] == 0) pos++;
   }

@@ -91,7 +91,8 @@ struct Inflated {
 };
 bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out);
 // gzip.open's reader restated (serial, exact errors): false with *sub = 1 BadGzipFile,
-// 2 EOFError, 3 zlib.error, 4 BadGzipFile (CRC / length) and *msg = the exception's message.
+// 2 EOFError, 3 zlib.error, 4 BadGzipFile (CRC / length) and *msg = the exception's message;
+// `out` then holds the bytes the reference's reader returned before raising (not cut to lines).
 bool gunzip_exact(const uint8_t* in, size_t n, Inflated& out, int* sub, std::string* msg);
 
 // convert CLI writers (g2n_writers.cpp)

@@ -60,6 +60,7 @@ struct g2n_context {
   int device = 0;
   int n_cu = 256;  // compute units: persistent launches size their grid from it
   uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
+  uint64_t err_line_off = 0;  // byte offset of the last build's error line (edge-list prefix)
   hipStream_t stream = nullptr;
   std::vector<g2n::DevBuf> bufs;
   g2n::Ctl* ctl = nullptr;    // device
@@ -848,6 +849,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (err_code) {
     R->status = err_code;
     R->err_line = (int64_t)err_line;
+    c->err_line_off = read_dev(c, ls + err_line);
     if (err_code == G2N_E_UNICODE && err_line != warn_line) {
       hipLaunchKernelGGL(k_error_detail, dim3(1), dim3(1), 0, c->stream, in, len, ls, err_line, c->ctl);
       sync_ctl(c);
@@ -964,6 +966,28 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
   b.output = G2N_OUT_COO;
   b.want_node_names = 1;
   const int rc = run_build(c, in, len, &b, R);
+  if (rc >= G2N_E_MALFORMED_L && rc <= G2N_E_INT_TOO_LARGE && R->err_line >= 0) {
+    // the reference's loop wrote the lines of the records before the failing one
+    // (cli.py:270-281): render the prefix [0, start of the failing line) from the same input
+    const g2n_result first = *R;
+    const uint64_t off = c->err_line_off;
+    fill_defaults(R);
+    if (run_edge_list(c, in, off, o, R) == G2N_OK) {  // a key before it that is not UTF-8 comes first
+      R->status = first.status;
+      R->err_line = first.err_line;
+      R->err_index = first.err_index;
+      R->err_value = first.err_value;
+      R->err_detail = first.err_detail;
+      R->err_detail_len = first.err_detail_len;
+      R->n_records_before_error = first.n_records_before_error;
+    }
+    R->has_warning = first.has_warning;
+    R->warn_byte = first.warn_byte;
+    R->warn_line = first.warn_line;
+    R->n_lines = first.n_lines;
+    R->n_records = first.n_records;
+    return R->status;
+  }
   if (rc != G2N_OK) return rc;
   const uint64_t n = (uint64_t)R->nnz, n_names = (uint64_t)R->n_nodes;
   const auto* rows = (const int32_t*)R->rows;
@@ -1084,7 +1108,7 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
   R.names_offsets = nullptr;
   R.rows = R.cols = R.indptr = R.indices = R.data = nullptr;
   if (D.err_detail) R.err_detail = (const uint8_t*)download(c, H->detail, D.err_detail, (size_t)D.err_detail_len);
-  if (D.status == G2N_OK || (D.format == G2N_FMT_TEXT && D.status == G2N_E_UNICODE)) {
+  if (D.status == G2N_OK || D.format == G2N_FMT_TEXT) {  // edge-list text: the lines before a failure too
     if (D.names_blob) {
       const int64_t* offs =
           (const int64_t*)download(c, H->offs, D.names_offsets, (size_t)(D.n_nodes + 1) * sizeof(int64_t));

@@ -171,8 +171,9 @@ void g2n_result_free(g2n_result *res);
  * on host threads (G2N_HOST_THREADS) when the file is a clean member chain, else serially;
  * parallel = 0: always the serial reader.  On success *out (free with g2n_free) holds *out_len
  * bytes and *members the member count.  On failure returns G2N_E_GZIP, *sub = the exception
- * gzip.py raises (1 BadGzipFile, 2 EOFError, 3 zlib.error, 4 BadGzipFile CRC/length) and
- * g2n_last_error() its message. */
+ * gzip.py raises (1 BadGzipFile, 2 EOFError, 3 zlib.error, 4 BadGzipFile CRC/length),
+ * g2n_last_error() its message, and *out / *out_len the bytes gzip.py's reader returned before
+ * raising (io.BufferedReader refills of 8192: what a line loop over gzip.open sees; g2n_free it). */
 int g2n_gunzip(const void *buf, size_t len, int32_t parallel, void **out, size_t *out_len, int32_t *members,
                int32_t *sub);
 void g2n_free(void *p);

@@ -48,6 +48,17 @@ def python_read(blob: bytes):
         return None, e
 
 
+def python_lines_before_error(blob: bytes) -> bytes:
+    """The lines parser.py:114's `for line in fh` sees on gzip.open before the exception."""
+    seen = []
+    try:
+        for line in gzip.GzipFile(fileobj=io.BytesIO(blob)):
+            seen.append(line)
+    except (gzip.BadGzipFile, EOFError, zlib.error):
+        pass
+    return b"".join(seen)
+
+
 def check(blob: bytes, members: int | None = None):
     want, exc = python_read(blob)
     for parallel in (True, False):
@@ -62,6 +73,10 @@ def check(blob: bytes, members: int | None = None):
             f = ei.value
             assert EXC[f.sub] is type(exc), (f.sub, f.message, exc)
             assert f.message == str(exc)
+            # the whole lines of what the reader returned first (the prefix g2n_build_from_path
+            # parses before raising the gzip error)
+            cut = f.prefix.rfind(b"\n") + 1
+            assert f.prefix[:cut] == python_lines_before_error(blob), (f.sub, f.message)
 
 
 T = gfa_text(3000, 1)
@@ -132,3 +147,43 @@ def test_random_member_chains(seed):
     if r.random() < 0.5:
         cut = r.randrange(len(blob))
         check(blob[:cut])
+
+
+def stored_block_headers(m: bytes, hdr_len: int = 10) -> list[int]:
+    """Offsets of the stored-block headers of a level-0 member (RFC 1951 3.2.4: one byte of
+    BFINAL / BTYPE = 00 bits, then LEN, NLEN; the block's bytes follow)."""
+    pos, out = hdr_len, []
+    while True:
+        out.append(pos)
+        final = m[pos] & 1
+        ln = m[pos + 1] | (m[pos + 2] << 8)
+        pos += 5 + ln
+        if final:
+            return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_corrupt_deflate_prefix_follows_8k_refills(seed):
+    """zlib.error mid-member: gzip.py discards the output of the failing decompress call, whose
+    input and output windows follow io.BufferedReader's 8192-byte refills — the prefix the
+    library reports is exactly the lines a line loop saw.  Stored blocks with a broken NLEN
+    ("invalid stored block lengths") put the error at every block of the member in turn;
+    random overwrites of compressed members and truncations add the other error kinds."""
+    r = random.Random(100 + seed)
+    text = gfa_text(r.randint(3000, 9000), seed)
+    m0 = member(text, level=0)
+    n_zlib = 0
+    for at in stored_block_headers(m0):
+        bad = bytearray(m0)
+        bad[at + 3] ^= 0x5A  # NLEN no longer ~LEN
+        n_zlib += python_read(bytes(bad))[1].__class__ is zlib.error
+        check(bytes(bad))
+    assert n_zlib >= 2
+    m = member(text, level=r.choice([1, 6, 9]))
+    for _ in range(12):
+        bad = bytearray(m)
+        at = r.randrange(12, len(bad) - 8)
+        k = r.randint(4, 64)
+        bad[at:at + k] = bytes(r.randrange(256) for _ in range(len(bad[at:at + k])))
+        check(bytes(bad))
+        check(m[:at])  # truncated there
