@@ -836,6 +836,91 @@ __device__ inline bool parse_line(const Src& in, uint64_t len, uint64_t bound, b
   return true;
 }
 
+// Lean decimal-id parse (ParseOpts.rows, not bidirected, no weight tag, no strip) of the two
+// common shapes, in tile-local 32-bit arithmetic straight from the staged tile: an S line
+// "S\t<name>[\t...]" and the L / E / C line link_fast accepts, at most 48 bytes before the '\n'
+// at next - 1 (the next line's start in the same tile).  Same results as parse_line's
+// put_segment / link_fast + int_edge_id path for these lines; false for anything else (the
+// general path then parses the line).
+__device__ inline bool dec_lds(const uint8_t* buf, uint32_t x, uint32_t l, uint64_t* v) {
+  if (l == 0 || l > 10) return false;
+  if (l > 8) {  // 9-10 digits (src_dec's loop)
+    uint64_t y = 0;
+    for (uint32_t j = 0; j < l; j++) {
+      const uint32_t c = buf[x + j];
+      if (c - '0' > 9u || (j == 0 && c == '0')) return false;
+      y = y * 10 + (c - '0');
+    }
+    *v = y;
+    return true;
+  }
+  const uint32_t a = x & ~7u, sh = (x - a) * 8;
+  uint64_t w = *(const uint64_t*)(buf + a) >> sh;
+  if (sh && (x - a) + l > 8) w |= *(const uint64_t*)(buf + a + 8) << (64 - sh);
+  const uint64_t keep = l == 8 ? ~0ull : ((1ull << (8 * l)) - 1);
+  w &= keep;
+  const uint64_t zeros = 0x3030303030303030ull & keep;
+  if ((w & 0xF0F0F0F0F0F0F0F0ull & keep) != zeros ||
+      (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) != 0 ||
+      (w & 0xFF) == '0')
+    return false;
+  const uint64_t d = (w - zeros) << (8 * (8 - l));
+  auto four = [](uint32_t y) {
+    y = ((y << 3) + (y << 1) + (y >> 8)) & 0x00FF00FFu;
+    return ((y << 6) + (y << 5) + (y << 2) + (y >> 16)) & 0xFFFFu;
+  };
+  *v = (uint64_t)(four((uint32_t)d) * 10000u + four((uint32_t)(d >> 32)));
+  return true;
+}
+
+__device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next, uint8_t k,
+                                 uint64_t t0, uint64_t tb, uint64_t eb, const ParseOpts& op, const TouchOut& T,
+                                 IntState& is) {
+  const uint32_t n = next - 1 - so;
+  if (n > 48) return false;
+  const uint32_t q = so >> 4, sh = so & 15;
+  const uint64_t w = (uint64_t)tabm[q] | ((uint64_t)tabm[q + 1] << 16) | ((uint64_t)tabm[q + 2] << 32) |
+                     ((uint64_t)tabm[q + 3] << 48);
+  uint64_t m = (w >> sh) & ((1ull << n) - 1);
+  if (k == kS) {
+    if (!m) return false;  // one field: the general path raises
+    const uint32_t t1 = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const uint32_t t2 = m ? (uint32_t)__builtin_ctzll(m) : n;
+    put_touch(T, tb, t0 + so + t1 + 1, t2 - t1 - 1, 0, 0, false, 1);
+    if (op.tid && !is.fail) {
+      uint64_t v;
+      if (eb != 0 || !dec_lds(buf, so + t1 + 1, t2 - t1 - 1, &v) || v != op.s_base + tb + 1) is.fail = 1;
+    }
+    return true;
+  }
+  if (k != kEdge || __popcll(m) < 5) return false;
+  uint32_t p[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    p[j] = m ? (uint32_t)__builtin_ctzll(m) : n;
+    m &= m - 1;
+  }
+  if (p[2] - p[1] != 2 || p[4] - p[3] != 2) return false;
+  const uint32_t c2 = buf[so + p[1] + 1], c4 = buf[so + p[3] + 1];
+  if ((c2 != '+' && c2 != '-') || (c4 != '+' && c4 != '-')) return false;
+  if (is.fail) return true;
+  uint64_t a, b;
+  if (!dec_lds(buf, so + p[0] + 1, p[1] - p[0] - 1, &a) || !dec_lds(buf, so + p[2] + 1, p[3] - p[2] - 1, &b) ||
+      a > op.n_seg || b > op.n_seg) {  // not an S key: the premise breaks (int_edge_id)
+    is.fail = 1;
+    return true;
+  }
+  const uint64_t o = eb * op.ktrip;
+  op.rows[o] = (int32_t)(a - 1);
+  op.cols[o] = (int32_t)(b - 1);
+  if (op.ktrip >= 2) {
+    op.rows[o + 1] = (int32_t)(b - 1);
+    op.cols[o + 1] = (int32_t)(a - 1);
+  }
+  return true;
+}
+
 struct DeferredLine {  // at most one per tile: the line holding the tile window's last byte
   unsigned long long line;
   unsigned long long start;
@@ -938,6 +1023,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   uint64_t t_run = b.touches, e_run = b.edges;
   unsigned long long unk = ~0ull;
   IntState is;
+  const bool lean_fast = op.rows && !op.bidir && !op.has_wt && !op.strip;
   for (uint32_t w0 = 0; w0 < n_starts; w0 += kTileLines) {
     const uint32_t n_win = n_starts - w0 < kTileLines ? n_starts - w0 : kTileLines;
     __syncthreads();  // `pre` (ranks, or the last window's prefixes) is no longer read
@@ -998,6 +1084,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
         const uint64_t eb = e_run + (pr & 0xFFFF);
         // the line ends where the next one starts; the window's last line: search the staged bytes
         const bool known = j + 1 < n_win;
+        if (lean_fast && known && lean_line(buf, tabm, o, starts[j + 1], k, t0, tb, eb, op, T, is)) continue;
         const uint64_t bound = known ? t0 + starts[j + 1] : w1;
         if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, is)) {
           const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
