@@ -887,7 +887,8 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
     const uint32_t t1 = (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
     const uint32_t t2 = m ? (uint32_t)__builtin_ctzll(m) : n;
-    put_touch(T, tb, t0 + so + t1 + 1, t2 - t1 - 1, 0, 0, false, 1);
+    // no touch descriptor: a lean build that holds its premise derives the names (k_names_dec);
+    // one that breaks it re-parses in full
     if (op.tid && !is.fail) {
       uint64_t v;
       if (eb != 0 || !dec_lds(buf, so + t1 + 1, t2 - t1 - 1, &v) || v != op.s_base + tb + 1) is.fail = 1;
@@ -1591,6 +1592,47 @@ __global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, 
     const uint32_t ol = T.olen[t];
     blob[o + nl] = ':';
     for (uint32_t j = 0; j < ol; j++) blob[o + nl + 1 + j] = (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + j];
+  }
+}
+
+// Names of a decimal-id build (the premise held: S line k names "k+1", S lines first): node id's
+// key is str(k + 1) (bidirected: id = 2k + [ori == '-'], key str(k + 1) + ":+" / ":-"), so the
+// names blob and its offsets are arithmetic — no key lengths, scan or gathers from the input.
+__device__ __host__ inline uint32_t dec_digits(uint64_t v) {
+  uint32_t d = 1;
+  for (uint64_t p = 10; v >= p && d < 20; p *= 10) d++;
+  return d;
+}
+__device__ __host__ inline uint64_t dec_digits_upto(uint64_t v) {  // sum of dec_digits(k), k = 1..v
+  uint64_t s = 0, lo = 1;
+  for (uint32_t d = 1; lo <= v && d < 20; d++, lo *= 10) {
+    const uint64_t hi = lo * 10 - 1, top = v < hi ? v : hi;
+    s += (top - lo + 1) * d;
+  }
+  return s;
+}
+__device__ __host__ inline uint64_t dec_name_off(uint64_t id, int bidir) {  // offset of node id's key
+  if (!bidir) return dec_digits_upto(id);
+  const uint64_t k = id >> 1;
+  return 2 * (dec_digits_upto(k) + 2 * k) + ((id & 1) ? dec_digits(k + 1) + 2 : 0);
+}
+
+__global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir, int64_t* __restrict__ offs,
+                                                    uint8_t* __restrict__ blob) {
+  const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (id > n_nodes) return;
+  const uint64_t o = dec_name_off(id, bidir);
+  offs[id] = (int64_t)o;
+  if (id == n_nodes) return;
+  uint32_t v = (uint32_t)((bidir ? id >> 1 : id) + 1);  // node ids < 2^31
+  const uint32_t d = dec_digits(v);
+  for (uint32_t j = d; j-- > 0;) {
+    blob[o + j] = (uint8_t)('0' + v % 10u);
+    v /= 10u;
+  }
+  if (bidir) {
+    blob[o + d] = ':';
+    blob[o + d + 1] = (id & 1) ? '-' : '+';
   }
 }
 

@@ -223,7 +223,8 @@ def test_s_first_fast_path_taken_and_exact(gpu, oracle_lib, long_names, interlea
     data = _canonical_gfa(7 + long_names, 3000, 12000, long_names, interleave)
     for mode in MODES:
         st, ph = _phases(data, **mode)
-        assert st == 0 and "ids_fast" in ph and "ids_general" not in ph, (mode, sorted(ph))
+        # decimal names: the lean parse needs no dictionary phase at all; long names: the S-first table
+        assert st == 0 and "ids_general" not in ph and ("ids_fast" in ph or not long_names), (mode, sorted(ph))
         for dtype, wt in (("float64", "RC"), ("int8", None), ("float32", "RC")):
             a = outcome(gpu_run(data, mode, dtype, wt))
             b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
