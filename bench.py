@@ -516,11 +516,10 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
     k_trip = tpe if tpe == 4 else (1 if directed_csr else 2)
     if phase == "tiles":  # K1 reads every byte once; 48 B of counts per 32 KiB tile
         return in_bytes, "B_in (K1: every input byte read once)"
-    if phase == "parse" and lean:  # decimal ids: S touch descriptors, COO coordinates (+ weights) per edge;
-        # the lean parse writes no line starts / kinds (k_tile_parse skips them when op.rows is set)
-        per_s, per_e = 13 + d_o, 4 * k_trip * 2 + (8 if weighted else 0)
-        return (in_bytes + per_s * n_s * tps + per_e * n_edges,
-                f"B_in + {per_s} B/S touch + {per_e} B/edge (lean decimal-id parse)")
+    if phase == "parse" and lean:  # decimal ids: the COO coordinates (+ weights) per edge; the lean parse
+        # writes no line starts / kinds and no S touch descriptors (names by arithmetic, k_names_dec)
+        per_e = 4 * k_trip * 2 + (8 if weighted else 0)
+        return in_bytes + per_e * n_edges, f"B_in + {per_e} B/edge (lean decimal-id parse)"
     if phase == "parse":  # every input byte once; line start + kind per line; descriptors per touch / edge
         per_t, per_e = 13 + d_o, 12
         return (in_bytes + 9 * n_lines + per_t * n_t + per_e * n_edges,
