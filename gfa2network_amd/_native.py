@@ -42,7 +42,6 @@ EXPORTED = [
 
 # options.reserved[1] test flags (include/g2n.h): the builds of this process take normally-rare
 # paths when a test sets them; 0 in every real use
-TEST_NO_LOOKBACK = 1     # MAX-SYM bucket finish: every bucket staged + fix-up kernel
 TEST_NO_BUCKETS = 2      # MAX-SYM through the general row-sum path
 TEST_NO_LEAN = 4         # decimal ids without the lean parse (ids per touch, then k_triplets)
 TEST_DICT_HASH = 8       # no decimal ids: the hash dictionary tiers

@@ -38,11 +38,10 @@ enum Slot {
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
-  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_LBST, S_SCANST, S_RBOUND, S_NSLOTS
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
-constexpr uint32_t kTestNoLookback = 1;     // k_sym_finish: every bucket staged + k_sym_fixup
 constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-sum path
 constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean parse (ids per touch, k_triplets)
 constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
@@ -329,29 +328,21 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   auto* indices = dget<int32_t>(c, S_INDICES, n_el);
   T* odata = dget<T>(c, S_ODATA, n_el);
   auto* btot = dget<uint32_t>(c, S_BTOT, n_bk);
-  auto* fixq = dget<uint32_t>(c, S_MCNT, n_bk);
-  auto* status = dget<unsigned long long>(c, S_LBST, n_bk);
   uint2* tmp = el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1;  // the pass-1 output is dead by now
-  G2N_HIP(hipMemsetAsync(status, 0, n_bk * sizeof(unsigned long long), c->stream));
-  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, 2 * sizeof(unsigned long long), c->stream));
-  const uint32_t spin = (c->test_flags & kTestNoLookback) ? 0u : kSpinLimit;
+  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices,
-                       odata, c->ctl, spin);
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tmp, indptr, c->ctl);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, status, tmp, fixq, indptr, indices,
-                       odata, c->ctl, spin);
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tmp, indptr, c->ctl);
+  auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
+  scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
-  if (c->h_ctl->n_fix) {  // buckets that gave up waiting on their predecessors
-    auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
-    scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
-    hipLaunchKernelGGL((k_sym_fixup<T>), dim3((unsigned)c->h_ctl->n_fix), dim3(kTPB), 0, c->stream,
-                       (const uint32_t*)fixq, (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff,
-                       (uint32_t)low, n_rows, (T)1, (const uint2*)tmp, indptr, indices, odata);
-  }
+  hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, (const uint32_t*)bst,
+                     (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint2*)tmp,
+                     indptr, indices, odata);
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
   R->nnz = (int64_t)read_dev(c, indptr + n_rows);

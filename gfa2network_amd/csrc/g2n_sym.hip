@@ -10,17 +10,18 @@
 // partition need not be stable.
 //
 //   P1 (one or two passes, MSD): elements are partitioned by the high bits of their row into
-//      buckets of 2^low rows — per block, a 16-byte-coalesced load of 4096 elements, an LDS
-//      histogram (written to a digit-major count matrix), a device scan of that matrix
-//      (g2n_scan.hip), then the same block re-ranks its elements with LDS atomics, stages them
-//      in LDS in digit order and writes each digit's run contiguously.  Pass 1 reads the COO
-//      coordinates themselves (both sides generated on the fly); pass 2 works inside each
-//      pass-1 group, blocks mapped to (group, chunk) on the device.
-//   F  one block per bucket (<= kSymCap elements): count rows in LDS, scatter by row, sort each
+//      buckets of 2^low rows — per 1024-thread block of 65536 elements, an LDS histogram
+//      (written to a digit-major count matrix), a device scan of that matrix (g2n_scan.hip),
+//      then the same block re-ranks each 8192-element sub-tile with per-digit cursors in LDS and
+//      writes each digit's run contiguously.  Pass 1 reads the COO coordinates themselves (both
+//      sides generated on the fly); pass 2 works inside each pass-1 group, blocks mapped to
+//      (group, chunk) on the device.  The SUM CSR (coo.tocsr of an unweighted undirected build)
+//      and a sharded rank's row slice (pair streams, row base) use the same partition.
+//   F1 one block per bucket (<= kSymCap elements): count rows in LDS, scatter by row, sort each
 //      row (registers, or Shell sort for long rows), merge the two sides per column, stage the
-//      merged entries in LDS; the bucket's CSR offset comes from a decoupled look-back over the
-//      buckets' entry counts (bucket order = ticket order), so indptr / indices / data are
-//      written once, at their final place, with coalesced stores.
+//      merged entries in LDS and write them, coalesced, at the bucket's input offset;
+//   F2 after a scan of the buckets' entry counts, one block per bucket copies them to their CSR
+//      place (indices, data) and rebases the bucket's indptr.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -334,80 +335,21 @@ __device__ inline void sym_sort_row(uint32_t* seg, uint32_t n) {
   }
 }
 
-// One block per bucket of 2^low <= 256 rows; the bucket's CSR offset comes from a decoupled
-// look-back over the buckets' entry counts in blockIdx order.  The order needs no atomic ticket
-// (a ticket on ONE counter serializes at ~11 ns per block — 2.2 ms for C4's 195K buckets,
-// tools/microbench/dispatch.hip) because the look-back is BOUNDED: a block whose predecessors do
-// not publish within kSpinLimit polls (a dispatch order that is not by blockIdx, another process
-// holding the CUs) gives up waiting, stages its merged entries in `tmp` at its input offset, keeps
-// its rows' local offsets in indptr and queues itself; k_sym_fixup then moves the queued buckets
-// once the host has scanned btot.  Every block therefore finishes: no order assumption is needed
-// for progress, only for speed.  A bucket over kSymCap elements sets ctl->bucket_overflow (the
-// host then takes the general path).
-//
-constexpr uint32_t kSpinLimit = 1u << 14;
-
-// look-back of bucket b with aggregate agg, by the whole block (256 predecessors per probe):
-// true and *excl = the exclusive prefix, or false when a predecessor did not publish within the
-// spin budget.  Block-uniform result; every thread calls it.
-__device__ inline bool lookback_bounded(unsigned long long* __restrict__ status, uint64_t b, unsigned long long agg,
-                                        unsigned long long* excl_out, uint32_t spin_limit, unsigned long long* red64,
-                                        uint32_t* redf) {
-  if (b == 0) {
-    if (threadIdx.x == 0) status_store(&status[0], kStInc | agg);
-    *excl_out = 0;
-    return true;
-  }
-  if (threadIdx.x == 0) status_store(&status[b], kStAgg | agg);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long excl = 0;
-  int64_t w = (int64_t)b - 1;
-  uint32_t spins = 0;
-  while (true) {
-    const int64_t q = w - (int64_t)threadIdx.x;
-    unsigned long long st = q >= 0 ? status_load(&status[q]) : kStInc;
-    bool gave_up = false;
-    while (true) {  // until every thread of the block sees a published word
-      const uint32_t pending = __syncthreads_or((st >> 62) == 0);
-      if (!pending) break;
-      if (++spins > spin_limit) {
-        gave_up = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      if ((st >> 62) == 0) st = status_load(&status[q]);
-    }
-    if (gave_up) return false;
-    // closest predecessor with an inclusive prefix: the lowest thread index holding one
-    const unsigned long long inc = __ballot((st >> 62) == 2);
-    if (lane == 0) redf[wid] = inc ? (uint32_t)(wid * 64 + __builtin_ctzll(inc)) : 0xFFFFFFFFu;
-    __syncthreads();
-    uint32_t stop = 0xFFFFFFFFu;
-    for (int k = 0; k < kTPB / 64; k++) stop = min(stop, redf[k]);
-    unsigned long long v = threadIdx.x <= stop ? (st & kStVal) : 0ull;
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red64[wid] = v;
-    __syncthreads();
-    for (int k = 0; k < kTPB / 64; k++) excl += red64[k];
-    __syncthreads();
-    if (stop != 0xFFFFFFFFu) break;
-    w -= kTPB;
-  }
-  if (threadIdx.x == 0) status_store(&status[b], kStInc | (excl + agg));
-  *excl_out = excl;
-  return true;
-}
-
+// One block per bucket of 2^low <= 256 rows.  F1 (k_sym_finish) merges the bucket and writes its
+// entries, coalesced through LDS, at the bucket's INPUT offset in `tmp` (a bucket's output never
+// outgrows its input), its rows' local offsets in indptr and its entry count in btot; after one
+// scan of btot, F2 (k_sym_place) copies each bucket to its CSR place and rebases its indptr.
+// (A single kernel that found each bucket's offset by a look-back over its predecessors in block
+// order measured 4.32 ms on C4 against 3.94 ms for F1 + scan + F2: the cross-XCD status polling
+// costs more than the extra 4.6 GB of staging traffic.)  A bucket over kSymCap elements sets
+// ctl->bucket_overflow (the host then takes the general path).
 constexpr uint32_t kShortRow = 16;
 constexpr uint32_t kStagedSkip = 0xFFFFFFFFu;
 
 template <class T, bool kSum>
 __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
-                                                     unsigned long long* __restrict__ status, uint2* __restrict__ tmp,
-                                                     uint32_t* __restrict__ fixq, int32_t* __restrict__ indptr,
-                                                     int32_t* __restrict__ indices, T* __restrict__ data, Ctl* ctl,
-                                                     uint32_t spin_limit) {
+                                                     uint2* __restrict__ tmp, int32_t* __restrict__ indptr, Ctl* ctl) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
   __shared__ uint32_t cnt[kTPB];
@@ -416,11 +358,10 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   const uint64_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
   const bool over = n > kSymCap;  // block-uniform
-  if (over) {  // the build's sums go through the general path; successors must not wait on b
+  if (over) {  // the build's sums go through the general path
     if (threadIdx.x == 0) {
       ctl->bucket_overflow = 1;
       btot[b] = 0;
-      status_store(&status[b], kStAgg);
     }
     return;
   }
@@ -528,31 +469,13 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   const uint32_t m = !live ? 0u : (shortrow ? short_merge(none, false) : long_merge(none));
   uint32_t off;
   const uint32_t tot = block_excl_scan_u32(m, &off, red);
-  __shared__ unsigned long long red64[kTPB / 64];
-  unsigned long long base = 0;
-  const bool ok = spin_limit && lookback_bounded(status, b, tot, &base, spin_limit, red64, red);
-  if (threadIdx.x == 0) {
-    btot[b] = tot;
-    if (!ok) fixq[atomicAdd(&ctl->n_fix, 1ull)] = (uint32_t)b;
-  }
-  if (!ok) {  // staged at the bucket's input offset for k_sym_fixup; indptr holds local offsets
-    if (live) {
-      indptr[row] = (int32_t)off;
-      if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
-      auto put = [&](uint32_t j, uint32_t c, uint32_t kk) { tmp[e0 + off + j] = make_uint2(c, kk); };
-      if (shortrow) short_merge(put, true);
-      else long_merge(put);
-    }
-    return;
-  }
+  if (threadIdx.x == 0) btot[b] = tot;
+  uint2* out = tmp + e0;  // tot <= n: the bucket's staged entries stay inside its input range
   if (live) {
-    indptr[row] = (int32_t)(base + off);
-    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(base + off + m);
-    if (!shortrow)  // straight to HBM, before the staging below reuses the segments
-      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
-        indices[base + off + j] = (int32_t)c;
-        data[base + off + j] = sum_copies<T>(one, kk);
-      });
+    indptr[row] = (int32_t)off;  // local; k_sym_place adds the bucket's offset
+    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
+    if (!shortrow)  // straight out, before the staging below reuses the segments
+      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { out[off + j] = make_uint2(c, kk); });
   }
   __syncthreads();
   if (live) {
@@ -568,21 +491,17 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
     const uint32_t c = seg[i];
-    if (c != kStagedSkip) {
-      indices[base + i] = (int32_t)c;
-      data[base + i] = sum_copies<T>(one, ocnt[i]);
-    }
+    if (c != kStagedSkip) out[i] = make_uint2(c, ocnt[i]);
   }
 }
 
-// Buckets whose look-back gave up: their staged entries to the final place (boff = scan of btot).
+// F2: bucket b's staged entries to their CSR place (boff = exclusive scan of btot), indptr rebased.
 template <class T>
-__global__ void __launch_bounds__(kTPB) k_sym_fixup(const uint32_t* __restrict__ fixq, const uint32_t* __restrict__ bstart,
-                                                    const uint32_t* __restrict__ btot, const uint32_t* __restrict__ boff,
-                                                    uint32_t low, uint64_t n_rows, T one, const uint2* __restrict__ tmp,
-                                                    int32_t* __restrict__ indptr, int32_t* __restrict__ indices,
-                                                    T* __restrict__ data) {
-  const uint32_t b = fixq[blockIdx.x];
+__global__ void __launch_bounds__(kTPB) k_sym_place(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ btot,
+                                                    const uint32_t* __restrict__ boff, uint32_t low, uint64_t n_rows,
+                                                    T one, const uint2* __restrict__ tmp, int32_t* __restrict__ indptr,
+                                                    int32_t* __restrict__ indices, T* __restrict__ data) {
+  const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
   for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
     const uint2 x = tmp[e0 + i];

@@ -92,8 +92,7 @@ typedef struct g2n_options {
   int32_t device;              /* HIP device ordinal, default 0 */
   int32_t reserved[6];         /* [0]: unsupported records skipped silently (an earlier shard of a
                                   sharded build warned already);
-                                  [1]: test flags (normally rare paths, same results): 1 = MAX-SYM
-                                  bucket finish without its look-back, 2 = MAX-SYM / SUM CSR through
+                                  [1]: test flags (normally rare paths, same results): 2 = MAX-SYM / SUM CSR through
                                   the general row sums, 4 = decimal ids without the lean parse,
                                   8 = hash dictionary, 16 = general dictionary rounds;
                                   [2], [3], [4] bit 0: sharded decimal-id build — this byte range's
