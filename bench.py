@@ -497,7 +497,7 @@ class _DevBytes:
 
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
     "tiles": "g2n::k_tile_count",
-    "parse": "g2n::k_tile_parse",
+    "parse": "g2n::k_tile_parse<true>",  # the tile-local lean parse (decimal ids, no K1); <false> after K1
     "insert_claim": "g2n::k_insert_round<0>",
     "insert_lookup": "g2n::k_lookup_fast<2>",
     "triplets": "g2n::k_triplets<double>",

@@ -90,6 +90,17 @@ struct ParseOpts {
   int32_t* rows;
   int32_t* cols;
   uint32_t ktrip;
+  // tile-local lean parse (no K1): tile t's COO goes to rows / cols from t * tile_pad * ktrip,
+  // its counts to TileCnt and its premise evidence to TileLean; 0 = positions from K1's bases
+  uint32_t tile_pad;
+};
+
+// per-tile evidence of the decimal-id premise in a tile-local parse: every S line's name value
+// minus (its S index within the tile + 1), min and max (equal, = the S lines before the tile, when
+// the premise holds); the largest edge-key value
+struct TileLean {
+  long long dmin, dmax;
+  unsigned long long vmax;
 };
 
 struct TouchOut {

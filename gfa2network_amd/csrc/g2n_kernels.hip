@@ -661,9 +661,23 @@ __device__ inline bool src_dec(const Src& in, uint64_t o, uint32_t l, uint64_t* 
   return true;
 }
 
-// Decimal-id premise state of one thread: fail = a premise broke.
+// Decimal-id premise state of one thread: fail = a premise broke; in a tile-local parse the
+// S-line evidence (value - tile-local index - 1, min / max) and the largest edge-key value, checked
+// against the tile bases afterwards (k_tile_lean_check)
+constexpr int32_t kNoS = (int32_t)0x80000000;  // IntState.dref: no S line seen yet
 struct IntState {
   uint32_t fail = 0;
+  uint32_t vmax = 0;    // tile-local: largest edge-key value (< 2^31 by the parse's bound)
+  int32_t dref = kNoS;  // tile-local: value - (tile-local S index + 1), the same for every S line
+  __device__ void s_name(const ParseOpts& op, uint64_t v, uint64_t tb) {  // S touch tb names v
+    if (op.tile_pad) {
+      const int32_t d = (int32_t)((int64_t)v - (int64_t)(tb + 1));  // node ids < 2^31, tb < 2^16
+      if (v > 0x7FFFFFFFull || (dref != kNoS && d != dref)) fail = 1;
+      dref = d;
+    } else if (v != op.s_base + tb + 1) {
+      fail = 1;
+    }
+  }
 };
 
 // an edge touch's node id from its bytes, or false (no S key: the premise fails)
@@ -671,6 +685,7 @@ __device__ inline bool int_edge_id(const Src& in, const ParseOpts& op, uint64_t 
                                    uint32_t ol, uint32_t* id, IntState& is) {
   uint64_t v;
   if (!src_dec(in, no, nl, &v) || v < 1 || v > op.n_seg) return false;
+  is.vmax = (uint32_t)v > is.vmax ? (uint32_t)v : is.vmax;
   *id = (uint32_t)(v - 1);
   if (op.bidir) {
     const uint32_t oc = (oo & kConstFlag) ? (uint32_t)(oo & 0xFF) : (ol ? (uint32_t)in[oo] : 0u);
@@ -684,7 +699,8 @@ __device__ inline bool int_edge_id(const Src& in, const ParseOpts& op, uint64_t 
 __device__ inline void put_segment(const Src& in, const ParseOpts& op, const TouchOut& T, uint64_t tb, uint64_t eb,
                                    uint64_t ns, uint64_t ne, IntState& is) {
   const uint32_t nl = (uint32_t)(ne - ns);
-  if (!op.bidir) {
+  if (op.tile_pad) {  // tile-local lean parse: no touch descriptors (tb is tile-local)
+  } else if (!op.bidir) {
     put_touch(T, tb, ns, nl, 0, 0, false, 1);
   } else {
     put_touch(T, tb, ns, nl, kConstFlag | '+', 1, true, 1);
@@ -692,9 +708,9 @@ __device__ inline void put_segment(const Src& in, const ParseOpts& op, const Tou
   }
   if (op.tid && !is.fail) {  // no edge line before it (eb = 0), so S touch tb is node tb: its name
                               // must be str(k + 1), k = tb / tps = the S lines before it
-    uint64_t v;
-    const uint64_t line = op.s_base + (op.bidir ? tb >> 1 : tb);  // s_base: S lines of earlier ranges
-    if (eb != 0 || !src_dec(in, ns, nl, &v) || v != line + 1) is.fail = 1;
+    uint64_t v;  // (s_base: S lines of earlier ranges)
+    if (eb != 0 || !src_dec(in, ns, nl, &v)) is.fail = 1;
+    else is.s_name(op, v, op.bidir ? tb >> 1 : tb);
   }
 }
 
@@ -723,6 +739,7 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
   }
   if (op.rows) {  // lean: ids straight into the COO coordinates (k_triplets' layout)
     if (op.has_wt) E.w[eb] = w;
+    if (op.tile_pad && eb >= op.tile_pad) is.fail = 1;  // the tile's slot is full: give up
     if (is.fail) return;
     uint32_t a, b, c = 0, d = 0;
     bool ok = int_edge_id(in, op, L.uo, L.ul, L.ouo, L.oul, &a, is) && int_edge_id(in, op, L.vo, L.vl, L.ovo, L.ovl, &b, is);
@@ -733,7 +750,7 @@ __device__ inline void parse_edge(const Src& in, uint64_t i, uint64_t s, uint64_
       is.fail = 1;
       return;
     }
-    const uint64_t o = eb * op.ktrip;
+    const uint64_t o = ((op.tile_pad ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
     op.rows[o] = (int32_t)a;
     op.cols[o] = (int32_t)b;
     if (op.ktrip >= 2) {
@@ -891,7 +908,8 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
     // one that breaks it re-parses in full
     if (op.tid && !is.fail) {
       uint64_t v;
-      if (eb != 0 || !dec_lds(buf, so + t1 + 1, t2 - t1 - 1, &v) || v != op.s_base + tb + 1) is.fail = 1;
+      if (eb != 0 || !dec_lds(buf, so + t1 + 1, t2 - t1 - 1, &v)) is.fail = 1;
+      else is.s_name(op, v, tb);
     }
     return true;
   }
@@ -905,6 +923,7 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
   if (p[2] - p[1] != 2 || p[4] - p[3] != 2) return false;
   const uint32_t c2 = buf[so + p[1] + 1], c4 = buf[so + p[3] + 1];
   if ((c2 != '+' && c2 != '-') || (c4 != '+' && c4 != '-')) return false;
+  if (op.tile_pad && eb >= op.tile_pad) is.fail = 1;  // the tile's slot is full: give up
   if (is.fail) return true;
   uint64_t a, b;
   if (!dec_lds(buf, so + p[0] + 1, p[1] - p[0] - 1, &a) || !dec_lds(buf, so + p[2] + 1, p[3] - p[2] - 1, &b) ||
@@ -912,7 +931,9 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
     is.fail = 1;
     return true;
   }
-  const uint64_t o = eb * op.ktrip;
+  const uint32_t vm = (uint32_t)(a > b ? a : b);
+  is.vmax = vm > is.vmax ? vm : is.vmax;
+  const uint64_t o = ((op.tile_pad ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
   op.rows[o] = (int32_t)(a - 1);
   op.cols[o] = (int32_t)(b - 1);
   if (op.ktrip >= 2) {
@@ -942,12 +963,16 @@ constexpr uint32_t kTileLines = kTileChunks;            // line starts per windo
 constexpr uint32_t kLinesPer = kTileLines / kTPB;       // lines classified per thread
 static_assert(kChunkIters % 4 == 0 && kTile <= 32768, "tile layout: per-tile counts fit 16 bits");
 
+// kLocal: the tile-local lean parse (ParseOpts.tile_pad; lean, not bidirected, no weight tag, no
+// strip — fixed at compile time, so that instance carries none of the other paths' code)
+template <bool kLocal>
 __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__ in, uint64_t len,
                                                      const TileCnt* __restrict__ base, uint32_t tps, uint32_t tpe,
                                                      ParseOpts op, uint64_t* __restrict__ ls,
                                                      uint8_t* __restrict__ kind, TouchOut T, EdgeOut E, Ctl* ctl,
                                                      uint64_t* __restrict__ worklist,
-                                                     DeferredLine* __restrict__ deferred, uint64_t n_tiles) {
+                                                     DeferredLine* __restrict__ deferred, uint64_t n_tiles,
+                                                     TileCnt* __restrict__ tcnt_out, TileLean* __restrict__ tlean) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
   __shared__ __attribute__((aligned(16))) uint16_t starts[kTileLines];
   __shared__ __attribute__((aligned(16))) uint32_t pre[kTileChunks];  // chunk ranks, then line prefixes
@@ -963,7 +988,16 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     R.store(buf);
   }
   const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
-  const TileCnt b = base[tile];
+  constexpr bool local = kLocal;  // tile-local lean parse: no bases (no K1); counts come out
+  if constexpr (kLocal) {
+    op.bidir = op.keep = op.strip = op.has_wt = 0;
+    tps = 1;
+    tpe = 2;
+    __builtin_assume(op.rows != nullptr && op.tile_pad != 0);
+  } else {
+    op.tile_pad = 0;
+  }
+  const TileCnt b = local ? TileCnt{} : base[tile];
   __syncthreads();
   for (uint32_t c = threadIdx.x; c < kMaskChunks; c += kTPB) {  // the tile's tab bitmap (bytes past len: 0)
     uint32_t m = 0;
@@ -980,6 +1014,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   L.tm_lim = t0 + kTile + kTileHalo;
   // (1) start masks of this thread's chunks (kept), counts -> ranks
   uint32_t stm[kChunkIters / 2];
+  uint32_t n_nl = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kChunkIters; j++) {
     const uint32_t c = j * kTPB + threadIdx.x;
@@ -988,6 +1023,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     if (j & 1) stm[j >> 1] |= st << 16;
     else stm[j >> 1] = st;
     pre[c] = (uint32_t)__popc(st);
+    if constexpr (kLocal) n_nl += (uint32_t)__popc(m);
   }
   __syncthreads();
   uint32_t n_starts;
@@ -1021,7 +1057,8 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   uint32_t rank[kChunkIters];
 #pragma unroll
   for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = pre[j * kTPB + threadIdx.x];
-  uint64_t t_run = b.touches, e_run = b.edges;
+  uint64_t t_run = b.touches, e_run = b.edges, s_run = 0;
+  uint32_t n_po = 0;
   unsigned long long unk = ~0ull;
   IntState is;
   const bool lean_fast = op.rows && !op.bidir && !op.has_wt && !op.strip;
@@ -1057,6 +1094,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       kk[q] = k;
       cs += k == kS;
       ce += k == kEdge;
+      if constexpr (kLocal) n_po += k == kPO;
     }
     uint32_t ex;
     const uint32_t tot = block_excl_scan_u32((cs << 16) | ce, &ex, red);
@@ -1088,17 +1126,85 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
         if (lean_fast && known && lean_line(buf, tabm, o, starts[j + 1], k, t0, tb, eb, op, T, is)) continue;
         const uint64_t bound = known ? t0 + starts[j + 1] : w1;
         if (!parse_line(L, len, bound, known, i, k, p, tb, eb, op, T, E, ctl, worklist, is)) {
-          const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
-          if (d < n_tiles) deferred[d] = DeferredLine{i, p, (uint32_t)tb, (uint32_t)eb, k, 0};
+          if (local) {  // no global positions for a deferred line: the tile-local parse gives up
+            is.fail = 1;
+          } else {
+            const unsigned long long d = atomicAdd(&ctl->n_deferred, 1ull);
+            if (d < n_tiles) deferred[d] = DeferredLine{i, p, (uint32_t)tb, (uint32_t)eb, k, 0};
+          }
         }
       }
     }
     t_run += (uint64_t)(tot >> 16) * tps + (uint64_t)(tot & 0xFFFF) * tpe;
     e_run += tot & 0xFFFF;
+    s_run += tot >> 16;
   }
   unk = wave_reduce_min(unk);
   if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
+  if constexpr (kLocal) {  // the tile's counts (K1's) and its premise evidence
+    if (e_run > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
+    uint32_t vm = is.vmax;
+    int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
+    for (int o = 32; o > 0; o >>= 1) {
+      vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
+      dmn = min(dmn, (int32_t)__shfl_xor(dmn, o, 64));
+      dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
+    }
+    __shared__ uint32_t rv[kTPB / 64];
+    __shared__ int32_t rmn[kTPB / 64], rmx[kTPB / 64];
+    if ((threadIdx.x & 63) == 0) {
+      rv[threadIdx.x >> 6] = vm;
+      rmn[threadIdx.x >> 6] = dmn;
+      rmx[threadIdx.x >> 6] = dmx;
+    }
+    const uint32_t nlpo = block_sum(n_nl | (n_po << 16), red);  // per-tile counts < 2^16 (barriers)
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kTPB / 64; w++) {
+        vm = max(vm, rv[w]);
+        dmn = min(dmn, rmn[w]);
+        dmx = max(dmx, rmx[w]);
+      }
+      TileCnt c;
+      c.nl = nlpo & 0xFFFF;
+      c.lines = n_starts;
+      c.segs = s_run;
+      c.edges = e_run;
+      c.touches = t_run;
+      c.recs = s_run + e_run + (nlpo >> 16);
+      tcnt_out[tile] = c;
+      tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
+    }
+  }
   if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+}
+
+// Tile-local lean parse, afterwards: tile t's S lines must name (S lines before t) + their index
+// + 1 and no edge may precede them; every edge key at most the file's S count.
+__global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restrict__ cnt,
+                                                          const TileCnt* __restrict__ tbase,
+                                                          const TileLean* __restrict__ tlean, uint64_t n_tiles,
+                                                          uint64_t n_seg, Ctl* ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t >= n_tiles) return;
+  const TileLean e = tlean[t];
+  bool bad = e.vmax > n_seg;
+  if (cnt[t].segs)
+    bad |= tbase[t].edges != 0 || e.dmin != e.dmax || e.dmin != (long long)tbase[t].segs;
+  if (bad) ctl->int_fail = 1;
+}
+
+// Tile-local lean parse, last: each tile's COO slot to its stream-order place.
+__global__ void __launch_bounds__(kTPB) k_tile_compact(const int32_t* __restrict__ rows_p,
+                                                       const int32_t* __restrict__ cols_p, uint32_t pad,
+                                                       uint32_t ktrip, const TileCnt* __restrict__ cnt,
+                                                       const TileCnt* __restrict__ tbase, int32_t* __restrict__ rows,
+                                                       int32_t* __restrict__ cols) {
+  const uint64_t t = blockIdx.x;
+  const uint64_t n = cnt[t].edges * ktrip, src = t * (uint64_t)pad * ktrip, dst = tbase[t].edges * ktrip;
+  for (uint64_t i = threadIdx.x; i < n; i += kTPB) {
+    rows[dst + i] = rows_p[src + i];
+    cols[dst + i] = cols_p[src + i];
+  }
 }
 
 // Lines whose fields run past their tile's staged window: parsed from global memory.

@@ -38,7 +38,7 @@ enum Slot {
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
-  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_NSLOTS
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -46,6 +46,7 @@ constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-s
 constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean parse (ids per touch, k_triplets)
 constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
 constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast path: the general rounds
+constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bases) instead of tile-local
 
 
 struct DevBuf {
@@ -682,6 +683,63 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
   return true;  // no S line seen yet (long header lines): try
 }
 
+// The lean decimal-id parse in one pass over the input, without K1: every tile parses with
+// tile-local positions, writes its COO to a slot of kTileEdgeCap edges and its own counts
+// (k_tile_parse with ParseOpts.tile_pad); one scan of those counts gives the tile bases, a check
+// confirms the premise across tiles (each tile's S names continue the S lines before it, no edge
+// precedes an S line, every edge key names an S line), and the slots are compacted into the
+// stream-order COO (S_ROWS / S_COLS, sized n_edges * ktrip as run_build will ask).  False when
+// anything breaks the premise or needs the full parse (errors, warnings, deferred lines, a full
+// slot): the caller then runs K1 and the classic parse, as if this had not run.
+constexpr uint32_t kTileEdgeCap = 2736;  // > 32 KiB / 12 B: a lean edge line is at least 12 bytes
+
+static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
+                             TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out) {
+  auto* rows_p = dget<int32_t>(c, S_ROWSP, n_tiles * kTileEdgeCap * ktrip);
+  auto* cols_p = dget<int32_t>(c, S_COLSP, n_tiles * kTileEdgeCap * ktrip);
+  auto* tlean = dget<TileLean>(c, S_TLEAN, n_tiles);
+  ParseOpts lo{};
+  lo.rows = rows_p;
+  lo.cols = cols_p;
+  lo.ktrip = ktrip;
+  lo.tile_pad = kTileEdgeCap;
+  lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
+  lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
+  hipLaunchKernelGGL(k_tile_parse<true>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, (const TileCnt*)nullptr,
+                     1u, 2u, lo, (uint64_t*)nullptr, (uint8_t*)nullptr, TouchOut{}, EdgeOut{}, c->ctl,
+                     (uint64_t*)nullptr, (DeferredLine*)nullptr, n_tiles, tcnt, tlean);
+  phase(c, "parse");
+  sync_ctl(c);
+  bool ok = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && c->h_ctl->warn_line == ~0ull;
+  if (ok) {
+    const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
+    auto* part = dget<TileCnt>(c, S_TEMP, n_parts + 1);
+    hipLaunchKernelGGL(k_struct_reduce<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
+                       (const TileCnt*)tcnt, n_tiles, part);
+    hipLaunchKernelGGL(k_struct_scan_parts<TileCnt>, dim3(1), dim3(256), 0, c->stream, part, n_parts, part + n_parts);
+    hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
+                       (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
+    const TileCnt tot = read_dev(c, part + n_parts);
+    hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
+                       (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, (uint64_t)tot.segs, c->ctl);
+    sync_ctl(c);
+    ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0x7FFFFFFFull;
+    if (ok) {
+      const uint64_t n_trip = tot.edges * ktrip;
+      auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
+      auto* cols = dget<int32_t>(c, S_COLS, n_trip);
+      hipLaunchKernelGGL(k_tile_compact, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, (const int32_t*)rows_p,
+                         (const int32_t*)cols_p, kTileEdgeCap, ktrip, (const TileCnt*)tcnt, (const TileCnt*)tbase,
+                         rows, cols);
+      phase(c, "place");
+      *tot_out = tot;
+      return true;
+    }
+  }
+  reset_ctl(c);  // the classic path starts from a clean slate
+  return false;
+}
+
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   c->test_flags = (uint32_t)o->reserved[1];
@@ -698,12 +756,18 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   R->dtype = dt;
   R->index_width = 4;
 
-  // ---- K1: per-tile counts -> tile bases
   const uint64_t n_tiles = (len + kTile - 1) / kTile;
   auto* tcnt = dget<TileCnt>(c, S_TILE_CNT, n_tiles + 1);
   auto* tbase = dget<TileCnt>(c, S_TILE_BASE, n_tiles + 1);
   TileCnt tot{};
-  if (n_tiles) {
+  const bool shard_dec = (o->reserved[4] & 1) != 0;
+  const bool first_one = !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
+  // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
+  const bool local_done = n_tiles && first_one && !shard_dec && !bidir && !(o->weight_tag && *o->weight_tag) &&
+                          !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
+                          tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot);
+  // ---- K1: per-tile counts -> tile bases
+  if (n_tiles && !local_done) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
     const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
     auto* part = dget<TileCnt>(c, S_TEMP, n_parts + 1);  // chunk sums, then the total
@@ -722,7 +786,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   R->n_records = (int64_t)tot.recs;
   if (n_t >= 0xFFFFFFFFull || n_e >= 0xFFFFFFFFull)
     throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 node touches in one build");
-  phase(c, "tiles");
+  if (!local_done) phase(c, "tiles");
 
   // ---- K2: parse every line from its tile's LDS window
   auto* ls = dget<uint64_t>(c, S_LS, n_lines + 1);
@@ -753,11 +817,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   // options.reserved[4] bit 0: one byte range of a sharded build whose node ids are decimal and
   // GLOBAL: reserved[2] S lines precede the range, reserved[3] S lines in the whole file (the
   // caller checked across ranges that no edge line precedes an S line).  Lean parse or nothing.
-  const bool shard_dec = (o->reserved[4] & 1) != 0;
   if (shard_dec && (o->output != G2N_OUT_COO || o->want_node_names || o->reserved[2] < 0 || o->reserved[3] < 0))
     throw Failure(G2N_E_ARG, "sharded decimal-id build: output COO without names, s_base / n_seg >= 0");
-  const bool int_ids = n_t && (shard_dec || (!(c->test_flags & (kTestDictHash | kTestDictGeneral)) &&
-                                              first_segment_is_one(c, in, len)));
+  const bool int_ids = n_t && (shard_dec || first_one);
   const bool lean = int_ids && (shard_dec || !(c->test_flags & kTestNoLean));
   if (int_ids) {
     op.tid = dget<uint32_t>(c, S_TID, n_t);
@@ -770,8 +832,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   phase(c, "_prep");
   auto parse = [&](const ParseOpts& po) {
     if (n_tiles)
-      hipLaunchKernelGGL(k_tile_parse, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe,
-                         po, ls, kind, T, E, c->ctl, wl, deferred, n_tiles);
+      hipLaunchKernelGGL(k_tile_parse<false>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tbase, tps, tpe,
+                         po, ls, kind, T, E, c->ctl, wl, deferred, n_tiles, (TileCnt*)nullptr, (TileLean*)nullptr);
     sync_ctl(c);
     const uint64_t n_def = c->h_ctl->n_deferred;
     if (n_def > n_tiles) throw Failure(G2N_E_DEVICE, "internal: more deferred lines than tiles");
@@ -781,8 +843,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     phase(c, "parse");
     sync_ctl(c);
   };
-  bool lean_done = false;
-  if (lean) {
+  bool lean_done = local_done;  // rows / cols hold the stream-order COO already
+  if (lean && !local_done) {
     ParseOpts lo = op;
     lo.rows = rows;
     lo.cols = cols;

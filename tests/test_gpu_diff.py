@@ -368,6 +368,39 @@ def test_decimal_id_dictionary(gpu, oracle_lib, case):
             assert a == b, (case, mode, dtype, wt)
 
 
+TILE_LOCAL_CASES = {  # inputs of ~60 tiles: the premise checked ACROSS tiles after the tile-local parse
+    "canonical": lambda L: L,
+    "s_renamed_late": lambda L: L[:15001] + ["S\t15001x\t*\n"] + L[15002:],  # a later tile's S name
+    "s_skips_a_number": lambda L: L[:9000] + L[9001:],  # S lines 1..8999, 9001..: ids off by one
+    "edge_between_s_tiles": lambda L: L[:12000] + [L[-1]] + L[12000:],  # an L line before later S lines
+    "edge_names_n_plus_1": lambda L: L + ["L\t20001\t+\t1\t-\t0M\n"],  # no such S line (N = 20000)
+    "long_line_deferred": lambda L: L[:30000] + ["L\t1\t+\t2\t-\t0M\tXX:Z:" + "a" * 40000 + "\n"] + L[30000:],
+}
+
+
+@pytest.mark.parametrize("case", sorted(TILE_LOCAL_CASES))
+def test_tile_local_parse_premise_across_tiles(gpu, oracle_lib, monkeypatch, case):
+    """The decimal-id parse without K1 (tile-local positions; the premise checked per tile after one
+    scan, then the COO compacted) against the oracle and against the lean parse after K1
+    (TEST_NO_TILE_LOCAL); cases that break the premise only across tiles must fall back."""
+    from gfa2network_amd import _native as nat
+
+    data = "".join(TILE_LOCAL_CASES[case](_decimal_gfa(9, 20000, 80000))).encode()
+    assert len(data) > 40 * 32768
+    for mode in MODES:
+        st, ph = _phases(data, **mode)
+        assert st == 0
+        local = "place" in ph and "tiles" not in ph
+        eligible = not mode.get("bidirected") and not mode.get("strip_orientation")
+        assert local == (eligible and case == "canonical"), (case, mode, sorted(ph))
+        for dtype, wt in (("float64", None), ("int8", None), ("float64", "RC")):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, wt)), (case, mode, dtype, wt)
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_TILE_LOCAL)
+            assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, dtype, wt)
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+
+
 def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
     """The lean decimal-id parse (coordinates written by the parse), the non-lean one (TEST_NO_LEAN:
     ids per touch, then k_triplets) and the hash dictionary (TEST_DICT_HASH) agree bit for bit at
