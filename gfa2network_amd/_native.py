@@ -47,6 +47,7 @@ TEST_NO_LEAN = 4         # decimal ids without the lean parse (ids per touch, th
 TEST_DICT_HASH = 8       # no decimal ids: the hash dictionary tiers
 TEST_DICT_GENERAL = 16   # no decimal ids, no S-first fast path: the general insert rounds
 TEST_NO_TILE_LOCAL = 32  # decimal ids: the lean parse after K1's tile bases, not the tile-local pass
+TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of the GPU inflate
 TEST_FLAGS = 0
 
 

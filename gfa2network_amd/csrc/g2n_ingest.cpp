@@ -378,6 +378,39 @@ bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out) {
   return true;
 }
 
+// ------------------------------------------------------------- BGZF chains ---------------
+bool bgzf_members(const uint8_t* in, size_t n, std::vector<ZMember>& out, size_t* total_out) {
+  out.clear();
+  size_t pos = 0, total = 0;
+  auto u16 = [&](size_t p) { return (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8); };
+  auto u32 = [&](size_t p) { return u16(p) | (u16(p + 2) << 16); };
+  while (pos < n) {
+    if (n - pos < 26 || in[pos] != 0x1F || in[pos + 1] != 0x8B || in[pos + 2] != 8 || in[pos + 3] != 4)
+      return false;  // FEXTRA only: bgzip's header
+    const size_t xlen = u16(pos + 10);
+    if (n - pos < 12 + xlen + 8) return false;
+    size_t bsize = 0;
+    for (size_t q = pos + 12; q + 4 <= pos + 12 + xlen;) {  // extra subfields: SI1 SI2 SLEN data
+      const size_t slen = u16(q + 2);
+      if (in[q] == 66 && in[q + 1] == 67 && slen == 2 && q + 6 <= pos + 12 + xlen) bsize = u16(q + 4) + 1;
+      q += 4 + slen;
+    }
+    if (!bsize || bsize < 12 + xlen + 8 || bsize > n - pos) return false;
+    ZMember m{};
+    m.in_off = pos + 12 + xlen;
+    m.in_len = (uint32_t)(bsize - 12 - xlen - 8);
+    m.crc = u32(pos + bsize - 8);
+    m.out_len = u32(pos + bsize - 4);
+    if (m.out_len > 65536) return false;
+    m.out_off = total;
+    total += m.out_len;
+    out.push_back(m);
+    pos += bsize;
+  }
+  *total_out = total;
+  return !out.empty() && total > 0;
+}
+
 // ------------------------------------------------- gzip.open's reader, restated ---------
 // CPython 3.10 Lib/gzip.py _GzipReader: _read_gzip_header (:430-462), read (:464-510),
 // _read_eof (:518-537); raw deflate as zlib.decompressobj(-MAX_WBITS).  Errors carry the

@@ -90,6 +90,22 @@ struct Inflated {
   int members = 0;
 };
 bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out);
+// One member of a BGZF chain: its deflate data z[in_off, in_off + in_len), its output
+// [out_off, out_off + out_len) (ISIZE) and the trailer's CRC-32.
+struct ZMember {
+  unsigned long long in_off, out_off;
+  uint32_t in_len, out_len, crc, pad_;
+};
+// A clean BGZF chain (every member's size from its 'BC' subfield, members back to back, no
+// other header fields, ISIZE <= 64 KiB): true with the members and the total output size.
+bool bgzf_members(const uint8_t* in, size_t n, std::vector<ZMember>& out, size_t* total_out);
+// g2n_build_from_path's ".gz" path for a BGZF chain: the compressed bytes to the GPU, the members
+// inflated there (g2n_inflate.hip), then the build.  kBgzfFallback: a member did not inflate
+// cleanly — the caller reads the file with the host readers instead.
+constexpr int kBgzfFallback = -1;
+constexpr int32_t kTestHostInflate = 64;  // options.reserved[1]: BGZF read by the host readers
+int build_host_bgzf(const uint8_t* z, size_t zlen, const std::vector<ZMember>& members, size_t total_out,
+                    const g2n_options* opts, g2n_result** out, double read_ms);
 // gzip.open's reader restated (serial, exact errors): false with *sub = 1 BadGzipFile,
 // 2 EOFError, 3 zlib.error, 4 BadGzipFile (CRC / length) and *msg = the exception's message;
 // `out` then holds the bytes the reference's reader returned before raising (not cut to lines).

@@ -21,6 +21,7 @@
 #include "g2n_scan.hip"
 #include "g2n_sym.hip"
 #include "g2n_route.hip"
+#include "g2n_inflate.hip"
 
 #define G2N_HIP(call)                                                                                      \
   do {                                                                                                     \
@@ -38,7 +39,7 @@ enum Slot {
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
-  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_NSLOTS
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -1222,6 +1223,55 @@ int build_host_fill(size_t len, const FillFn& fill, const g2n_options* opts, g2n
   H->r.host_ms_read = read_ms;
   H->r.host_ms_h2d = t1 - t0;
   H->r.host_ms_d2h = now_ms() - t2;
+  *out = &H->r;
+  return H->r.status;
+}
+
+int build_host_bgzf(const uint8_t* z, size_t zlen, const std::vector<ZMember>& members, size_t total_out,
+                    const g2n_options* opts, g2n_result** out, double read_ms) {
+  g2n_context* c = shared_context(opts->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  G2N_HIP(hipSetDevice(c->device));
+  const double t0 = now_ms();
+  auto* dz = dget<uint8_t>(c, S_ZIN, zlen + 16);
+  auto* dm = dget<ZMember>(c, S_ZMEM, members.size());
+  auto* bad = dget<unsigned int>(c, S_ZBAD, 1);
+  auto* din = dget<uint8_t>(c, S_IN, total_out + 16);
+  G2N_HIP(hipStreamSynchronize(c->stream));  // the slots may still be read by an earlier build
+  staged_upload(c->device, dz, zlen, [z](size_t off, uint8_t* dst, size_t n) { std::memcpy(dst, z + off, n); });
+  G2N_HIP(hipMemcpyAsync(dm, members.data(), members.size() * sizeof(ZMember), hipMemcpyHostToDevice, c->stream));
+  G2N_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned int), c->stream));
+  hipEvent_t e0, e1;
+  G2N_HIP(hipEventCreate(&e0));
+  G2N_HIP(hipEventCreate(&e1));
+  G2N_HIP(hipEventRecord(e0, c->stream));
+  hipLaunchKernelGGL(k_inflate_members, dim3((unsigned)((members.size() + kInflTPB - 1) / kInflTPB)), dim3(kInflTPB), 0,
+                     c->stream, (const uint8_t*)dz, (const ZMember*)dm, (uint64_t)members.size(), din, bad);
+  G2N_HIP(hipEventRecord(e1, c->stream));
+  const unsigned int n_bad = read_dev(c, bad);
+  float inflate_ms = 0.f;
+  G2N_HIP(hipEventElapsedTime(&inflate_ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (n_bad) return kBgzfFallback;
+  const double t1 = now_ms();
+  g2n_result D;
+  run_pipeline(c, din, total_out, opts, &D);
+  const double t2 = now_ms();
+  HostResult* H = new_host_result();
+  try {
+    download_result(c, D, H);
+  } catch (...) {
+    delete H;
+    throw;
+  }
+  H->r.host_ms_read = read_ms;
+  H->r.host_ms_h2d = t1 - t0;  // upload of the compressed bytes + GPU inflate
+  H->r.host_ms_d2h = now_ms() - t2;
+  if (H->r.n_phases < G2N_MAX_PHASES) {  // the inflate kernel as one more device phase
+    H->r.phase_names[H->r.n_phases] = "gz_inflate";
+    H->r.phase_ms[H->r.n_phases++] = inflate_ms;
+  }
   *out = &H->r;
   return H->r.status;
 }

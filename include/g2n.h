@@ -95,7 +95,8 @@ typedef struct g2n_options {
                                   [1]: test flags (normally rare paths, same results): 2 = MAX-SYM / SUM CSR through
                                   the general row sums, 4 = decimal ids without the lean parse,
                                   8 = hash dictionary, 16 = general dictionary rounds,
-                                  32 = decimal ids parsed after K1 (not the tile-local pass);
+                                  32 = decimal ids parsed after K1 (not the tile-local pass),
+                                  64 = a BGZF .gz read by the host readers (not inflated on the GPU);
                                   [2], [3], [4] bit 0: sharded decimal-id build — this byte range's
                                   node ids are global decimals: [2] = S lines before the range,
                                   [3] = S lines in the file (output G2N_OUT_COO, no names; returns
