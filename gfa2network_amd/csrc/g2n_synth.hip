@@ -4,12 +4,12 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 #include <thread>
 #include <vector>
 
 #include "../../include/g2n_synth.h"
 #include "g2n_internal.h"
+#include "g2n_scan.hip"
 #include "synth.h"
 
 namespace g2n {
@@ -100,11 +100,15 @@ int g2n_synth_device(int device, const g2n_synth_spec* spec, void** d_out, size_
   const unsigned grid = (unsigned)((n + 255) / 256);
   if (hipMalloc(&dlen, n * 8) != hipSuccess || hipMalloc(&doff, n * 8) != hipSuccess) { rc = G2N_E_NOMEM; goto done; }
   hipLaunchKernelGGL(k_synth_len, dim3(grid), dim3(256), 0, 0, s, n, dlen);
-  if (rocprim::exclusive_scan(nullptr, tb, dlen, doff, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>()) !=
-      hipSuccess) { rc = G2N_E_DEVICE; goto done; }
-  if (hipMalloc(&tmp, tb ? tb : 16) != hipSuccess) { rc = G2N_E_NOMEM; goto done; }
-  if (rocprim::exclusive_scan(tmp, tb, dlen, doff, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>()) !=
-      hipSuccess) { rc = G2N_E_DEVICE; goto done; }
+  {  // line offsets: the pipeline's single-pass scan (g2n_scan.hip)
+    const uint64_t tiles = scan_tiles(n);
+    tb = (tiles + 1) * sizeof(unsigned long long);
+    if (hipMalloc(&tmp, tb) != hipSuccess) { rc = G2N_E_NOMEM; goto done; }
+    if (hipMemset(tmp, 0, tb) != hipSuccess) { rc = G2N_E_DEVICE; goto done; }
+    auto* st = (unsigned long long*)tmp;
+    hipLaunchKernelGGL((k_scan_excl<uint64_t, uint64_t>), dim3((unsigned)tiles), dim3(256), 0, 0, (const uint64_t*)dlen,
+                       doff, n, st, (uint32_t*)(st + tiles), (uint64_t*)nullptr);
+  }
   if (hipMemcpy(&last_len, dlen + n - 1, 8, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(&last_off, doff + n - 1, 8, hipMemcpyDeviceToHost) != hipSuccess) { rc = G2N_E_DEVICE; goto done; }
   total = last_off + last_len;
