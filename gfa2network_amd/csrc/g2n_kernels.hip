@@ -245,17 +245,26 @@ __device__ inline uint8_t kind_at(const uint8_t* buf, uint32_t o, uint64_t p, ui
   return line_kind(c0, p + 1 >= len || c0 == '\n' || buf[o + 1] == '\t' || buf[o + 1] == '\n');
 }
 
-__device__ inline uint32_t nl_bits4(uint32_t w) {  // bit b: byte b of w is '\n'
-  const uint32_t m = byte_match_mask(w, 0x0A0A0A0Au);
-  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+// bit b (b < 16): byte b of the 16-byte chunk v equals pat's byte (pat = byte * 0x01010101).
+// The four words' match bytes are merged into one register (bit 8 b + k = byte b of word k),
+// compressed to 16 bits (bit 4 b + k) and transposed as a 4 x 4 bit matrix (two delta swaps)
+// into byte order — fewer VALU than four per-word gathers.
+__device__ inline uint32_t mask16(uint4 v, uint32_t pat) {
+  const uint32_t t = (byte_match_mask(v.x, pat) >> 7) | (byte_match_mask(v.y, pat) >> 6) |
+                     (byte_match_mask(v.z, pat) >> 5) | (byte_match_mask(v.w, pat) >> 4);
+  uint32_t x = (t & 0xFu) | ((t >> 4) & 0xF0u) | ((t >> 8) & 0xF00u) | ((t >> 12) & 0xF000u);
+  const uint32_t t1 = (x ^ (x >> 3)) & 0x0A0Au;
+  x ^= t1 ^ (t1 << 3);
+  const uint32_t t2 = (x ^ (x >> 6)) & 0x00CCu;
+  x ^= t2 ^ (t2 << 6);
+  return x;
 }
 
-// Newlines (bit b = byte b) and line starts of chunk c of the staged tile.  Bytes at or past
-// len hold neither; a start needs the byte before it to be '\n' (or to be the input's start).
+// Newlines (bit b = byte b) and line starts of chunk c (bytes v) of the staged tile.  Bytes at
+// or past len hold neither; a start needs the byte before it to be '\n' (or the input's start).
 __device__ inline void chunk_masks(const uint8_t* buf, uint32_t c, uint64_t t0, uint64_t len, bool tile_prev_nl,
-                                   uint32_t& nl, uint32_t& st) {
-  const uint4 v = *(const uint4*)(buf + 16 * c);
-  nl = nl_bits4(v.x) | (nl_bits4(v.y) << 4) | (nl_bits4(v.z) << 8) | (nl_bits4(v.w) << 12);
+                                   uint32_t& nl, uint32_t& st, uint4 v) {
+  nl = mask16(v, 0x0A0A0A0Au);
   const bool prev = c ? buf[16 * c - 1] == '\n' : tile_prev_nl;
   st = ((nl << 1) | (prev ? 1u : 0u)) & 0xFFFFu;
   const uint64_t pos = t0 + 16ull * c;
@@ -328,7 +337,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_count(const uint8_t* __restrict__
   for (uint32_t j = 0; j < kChunkIters; j++) {
     const uint32_t c = j * kTPB + threadIdx.x;
     uint32_t m, st;
-    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
+    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st, *(const uint4*)(buf + 16 * c));
     nl += __popc(m);
     lines += __popc(st);
     while (st) {
@@ -999,15 +1008,9 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   }
   const TileCnt b = local ? TileCnt{} : base[tile];
   __syncthreads();
-  for (uint32_t c = threadIdx.x; c < kMaskChunks; c += kTPB) {  // the tile's tab bitmap (bytes past len: 0)
-    uint32_t m = 0;
-    if (16 * c + 16 <= kTile + kTileHalo + 16) {
-      const uint4 v = *(const uint4*)(buf + 16 * c);
-      m = delim_bits4(v.x, false) | (delim_bits4(v.y, false) << 4) | (delim_bits4(v.z, false) << 8) |
-          (delim_bits4(v.w, false) << 12);
-    }
-    tabm[c] = (uint16_t)m;
-  }
+  // the tile's tab bitmap (bytes past len: 0): the tile's own chunks come with pass (1), here the halo's
+  for (uint32_t c = kTileChunks + threadIdx.x; c < kMaskChunks; c += kTPB)
+    tabm[c] = (uint16_t)(16 * c + 16 <= kTile + kTileHalo + 16 ? mask16(*(const uint4*)(buf + 16 * c), 0x09090909u) : 0u);
   const uint64_t w1 = t0 + kTile + kTileHalo < len ? t0 + kTile + kTileHalo : len;
   Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
   L.tm = tabm;
@@ -1018,8 +1021,10 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 #pragma unroll
   for (uint32_t j = 0; j < kChunkIters; j++) {
     const uint32_t c = j * kTPB + threadIdx.x;
+    const uint4 v = *(const uint4*)(buf + 16 * c);
+    tabm[c] = (uint16_t)mask16(v, 0x09090909u);
     uint32_t m, st;
-    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st);
+    chunk_masks(buf, c, t0, len, tile_prev_nl, m, st, v);
     if (j & 1) stm[j >> 1] |= st << 16;
     else stm[j >> 1] = st;
     pre[c] = (uint32_t)__popc(st);
