@@ -132,6 +132,70 @@ def write_gz_members(data, path: str, member_bytes: int = 64 << 20, level: int =
     return total
 
 
+def write_gz_single(data, path: str, level: int = 6, threads: int = 16, piece: int = 32 << 20) -> int:
+    """ONE gzip member over the whole input (pigz's layout: pieces deflated in parallel, each primed
+    with the 32 KiB before it and ended by a sync flush, so back-references cross the piece
+    boundaries; gzip.open reads it as one deflate stream).  Returns the compressed size."""
+    import struct
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+
+    mv = memoryview(data)
+    offs = list(range(0, len(data), piece)) or [0]
+
+    def one(off):
+        last = off + piece >= len(data)
+        co = zlib.compressobj(level, zlib.DEFLATED, -zlib.MAX_WBITS,
+                              **({"zdict": bytes(mv[max(0, off - 32768):off])} if off else {}))
+        chunk = mv[off:off + piece]
+        return co.compress(chunk) + co.flush(zlib.Z_FINISH if last else zlib.Z_SYNC_FLUSH), zlib.crc32(chunk), len(chunk)
+
+    total, crc = 10, 0
+    with open(path, "wb") as fh, ThreadPoolExecutor(threads) as ex:
+        fh.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\xff")
+        for body, c, n in ex.map(one, offs):
+            fh.write(body)
+            total += len(body)
+            crc = _crc32_combine(crc, c, n)
+        fh.write(struct.pack("<II", crc, len(data) & 0xFFFFFFFF))
+    return total + 8
+
+
+def _crc32_combine(crc1: int, crc2: int, len2: int) -> int:
+    """zlib's crc32_combine (CRC of A+B from CRC(A), CRC(B), len(B)) by GF(2) matrix powers."""
+    def times(mat, vec):
+        s, i = 0, 0
+        while vec:
+            if vec & 1:
+                s ^= mat[i]
+            vec >>= 1
+            i += 1
+        return s
+
+    def square(mat):
+        return [times(mat, mat[n]) for n in range(32)]
+
+    if len2 <= 0:
+        return crc1
+    odd = [0xEDB88320] + [1 << n for n in range(31)]
+    even = square(odd)
+    odd = square(even)
+    while True:
+        even = square(odd)
+        if len2 & 1:
+            crc1 = times(even, crc1)
+        len2 >>= 1
+        if not len2:
+            break
+        odd = square(even)
+        if len2 & 1:
+            crc1 = times(odd, crc1)
+        len2 >>= 1
+        if not len2:
+            break
+    return crc1 ^ crc2
+
+
 def write_bgzf(data, path: str, level: int = 6, threads: int = 16) -> int:
     """BGZF (htslib's bgzip layout: members of 65280 input bytes, 'BC' size subfield, EOF marker),
     members deflated in parallel batches.  Returns the compressed size."""
@@ -187,6 +251,8 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
             fh.write(data)
         gz = os.path.join(tmp, "c.gfa.gz")
         out["gz_bytes"] = write_gz_members(data, gz, threads=threads)
+        gz1 = os.path.join(tmp, "c.single.gfa.gz")
+        out["gz_single_bytes"] = write_gz_single(data, gz1, threads=threads)
         bgz = os.path.join(tmp, "c.bgzf.gz")
         out["bgzf_bytes"] = write_bgzf(data, bgz, threads=threads)
         out["prep_s"] = round(time.perf_counter() - t0, 1)
@@ -196,7 +262,8 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
         opts = nat.make_options(dtype="float64", output=nat.OUT_PARSE, want_node_names=True, device=device,
                                 directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
                                 weight_tag=mode.get("weight_tag"))
-        for name, path in (("plain", plain), ("gzip_64MiB_members", gz), ("bgzf_gpu_inflate", bgz)):
+        for name, path in (("plain", plain), ("gzip_64MiB_members", gz), ("gzip_single_member", gz1),
+                           ("bgzf_gpu_inflate", bgz)):
             for it in range(2):
                 t0 = time.perf_counter()
                 raw = nat.build_from_path(path, opts)

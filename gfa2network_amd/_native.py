@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
-    "g2n_gunzip", "g2n_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
+    "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
 
@@ -177,6 +177,9 @@ def load() -> ctypes.CDLL:
     lib.g2n_gunzip.argtypes = [P, ctypes.c_size_t, I32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
                                ctypes.POINTER(I32), ctypes.POINTER(I32)]
     lib.g2n_gunzip.restype = ctypes.c_int
+    lib.g2n_gunzip_chunked.argtypes = [P, ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(P),
+                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(I32)]
+    lib.g2n_gunzip_chunked.restype = ctypes.c_int
     lib.g2n_free.argtypes = [P]
     lib.g2n_join_names.argtypes = [P, P, U64, ctypes.c_uint8, P]
     lib.g2n_join_names.restype = ctypes.c_int
@@ -365,6 +368,26 @@ def host_bytes_at(addr: int, n: int) -> bytes:
     if not n:
         return b""
     return (ctypes.c_char * n).from_address(addr).raw
+
+
+def gunzip_chunked(data: bytes, chunk_bytes: int = 0) -> tuple[bytes, int] | None:
+    """The chunk-parallel single-member inflate alone: (bytes, chunks that decoded from a block
+    start of their own), or None when it declines."""
+    lib = load()
+    arr = np.frombuffer(data, dtype=np.uint8)
+    if not arr.size:
+        return None
+    out, n, chunks = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_int32()
+    rc = lib.g2n_gunzip_chunked(arr.ctypes.data, arr.size, chunk_bytes, ctypes.byref(out), ctypes.byref(n),
+                                ctypes.byref(chunks))
+    if rc == E_UNSUPPORTED:
+        return None
+    if rc != OK:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    try:
+        return host_bytes_at(out.value, n.value), int(chunks.value)
+    finally:
+        lib.g2n_free(out)
 
 
 class GzipFailure(Exception):

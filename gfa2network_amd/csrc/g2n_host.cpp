@@ -349,6 +349,24 @@ int g2n_gunzip(const void* buf, size_t len, int32_t parallel, void** out, size_t
   });
 }
 
+int g2n_gunzip_chunked(const void* buf, size_t len, size_t chunk_bytes, void** out, size_t* out_len,
+                       int32_t* chunks) {
+  if (!out || !out_len || !buf) return G2N_E_ARG;
+  *out = nullptr;
+  *out_len = 0;
+  return g2n::guarded([&]() -> int {
+    g2n::Inflated z;
+    if (!g2n::gunzip_chunked((const uint8_t*)buf, len, chunk_bytes, z)) return G2N_E_UNSUPPORTED;
+    auto* o = (uint8_t*)std::malloc(z.total ? z.total : 1);
+    if (!o) return G2N_E_NOMEM;
+    for (size_t k = 0; k < z.parts.size(); k++) std::memcpy(o + z.start[k], z.parts[k].p, z.parts[k].n);
+    *out = o;
+    *out_len = z.total;
+    if (chunks) *chunks = (int32_t)z.parts.size();
+    return G2N_OK;
+  });
+}
+
 void g2n_free(void* p) { std::free(p); }
 
 int g2n_join_names(const uint8_t* blob, const int64_t* offsets, uint64_t n_names, uint8_t sep, uint8_t* out) {

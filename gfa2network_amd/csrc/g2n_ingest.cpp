@@ -294,6 +294,9 @@ bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out) {
   found.clear();
   const size_t nc = cand.size();
   if (nc > ((size_t)1 << 22)) return false;  // pathological; let the serial reader handle it
+  // few member candidates in a large file: most likely one big member, which the member-level
+  // speculation below would inflate on one thread — split its deflate stream instead
+  if (n >= ((size_t)64 << 20) && nc <= 64 && gunzip_chunked(in, n, 0, out)) return true;
 
   // 2. speculative inflate of every candidate; the chain walker marks candidates that fall
   //    inside a resolved member as dead, which stops (or skips) their speculation

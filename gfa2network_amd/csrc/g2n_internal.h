@@ -90,6 +90,10 @@ struct Inflated {
   int members = 0;
 };
 bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out);
+// One gzip member spanning the whole file (zero padding after it allowed), inflated chunk-parallel
+// (g2n_pinflate.cpp); chunk_bytes 0 = sized for the host threads.  false = declined (not one
+// clean member, or anything the decoder refuses): the caller runs the member-chain readers.
+bool gunzip_chunked(const uint8_t* in, size_t n, size_t chunk_bytes, Inflated& out);
 // One member of a BGZF chain: its deflate data z[in_off, in_off + in_len), its output
 // [out_off, out_off + out_len) (ISIZE) and the trailer's CRC-32.
 struct ZMember {

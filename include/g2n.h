@@ -177,6 +177,15 @@ void g2n_result_free(g2n_result *res);
  * raising (io.BufferedReader refills of 8192: what a line loop over gzip.open sees; g2n_free it). */
 int g2n_gunzip(const void *buf, size_t len, int32_t parallel, void **out, size_t *out_len, int32_t *members,
                int32_t *sub);
+/* The chunk-parallel single-member inflate alone (what g2n_gunzip's parallel path tries first
+ * for a file of >= 64 MiB with few member candidates): one gzip member to the end of the file
+ * (zero padding allowed), its deflate stream cut into chunks of chunk_bytes compressed bytes
+ * (0 = sized for the host threads) that are inflated concurrently.  G2N_OK with *out / *out_len
+ * (g2n_free) and *chunks = the chunks that decoded from a block start of their own; G2N_E_UNSUPPORTED
+ * when it declines (not one clean member, or a stream its decoder refuses: the exact reader decides).
+ * Replaces gzip.open's serial read of one member (parser.py:108-109). */
+int g2n_gunzip_chunked(const void *buf, size_t len, size_t chunk_bytes, void **out, size_t *out_len,
+                       int32_t *chunks);
 void g2n_free(void *p);
 
 /* The node list's bytes joined by `sep` (builders.py:284-288 node_list, built in one pass by

@@ -80,6 +80,24 @@ static void gzip_checks() {
     CHECK(g2n::gunzip_exact(blob.data(), blob.size(), b, &sub, &msg));
     CHECK(flat(b) == text);
   }
+  {  // one member over the whole text: the chunk-parallel inflate, clean and damaged
+    auto one = member(text, 6);
+    g2n::Inflated a;
+    CHECK(g2n::gunzip_chunked(one.data(), one.size(), 1 << 14, a));
+    CHECK(flat(a) == text && a.parts.size() > 1);
+    for (int trial = 0; trial < 40; trial++) {
+      std::vector<uint8_t> bad = one;
+      const size_t at = 10 + rng() % (bad.size() - 10);
+      if (trial % 2) bad.resize(at);
+      else bad[at] ^= (uint8_t)(1u << (rng() % 8));
+      g2n::Inflated c, d;
+      int sub = 0;
+      std::string msg;
+      const bool ok_ch = g2n::gunzip_chunked(bad.data(), bad.size(), 1 << 13, c);
+      const bool ok = g2n::gunzip_exact(bad.data(), bad.size(), d, &sub, &msg);
+      if (ok_ch) CHECK(ok && flat(c) == flat(d));
+    }
+  }
   for (int trial = 0; trial < 60; trial++) {  // damaged: no crash; the prefix is a prefix
     std::vector<uint8_t> bad = blob;
     const size_t at = rng() % bad.size();

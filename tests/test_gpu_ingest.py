@@ -136,3 +136,32 @@ def test_bgzf_damaged_falls_back_to_exact_reader(gpu, tmp_path):
         with pytest.raises(Exception) as ei:
             parse_gfa(p, build_graph=False, build_matrix=True)
         assert want is not None and (type(ei.value), str(ei.value)) == want, name
+
+
+@pytest.mark.parametrize("layout", ["zlib_level1", "pigz_pieces"])
+def test_single_member_gzip_chunk_parallel(gpu, tmp_path, layout):
+    """A single-member .gz of >= 64 MiB takes the chunk-parallel inflate (g2n_pinflate.cpp,
+    SURVEY.md §8(f)2) inside g2n_build_from_path; the build equals the plain file's."""
+    import gzip
+    import sys
+    from pathlib import Path
+
+    from gfa2network_amd import _native, parse_gfa, synth
+
+    data = synth.host_bytes(3_000_000, 12_000_000, seed=11)
+    single = tmp_path / "s.gfa.gz"
+    if layout == "zlib_level1":
+        single.write_bytes(gzip.compress(data, 1, mtime=0))
+    else:
+        sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+        import bench
+
+        bench.write_gz_single(data, str(single), level=6, threads=16, piece=16 << 20)
+    blob = single.read_bytes()
+    assert len(blob) >= 64 << 20, len(blob)
+    got = _native.gunzip_chunked(blob)
+    assert got is not None and got[1] > 1 and got[0] == data
+    del got, blob
+    kw = dict(build_graph=False, build_matrix=True, return_node_list=True, directed=False)
+    want = _key(parse_gfa(io.BytesIO(data), **kw))
+    assert _key(parse_gfa(single, **kw)) == want

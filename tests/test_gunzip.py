@@ -187,3 +187,106 @@ def test_corrupt_deflate_prefix_follows_8k_refills(seed):
         bad[at:at + k] = bytes(r.randrange(256) for _ in range(len(bad[at:at + k])))
         check(bytes(bad))
         check(m[:at])  # truncated there
+
+
+# ---- chunk-parallel single-member inflate (g2n_pinflate.cpp) -------------
+def _single_member_pieces(data: bytes, piece: int, level: int = 6) -> bytes:
+    """pigz-style ONE member: pieces primed with the 32 KiB before them, sync-flushed."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    import tempfile
+    with tempfile.NamedTemporaryFile(suffix=".gz") as fh:
+        bench.write_gz_single(data, fh.name, level=level, threads=4, piece=piece)
+        return Path(fh.name).read_bytes()
+
+
+@pytest.fixture(scope="module")
+def big_text() -> bytes:
+    return gfa_text(60_000, 7) * 2
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+@pytest.mark.parametrize("strategy", [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE])
+@pytest.mark.parametrize("chunk", [1 << 16, 1 << 18, 0])
+def test_chunked_equals_zlib(big_text, level, strategy, chunk):
+    co = zlib.compressobj(level, zlib.DEFLATED, 31, 8, strategy)
+    blob = co.compress(big_text) + co.flush()
+    got = _native.gunzip_chunked(blob, chunk)
+    assert got is not None, "a zlib single member with dynamic blocks must be taken"
+    assert got[0] == big_text
+    if chunk and chunk < len(blob) // 4:
+        assert got[1] > 1, "more than one chunk must decode from a block start of its own"
+
+
+def test_chunked_fixed_and_stored_blocks(big_text):
+    # fixed-Huffman-only and stored-only streams: no dynamic block start to sync on, so the
+    # first chunk decodes everything; the result is still exact
+    for co in (zlib.compressobj(6, zlib.DEFLATED, 31, 8, zlib.Z_FIXED), zlib.compressobj(0, zlib.DEFLATED, 31)):
+        blob = co.compress(big_text[:400_000]) + co.flush()
+        got = _native.gunzip_chunked(blob, 1 << 14)
+        assert got is not None and got[0] == big_text[:400_000] and got[1] == 1
+
+
+def test_chunked_pigz_layout_and_mixed_blocks(big_text):
+    blob = _single_member_pieces(big_text, piece=300_000)
+    assert gzip.decompress(blob) == big_text
+    got = _native.gunzip_chunked(blob, 1 << 16)
+    assert got is not None and got[0] == big_text and got[1] > 1
+    # incompressible stretches (stored blocks) between text
+    r = random.Random(3)
+    mixed = b"".join(big_text[i:i + 200_000] + bytes(r.getrandbits(8) for _ in range(70_000))
+                     for i in range(0, 1_000_000, 200_000))
+    blob = gzip.compress(mixed, 6)
+    got = _native.gunzip_chunked(blob, 1 << 15)
+    assert got is not None and got[0] == mixed
+
+
+@pytest.mark.parametrize("damage", ["trailing_member", "trailing_garbage", "truncated", "crc", "isize",
+                                    "bitflip", "zero_padding"])
+def test_chunked_declines_or_matches(big_text, damage):
+    blob = bytearray(gzip.compress(big_text, 6))
+    if damage == "trailing_member":
+        blob += gzip.compress(b"S\t1\n")
+    elif damage == "trailing_garbage":
+        blob += b"garbage"
+    elif damage == "truncated":
+        del blob[len(blob) // 2:]
+    elif damage == "crc":
+        blob[-8] ^= 1
+    elif damage == "isize":
+        blob[-4] ^= 1
+    elif damage == "bitflip":
+        blob[len(blob) // 3] ^= 0x10
+    elif damage == "zero_padding":
+        blob += b"\x00" * 100
+    blob = bytes(blob)
+    got = _native.gunzip_chunked(blob, 1 << 16)
+    want, err = python_read(blob)
+    if damage == "zero_padding":
+        assert got is not None and got[0] == want
+    elif got is not None:
+        # taken only when gzip.py reads exactly one clean member to the end
+        assert err is None and got[0] == want
+    else:
+        assert damage != "zero_padding"
+    # the full reader (which tries the chunked path first on big files) stays exact
+    for parallel in (True, False):
+        try:
+            out, _ = _native.gunzip(blob, parallel=parallel)
+            assert err is None and out == want
+        except _native.GzipFailure as e:
+            assert err is not None and isinstance(err, EXC[e.sub]) and e.message == str(err)
+
+
+def test_chunked_reference_before_stream_start():
+    # a stream whose first chunk is shorter than the window the next chunk reads from: a
+    # back-reference before the stream's first byte must never be filled from nowhere
+    text = b"ACGT" * 5 + gfa_text(3000, 1)
+    blob = gzip.compress(text, 9)
+    for chunk in (64, 256, 1024):
+        got = _native.gunzip_chunked(blob, chunk)
+        assert got is None or got[0] == text
