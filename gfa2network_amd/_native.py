@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
-    "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
+    "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
 
@@ -181,6 +181,14 @@ def load() -> ctypes.CDLL:
                                        ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(I32)]
     lib.g2n_gunzip_chunked.restype = ctypes.c_int
     lib.g2n_free.argtypes = [P]
+    lib.g2n_split_render.argtypes = [P, ctypes.c_size_t, I32, ctypes.POINTER(P)]
+    lib.g2n_split_render.restype = ctypes.c_int
+    PP, PU = ctypes.POINTER(P), ctypes.POINTER(U64)
+    lib.g2n_split_get.argtypes = [P, PP, PU, PP, PP, PU, PP, PP, PP, PU, ctypes.POINTER(I32)]
+    lib.g2n_split_get.restype = None
+    lib.g2n_split_segments.argtypes = [P, PP, PU]
+    lib.g2n_split_segments.restype = None
+    lib.g2n_split_free.argtypes = [P]
     lib.g2n_join_names.argtypes = [P, P, U64, ctypes.c_uint8, P]
     lib.g2n_join_names.restype = ctypes.c_int
     lib.g2n_write_npz.argtypes = [ctypes.c_char_p, I32, P, P, P, P, P, I32]
@@ -388,6 +396,42 @@ def gunzip_chunked(data: bytes, chunk_bytes: int = 0) -> tuple[bytes, int] | Non
         return host_bytes_at(out.value, n.value), int(chunks.value)
     finally:
         lib.g2n_free(out)
+
+
+def split_render(data, bidirected: bool):
+    """g2n_split_render: (text, names_blob, names_offsets, warnings [(kind, segment bytes)],
+    many_nodes, intervals per segment) for parse_gfa(..., split_on_alignment=True)
+    (api._parse_gfa_split)."""
+    lib = load()
+    arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data,
+                               dtype=np.uint8)
+    h = ctypes.c_void_p()
+    rc = lib.g2n_split_render(arr.ctypes.data if arr.size else None, arr.size, int(bool(bidirected)), ctypes.byref(h))
+    if rc != OK:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}") if rc != E_UNSUPPORTED else \
+            NotImplementedError(last_error())
+    try:
+        t, nm, no, ws, wo, wk = (ctypes.c_void_p() for _ in range(6))
+        tl, nn, nw = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        many = ctypes.c_int32()
+        lib.g2n_split_get(h, ctypes.byref(t), ctypes.byref(tl), ctypes.byref(nm), ctypes.byref(no), ctypes.byref(nn),
+                          ctypes.byref(ws), ctypes.byref(wo), ctypes.byref(wk), ctypes.byref(nw), ctypes.byref(many))
+        text = np.frombuffer(host_bytes_at(t.value, tl.value), dtype=np.uint8)
+        offs = np.ctypeslib.as_array((ctypes.c_int64 * (nn.value + 1)).from_address(no.value)).copy()
+        blob = np.frombuffer(host_bytes_at(nm.value, int(offs[-1])), dtype=np.uint8)
+        warns = []
+        if nw.value:
+            wof = np.ctypeslib.as_array((ctypes.c_int64 * (nw.value + 1)).from_address(wo.value))
+            wkd = np.ctypeslib.as_array((ctypes.c_int32 * nw.value).from_address(wk.value))
+            segs = host_bytes_at(ws.value, int(wof[-1]))
+            warns = [(int(wkd[i]), segs[wof[i]:wof[i + 1]]) for i in range(nw.value)]
+        si, ns = ctypes.c_void_p(), ctypes.c_uint64()
+        lib.g2n_split_segments(h, ctypes.byref(si), ctypes.byref(ns))
+        per_seg = np.ctypeslib.as_array((ctypes.c_int64 * ns.value).from_address(si.value)).copy() if ns.value \
+            else np.zeros(0, dtype=np.int64)
+        return text, blob, offs, warns, bool(many.value), per_seg
+    finally:
+        lib.g2n_split_free(h)
 
 
 class GzipFailure(Exception):

@@ -182,8 +182,13 @@ def parse_gfa(
     """
     if backend == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
-    if split_on_alignment:
-        raise NotImplementedError("split_on_alignment is outside the GPU GFA->CSR path")
+    if split_on_alignment:  # builders.py:110-128 (before the return_node_list check)
+        if build_graph:
+            raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
+        return _parse_gfa_split(path, build_matrix=build_matrix, directed=directed, weight_tag=weight_tag,
+                                strip_orientation=strip_orientation, bidirected=bidirected,
+                                keep_directed_bidir=keep_directed_bidir, dtype=dtype, asymmetric=asymmetric,
+                                raw_bytes_id=raw_bytes_id, return_node_list=return_node_list, device=device)
     if return_node_list and not build_matrix:  # builders.py:129-130
         raise ValueError("return_node_list requires build_matrix=True")
     if build_graph:
@@ -204,6 +209,115 @@ def parse_gfa(
     raw = _run(path, opts)
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
                     verbose=verbose, build_matrix=build_matrix, path=path)
+
+
+def _parse_gfa_split(path, *, build_matrix: bool, directed: bool, weight_tag, strip_orientation: bool,
+                     bidirected: bool, keep_directed_bidir: bool, dtype, asymmetric: bool, raw_bytes_id: bool,
+                     return_node_list: bool, device: int, build=None):
+    """``parse_gfa(..., split_on_alignment=True)`` matrix outputs (builders.py:302-568).
+
+    1. The input is parsed on the GPU as the plain path parses it: every parser error, the
+       one-shot unsupported-record warning and gzip failures are the reference's (its split
+       path runs the same GFAParser loop over the whole input first, builders.py:330-346).
+    2. ``g2n_split_render`` (csrc/g2n_split.cpp) cuts the segments at the E/C coordinates,
+       re-targets the records (builders.py:348-430) and renders that record stream as GFA text;
+       the ">10x" and "skipping ..." warnings are emitted here in the reference's order.
+    3. The GPU builds the rendered stream with the caller's options (builders.py:460-557: the
+       same matrix loop, COO, ``A.maximum(A.T)`` and node list).  Bidirected: the interval
+       segments mint their plain keys first (builders.py:474-476), ahead of the GPU's nodes.
+    verbose prints nothing on this path for matrix outputs (builders.py:536-537 is graph-only).
+    ``build(src, mode, want_names) -> RawResult`` runs one build (default: the GPU through the
+    C-ABI; src is a path or bytes) — the CPU tests pass the oracle as the checker.
+    """
+    dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
+    if build is None:
+        def build(src, mode: dict, want_names: bool):
+            o = nat.make_options(output=nat.OUT_PARSE, want_node_names=want_names, device=device,
+                                 **{k: v for k, v in mode.items() if k != "dtype"}, dtype=mode.get("dtype", "float64"))
+            return nat.build_from_path(src, o) if isinstance(src, str) else nat.build_from_buffer(src, o)
+    data = None
+    if hasattr(path, "read"):
+        data = path.read()
+    elif str(path) == "-":
+        data = sys.stdin.buffer.read()
+    else:
+        p = str(path)
+        try:
+            with open(p, "rb") as fh:
+                blob = fh.read()
+        except OSError:
+            blob = None  # the build raises the reference's OSError
+        if blob is not None and p.endswith(".gz"):
+            try:
+                data, _ = nat.gunzip(blob)
+            except nat.GzipFailure:
+                data = None  # corrupt gzip: the plain path's prefix semantics decide
+        else:
+            data = blob
+    raw0 = build(str(path) if data is None else data, {"asymmetric": True}, False)
+    finalize(raw0, dtype=np.dtype("float64"), return_node_list=False, raw_bytes_id=raw_bytes_id, verbose=False,
+             build_matrix=False, path=path)
+    if raw0.status != nat.OK:
+        raise_for_status(raw0, np.dtype("float64"), path)
+    del raw0
+    text, blob, offs, warns, many, per_seg = nat.split_render(data, bidirected)
+    if many:
+        warnings.warn("split-on-alignment created >10x more nodes", RuntimeWarning, stacklevel=3)
+    for kind, seg in warns:
+        if kind == 0:
+            warnings.warn(f"skipping edge with undefined coordinates on segment {seg.decode()}", RuntimeWarning,
+                          stacklevel=3)
+        else:
+            warnings.warn(f"skipping link with undefined segment {seg.decode()}", RuntimeWarning, stacklevel=3)
+    if not build_matrix:
+        return None
+    raw = build(text, dict(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                           asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
+                           weight_tag=weight_tag or None), bool(return_node_list))
+    m = len(offs) - 1
+    if bidirected and raw.status == nat.OK and m:
+        # builders.py:348-377 + 460-476: segment s's records are its k intervals (plain keys), then
+        # its k - 1 chain links, which mint its 2k oriented keys (k with keep_directed_bidir) in
+        # the GPU's order; the edges' keys follow.  So GPU node g of block s moves to
+        # (nodes before s) + k + (g - its block start): a monotonic map.
+        n_gpu = int(raw.n_nodes)
+        k = per_seg.astype(np.int64)
+        c = np.where(k >= 2, k if keep_directed_bidir else 2 * k, 0)
+        if m + n_gpu >= 2 ** 31:
+            raise NotImplementedError("more than 2**31-1 nodes")
+        gmap = np.arange(n_gpu, dtype=np.int64) + m
+        blk_start = np.concatenate([[0], np.cumsum(c)])[:-1]
+        before = np.concatenate([[0], np.cumsum(k + c)])[:-1]
+        n_blk = int(c.sum())
+        seg_of_g = np.repeat(np.arange(len(k)), c)
+        gmap[:n_blk] = before[seg_of_g] + k[seg_of_g] + (np.arange(n_blk) - blk_start[seg_of_g])
+        gmap = gmap.astype(np.int32)
+        n_fin = m + n_gpu
+        if raw.format == "coo":
+            raw.rows = gmap[raw.rows]
+            raw.cols = gmap[raw.cols]
+        else:
+            cnt = np.zeros(n_fin, dtype=np.int64)
+            cnt[gmap] = np.diff(raw.indptr.astype(np.int64))
+            raw.indptr = np.concatenate([[0], np.cumsum(cnt)]).astype(raw.indptr.dtype)
+            raw.indices = gmap[raw.indices]
+        if return_node_list:
+            gb = raw.names_blob if raw.names_blob is not None else np.zeros(0, dtype=np.uint8)
+            go = raw.names_offsets if raw.names_offsets is not None else np.zeros(1, dtype=np.int64)
+            pieces = [None] * n_fin
+            is_gpu = np.zeros(n_fin, dtype=bool)
+            is_gpu[gmap] = True
+            for dst, i in zip(np.flatnonzero(~is_gpu), range(m)):
+                pieces[dst] = blob[offs[i]:offs[i + 1]].tobytes()
+            for g in range(n_gpu):
+                pieces[gmap[g]] = gb[go[g]:go[g + 1]].tobytes()
+            raw.names_blob = np.frombuffer(b"".join(pieces), dtype=np.uint8)
+            raw.names_offsets = np.concatenate([[0], np.cumsum([len(x) for x in pieces])]).astype(np.int64)
+        raw.n_nodes = n_fin
+    elif not bidirected and return_node_list and raw.status == nat.OK and raw.names_offsets is None:
+        raw.names_blob, raw.names_offsets = np.zeros(0, dtype=np.uint8), np.zeros(1, dtype=np.int64)
+    return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=False,
+                    path=path)
 
 
 def _dist_world() -> int:
@@ -305,7 +419,7 @@ def parse_gfa_names(path, *, raw_bytes_id: bool = False, **kw):
     if kw.get("backend", "networkx") == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
     if kw.pop("split_on_alignment", False):
-        raise NotImplementedError("split_on_alignment is outside the GPU GFA->CSR path")
+        raise NotImplementedError("split_on_alignment is not offered by the convert CLI path (use parse_gfa)")
     if kw.pop("build_graph", False):
         raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
     for k in ("store_seq", "store_tags", "max_tag_mb", "backend"):

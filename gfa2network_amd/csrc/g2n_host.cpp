@@ -111,7 +111,7 @@ static FillFn fill_from(const Inflated& z) {
   };
 }
 
-static int guarded(const std::function<int()>& f) {
+int guarded(const std::function<int()>& f) {
   try {
     return f();
   } catch (const Failure& e) {

@@ -89,6 +89,8 @@ struct Inflated {
   size_t total = 0;
   int members = 0;
 };
+// Runs f; a Failure / bad_alloc / std::exception becomes its status + g2n_last_error().
+int guarded(const std::function<int()>& f);
 bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out);
 // One gzip member spanning the whole file (zero padding after it allowed), inflated chunk-parallel
 // (g2n_pinflate.cpp); chunk_bytes 0 = sized for the host threads.  false = declined (not one

@@ -188,6 +188,25 @@ int g2n_gunzip_chunked(const void *buf, size_t len, size_t chunk_bytes, void **o
                        int32_t *chunks);
 void g2n_free(void *p);
 
+/* parse_gfa(..., split_on_alignment=True) (builders.py:110-128 -> _parse_gfa_split,
+ * builders.py:302-568), host side: the segments cut at the E / C alignment coordinates, the
+ * records re-targeted to the intervals, and that record stream rendered as GFA text ("S" lines
+ * for the interval segments unless bidirected, "E\t*\tu\tori\tv\tori[\ttags]" for every link
+ * and edge) for g2n_build_from_buffer to build with the reference's main-path semantics.  The
+ * input must have parsed cleanly first (errors are the plain parse's).  names = the interval
+ * segments in mint order (bidirected: placed before the GPU build's nodes); warn_* = the
+ * "skipping edge / link" warnings in order (kind 0 edge, 1 link; the segment bytes);
+ * many_nodes = the ">10x more nodes" warning; g2n_split_segments = intervals per segment.  G2N_E_UNSUPPORTED for a length or coordinate
+ * beyond int64.  Free with g2n_split_free. */
+typedef struct g2n_split_out g2n_split_out;
+int g2n_split_render(const void *buf, size_t len, int32_t bidirected, g2n_split_out **out);
+void g2n_split_get(const g2n_split_out *o, const uint8_t **text, uint64_t *text_len, const uint8_t **names,
+                   const int64_t **name_offs, uint64_t *n_names, const uint8_t **warn_segs,
+                   const int64_t **warn_offs, const int32_t **warn_kind, uint64_t *n_warn, int32_t *many_nodes);
+/* intervals per segment (the segments dict's order): the bidirected id map's block sizes */
+void g2n_split_segments(const g2n_split_out *o, const int64_t **intervals, uint64_t *n_segments);
+void g2n_split_free(g2n_split_out *o);
+
 /* The node list's bytes joined by `sep` (builders.py:284-288 node_list, built in one pass by
  * the Python shim): out (n_names ? blob_len + n_names - 1 : 0 bytes) = name 0, sep, name 1, ...
  * with name i = blob[offsets[i] .. offsets[i+1]).  Host memory, parallel over host threads. */

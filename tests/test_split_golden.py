@@ -1,0 +1,114 @@
+"""parse_gfa(..., split_on_alignment=True) (builders.py:110-128 -> _parse_gfa_split,
+builders.py:302-568) against fixtures the REAL reference produced
+(tests/golden/make_split_golden.py -> expected/split.json: 60+ inputs x 8 flag modes; the
+returned matrix bit for bit, node list, RuntimeWarnings in order, exception type + message).
+
+CPU: the product's host logic (api._parse_gfa_split: the split mapping and rendering of
+csrc/g2n_split.cpp, the warnings, the bidirected id shift) with the ORACLE as the build engine
+(the checker stands in for the GPU build only).  GPU: the product end to end (the GPU parse,
+the native split render, the GPU build of the rendered stream)."""
+from __future__ import annotations
+
+import base64
+import json
+import warnings
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+HERE = Path(__file__).resolve().parent / "golden"
+DATA = json.loads((HERE / "expected" / "split.json").read_text())
+MODES, CASES = DATA["modes"], DATA["cases"]
+KEYS = sorted(CASES)
+
+
+def _check(key: str, call) -> None:
+    exp = CASES[key]
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        try:
+            A, nodes = call()
+            exc = None
+        except Exception as e:  # noqa: BLE001 - compared as data
+            exc = [type(e).__name__, str(e)]
+    got_w = [[w.category.__name__, str(w.message)] for w in ws]
+    assert exc == exp["exc"], key
+    assert got_w == exp["warnings"], key
+    if exc is not None:
+        return
+    assert A.format == exp["format"] and list(A.shape) == exp["shape"] and str(A.dtype) == exp["dtype"], key
+    arrs = {"indptr": A.indptr, "indices": A.indices} if A.format == "csr" else {"row": A.row, "col": A.col}
+    arrs["data"] = A.data
+    for name, (dt, b64) in exp["arrays"].items():
+        assert str(arrs[name].dtype) == dt, (key, name)
+        assert np.ascontiguousarray(arrs[name]).tobytes() == base64.b64decode(b64), (key, name)
+    want = [base64.b64decode(x) for x in exp["nodes"]]
+    got = [x if isinstance(x, bytes) else x.encode() for x in nodes]
+    assert got == want, key
+    assert (bool(nodes) and isinstance(nodes[0], bytes)) == exp["nodes_bytes"], key
+
+
+def _oracle_build(oracle_lib):
+    from oracle import oracle
+
+    def build(src, mode, want_names):
+        assert not isinstance(src, str), "golden inputs are clean: the bytes are always in hand"
+        return oracle.to_raw(oracle.run(bytes(src), **mode), "parse")
+
+    return build
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_split_host_logic_with_oracle_engine(oracle_lib, key):
+    from gfa2network_amd.api import _parse_gfa_split
+
+    path, mode = key.split("|")
+    kw = dict(MODES[mode])
+    kw.setdefault("directed", True)
+    _check(key, lambda: _parse_gfa_split(
+        str(HERE / path), build_matrix=True, directed=kw.get("directed", True), weight_tag=kw.get("weight_tag"),
+        strip_orientation=kw.get("strip_orientation", False), bidirected=kw.get("bidirected", False),
+        keep_directed_bidir=kw.get("keep_directed_bidir", False), dtype=kw.get("dtype", "float64"),
+        asymmetric=kw.get("asymmetric", False), raw_bytes_id=kw.get("raw_bytes_id", False), return_node_list=True,
+        device=0, build=_oracle_build(oracle_lib)))
+
+
+def test_split_render_text_shapes():
+    from gfa2network_amd import _native
+
+    text, blob, offs, warns, many, _ = _native.split_render(
+        b"S\ta\t10\t*\nS\tb\t4\t*\nE\te\ta+\t2\t6\tb-\t0\t4\t*\tRC:i:3\nL\ta\t+\tq\t-\t0M\n", False)
+    names = [bytes(blob[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    assert names == [b"a:0-2", b"a:2-6", b"a:6-10", b"b:0-4"]
+    assert bytes(text).splitlines() == [
+        b"S\ta:0-2", b"S\ta:2-6", b"S\ta:6-10", b"E\t*\ta:0-2\t+\ta:2-6\t+", b"E\t*\ta:2-6\t+\ta:6-10\t+",
+        b"S\tb:0-4", b"E\t*\ta:2-6\t+\tb:0-4\t-\tRC:i:3"]
+    assert warns == [(1, b"q")] and not many
+    # a coordinate beyond int64 is outside this implementation (Python ints are unbounded)
+    with pytest.raises(NotImplementedError):
+        _native.split_render(b"S\ta\t99999999999999999999\t*\n", False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", KEYS)
+def test_split_gpu_equals_reference(gpu, key):
+    from gfa2network_amd import parse_gfa
+
+    path, mode = key.split("|")
+    _check(key, lambda: parse_gfa(str(HERE / path), build_graph=False, build_matrix=True, return_node_list=True,
+                                  split_on_alignment=True, **MODES[mode]))
+
+
+@pytest.mark.gpu
+def test_split_gpu_file_object_and_build_matrix_false(gpu):
+    import io
+
+    from gfa2network_amd import parse_gfa
+
+    key = "inputs_split/e_coords.gfa|bidir"
+    data = (HERE / "inputs_split" / "e_coords.gfa").read_bytes()
+    _check(key, lambda: parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, return_node_list=True,
+                                  split_on_alignment=True, **MODES["bidir"]))
+    # builders.py:563-568: neither output requested -> None (after the parse and the warnings)
+    assert parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=False, split_on_alignment=True) is None
