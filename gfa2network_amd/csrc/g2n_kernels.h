@@ -19,8 +19,14 @@
 namespace g2n {
 
 constexpr int kTPB = 256;
-constexpr uint64_t kTile = 32768;     // input bytes per front-end block (K1, K2)
-constexpr uint32_t kTileHalo = 2048;  // bytes staged past the tile for lines that end beyond it
+#ifndef G2N_TILE_BYTES  // experiment builds (tools/exp_build.sh) may override the tile shape
+#define G2N_TILE_BYTES 32768
+#endif
+#ifndef G2N_TILE_HALO
+#define G2N_TILE_HALO 2048
+#endif
+constexpr uint64_t kTile = G2N_TILE_BYTES;    // input bytes per front-end block (K1, K2)
+constexpr uint32_t kTileHalo = G2N_TILE_HALO; // bytes staged past the tile for lines that end beyond it
 
 enum : uint8_t { kSkip = 0, kUnknown = 1, kS = 2, kEdge = 3, kPO = 4 };
 

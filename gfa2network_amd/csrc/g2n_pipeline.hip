@@ -692,7 +692,7 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
 // stream-order COO (S_ROWS / S_COLS, sized n_edges * ktrip as run_build will ask).  False when
 // anything breaks the premise or needs the full parse (errors, warnings, deferred lines, a full
 // slot): the caller then runs K1 and the classic parse, as if this had not run.
-constexpr uint32_t kTileEdgeCap = 2736;  // > 32 KiB / 12 B: a lean edge line is at least 12 bytes
+constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge line is at least 12 bytes (2736 for 32 KiB)
 
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out) {
