@@ -10,6 +10,7 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include <functional>
 #include <random>
 #include <string>
 #include <vector>
@@ -19,6 +20,14 @@
 namespace g2n {
 static thread_local std::string t_err;
 void set_last_error(const std::string& msg) { t_err = msg; }  // g2n_host.cpp's, not linked here
+int guarded(const std::function<int()>& f) {  // g2n_host.cpp's, not linked here
+  try {
+    return f();
+  } catch (const Failure& e) {
+    set_last_error(e.what());
+    return e.status;
+  }
+}
 }  // namespace g2n
 
 static int failures = 0;
@@ -159,7 +168,54 @@ static void writer_checks() {
   rmdir(dir);
 }
 
+// g2n_split_render (split_on_alignment's record mapping) on random GFA2 / GFA1 records:
+// coordinates in and out of range, missing segments, duplicate S, fallbacks, ragged lines.
+static void split_checks() {
+  std::mt19937_64 rng(11);
+  for (int trial = 0; trial < 200; trial++) {
+    std::string t;
+    const int ns = 1 + (int)(rng() % 6);
+    auto seg = [&] { return std::string(1, (char)('a' + rng() % (ns + 2))); };
+    for (int i = 0; i < 40; i++) {
+      switch (rng() % 6) {
+        case 0: t += "S\t" + seg() + "\t" + std::to_string((int)(rng() % 12) - 2) + "\t*\n"; break;
+        case 1: t += "S\t" + seg() + (rng() % 2 ? "\t*" : "") + "\n"; break;
+        case 2:
+          t += "E\te\t" + seg() + "+\t" + std::to_string(rng() % 9) + "\t" + std::to_string(rng() % 12) + "\t" + seg() +
+               "-\t" + std::to_string((int)(rng() % 9) - 1) + "\t" + std::to_string(rng() % 12) + "\t*" +
+               (rng() % 2 ? "\tRC:i:3" : "") + "\n";
+          break;
+        case 3: t += "C\t" + seg() + "\t+\t" + seg() + "\t-\t" + std::to_string(rng() % 5) + "\t*\n"; break;
+        case 4: t += "L\t" + seg() + "\t+\t" + seg() + "\t-\t0M\n"; break;
+        default: t += "L\t" + seg() + "+\t" + seg() + "\t*\r\n"; break;
+      }
+    }
+    if (rng() % 3 == 0) t.resize(rng() % (t.size() + 1));  // ragged last line
+    for (int bidir = 0; bidir < 2; bidir++) {
+      g2n_split_out* o = nullptr;
+      const int rc = g2n_split_render(t.data(), t.size(), bidir, &o);
+      if (rc != G2N_OK) {
+        CHECK(o == nullptr);  // a short record the GPU parse would have rejected first
+        continue;
+      }
+      const uint8_t *text, *names, *ws;
+      const int64_t *no, *wo, *per;
+      const int32_t* wk;
+      uint64_t tl, nn, nw, nsg;
+      int32_t many;
+      g2n_split_get(o, &text, &tl, &names, &no, &nn, &ws, &wo, &wk, &nw, &many);
+      g2n_split_segments(o, &per, &nsg);
+      int64_t sum = 0;
+      for (uint64_t k = 0; k < nsg; k++) sum += per[k];
+      CHECK((uint64_t)sum == nn && no[0] == 0);
+      CHECK(tl == 0 || text[tl - 1] == '\n');
+      g2n_split_free(o);
+    }
+  }
+}
+
 int main() {
+  split_checks();
   gzip_checks();
   writer_checks();
   if (failures) return 1;

@@ -20,7 +20,7 @@ def test_host_code_under_asan_ubsan(tmp_path):
     exe = tmp_path / "sancheck"
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
            "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-           str(ROOT / "tests" / "native" / "sancheck.cpp"), str(CSRC / "g2n_ingest.cpp"), str(CSRC / "g2n_pinflate.cpp"),
+           str(ROOT / "tests" / "native" / "sancheck.cpp"), str(CSRC / "g2n_ingest.cpp"), str(CSRC / "g2n_pinflate.cpp"), str(CSRC / "g2n_split.cpp"),
            str(CSRC / "g2n_writers.cpp"), "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lamdhip64", "-lz",
            "-lpthread", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, timeout=300)
