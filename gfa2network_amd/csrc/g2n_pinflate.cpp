@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <immintrin.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -471,6 +472,68 @@ bool plausible_start(const uint8_t* in, size_t n, uint64_t p) {
   return true;
 }
 
+// CRC-32 (gzip's reflected 0x04C11DB7) by carry-less multiplication: four 128-bit lanes folded
+// over 64-byte blocks, folded to one lane, to 64 bits, then a Barrett reduction (Intel's
+// "Fast CRC Computation for Generic Polynomials Using PCLMULQDQ"; the constants are
+// x^k mod P for the fold distances and the Barrett pair).  crc is zlib's running value.
+__attribute__((target("pclmul,sse4.1"))) inline __m128i fold(__m128i x, __m128i kk, __m128i y) {
+  return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, kk, 0x00), _mm_clmulepi64_si128(x, kk, 0x11)), y);
+}
+
+__attribute__((target("pclmul,sse4.1"))) uint32_t crc32_fold(uint32_t crc, const uint8_t* p, size_t n) {
+  if (n < 64) return (uint32_t)crc32(crc, p, (uInt)n);
+  alignas(16) static const uint64_t k12[2] = {0x0154442bd4ull, 0x01c6e41596ull};
+  alignas(16) static const uint64_t k34[2] = {0x01751997d0ull, 0x00ccaa009eull};
+  alignas(16) static const uint64_t k50[2] = {0x0163cd6124ull, 0};
+  alignas(16) static const uint64_t pmu[2] = {0x01db710641ull, 0x01f7011641ull};
+  const size_t body = n & ~(size_t)15;
+  const uint8_t* q = p;
+  size_t left = body;
+  __m128i a0 = _mm_loadu_si128((const __m128i*)q), a1 = _mm_loadu_si128((const __m128i*)(q + 16));
+  __m128i a2 = _mm_loadu_si128((const __m128i*)(q + 32)), a3 = _mm_loadu_si128((const __m128i*)(q + 48));
+  a0 = _mm_xor_si128(a0, _mm_cvtsi32_si128((int)~crc));
+  __m128i k = _mm_load_si128((const __m128i*)k12);
+  q += 64;
+  left -= 64;
+  while (left >= 64) {
+    a0 = fold(a0, k, _mm_loadu_si128((const __m128i*)q));
+    a1 = fold(a1, k, _mm_loadu_si128((const __m128i*)(q + 16)));
+    a2 = fold(a2, k, _mm_loadu_si128((const __m128i*)(q + 32)));
+    a3 = fold(a3, k, _mm_loadu_si128((const __m128i*)(q + 48)));
+    q += 64;
+    left -= 64;
+  }
+  k = _mm_load_si128((const __m128i*)k34);
+  a0 = fold(a0, k, a1);
+  a0 = fold(a0, k, a2);
+  a0 = fold(a0, k, a3);
+  while (left >= 16) {
+    a0 = fold(a0, k, _mm_loadu_si128((const __m128i*)q));
+    q += 16;
+    left -= 16;
+  }
+  const __m128i lo32 = _mm_setr_epi32(~0, 0, ~0, 0);
+  __m128i x = _mm_xor_si128(_mm_srli_si128(a0, 8), _mm_clmulepi64_si128(a0, k, 0x10));  // 128 -> 64 bits
+  const __m128i k5 = _mm_loadl_epi64((const __m128i*)k50);
+  x = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(x, lo32), k5, 0x00), _mm_srli_si128(x, 4));
+  const __m128i pm = _mm_load_si128((const __m128i*)pmu);  // Barrett reduction to 32 bits
+  __m128i t = _mm_clmulepi64_si128(_mm_and_si128(x, lo32), pm, 0x10);
+  t = _mm_clmulepi64_si128(_mm_and_si128(t, lo32), pm, 0x00);
+  crc = ~(uint32_t)_mm_extract_epi32(_mm_xor_si128(x, t), 1);
+  return n > body ? (uint32_t)crc32(crc, p + body, (uInt)(n - body)) : crc;
+}
+
+uint32_t crc32_any(uint32_t crc, const uint8_t* p, size_t n) {
+  static const bool clmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+  if (clmul) return crc32_fold(crc, p, n);
+  for (size_t o = 0; o < n;) {
+    const size_t step = std::min<size_t>(n - o, (size_t)1 << 30);
+    crc = (uint32_t)crc32(crc, p + o, (uInt)step);
+    o += step;
+  }
+  return crc;
+}
+
 size_t gzip_header_end(const uint8_t* in, size_t n) {
   if (n < 18 || in[0] != 0x1F || in[1] != 0x8B || in[2] != 8) return 0;
   const uint8_t flg = in[3];
@@ -597,18 +660,19 @@ bool gunzip_chunked(const uint8_t* in, size_t n, size_t chunk_bytes, Inflated& o
   parallel_for(chain.size(), T, [&](size_t i) {
     Chunk& x = ch[chain[i]];
     const uint8_t* w = x.win.get();
-    for (size_t p = 0; p < x.dirty_len; p++) {
-      const uint16_t v = x.sh.p[kWin + p];
-      x.out.p[p] = v < 256 ? (uint8_t)v : w[v - 256];
+    const uint16_t* sh = x.sh.p ? x.sh.p + kWin : nullptr;
+    uint32_t c = 0;
+    for (size_t o = 0; o < x.out.n;) {  // 64 KiB pieces: resolved, then CRC'd while in cache
+      const size_t e = std::min(x.out.n, o + ((size_t)1 << 16));
+      for (size_t p = o; p < std::min(e, x.dirty_len); p++) {
+        const uint16_t v = sh[p];
+        x.out.p[p] = v < 256 ? (uint8_t)v : w[v - 256];
+      }
+      c = crc32_any(c, x.out.p + o, e - o);
+      o = e;
     }
     free(x.sh.p);
     x.sh.p = nullptr;
-    uLong c = crc32(0L, Z_NULL, 0);
-    for (size_t o = 0; o < x.out.n;) {
-      const size_t step = std::min<size_t>(x.out.n - o, (size_t)1 << 30);
-      c = crc32(c, x.out.p + o, (uInt)step);
-      o += step;
-    }
     crc[i] = c;
   });
   uLong total_crc = crc32(0L, Z_NULL, 0);
