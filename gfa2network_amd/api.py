@@ -418,10 +418,15 @@ def parse_gfa_names(path, *, raw_bytes_id: bool = False, **kw):
     here unless raw_bytes_id, exactly where building the list would (builders.py:284-288)."""
     if kw.get("backend", "networkx") == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
-    if kw.pop("split_on_alignment", False):
-        raise NotImplementedError("split_on_alignment is not offered by the convert CLI path (use parse_gfa)")
     if kw.pop("build_graph", False):
         raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
+    if kw.pop("split_on_alignment", False):  # cli.py:111-115 --split-on-alignment: through the list
+        A, nodes = parse_gfa(path, build_graph=False, build_matrix=True, return_node_list=True,
+                             split_on_alignment=True, raw_bytes_id=raw_bytes_id, **kw)
+        enc = [x if raw_bytes_id else x.encode() for x in nodes]
+        offs = np.zeros(len(enc) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(x) for x in enc], dtype=np.int64)
+        return A, np.frombuffer(b"".join(enc), dtype=np.uint8), offs
     for k in ("store_seq", "store_tags", "max_tag_mb", "backend"):
         kw.pop(k, None)
     verbose = kw.pop("verbose", False)

@@ -112,3 +112,33 @@ def test_split_gpu_file_object_and_build_matrix_false(gpu):
                                   split_on_alignment=True, **MODES["bidir"]))
     # builders.py:563-568: neither output requested -> None (after the parse and the warnings)
     assert parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=False, split_on_alignment=True) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode,flags", [("e_coords", "default", []), ("c_records", "bidir", ["--bidirected"]),
+                                            ("many_nodes", "asym", ["--asymmetric"])])
+def test_split_cli_convert(gpu, tmp_path, name, mode, flags):
+    """`convert --split-on-alignment --matrix x.npz` (cli.py:111-115, 193-250): the .npz holds
+    convert_format(A, "csr") of the reference's split matrix, the sidecar its node list."""
+    import subprocess
+    import sys
+
+    import scipy.sparse as sp
+
+    out = tmp_path / "x.npz"
+    subprocess.run([sys.executable, "-m", "gfa2network_amd", "convert", str(HERE / "inputs_split" / f"{name}.gfa"),
+                    "--matrix", str(out), "--split-on-alignment", *flags], check=True, capture_output=True,
+                   cwd=Path(__file__).resolve().parents[1])
+    exp = CASES[f"inputs_split/{name}.gfa|{mode}"]
+    arr = {k: np.frombuffer(base64.b64decode(b), dtype=dt) for k, (dt, b) in exp["arrays"].items()}
+    n = exp["shape"][0]
+    if exp["format"] == "csr":
+        want = sp.csr_matrix((arr["data"], arr["indices"], arr["indptr"]), shape=(n, n))
+    else:
+        want = sp.coo_matrix((arr["data"], (arr["row"], arr["col"])), shape=(n, n)).tocsr()
+    A = sp.load_npz(out)
+    assert A.format == "csr"
+    for k in ("indptr", "indices", "data"):
+        assert np.array_equal(getattr(A, k), getattr(want, k)), k
+    names = [base64.b64decode(x).decode() for x in exp["nodes"]]
+    assert Path(str(out) + ".nodes.tsv").read_text() == "".join(f"{i}\t{v}\n" for i, v in enumerate(names))
