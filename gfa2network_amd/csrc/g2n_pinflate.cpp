@@ -296,6 +296,7 @@ struct Dec {
   Chunk& c;
   bool dirty;
   uint64_t last_dirty_end = 0;  // 1 + position of the latest unknown-window byte
+  size_t trial_cap = ~(size_t)0;  // output bound of a trial decode (a false block start may babble)
   Dec(Chunk& c_, bool unknown_window) : c(c_), dirty(unknown_window) {
     if (dirty) {
       c.sh.room(std::max<size_t>(kWin + ((size_t)1 << 20), kWin + c.out.cap));
@@ -323,6 +324,7 @@ struct Dec {
           break;
         }
         if (cap - n < 300 || shcap - n < 300) {
+          if (n > trial_cap) goto done;
           out.n = n;
           out.room(300);
           op = out.p;
@@ -366,6 +368,7 @@ struct Dec {
     }
     for (;;) {
       if (cap - n < 300) {
+        if (n > trial_cap) break;
         out.n = n;
         out.room(300);
         op = out.p;
@@ -460,6 +463,7 @@ bool plausible_start(const uint8_t* in, size_t n, uint64_t p) {
   if (!read_dynamic(br, lit, dist)) return false;
   Chunk scratch;
   Dec dec(scratch, true);
+  dec.trial_cap = (size_t)8 << 20;  // a real block holds <= 16K symbols (zlib): <= 4.2 MB of output
   if (!dec.codes(br, lit, dist) || br.over || scratch.out.n == 0) return false;
   br.refill();
   const unsigned type = (unsigned)((br.bb >> 1) & 3);
