@@ -903,15 +903,16 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
                                  uint64_t t0, uint64_t tb, uint64_t eb, const ParseOpts& op, const TouchOut& T,
                                  IntState& is) {
   const uint32_t n = next - 1 - so;
-  if (n > 48) return false;
+  if (n > 48 && k != kS) return false;
   const uint32_t q = so >> 4, sh = so & 15;
   const uint64_t w = (uint64_t)tabm[q] | ((uint64_t)tabm[q + 1] << 16) | ((uint64_t)tabm[q + 2] << 32) |
                      ((uint64_t)tabm[q + 3] << 48);
-  uint64_t m = (w >> sh) & ((1ull << n) - 1);
-  if (k == kS) {
-    if (!m) return false;  // one field: the general path raises
+  uint64_t m = (w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1);
+  if (k == kS) {  // the name is all it needs: any length, as long as both its tabs are in view
+    if (!m) return false;  // one field (or a name past the view): the general path decides
     const uint32_t t1 = (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
+    if (!m && n > 48) return false;
     const uint32_t t2 = m ? (uint32_t)__builtin_ctzll(m) : n;
     // no touch descriptor: a lean build that holds its premise derives the names (k_names_dec);
     // one that breaks it re-parses in full
@@ -968,6 +969,12 @@ struct DeferredLine {  // at most one per tile: the line holding the tile window
 // decoupled look-back over the tiles instead (no K1) measured 12.0 ms on C4 against 2.2 + 6.3
 // ms: in-order waiting across the 8 XCDs (status words polled past the non-coherent L2s) stalls
 // every tile behind the slowest.
+// The tile-local lean instance parses every line through the lean shapes (a line outside them
+// gives that parse up: the full parse runs instead), so it carries none of the general parser's
+// registers (166 -> 116 VGPRs; parse 5.64 -> 5.45 ms on C4).  0: the general parser inline.
+#ifndef G2N_LEAN_ONLY
+#define G2N_LEAN_ONLY 1
+#endif
 constexpr uint32_t kTileLines = kTileChunks;            // line starts per window (= chunks: pre[] holds both)
 constexpr uint32_t kLinesPer = kTileLines / kTPB;       // lines classified per thread
 static_assert(kChunkIters % 4 == 0 && kTile <= 32768, "tile layout: per-tile counts fit 16 bits");
@@ -1111,6 +1118,44 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     }
     __syncthreads();
     // (4) parse: lane-parallel lines
+#if G2N_LEAN_ONLY
+    if constexpr (kLocal) {  // the lean shapes only: any other line gives the tile-local parse up
+#pragma unroll 1
+      for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
+        const uint32_t o = starts[j];
+        const uint8_t k = lkind[j];
+        if (k == kUnknown) {
+          const uint64_t i = idx0 + w0 + j;
+          unk = i < unk ? i : unk;
+        }
+        if (k != kS && k != kEdge && k != kPO) continue;
+        uint32_t next = 0;  // 1 + the line's '\n' (or its virtual one at EOF), tile-local
+        if (j + 1 < n_win) {
+          next = starts[j + 1];
+        } else {
+          const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);
+          uint32_t x = o;
+          while (x < lim && buf[x] != '\n') x++;
+          if (x < lim || lim == len - t0) next = x + 1;
+        }
+        if (!next) {
+          is.fail = 1;
+          continue;
+        }
+        if (k == kPO) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
+          const uint32_t n = next - 1 - o, qq = o >> 4, sh = o & 15;
+          const uint64_t w = (uint64_t)tabm[qq] | ((uint64_t)tabm[qq + 1] << 16) | ((uint64_t)tabm[qq + 2] << 32) |
+                             ((uint64_t)tabm[qq + 3] << 48);
+          if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
+          continue;
+        }
+        const uint32_t pr = pre[j];
+        const uint64_t tb = t_run + (uint64_t)(pr >> 16) + 2 * (uint64_t)(pr & 0xFFFF);
+        const uint64_t eb = e_run + (pr & 0xFFFF);
+        if (!lean_line(buf, tabm, o, next, k, t0, tb, eb, op, T, is)) is.fail = 1;
+      }
+    } else
+#endif
 #pragma unroll 1
     for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
       const uint32_t o = starts[j];
