@@ -899,14 +899,25 @@ __device__ inline bool dec_lds(const uint8_t* buf, uint32_t x, uint32_t l, uint6
   return true;
 }
 
+// tab bits of the 64 staged bytes from chunk q: from the tile's tab bitmap, or (tabm == nullptr)
+// recomputed from the staged bytes (the LDS-lean instance keeps no bitmap)
+__device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, uint32_t q) {
+  if (tabm)
+    return (uint64_t)tabm[q] | ((uint64_t)tabm[q + 1] << 16) | ((uint64_t)tabm[q + 2] << 32) |
+           ((uint64_t)tabm[q + 3] << 48);
+  uint64_t w = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) w |= (uint64_t)mask16(*(const uint4*)(buf + 16 * (q + i)), 0x09090909u) << (16 * i);
+  return w;
+}
+
 __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next, uint8_t k,
                                  uint64_t t0, uint64_t tb, uint64_t eb, const ParseOpts& op, const TouchOut& T,
                                  IntState& is) {
   const uint32_t n = next - 1 - so;
   if (n > 48 && k != kS) return false;
-  const uint32_t q = so >> 4, sh = so & 15;
-  const uint64_t w = (uint64_t)tabm[q] | ((uint64_t)tabm[q + 1] << 16) | ((uint64_t)tabm[q + 2] << 32) |
-                     ((uint64_t)tabm[q + 3] << 48);
+  const uint32_t sh = so & 15;
+  const uint64_t w = tab_window(buf, tabm, so >> 4);
   uint64_t m = (w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1);
   if (k == kS) {  // the name is all it needs: any length, as long as both its tabs are in view
     if (!m) return false;  // one field (or a name past the view): the general path decides
@@ -975,6 +986,9 @@ struct DeferredLine {  // at most one per tile: the line holding the tile window
 #ifndef G2N_LEAN_ONLY
 #define G2N_LEAN_ONLY 1
 #endif
+#ifndef G2N_LEAN_LDS  // experiment: the LDS-lean tile-local instance (4 blocks per CU)
+#define G2N_LEAN_LDS 0
+#endif
 constexpr uint32_t kTileLines = kTileChunks;            // line starts per window (= chunks: pre[] holds both)
 constexpr uint32_t kLinesPer = kTileLines / kTPB;       // lines classified per thread
 static_assert(kChunkIters % 4 == 0 && kTile <= 32768, "tile layout: per-tile counts fit 16 bits");
@@ -989,13 +1003,20 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
                                                      uint64_t* __restrict__ worklist,
                                                      DeferredLine* __restrict__ deferred, uint64_t n_tiles,
                                                      TileCnt* __restrict__ tcnt_out, TileLean* __restrict__ tlean) {
+  // kDiet (the LDS-lean tile-local instance): half-size line windows, u16 chunk ranks aliased with
+  // the u32 line prefixes, no kind array and no tab bitmap (both re-read from the staged bytes)
+  constexpr bool kDiet = kLocal && G2N_LEAN_LDS;
+  constexpr uint32_t kWinL = kDiet ? kTileLines / 2 : kTileLines;
+  constexpr uint32_t kLinesPerW = kWinL / kTPB;
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t starts[kTileLines];
-  __shared__ __attribute__((aligned(16))) uint32_t pre[kTileChunks];  // chunk ranks, then line prefixes
-  __shared__ uint8_t lkind[kTileLines];
+  __shared__ __attribute__((aligned(16))) uint16_t starts[kWinL];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[kDiet ? kTileChunks / 2 : kTileChunks];  // chunk ranks, then line prefixes
+  uint16_t* const pre16 = (uint16_t*)pre;
+  __shared__ uint8_t lkind[kDiet ? 1 : kTileLines];
   __shared__ uint32_t red[kTPB / 64];
   constexpr uint32_t kMaskChunks = (uint32_t)((kTile + kTileHalo) / 16) + 4;  // + 4: tab_bits reads 4 ahead
-  __shared__ __attribute__((aligned(16))) uint16_t tabm[kMaskChunks];
+  __shared__ __attribute__((aligned(16))) uint16_t tabm_s[kDiet ? 1 : kMaskChunks];
+  uint16_t* const tabm = kDiet ? nullptr : tabm_s;
   const uint64_t tile = blockIdx.x;
   const uint64_t t0 = tile * kTile;
   {
@@ -1016,8 +1037,9 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   const TileCnt b = local ? TileCnt{} : base[tile];
   __syncthreads();
   // the tile's tab bitmap (bytes past len: 0): the tile's own chunks come with pass (1), here the halo's
-  for (uint32_t c = kTileChunks + threadIdx.x; c < kMaskChunks; c += kTPB)
-    tabm[c] = (uint16_t)(16 * c + 16 <= kTile + kTileHalo + 16 ? mask16(*(const uint4*)(buf + 16 * c), 0x09090909u) : 0u);
+  if constexpr (!kDiet)
+    for (uint32_t c = kTileChunks + threadIdx.x; c < kMaskChunks; c += kTPB)
+      tabm[c] = (uint16_t)(16 * c + 16 <= kTile + kTileHalo + 16 ? mask16(*(const uint4*)(buf + 16 * c), 0x09090909u) : 0u);
   const uint64_t w1 = t0 + kTile + kTileHalo < len ? t0 + kTile + kTileHalo : len;
   Src L{buf, t0, t0 + kTile + kTileHalo + 16};  // bytes past len are staged as 0
   L.tm = tabm;
@@ -1029,25 +1051,39 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   for (uint32_t j = 0; j < kChunkIters; j++) {
     const uint32_t c = j * kTPB + threadIdx.x;
     const uint4 v = *(const uint4*)(buf + 16 * c);
-    tabm[c] = (uint16_t)mask16(v, 0x09090909u);
+    if constexpr (!kDiet) tabm[c] = (uint16_t)mask16(v, 0x09090909u);
     uint32_t m, st;
     chunk_masks(buf, c, t0, len, tile_prev_nl, m, st, v);
     if (j & 1) stm[j >> 1] |= st << 16;
     else stm[j >> 1] = st;
-    pre[c] = (uint32_t)__popc(st);
+    if constexpr (kDiet) pre16[c] = (uint16_t)__popc(st);
+    else pre[c] = (uint32_t)__popc(st);
     if constexpr (kLocal) n_nl += (uint32_t)__popc(m);
   }
   __syncthreads();
   uint32_t n_starts;
   {  // kChunkIters consecutive chunk counts per thread (4-word vector accesses)
     uint32_t q[kChunkIters];
+    if constexpr (kDiet) {  // 8 u16 counts per 16-byte access
 #pragma unroll
-    for (uint32_t k = 0; k < kChunkIters; k += 4) {
-      const uint4 v = *(const uint4*)(pre + kChunkIters * threadIdx.x + k);
-      q[k] = v.x;
-      q[k + 1] = v.y;
-      q[k + 2] = v.z;
-      q[k + 3] = v.w;
+      for (uint32_t k = 0; k < kChunkIters; k += 8) {
+        const uint4 v = *(const uint4*)(pre16 + kChunkIters * threadIdx.x + k);
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          q[k + 2 * i] = x[i] & 0xFFFFu;
+          q[k + 2 * i + 1] = x[i] >> 16;
+        }
+      }
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kChunkIters; k += 4) {
+        const uint4 v = *(const uint4*)(pre + kChunkIters * threadIdx.x + k);
+        q[k] = v.x;
+        q[k + 1] = v.y;
+        q[k + 2] = v.z;
+        q[k + 3] = v.w;
+      }
     }
     uint32_t sum = 0;
 #pragma unroll
@@ -1060,22 +1096,30 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       q[k] = ex;
       ex += t;
     }
+    if constexpr (kDiet) {  // ranks < 2^15 (a chunk past the last start may wrap: never read)
 #pragma unroll
-    for (uint32_t k = 0; k < kChunkIters; k += 4)
-      *(uint4*)(pre + kChunkIters * threadIdx.x + k) = make_uint4(q[k], q[k + 1], q[k + 2], q[k + 3]);
+      for (uint32_t k = 0; k < kChunkIters; k += 8)
+        *(uint4*)(pre16 + kChunkIters * threadIdx.x + k) =
+            make_uint4((q[k] & 0xFFFFu) | (q[k + 1] << 16), (q[k + 2] & 0xFFFFu) | (q[k + 3] << 16),
+                       (q[k + 4] & 0xFFFFu) | (q[k + 5] << 16), (q[k + 6] & 0xFFFFu) | (q[k + 7] << 16));
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kChunkIters; k += 4)
+        *(uint4*)(pre + kChunkIters * threadIdx.x + k) = make_uint4(q[k], q[k + 1], q[k + 2], q[k + 3]);
+    }
   }
   const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
   __syncthreads();
   uint32_t rank[kChunkIters];
 #pragma unroll
-  for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = pre[j * kTPB + threadIdx.x];
+  for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = kDiet ? (uint32_t)pre16[j * kTPB + threadIdx.x] : pre[j * kTPB + threadIdx.x];
   uint64_t t_run = b.touches, e_run = b.edges, s_run = 0;
   uint32_t n_po = 0;
   unsigned long long unk = ~0ull;
   IntState is;
   const bool lean_fast = op.rows && !op.bidir && !op.has_wt && !op.strip;
-  for (uint32_t w0 = 0; w0 < n_starts; w0 += kTileLines) {
-    const uint32_t n_win = n_starts - w0 < kTileLines ? n_starts - w0 : kTileLines;
+  for (uint32_t w0 = 0; w0 < n_starts; w0 += kWinL) {
+    const uint32_t n_win = n_starts - w0 < kWinL ? n_starts - w0 : kWinL;
     __syncthreads();  // `pre` (ranks, or the last window's prefixes) is no longer read
     // (3) the window's starts, in order
 #pragma unroll
@@ -1086,22 +1130,22 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       while (st) {
         const uint32_t o = 16 * c + __builtin_ctz(st);
         st &= st - 1;
-        if (r >= w0 && r < w0 + kTileLines) starts[r - w0] = (uint16_t)o;
+        if (r >= w0 && r < w0 + kWinL) starts[r - w0] = (uint16_t)o;
         r++;
       }
     }
     __syncthreads();
     // kinds of kLinesPer consecutive lines per thread; prefix counts of S and edge lines
     uint32_t cs = 0, ce = 0;
-    uint8_t kk[kLinesPer];
+    uint8_t kk[kLinesPerW];
 #pragma unroll
-    for (uint32_t q = 0; q < kLinesPer; q++) {
-      const uint32_t j = kLinesPer * threadIdx.x + q;
+    for (uint32_t q = 0; q < kLinesPerW; q++) {
+      const uint32_t j = kLinesPerW * threadIdx.x + q;
       uint8_t k = kSkip;
       if (j < n_win) {
         const uint32_t o = starts[j];
         k = kind_at(buf, o, t0 + o, len);
-        lkind[j] = k;
+        if constexpr (!kDiet) lkind[j] = k;
       }
       kk[q] = k;
       cs += k == kS;
@@ -1111,8 +1155,8 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     uint32_t ex;
     const uint32_t tot = block_excl_scan_u32((cs << 16) | ce, &ex, red);
 #pragma unroll
-    for (uint32_t q = 0; q < kLinesPer; q++) {
-      const uint32_t j = kLinesPer * threadIdx.x + q;
+    for (uint32_t q = 0; q < kLinesPerW; q++) {
+      const uint32_t j = kLinesPerW * threadIdx.x + q;
       if (j < n_win) pre[j] = ex;
       ex += ((uint32_t)(kk[q] == kS) << 16) | (uint32_t)(kk[q] == kEdge);
     }
@@ -1123,7 +1167,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 #pragma unroll 1
       for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
         const uint32_t o = starts[j];
-        const uint8_t k = lkind[j];
+        const uint8_t k = kDiet ? kind_at(buf, o, t0 + o, len) : lkind[j];
         if (k == kUnknown) {
           const uint64_t i = idx0 + w0 + j;
           unk = i < unk ? i : unk;
@@ -1143,9 +1187,8 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
           continue;
         }
         if (k == kPO) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
-          const uint32_t n = next - 1 - o, qq = o >> 4, sh = o & 15;
-          const uint64_t w = (uint64_t)tabm[qq] | ((uint64_t)tabm[qq + 1] << 16) | ((uint64_t)tabm[qq + 2] << 32) |
-                             ((uint64_t)tabm[qq + 3] << 48);
+          const uint32_t n = next - 1 - o, sh = o & 15;
+          const uint64_t w = tab_window(buf, tabm, o >> 4);
           if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
           continue;
         }
