@@ -321,6 +321,7 @@ struct Dec {
         if (n >= ldirty + kWin) {  // window free of unknown bytes: plain decoding
           dirty = false;
           c.dirty_len = n;
+          for (size_t p = n - kWin; p < n; p++) op[p] = (uint8_t)sh[p];  // the plain decoder's history
           break;
         }
         if (cap - n < 300 || shcap - n < 300) {
@@ -338,8 +339,7 @@ struct Dec {
         const int s = br.decode(lit);
         if (s < 0) goto done;
         if (s < 256) {
-          sh[n] = (uint16_t)s;
-          op[n++] = (uint8_t)s;
+          sh[n++] = (uint16_t)s;  // out[0, dirty_len) is written once, from the shadow, when resolved
           continue;
         }
         if (s == 256) {
@@ -358,7 +358,6 @@ struct Dec {
         for (unsigned k = 0; k < len; k++) {
           const uint16_t v = src[k];
           sh[n + k] = v;
-          op[n + k] = (uint8_t)v;
           unk |= v;
         }
         n += len;
