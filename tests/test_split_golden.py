@@ -142,3 +142,53 @@ def test_split_cli_convert(gpu, tmp_path, name, mode, flags):
         assert np.array_equal(getattr(A, k), getattr(want, k)), k
     names = [base64.b64decode(x).decode() for x in exp["nodes"]]
     assert Path(str(out) + ".nodes.tsv").read_text() == "".join(f"{i}\t{v}\n" for i, v in enumerate(names))
+
+
+@pytest.mark.gpu
+def test_split_gpu_gzip_and_stdin(gpu, tmp_path):
+    """The split path reads its input by the reference's source rules (parser.py:100-112): a .gz
+    by name (gzip.open), '-' as stdin; the result equals the plain file's golden."""
+    import gzip
+    import subprocess
+    import sys
+
+    key = "inputs_split/missing_segments.gfa|undirected"
+    data = (HERE / "inputs_split" / "missing_segments.gfa").read_bytes()
+    gz = tmp_path / "m.gfa.gz"
+    gz.write_bytes(gzip.compress(data))
+    from gfa2network_amd import parse_gfa
+
+    _check(key, lambda: parse_gfa(str(gz), build_graph=False, build_matrix=True, return_node_list=True,
+                                  split_on_alignment=True, **MODES["undirected"]))
+    code = ("import sys, json; sys.path.insert(0, %r); from gfa2network_amd import parse_gfa; "
+            "A, n = parse_gfa('-', build_graph=False, build_matrix=True, return_node_list=True, "
+            "split_on_alignment=True, directed=False); A = A.tocoo(); "
+            "print(json.dumps([list(A.shape), A.row.tolist(), A.col.tolist(), A.data.tolist(), n]))"
+            % str(Path(__file__).resolve().parents[1]))
+    out = subprocess.run([sys.executable, "-W", "ignore", "-c", code], input=data, capture_output=True, check=True)
+    shape, rows, cols, vals, nodes = json.loads(out.stdout.decode().strip().splitlines()[-1])
+    exp = CASES[key]
+    assert shape == exp["shape"]
+    assert rows == np.frombuffer(base64.b64decode(exp["arrays"]["row"][1]), dtype=exp["arrays"]["row"][0]).tolist()
+    assert cols == np.frombuffer(base64.b64decode(exp["arrays"]["col"][1]), dtype=exp["arrays"]["col"][0]).tolist()
+    assert vals == np.frombuffer(base64.b64decode(exp["arrays"]["data"][1]), dtype=exp["arrays"]["data"][0]).tolist()
+    assert [x.encode() for x in nodes] == [base64.b64decode(x) for x in exp["nodes"]]
+
+
+@pytest.mark.gpu
+def test_split_gpu_corrupt_gzip_raises_like_plain_path(gpu, tmp_path):
+    """A truncated .gz: the split path raises what the plain parse raises (gzip.py's EOFError
+    after the whole lines before it were parsed)."""
+    import gzip
+
+    from gfa2network_amd import parse_gfa
+
+    data = (HERE / "inputs_split" / "e_coords.gfa").read_bytes() * 50
+    gz = tmp_path / "t.gfa.gz"
+    gz.write_bytes(gzip.compress(data)[:-20])
+    kw = dict(build_graph=False, build_matrix=True, return_node_list=True)
+    with pytest.raises(EOFError) as plain:
+        parse_gfa(str(gz), **kw)
+    with pytest.raises(EOFError) as split:
+        parse_gfa(str(gz), split_on_alignment=True, **kw)
+    assert str(plain.value) == str(split.value)
