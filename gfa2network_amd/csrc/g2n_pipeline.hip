@@ -18,6 +18,9 @@
 
 #include "g2n_internal.h"
 #include "g2n_kernels.hip"
+#ifndef G2N_LOOKUP_BATCH  // touches per thread in the S-first lookup round (experiment builds vary it)
+#define G2N_LOOKUP_BATCH 2
+#endif
 #include "g2n_scan.hip"
 #include "g2n_sym.hip"
 #include "g2n_route.hip"
@@ -560,9 +563,9 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
       hipLaunchKernelGGL(k_insert_round<kModeLookup>, g, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
                          max_probes, slot, tstate, round, (int)bidir, c->ctl, first, nid_in, n_first, inv_in, tid_out);
     else {
-      const dim3 gb(grid_for(n_t, kTPB * 2));  // two touches per thread
-      hipLaunchKernelGGL(k_lookup_fast<2>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1, max_probes, tstate,
-                         (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
+      const dim3 gb(grid_for(n_t, kTPB * G2N_LOOKUP_BATCH));  // G2N_LOOKUP_BATCH touches per thread
+      hipLaunchKernelGGL(k_lookup_fast<G2N_LOOKUP_BATCH>, gb, b, 0, c->stream, in, len, TI, n_t, table, cap - 1,
+                         max_probes, tstate, (int)bidir, c->ctl, nid_in, n_first, inv_in, tid_out);
     }
     phase(c, mode == kModeClaim ? "insert_claim" : "insert_lookup");
     sync_ctl(c);
