@@ -43,6 +43,12 @@ def _args():
                     help="skip the end-to-end leg (file on the page cache -> scipy CSR + node list in host memory)")
     ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
     ap.add_argument("--no-alt", action="store_true", help="skip the hash-dictionary comparison build")
+    ap.add_argument("--names", default="decimal", choices=["decimal", "hashed"],
+                    help="segment names of the synthetic file: decimal ids 1..N (the configs' layout) or hashed "
+                         "(unique non-decimal names: the hash dictionary / the general sharded protocol)")
+    ap.add_argument("--force-protocol", action="store_true",
+                    help="sharded runs: the general owner protocol even where the decimal fast path (or, on one "
+                         "rank, no exchange at all) applies — to time the protocol itself")
     ap.add_argument("--shard", action="store_true",
                     help="byte-range-shard the workload's one file over the ranks (gfa2network_amd/shard.py; "
                          "always on for C5)")
@@ -360,12 +366,12 @@ def main_sharded(args, wl):
 
     n_s = max(1, int(wl.n_segments * args.scale))
     n_l = max(1, int(wl.n_links * args.scale))
-    dev_in = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=wl.rc_tag, device=local)
+    dev_in = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=wl.rc_tag, device=local, names=args.names)
     starts = [_line_start_device(dev_in.ptr, dev_in.len, r * dev_in.len // world) for r in range(world)] + [dev_in.len]
     lo, hi = starts[rank], starts[rank + 1]
     mode = dict(wl.mode)
     kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
-              weight_tag=mode.get("weight_tag"), dtype="float64")
+              weight_tag=mode.get("weight_tag"), dtype="float64", force_protocol=args.force_protocol)
     one = None
     lib = nat.load()
     if rank == 0:  # the whole file on one GPU: the scaling reference
@@ -412,7 +418,9 @@ def main_sharded(args, wl):
                    "nnz": int(slice_nnz.item()), "mode": mode or "default", "output": "csr row slice per rank",
                    "parallelism": f"shard x{world} (RCCL: all-gather of range counts, all-reduce of the "
                                   f"id premise, all-to-all of triplets to row owners)",
-                   "id_path": "decimal-id fast path" if res.fast_path else "general owner protocol"},
+                   "segment_names": args.names,
+                   "id_path": ("decimal-id fast path" if res.fast_path else
+                               "general owner protocol" + (" (forced)" if args.force_protocol else ""))},
         "gb_per_s_ingested": round(dev_in.len * args.steps / elapsed / 1e9, 2),
         "host_ms_per_stage_rank0": {k: round(sum(t.get(k, 0.0) for t in tms) / len(tms), 2) for k in tms[0]},
     }
@@ -451,7 +459,7 @@ def main():
     wl = synth.WORKLOADS[args.workload]
     n_s = max(1, int(wl.n_segments * args.scale))
     n_l = max(1, int(wl.n_links * args.scale))
-    dev_in = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local)
+    dev_in = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local, names=args.names)
     ctx = lib.g2n_context_create(local)
     if not ctx:
         raise RuntimeError(nat.last_error())

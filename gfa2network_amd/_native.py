@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
-    "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
+    "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
 
@@ -191,6 +191,8 @@ def load() -> ctypes.CDLL:
     lib.g2n_split_free.argtypes = [P]
     lib.g2n_join_names.argtypes = [P, P, U64, ctypes.c_uint8, P]
     lib.g2n_join_names.restype = ctypes.c_int
+    lib.g2n_gather_names.argtypes = [P, P, P, U64, P, P]
+    lib.g2n_gather_names.restype = ctypes.c_int
     lib.g2n_write_npz.argtypes = [ctypes.c_char_p, I32, P, P, P, P, P, I32]
     lib.g2n_write_npz.restype = ctypes.c_int
     lib.g2n_write_node_map.argtypes = [ctypes.c_char_p, P, P, U64, I32, ctypes.POINTER(I64)]
@@ -478,6 +480,58 @@ def join_names(blob: np.ndarray, offsets: np.ndarray, sep: int = 0x0A) -> bytear
         if rc != OK:
             raise RuntimeError(f"{status_name(rc)}: {last_error()}")
     return out
+
+
+def gather_names(blob: np.ndarray, offsets: np.ndarray, order: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """(blob, offsets) of the names in a new order: out name i = name order[i] (g2n_gather_names,
+    host threads)."""
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    order = np.ascontiguousarray(order, dtype=np.int64)
+    n = len(order)
+    out_offs = np.zeros(n + 1, dtype=np.int64)
+    if n:
+        np.cumsum((offsets[1:] - offsets[:-1])[order], out=out_offs[1:])
+    out = np.empty(int(out_offs[-1]), dtype=np.uint8)
+    if n and len(out):
+        rc = load().g2n_gather_names(blob.ctypes.data, offsets.ctypes.data, order.ctypes.data, n,
+                                     out_offs.ctypes.data, out.ctypes.data)
+        if rc != OK:
+            raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    return out, out_offs
+
+
+def decimal_names(n: int, bidirected: bool = False) -> tuple[np.ndarray, np.ndarray]:
+    """(blob, offsets) of the node keys of a decimal-id graph in id order (builders.py:190-198):
+    node k is str(k + 1), or (bidirected) node 2j / 2j + 1 is f"{j + 1}:+" / f"{j + 1}:-" — built
+    digit-width block by block with numpy, no per-name Python objects."""
+    m = (n + 1) // 2 if bidirected else n
+    sfx = 2 if bidirected else 0
+    pieces, lens = [], []
+    lo, d = 1, 1
+    while lo <= m:
+        hi = min(m, 10 ** d - 1)  # the d-digit values lo..hi
+        v = np.arange(lo, hi + 1, dtype=np.int64)
+        cols = [((v // 10 ** (d - 1 - j)) % 10 + 48).astype(np.uint8) for j in range(d)]
+        if bidirected:
+            w = d + 2
+            rows = np.empty((len(v), 2, w), dtype=np.uint8)
+            for j, c in enumerate(cols):
+                rows[:, :, j] = c[:, None]
+            rows[:, :, d] = ord(":")
+            rows[:, 0, d + 1] = ord("+")
+            rows[:, 1, d + 1] = ord("-")
+            pieces.append(rows.reshape(-1))
+            lens.append(np.full(2 * len(v), w, dtype=np.int64))
+        else:
+            pieces.append(np.stack(cols, axis=1).reshape(-1))
+            lens.append(np.full(len(v), d, dtype=np.int64))
+        lo, d = hi + 1, d + 1
+    blob = np.concatenate(pieces) if pieces else np.zeros(0, dtype=np.uint8)
+    ln = np.concatenate(lens)[:n] if lens else np.zeros(0, dtype=np.int64)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(ln, out=offs[1:])
+    return blob[:int(offs[-1])], offs
 
 
 def _io_error(rc: int, path: str):

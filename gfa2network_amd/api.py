@@ -8,8 +8,9 @@ Same keyword names, defaults, returned objects (scipy ``coo_matrix`` in stream o
 the MAX-SYM ``csr_matrix``; node list of ``str`` or raw ``bytes``), exception types and
 messages, the one-shot ``RuntimeWarning`` and the ``verbose`` progress strings.  Every
 numeric step runs on the GPU; only the Python objects are assembled here.  Graph-object
-outputs (NetworkX / igraph, split_on_alignment) are outside this port's scope and raise
-``NotImplementedError``.
+outputs (NetworkX / igraph, and ``split_on_alignment`` with ``build_graph=True``) are outside
+this path's scope and raise ``NotImplementedError``; ``split_on_alignment`` matrix outputs are
+served (``_parse_gfa_split``).
 """
 from __future__ import annotations
 
@@ -168,17 +169,18 @@ def parse_gfa(
     max_tag_mb: float = 100.0,
     split_on_alignment: bool = False,
     device: int = 0,
-    shard: str = "auto",
+    shard: str = "never",
 ):
     """GPU ``parse_gfa`` (gfa2network/builders.py:30-299), matrix outputs only.
 
     Returns ``A`` or ``(A, node_list)`` exactly as the reference does for
     ``build_graph=False, build_matrix=True``.
 
-    ``shard`` (extension; the reference has no such argument): with torch.distributed
-    initialized over more than one rank, ``"auto"`` splits the file over the ranks
-    (``parse_gfa_sharded``, every rank must make the same call) when its working set would not
-    fit this GPU's free HBM; ``"always"`` / ``"never"`` force the choice.
+    ``shard`` (extension; the reference has no such argument): ``"never"`` (default) builds on
+    this process's GPU.  With torch.distributed initialized over more than one rank, ``"auto"``
+    splits the file over the ranks (``parse_gfa_sharded``) when its working set would not fit a
+    GPU's free HBM on some rank, ``"always"`` splits it regardless; both are collectives — every
+    rank must make the same call on the same file (checked: a different path raises ValueError).
     """
     if backend == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
@@ -328,40 +330,72 @@ def _dist_world() -> int:
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def _want_shard(path, shard: str, device: int) -> bool:
-    """Split the file over the process group? Only for a plain file on disk, more than one rank,
-    and ("auto") a working set beyond this GPU's free HBM."""
-    if shard == "never" or _dist_world() < 2 or hasattr(path, "read"):
-        return False
-    p = str(path)
-    if p == "-" or not os.path.isfile(p):
-        return False
-    if shard == "always":
-        return True
-    import torch
+def _gz_inflated_estimate(p: str, size: int) -> int:
+    """Bytes a .gz inflates to, for the shard decision: the last member's ISIZE (RFC 1952: the
+    length mod 2^32) or 4x the compressed size (GFA text compresses 3-4x), whichever is larger."""
+    try:
+        with open(p, "rb") as fh:
+            fh.seek(max(size - 4, 0))
+            isize = int.from_bytes(fh.read(4), "little")
+    except OSError:
+        isize = 0
+    return max(isize, 4 * size)
 
-    free, _ = torch.cuda.mem_get_info(device)
-    return os.path.getsize(p) * WORKING_SET_PER_INPUT_BYTE > free
+
+def _want_shard(path, shard: str, device: int) -> bool:
+    """Split the file over the process group?  Only for a file on disk, more than one rank, and
+    ("auto") a working set beyond a GPU's free HBM.  "auto" and "always" are collectives: the
+    ranks agree on the path (every rank must pass the same file) and, for "auto", on the verdict
+    (all-reduce MAX of the per-rank "does not fit" flags), so no rank enters the sharded build
+    alone."""
+    if shard == "never" or _dist_world() < 2:
+        return False
+    import torch
+    import torch.distributed as dist
+
+    here = not hasattr(path, "read") and str(path) != "-" and os.path.isfile(str(path))
+    need = 0
+    if here and shard == "always":
+        need = 1
+    elif here:
+        p = str(path)
+        size = os.path.getsize(p)
+        work = (_gz_inflated_estimate(p, size) if p.endswith(".gz") else size) * WORKING_SET_PER_INPUT_BYTE
+        free, _ = torch.cuda.mem_get_info(device)
+        need = int(work > free)
+    ident = zlib.crc32(os.fsencode(os.path.abspath(str(path)))) if here else 0
+    size = os.path.getsize(str(path)) if here else -1
+    nccl = dist.get_backend() == "nccl"
+    t = torch.tensor([need, ident, size, -ident, -size, int(here), -int(here)], dtype=torch.int64,
+                     device=torch.device("cuda", torch.cuda.current_device()) if nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    v = t.tolist()
+    same = v[1] == -v[3] and v[2] == -v[4] and v[5] == -v[6]
+    if v[5] and not same:
+        raise ValueError(f"parse_gfa(shard={shard!r}) is a collective: every rank must pass the same file")
+    return bool(v[5]) and bool(v[0])
 
 
 def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = None,
                       strip_orientation: bool = False, verbose: bool = False, bidirected: bool = False,
                       keep_directed_bidir: bool = False, dtype="float64", asymmetric: bool = False,
                       raw_bytes_id: bool = False, return_node_list: bool = False, output: str = "parse",
-                      group=None, engine=None):
+                      group=None, engine=None, root=None):
     """``parse_gfa(path, build_graph=False, build_matrix=True, ...)`` with the file split over the
     ranks of a torch.distributed group — a collective: every rank calls it with
     the same path.  Each rank preads only its line-aligned byte range (``file_line_ranges``) into
     its GPU's HBM, the ranks reconcile node ids (the decimal-id fast path or the general owner
-    protocol, gfa2network_amd/shard.py) and route triplets to row owners, and every rank returns
-    the whole result: what parse_gfa returns (the MAX-SYM CSR, or the stream-order COO) — or, with
-    ``output="csr"``, what ``convert_format(parse_gfa(...), "csr")`` returns.  Exceptions, the
-    one-shot warning and the verbose strings are the reference's (builders.py:95-299).  A ``.gz``
-    file is inflated by every rank (its byte ranges are not seekable); plain files are read per
-    range."""
+    protocol, gfa2network_amd/shard.py) and route triplets to row owners.  The result — what
+    parse_gfa returns (the MAX-SYM CSR, or the stream-order COO), or with ``output="csr"`` what
+    ``convert_format(parse_gfa(...), "csr")`` returns — is assembled on every rank (``root=None``)
+    or on rank ``root`` only (the other ranks return None).  Index dtypes follow scipy (int64 once
+    the entries pass 2^31 - 1).  Exceptions, the one-shot warning and the verbose strings are the
+    reference's (builders.py:95-299).  A ``.gz`` file is inflated by every rank (its byte ranges
+    are not seekable); one that does not inflate cleanly is built by every rank on its own GPU
+    through the single-GPU path, whose gzip errors and prefix semantics are the reference's."""
     import torch
 
-    from .shard import HipEngine, build_sharded, file_line_ranges, gather_coo, gather_csr
+    from .shard import HipEngine, build_sharded, file_line_ranges, gather_coo, gather_csr, scipy_index_dtype
 
     dt = _dtype_of(dtype)
     if output not in ("parse", "csr"):
@@ -370,24 +404,42 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    eng = engine or HipEngine(torch.cuda.current_device())
     p = str(path)
-    if p.endswith(".gz"):
-        with open(p, "rb") as fh:
-            data, _ = nat.gunzip(fh.read())
-        from .shard import line_ranges
-
-        lo, hi = line_ranges(data, world)[rank]
-        buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
-    else:
-        lo, hi = file_line_ranges(p, world)[rank]
-        buf = eng.read_range(p, lo, hi - lo)
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
+    if p.endswith(".gz"):
+        with open(p, "rb") as fh:
+            blob = fh.read()
+        try:
+            data, _ = nat.gunzip(blob)
+        except nat.GzipFailure:
+            del blob
+            opts = nat.make_options(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                                    asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
+                                    weight_tag=weight_tag or None, output=nat.OUT_CSR if output == "csr" else nat.OUT_PARSE,
+                                    want_node_names=bool(return_node_list),
+                                    device=getattr(engine, "device_index", 0) if engine is not None
+                                    else torch.cuda.current_device())
+            raw = _run(p, opts)  # the exact reader raises gzip.py's error after the prefix's lines
+            out = finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
+                           verbose=verbose, path=path)
+            return out if root is None or rank == root else None
+        del blob
+        from .shard import line_ranges
+
+        eng = engine or HipEngine(torch.cuda.current_device())
+        lo, hi = line_ranges(data, world)[rank]
+        buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
+        del data
+    else:
+        eng = engine or HipEngine(torch.cuda.current_device())
+        lo, hi = file_line_ranges(p, world)[rank]
+        buf = eng.read_range(p, lo, hi - lo)
     res = build_sharded(buf, engine=eng, group=group, directed=directed, bidirected=bidirected,
                         keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
                         strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
-                        gather_names=return_node_list, keep_coo=not maxsym and output == "parse")
+                        gather_names=return_node_list, keep_coo=not maxsym and output == "parse", names_root=root)
+    del buf
     raw = RawResult(status=res.status, err_line=res.err_line, err_index=res.err_index, err_value=res.err_value,
                     err_detail=res.err_detail, has_warning=res.has_warning, warn_byte=res.warn_byte,
                     warn_line=res.warn_line, n_lines=res.n_lines, n_records=res.n_records,
@@ -396,17 +448,22 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     if res.status == 0:
         if not maxsym and output == "parse":
             raw.format = "coo"
-            raw.rows, raw.cols, raw.data = gather_coo(res, group)
+            got = gather_coo(res, group, root)
+            if got is not None:
+                raw.rows, raw.cols, raw.data = got
+                idt = scipy_index_dtype(0, res.n_nodes)
+                raw.rows, raw.cols = raw.rows.astype(idt, copy=False), raw.cols.astype(idt, copy=False)
         else:
             raw.format = "csr"
-            raw.indptr, raw.indices, raw.data = gather_csr(res, group)
-            raw.indptr = raw.indptr.astype(np.int32)
-            raw.indices = raw.indices.astype(np.int32)
+            got = gather_csr(res, group, root)
+            if got is not None:
+                raw.indptr, raw.indices, raw.data = got
+        if root is not None and rank != root:
+            return None
         if return_node_list:
-            blob = b"".join(res.names)
-            offs = np.zeros(len(res.names) + 1, dtype=np.int64)
-            offs[1:] = np.cumsum([len(x) for x in res.names])
-            raw.names_blob, raw.names_offsets = np.frombuffer(blob, dtype=np.uint8), offs
+            raw.names_blob, raw.names_offsets = res.names_blob, res.names_offsets
+    elif root is not None and rank != root:
+        return None
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=verbose,
                     path=path)
 

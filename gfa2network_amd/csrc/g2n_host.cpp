@@ -387,6 +387,23 @@ int g2n_join_names(const uint8_t* blob, const int64_t* offsets, uint64_t n_names
   });
 }
 
+int g2n_gather_names(const uint8_t* blob, const int64_t* offsets, const int64_t* order, uint64_t n_names,
+                     const int64_t* out_offsets, uint8_t* out) {
+  if (n_names == 0) return G2N_OK;
+  if (!blob || !offsets || !order || !out_offsets || !out) return G2N_E_ARG;
+  return g2n::guarded([&]() -> int {
+    const uint64_t chunk = 1 << 16;
+    g2n::parallel_for((n_names + chunk - 1) / chunk, g2n::host_threads(), [&](size_t c) {
+      const uint64_t lo = c * chunk, hi = std::min<uint64_t>(n_names, lo + chunk);
+      for (uint64_t i = lo; i < hi; i++) {
+        const int64_t k = order[i];
+        std::memcpy(out + out_offsets[i] - out_offsets[0], blob + offsets[k], (size_t)(offsets[k + 1] - offsets[k]));
+      }
+    });
+    return G2N_OK;
+  });
+}
+
 int g2n_write_npz(const char* path, int32_t n_members, const char* const* names, const uint8_t* const* heads,
                   const uint64_t* head_lens, const void* const* datas, const uint64_t* data_lens, int32_t level) {
   if (!path || n_members < 0 || (n_members && (!names || !heads || !head_lens || !datas || !data_lens)))

@@ -4,8 +4,8 @@
 //   lines -> classify -> parse (+ exact weights) -> dictionary -> names -> triplets
 //   -> [COO out]  or  sort + group sums (+ std::sort emulation rows) -> [SUM CSR]
 //   -> transposed sort + sums, merge, maximum -> [MAX-SYM CSR]
-// Scans / radix sort / merge are rocPRIM device primitives; every other step is a
-// hand-written kernel in g2n_kernels.hip.  Counts are read back between phases (a few
+// Every step is a hand-written kernel: g2n_kernels.hip (parse, dictionary, row sums), g2n_scan.hip
+// (scans), g2n_sort.hip (stable radix sort), g2n_sym.hip (bucket partition), g2n_route.hip.  Counts are read back between phases (a few
 // small synchronous copies per build) to size the next phase's buffers exactly.
 #include <hip/hip_runtime.h>
 
@@ -14,7 +14,6 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <rocprim/rocprim.hpp>
 
 #include "g2n_internal.h"
 #include "g2n_kernels.hip"
@@ -22,6 +21,7 @@
 #define G2N_LOOKUP_BATCH 2
 #endif
 #include "g2n_scan.hip"
+#include "g2n_sort.hip"
 #include "g2n_sym.hip"
 #include "g2n_route.hip"
 #include "g2n_inflate.hip"
@@ -42,7 +42,8 @@ enum Slot {
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
-  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_NSLOTS
+  S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
+  S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -164,34 +165,39 @@ struct RowSide {  // one orientation's per-row sums: row r's unique entries at [
   bool unsorted, flagged, local_unsorted;
 };
 
-// Stable LSD radix sort of (u32 key < 2^bits, V) pairs.  Onesweep with 9-bit digits whenever that
-// saves a pass over 8-bit ones (26-bit row ids: 3 passes instead of 4; measured on gfx950,
-// profiles/r01/sort_configs.jsonl: 4.2 vs 5.3 ms for 200M u32 pairs), 1024-thread x 8-item blocks.
-template <unsigned kBits>
-using SortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, kBits,
-                                        rocprim::block_radix_rank_algorithm::match>>;
-
-template <class Cfg, class V>
-static void sort_pairs_cfg(g2n_context* c, const uint32_t* kin, uint32_t* kout, const V* vin, V* vout, uint64_t n,
-                           int bits, int begin) {
-  size_t tb = 0;
-  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(nullptr, tb, kin, kout, vin, vout, (size_t)n, (unsigned)begin,
-                                         (unsigned)bits, c->stream));
-  void* tmp = dbuf(c, S_TEMP, tb);
-  G2N_HIP(rocprim::radix_sort_pairs<Cfg>(tmp, tb, kin, kout, vin, vout, (size_t)n, (unsigned)begin, (unsigned)bits,
-                                         c->stream));
-}
-
-// stable sort on key bits [begin, bits)
+// Stable LSD radix sort of (u32 key, V) pairs on key bits [begin, bits) (g2n_sort.hip): ceil(w / 8)
+// passes of equal digit width; kin / vin are left intact, the result lands in kout / vout.
 template <class V>
 static void sort_pairs_u32(g2n_context* c, const uint32_t* kin, uint32_t* kout, const V* vin, V* vout, uint64_t n,
                            int bits, int begin = 0) {
   if (n == 0) return;
-  const int w = bits - begin;
-  if ((w + 8) / 9 < (w + 7) / 8) sort_pairs_cfg<SortCfg<9>>(c, kin, kout, vin, vout, n, bits, begin);
-  else sort_pairs_cfg<SortCfg<8>>(c, kin, kout, vin, vout, n, bits, begin);
+  if (n >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "radix sort of 2^32 or more items");
+  const int w = bits - begin > 0 ? bits - begin : 1;
+  const int passes = (w + (int)kRsMaxBits - 1) / (int)kRsMaxBits;
+  const uint64_t n_blk = (n + kRsTile - 1) / kRsTile;
+  auto* tk = dget<uint32_t>(c, S_RSK, passes > 1 ? n : 1);
+  auto* tv = dget<V>(c, S_RSV, passes > 1 ? n : 1);
+  auto* cnt = dget<uint32_t>(c, S_RSCNT, (uint64_t)kRsMaxDig * n_blk);
+  auto* off = dget<uint32_t>(c, S_RSOFF, (uint64_t)kRsMaxDig * n_blk);
+  const uint32_t* ki = kin;
+  const V* vi = vin;
+  int lo = begin;
+  for (int p = 0; p < passes; p++) {
+    const int db = (w - (lo - begin) + (passes - p) - 1) / (passes - p);  // equal widths, rounded up first
+    const uint32_t n_dig = 1u << db;
+    // the last pass writes kout; earlier ones alternate so that it does
+    const bool to_out = ((passes - 1 - p) & 1) == 0;
+    uint32_t* ko = to_out ? kout : tk;
+    V* vo = to_out ? vout : tv;
+    hipLaunchKernelGGL(k_rsort_hist, dim3((unsigned)n_blk), dim3(kRsTPB), 0, c->stream, ki, n, (uint32_t)lo, n_dig,
+                       cnt, n_blk);
+    scan_excl<uint32_t, uint32_t>(c, cnt, off, (uint64_t)n_dig * n_blk);
+    hipLaunchKernelGGL((k_rsort_scatter<V>), dim3((unsigned)n_blk), dim3(kRsTPB), 0, c->stream, ki, vi, ko, vo, n,
+                       (uint32_t)lo, (uint32_t)db, (const uint32_t*)off, n_blk);
+    ki = ko;
+    vi = vo;
+    lo += db;
+  }
 }
 
 // coo.tocsr() of one orientation (transposed: of A.T), up to the per-row sorted unique entries.

@@ -31,6 +31,7 @@ static SynthSpec to_spec(const g2n_synth_spec* p) {
   s.n_l = p->n_links;
   s.seed = p->seed;
   s.rc = p->rc_tag;
+  s.names = p->names;
   return s;
 }
 
@@ -41,6 +42,7 @@ extern "C" {
 int g2n_synth_host(const g2n_synth_spec* spec, int n_threads, uint8_t** out, size_t* len) {
   using namespace g2n;
   if (!spec || !out || !len || (spec->n_links && !spec->n_segments)) return G2N_E_ARG;
+  if (spec->names && spec->n_segments >= (1ull << 32)) return G2N_E_ARG;  // hashed names: a u32 bijection
   const SynthSpec s = to_spec(spec);
   const uint64_t n = synth_n_lines(s);
   int T = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
@@ -88,6 +90,7 @@ void g2n_synth_free_host(uint8_t* buf) { std::free(buf); }
 int g2n_synth_device(int device, const g2n_synth_spec* spec, void** d_out, size_t* len) {
   using namespace g2n;
   if (!spec || !d_out || !len || (spec->n_links && !spec->n_segments)) return G2N_E_ARG;
+  if (spec->names && spec->n_segments >= (1ull << 32)) return G2N_E_ARG;
   const SynthSpec s = to_spec(spec);
   const uint64_t n = synth_n_lines(s);
   if (hipSetDevice(device) != hipSuccess) return G2N_E_DEVICE;

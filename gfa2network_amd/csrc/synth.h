@@ -4,8 +4,9 @@
 // timings) and on the GPU (bench.py builds its HBM-resident workload in place), and both
 // produce identical bytes for the same spec:
 //   line 0:            H\tVN:Z:1.0
-//   S lines i=1..N_S:  S\t{i}\t{seq}        |seq| ~ Geometric(1/8) over ACGT
-//   L lines j:         L\t{src}\t{o1}\t{dst}\t{o2}\t0M[\tRC:i:{k}]
+//   S lines i=1..N_S:  S\t{name(i)}\t{seq}  |seq| ~ Geometric(1/8) over ACGT;
+//                      name(i) = "i", or (names = 1) "s" + 8 hex digits of a u32 bijection of i
+//   L lines j:         L\t{name(src)}\t{o1}\t{name(dst)}\t{o2}\t0M[\tRC:i:{k}]
 //                      src ~ U[1,N_S], dst = min(src + Geometric(5/16), N_S),
 //                      o = '+' with probability 922/1024, k ~ U[1,99]
 // Integer-only draws (splitmix64 of (seed, stream, index, chunk)) keep host == device.
@@ -23,7 +24,7 @@ namespace g2n {
 struct SynthSpec {
   uint64_t n_s, n_l, seed;
   int32_t rc;
-  int32_t pad;
+  int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32)
 };
 
 G2N_HD inline uint64_t smix64(uint64_t x) {
@@ -82,13 +83,15 @@ G2N_HD inline SynthLink synth_link(const SynthSpec& s, uint64_t j) {
   return L;
 }
 
+G2N_HD inline uint32_t synth_name_len(const SynthSpec& s, uint64_t i);
+
 G2N_HD inline uint64_t synth_n_lines(const SynthSpec& s) { return 1 + s.n_s + s.n_l; }
 
 G2N_HD inline uint32_t synth_line_len(const SynthSpec& s, uint64_t line) {
   if (line == 0) return 11;  // "H\tVN:Z:1.0\n"
-  if (line <= s.n_s) return 2 + synth_digits(line) + 1 + synth_seq_len(s, line) + 1;
+  if (line <= s.n_s) return 2 + synth_name_len(s, line) + 1 + synth_seq_len(s, line) + 1;
   SynthLink L = synth_link(s, line - 1 - s.n_s);
-  uint32_t n = 2 + synth_digits(L.src) + 3 + synth_digits(L.dst) + 3 + 2 + 1;  // ...\t0M\n
+  uint32_t n = 2 + synth_name_len(s, L.src) + 3 + synth_name_len(s, L.dst) + 3 + 2 + 1;  // ...\t0M\n
   if (s.rc) n += 6 + synth_digits(L.k);
   return n;
 }
@@ -102,6 +105,29 @@ G2N_HD inline char* synth_put_u64(char* o, uint64_t x) {
   return o + d;
 }
 
+// a bijection of u32 (xor-shift / odd-multiply steps are each invertible mod 2^32)
+G2N_HD inline uint32_t synth_name_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+G2N_HD inline uint32_t synth_name_len(const SynthSpec& s, uint64_t i) { return s.names ? 9u : synth_digits(i); }
+
+G2N_HD inline char* synth_put_name(const SynthSpec& s, char* o, uint64_t i) {
+  if (!s.names) return synth_put_u64(o, i);
+  const uint32_t h = synth_name_mix((uint32_t)i);
+  *o++ = 's';
+  for (int k = 7; k >= 0; k--) {
+    const uint32_t d = (h >> (4 * k)) & 15u;
+    *o++ = (char)(d < 10 ? '0' + d : 'a' + d - 10);
+  }
+  return o;
+}
+
 G2N_HD inline void synth_write_line(const SynthSpec& s, uint64_t line, char* o) {
   if (line == 0) {
     const char h[11] = {'H', '\t', 'V', 'N', ':', 'Z', ':', '1', '.', '0', '\n'};
@@ -111,7 +137,7 @@ G2N_HD inline void synth_write_line(const SynthSpec& s, uint64_t line, char* o) 
   if (line <= s.n_s) {
     *o++ = 'S';
     *o++ = '\t';
-    o = synth_put_u64(o, line);
+    o = synth_put_name(s, o, line);
     *o++ = '\t';
     uint32_t n = synth_seq_len(s, line);
     const char acgt[4] = {'A', 'C', 'G', 'T'};
@@ -125,11 +151,11 @@ G2N_HD inline void synth_write_line(const SynthSpec& s, uint64_t line, char* o) 
   SynthLink L = synth_link(s, line - 1 - s.n_s);
   *o++ = 'L';
   *o++ = '\t';
-  o = synth_put_u64(o, L.src);
+  o = synth_put_name(s, o, L.src);
   *o++ = '\t';
   *o++ = L.o1;
   *o++ = '\t';
-  o = synth_put_u64(o, L.dst);
+  o = synth_put_name(s, o, L.dst);
   *o++ = '\t';
   *o++ = L.o2;
   *o++ = '\t';

@@ -96,11 +96,49 @@ class ShardResult:
     indptr: object = None
     indices: object = None
     data: object = None
-    names: list | None = None  # node keys in id order, when gather_names
+    names_blob: object = None  # node keys in id order (numpy uint8 blob + int64 offsets), when gather_names
+    names_offsets: object = None
+    index_maxval: int = 0  # what scipy sizes the result's index dtype by (scipy_index_dtype)
     n_cast_overflow: int = 0
     timings_ms: dict = field(default_factory=dict)
     fast_path: bool = False  # the decimal-id fast path built it
     coo: tuple | None = None  # keep_coo: this range's stream-order triplets over global ids
+
+    @property
+    def names(self) -> list | None:
+        """The node keys in id order as a list of bytes (None unless gather_names)."""
+        if self.names_offsets is None:
+            return None
+        b, o = self.names_blob, self.names_offsets
+        return [bytes(b[o[i]:o[i + 1]]) for i in range(len(o) - 1)]
+
+
+INT32_MAX = 2**31 - 1
+
+
+def scipy_index_dtype(maxval: int, n: int):
+    """The index dtype scipy gives the result (scipy 1.15 ``get_index_dtype(..., maxval,
+    check_contents=True)`` in the csr / coo constructors): int64 once a count or the shape passes
+    int32, else int32.  maxval: the MAX-SYM CSR's nnz (``csr_binop_csr`` result, builders.py:283);
+    for coo.tocsr() the triplet count with duplicates (``_coo_to_compressed`` sizes indptr by
+    ``max(coo.nnz, N)`` before summing, utils.py:55); 0 for the COO (shape only)."""
+    return np.int64 if max(int(maxval), int(n)) > INT32_MAX else np.int32
+
+
+def concat_indptr(parts, dtype) -> np.ndarray:
+    """The full indptr from the row slices' local indptrs (each starting at 0), in ``dtype``."""
+    n = sum(max(len(p) - 1, 0) for p in parts)
+    out = np.zeros(n + 1, dtype=dtype)
+    base, r = 0, 0
+    for p in parts:
+        p = np.asarray(p)
+        k = len(p) - 1
+        if k <= 0:
+            continue
+        out[r + 1:r + k + 1] = p[1:].astype(np.int64) + base
+        base += int(p[-1])
+        r += k
+    return out
 
 
 def line_ranges(data: bytes | np.ndarray, n_ranks: int) -> list[tuple[int, int]]:
@@ -400,22 +438,41 @@ class Comm:
         return outs, recv
 
     def allgather_v(self, x):
-        """every rank's (variable-length) tensor, in rank order"""
+        """every rank's (variable-length) tensor, in rank order (no padding: one broadcast per
+        rank when the lengths differ)"""
+        return [t for _, t in self.parts(x, root=None)]
+
+    def parts(self, x, root=None, sizes=None):
+        """Yield (rank, tensor) for every rank's (variable-length, 1-D) tensor in rank order — on
+        every rank (root None: one broadcast per rank) or on `root` only (point-to-point sends; the
+        other ranks send theirs and yield nothing).  Tensors come back on x's device."""
         torch = self.torch
         if self.world == 1:
-            return [x]
+            yield 0, x
+            return
         dev = x.device
-        xc = self._c(x)
-        n = torch.tensor([xc.numel()], dtype=torch.int64, device=xc.device)
-        ns = [torch.empty_like(n) for _ in range(self.world)]
-        self.dist.all_gather(ns, n, group=self.group)
-        ns = [int(v.item()) for v in ns]
-        m = max(ns)
-        pad = torch.zeros(m, dtype=xc.dtype, device=xc.device)
-        pad[:xc.numel()] = xc
-        outs = [torch.empty(m, dtype=xc.dtype, device=xc.device) for _ in range(self.world)]
-        self.dist.all_gather(outs, pad, group=self.group)
-        return [o[:k].to(dev) for o, k in zip(outs, ns)]
+        xc = self._c(x.contiguous())
+        if sizes is None:
+            n = torch.tensor([xc.numel()], dtype=torch.int64, device=xc.device)
+            ns = [torch.empty_like(n) for _ in range(self.world)]
+            self.dist.all_gather(ns, n, group=self.group)
+            sizes = [int(v.item()) for v in ns]
+        if root is not None and self.rank != root:
+            if sizes[self.rank]:
+                self.dist.send(xc, dst=self._global(root), group=self.group)
+            return
+        for k in range(self.world):
+            mine = k == self.rank
+            buf = xc if mine else torch.empty(sizes[k], dtype=xc.dtype, device=xc.device)
+            if sizes[k]:
+                if root is None:
+                    self.dist.broadcast(buf, src=self._global(k), group=self.group)
+                elif not mine:
+                    self.dist.recv(buf, src=self._global(k), group=self.group)
+            yield k, (x if mine else buf.to(dev))
+
+    def _global(self, k):
+        return k if self.group is None else self.dist.get_global_rank(self.group, k)
 
     def allgather_list(self, vals):
         """every rank's list of numbers (float64-exact up to 2^53)"""
@@ -437,6 +494,16 @@ class Comm:
         self.dist.broadcast(xc, src=src, group=self.group)
         return xc.to(dev)
 
+    def allreduce_sum(self, vals, device):
+        """element-wise sum over the ranks of a short list of ints"""
+        torch = self.torch
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=device)
+        if self.world > 1:
+            tc = self._c(t)
+            self.dist.all_reduce(tc, group=self.group)
+            t = tc
+        return [int(v) for v in t.tolist()]
+
     def allreduce_max(self, x):
         if self.world == 1:
             return x
@@ -452,13 +519,6 @@ class Comm:
         xc = self._c(x)
         self.dist.all_reduce(xc, op=self.dist.ReduceOp.MIN, group=self.group)
         return xc.to(dev)
-
-
-def _decimal_names(n: int, bidirected: bool) -> list:
-    """The node keys of a decimal-id graph in id order (builders.py:190-198: "k" or "k:+", "k:-")."""
-    if not bidirected:
-        return [str(k + 1).encode() for k in range(n)]
-    return [f"{k // 2 + 1}:{'+-'[k & 1]}".encode() for k in range(n)]
 
 
 def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm):
@@ -508,7 +568,7 @@ def _route(engine, C, local, dtype, gmap, n_global, maxsym, uniform, tm):
     return a, tstream
 
 
-def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo=False):
+def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo=False, names_root=None):
     """The decimal-id fast path (module docstring), or None when a range breaks its premise."""
     import time
 
@@ -540,19 +600,14 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"), tm)
     row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
                                                    opts.get("weight_tag"), tm)
-    casts = torch.tensor([local.n_cast_overflow], dtype=torch.int64, device=engine.device)
-    if world > 1:
-        import torch.distributed as dist
-
-        cc = C._c(casts)
-        dist.all_reduce(cc, group=C.group)
-        casts = cc
+    sums = C.allreduce_sum([local.n_cast_overflow, int(indices.numel()), int(local.rows.numel())], engine.device)
     out = ShardResult(status=0, n_lines=int(sum(c[0] for c in allc)), n_records=int(sum(c[3] for c in allc)),
                       n_edges=int(sum(c[2] for c in allc)), n_nodes=n_global, row_lo=row_lo, row_hi=row_hi,
-                      indptr=indptr, indices=indices, data=vals, n_cast_overflow=int(casts.item()))
+                      indptr=indptr, indices=indices, data=vals, n_cast_overflow=sums[0],
+                      index_maxval=sums[1] if maxsym else sums[2])
     out.n_records_before_error = out.n_records
-    if gather_names:
-        out.names = _decimal_names(n_global, bool(opts.get("bidirected")))
+    if gather_names and names_root in (None, rank):  # node k is str(k + 1) (bidirected: k // 2 + 1 and ":+" / ":-")
+        out.names_blob, out.names_offsets = nat.decimal_names(n_global, bool(opts.get("bidirected")))
     out.timings_ms = tm
     out.fast_path = True
     if keep_coo:
@@ -562,10 +617,13 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
 
 def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, keep_directed_bidir=False,
                   asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None,
-                  gather_names=False, keep_coo=False) -> ShardResult:
+                  gather_names=False, keep_coo=False, names_root=None, force_protocol=False) -> ShardResult:
     """Build this rank's byte range `buf` (uint8 tensor on the engine's device) as part of one
     file split over `group` in rank order; returns this rank's CSR row slice (and, keep_coo, the
-    range's stream-order triplets over global ids: res.coo = (rows, cols, data))."""
+    range's stream-order triplets over global ids: res.coo = (rows, cols, data)).
+    gather_names: the node names in id order (res.names_blob / names_offsets) on every rank, or
+    on rank `names_root` only.  force_protocol: run the general exchange even on one rank (whose
+    local ids are the global ones; measurement of the protocol's cost only)."""
     import time
 
     import torch
@@ -581,7 +639,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     tpe = 4 if (bidirected and not keep_directed_bidir) else 2
     ktrip = 4 if tpe == 4 else (1 if gd else 2)
     tm = {}
-    fast = _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo)
+    fast = None if force_protocol else _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm,
+                                                               keep_coo, names_root)
     if fast is not None:
         return fast
     t0 = time.perf_counter()
@@ -638,17 +697,27 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     out.n_cast_overflow = int(sum(s[7] for s in allst))
     tm["local_build"] = (time.perf_counter() - t0) * 1e3
 
+    if world == 1 and not force_protocol:  # one range: its local ids are the global ids
+        out.n_nodes = local.n_local_nodes
+        if gather_names:
+            out.names_blob = local.names_blob.cpu().numpy()
+            out.names_offsets = local.names_offsets.cpu().numpy()
+        local.dtype_name = dtype
+        if keep_coo:
+            out.coo = (local.rows, local.cols, local.data)
+        a, tstream = _route(engine, C, local, dtype, None, out.n_nodes, maxsym, not weight_tag, tm)
+        return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()))
+
     # 3. names to owners, owner dedup in arrival (= global first-touch) order
     t1 = time.perf_counter()
     pb, po, pidx, pst = engine.partition_keys(local.names_blob, local.names_offsets, world)
-    pst_l = [int(v) for v in pst.tolist()]
-    po_l = po[torch.tensor(pst_l, dtype=torch.int64, device=dev)].tolist() if local.n_local_nodes else [0] * (world + 1)
+    pst_l = pst.tolist()
+    po_l = po[pst.to(torch.int64)].tolist() if local.n_local_nodes else [0] * (world + 1)
     key_counts = [pst_l[k + 1] - pst_l[k] for k in range(world)]
     byte_counts = [int(po_l[k + 1] - po_l[k]) for k in range(world)]
     lens = (po[1:] - po[:-1]) if local.n_local_nodes else torch.zeros(0, dtype=torch.int64, device=dev)
     r_blob, _ = C.a2av(pb[:int(po_l[-1])] if local.n_local_nodes else pb[:0], byte_counts)
-    r_lens, r_kc = C.a2av(lens, key_counts)
-    r_idx, _ = C.a2av(pidx.to(torch.int64), key_counts)
+    (r_lens, r_idx), r_kc = C.a2av_multi([lens, pidx.to(torch.int64)], key_counts)
     r_src = torch.repeat_interleave(torch.arange(world, dtype=torch.int64, device=dev),
                                     torch.tensor(r_kc, dtype=torch.int64, device=dev))
     r_off = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
@@ -656,7 +725,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         r_off[1:] = torch.cumsum(r_lens, 0)
     ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
     okey = (r_src << 32) | r_idx  # (source rank, local id): global first-touch order
-    dkey = okey[first_of.to(torch.int64)] if nd else okey[:0]
+    fo = first_of.to(torch.int64)
+    dkey = okey[fo] if nd else okey[:0]
     tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
 
     # 4. global ids: rank of each distinct key's order key among all owners'
@@ -667,6 +737,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     for o, other in enumerate(all_dkey):
         if o != rank and other.numel() and nd:
             gid += torch.searchsorted(other, dkey)
+    del all_dkey
     back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
     gmap = torch.empty(local.n_local_nodes, dtype=torch.int32, device=dev)
     if local.n_local_nodes:
@@ -674,17 +745,29 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     tm["global_ids"] = (time.perf_counter() - t2) * 1e3
     out.n_nodes = n_global
     if gather_names:
-        names_d = [bytes(r_blob[int(r_off[i]):int(r_off[i + 1])].cpu().numpy()) for i in first_of.tolist()]
-        all_gid = C.allgather_v(gid)
-        blob = b"\n".join(names_d)
-        bt = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(dev)
-        all_blob = C.allgather_v(bt)
-        names = [None] * n_global
-        for g, b in zip(all_gid, all_blob):
-            parts = bytes(b.cpu().numpy()).split(b"\n") if g.numel() else []
-            for k, nm in zip(g.tolist(), parts):
-                names[k] = nm
-        out.names = names
+        # the owner's distinct keys (bytes at r_off[first_of]) with their global ids, to the
+        # gathering rank(s) in one blob + lengths each; put in id order there (g2n_gather_names)
+        t5 = time.perf_counter()
+        d_lens = r_lens[fo] if nd else r_lens[:0]
+        d_off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
+        if nd:
+            d_off[1:] = torch.cumsum(d_lens, 0)
+        tot = int(d_off[-1].item())
+        src = torch.repeat_interleave(r_off[fo] - d_off[:-1], d_lens) if nd else d_off[:0]
+        d_blob = r_blob[src + torch.arange(tot, dtype=torch.int64, device=dev)] if tot else r_blob[:0]
+        p_gid = list(C.parts(gid, root=names_root))
+        p_len = list(C.parts(d_lens, root=names_root))
+        p_blob = list(C.parts(d_blob, root=names_root))
+        if p_gid:
+            g_all = np.concatenate([x.cpu().numpy() for _, x in p_gid])
+            l_all = np.concatenate([x.cpu().numpy() for _, x in p_len])
+            b_all = np.concatenate([x.cpu().numpy() for _, x in p_blob])
+            o_all = np.zeros(len(l_all) + 1, dtype=np.int64)
+            np.cumsum(l_all, out=o_all[1:])
+            order = np.empty(n_global, dtype=np.int64)
+            order[g_all] = np.arange(n_global, dtype=np.int64)  # the key holding global id i
+            out.names_blob, out.names_offsets = nat.gather_names(b_all, o_all, order)
+        tm["names"] = (time.perf_counter() - t5) * 1e3
 
     # 5. triplets to row owners (and the A.T stream for MAX-SYM); 6. this rank's CSR row slice
     local.dtype_name = dtype
@@ -693,51 +776,77 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         out.coo = (g[local.rows.to(torch.int64)].to(torch.int32), g[local.cols.to(torch.int64)].to(torch.int32),
                    local.data)
     a, tstream = _route(engine, C, local, dtype, gmap.view(torch.int32), n_global, maxsym, not weight_tag, tm)
-    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm)
+    return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()))
+
+
+def _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, n_trip):
+    """Step 6 and the result's index-dtype count (scipy_index_dtype)."""
+    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, out.n_nodes, dtype, weight_tag, tm)
     out.row_lo, out.row_hi = row_lo, row_hi
     out.indptr, out.indices, out.data = indptr, indices, vals
+    nnz, trip = C.allreduce_sum([int(indices.numel()), n_trip], engine.device)
+    out.index_maxval = nnz if maxsym else trip
     out.timings_ms = tm
     return out
 
 
-def gather_coo(res: ShardResult, group=None):
-    """Every rank's stream-order triplets concatenated in rank order (numpy) on every rank: the
-    file's stream-order COO (builders.py:281), since the ranges are contiguous."""
+_NPDT = {"uint8": np.uint8, "int8": np.int8, "int32": np.int32, "float32": np.float32, "float64": np.float64}
+
+
+def _np_dtype(t):
+    return _NPDT[str(t.dtype).replace("torch.", "")]
+
+
+def _bytes_view(t):
+    """A tensor's raw bytes as a 1-D uint8 tensor (what the collectives move for any dtype)."""
     import torch
 
+    t = t.contiguous().reshape(-1)
+    return t if t.dtype == torch.uint8 else (t.view(torch.uint8) if t.numel() else t.to(torch.uint8))
+
+
+def gather_coo(res: ShardResult, group=None, root=None):
+    """Every rank's stream-order triplets concatenated in rank order (numpy): the file's
+    stream-order COO (builders.py:281), since the ranges are contiguous.  On every rank (root
+    None) or on `root` only (the others return None).  Index dtype from the shape (< 2^31 ids)."""
     C = Comm(group)
     rows, cols, data = res.coo
-    pr = C.allgather_v(rows)
-    pc = C.allgather_v(cols)
-    dt = data.dtype
-    raw = data.contiguous()
-    raw = raw.view(torch.uint8) if raw.numel() and dt != torch.uint8 else raw.reshape(-1).to(torch.uint8)
-    pd = C.allgather_v(raw)
-    npdt = {torch.uint8: np.uint8, torch.int8: np.int8, torch.int32: np.int32, torch.float32: np.float32,
-            torch.float64: np.float64}[dt]
-    return (np.concatenate([x.cpu().numpy() for x in pr]), np.concatenate([x.cpu().numpy() for x in pc]),
-            np.concatenate([x.cpu().numpy().view(npdt) if dt != torch.uint8 else x.cpu().numpy() for x in pd]))
+    npdt = _np_dtype(data)
+    pr = [x.cpu().numpy() for _, x in C.parts(rows, root)]
+    pc = [x.cpu().numpy() for _, x in C.parts(cols, root)]
+    pd = [x.cpu().numpy().view(npdt) for _, x in C.parts(_bytes_view(data), root)]
+    if not pr:
+        return None
+    return np.concatenate(pr), np.concatenate(pc), np.concatenate(pd)
 
 
-def gather_csr(res: ShardResult, group=None):
-    """Every rank's slice concatenated into the full CSR (numpy), on every rank."""
-    import torch
-
+def gather_csr(res: ShardResult, group=None, root=None):
+    """The row slices concatenated into the full CSR (numpy) on every rank (root None: one
+    broadcast per slice, no padding) or on `root` only (point-to-point; the others return None).
+    indptr / indices take scipy's index dtype for the whole matrix (scipy_index_dtype: int64 once
+    nnz — or the triplet count for coo.tocsr() — passes 2^31 - 1)."""
     C = Comm(group)
-    parts_p = C.allgather_v(res.indptr.to(torch.int64))
-    parts_i = C.allgather_v(res.indices.to(torch.int64))
-    dt = res.data.dtype
-    raw = res.data.contiguous()
-    raw = raw.view(torch.uint8) if raw.numel() and dt != torch.uint8 else raw.reshape(-1).to(torch.uint8)
-    parts_d = C.allgather_v(raw)
-    indptr = [np.zeros(1, dtype=np.int64)]
-    base = 0
-    for p in parts_p:
-        p = p.cpu().numpy()
-        indptr.append(p[1:] + base)
-        base += int(p[-1]) if len(p) else 0
-    indices = np.concatenate([x.cpu().numpy() for x in parts_i])
-    npdt = {torch.uint8: np.uint8, torch.int8: np.int8, torch.int32: np.int32, torch.float32: np.float32,
-            torch.float64: np.float64}[dt]
-    data = np.concatenate([x.cpu().numpy().view(npdt) if dt != torch.uint8 else x.cpu().numpy() for x in parts_d])
-    return np.concatenate(indptr), indices, data
+    idt = scipy_index_dtype(res.index_maxval, res.n_nodes)
+    npdt = _np_dtype(res.data)
+    parts_p = [x.cpu().numpy() for _, x in C.parts(res.indptr, root)]
+    if not parts_p:
+        for _ in C.parts(res.indices, root):
+            pass
+        for _ in C.parts(_bytes_view(res.data), root):
+            pass
+        return None
+    indptr = concat_indptr(parts_p, idt)
+    nnz = int(indptr[-1])
+    indices = np.empty(nnz, dtype=idt)
+    data = np.empty(nnz, dtype=npdt)
+    pos = 0
+    for _, x in C.parts(res.indices, root):
+        k = x.numel()
+        indices[pos:pos + k] = x.cpu().numpy()
+        pos += k
+    pos = 0
+    for _, x in C.parts(_bytes_view(res.data), root):
+        k = x.numel()
+        data.view(np.uint8)[pos:pos + k] = x.cpu().numpy()
+        pos += k
+    return indptr, indices, data

@@ -16,7 +16,7 @@ from . import _native
 
 class Spec(ctypes.Structure):
     _fields_ = [("n_segments", ctypes.c_uint64), ("n_links", ctypes.c_uint64), ("seed", ctypes.c_uint64),
-                ("rc_tag", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("rc_tag", ctypes.c_int32), ("names", ctypes.c_int32)]
 
 
 @dataclass(frozen=True)
@@ -59,10 +59,15 @@ def _lib():
     return lib
 
 
-def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, threads: int = 0) -> bytes:
-    """The synthetic GFA as bytes, generated on the CPU."""
+NAME_MODES = {"decimal": 0, "hashed": 1}
+
+
+def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, threads: int = 0,
+               names: str = "decimal") -> bytes:
+    """The synthetic GFA as bytes, generated on the CPU.  names="hashed": segment i is named
+    "s" + 8 hex digits of a bijection of i (unique, not the decimal ids "1".."N")."""
     lib = _lib()
-    spec = Spec(n_segments, n_links, seed, int(rc_tag), 0)
+    spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names])
     ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
     rc = lib.g2n_synth_host(ctypes.byref(spec), threads, ctypes.byref(ptr), ctypes.byref(n))
     if rc:
@@ -76,9 +81,10 @@ def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = Fals
 class DeviceInput:
     """Synthetic GFA generated directly in HBM; owns the device buffer."""
 
-    def __init__(self, n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, device: int = 0):
+    def __init__(self, n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, device: int = 0,
+                 names: str = "decimal"):
         lib = _lib()
-        spec = Spec(n_segments, n_links, seed, int(rc_tag), 0)
+        spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names])
         ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
         rc = lib.g2n_synth_device(device, ctypes.byref(spec), ctypes.byref(ptr), ctypes.byref(n))
         if rc:

@@ -212,6 +212,13 @@ void g2n_split_free(g2n_split_out *o);
  * with name i = blob[offsets[i] .. offsets[i+1]).  Host memory, parallel over host threads. */
 int g2n_join_names(const uint8_t *blob, const int64_t *offsets, uint64_t n_names, uint8_t sep, uint8_t *out);
 
+/* Names in a new order: out name i = name order[i] of (blob, offsets), written at out_offsets[i] -
+ * out_offsets[0] (the caller scans the reordered lengths).  The sharded build's node list: each
+ * owner rank's distinct keys arrive in owner order and are put in global id order
+ * (builders.py:284-288 node_list = keys in node2idx insertion order).  Host threads. */
+int g2n_gather_names(const uint8_t *blob, const int64_t *offsets, const int64_t *order, uint64_t n_names,
+                     const int64_t *out_offsets, uint8_t *out);
+
 /* ---- convert CLI writers (host threads) -------------------------------------------------
  * scipy.sparse.save_npz(path, A) as `convert --matrix x.npz` calls it (utils.py:85-86): a
  * zip64 archive of deflated members (numpy savez_compressed's layout).  Member i is named

@@ -15,11 +15,12 @@ extern "C" {
 #endif
 
 typedef struct g2n_synth_spec {
-  uint64_t n_segments; /* S lines, named 1..n_segments */
+  uint64_t n_segments; /* S lines, named 1..n_segments (names = 0) */
   uint64_t n_links;    /* L lines */
   uint64_t seed;
   int32_t rc_tag;      /* append RC:i:k to every L line */
-  int32_t pad_;
+  int32_t names;       /* 0: segment i is "i"; 1: "s" + 8 hex digits of a bijection of i
+                          (unique, not decimal: the hash-dictionary / general sharded paths) */
 } g2n_synth_spec;
 
 /* host: malloc'd buffer of the whole file (free with g2n_synth_free_host) */

@@ -182,3 +182,62 @@ def test_gpu_route_triplets_stable_partition(gpu, n_ranks):
         assert rr.numel() == 0 and np.array_equal(st.cpu().numpy(), np.zeros(n_ranks + 1))
     finally:
         eng.close()
+
+
+def _gz_worker(rank, world, port, paths, outdir):
+    """parse_gfa_sharded on .gz files: a clean one equals the single-GPU build; a truncated / corrupt
+    one raises exactly what the single-GPU parse_gfa raises (gzip.py's exception and message, after
+    the lines before the failure were parsed) on every rank."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+
+        from gfa2network_amd import parse_gfa, parse_gfa_sharded
+
+        for path in paths:
+            outs = []
+            for fn in (lambda: parse_gfa_sharded(path, return_node_list=True),
+                       lambda: parse_gfa(path, build_graph=False, build_matrix=True, return_node_list=True)):
+                with warnings.catch_warnings(record=True) as w:
+                    warnings.simplefilter("always")
+                    try:
+                        outs.append(("ok", fn(), [str(x.message) for x in w]))
+                    except Exception as exc:  # noqa: BLE001 - compared below
+                        outs.append(("exc", (type(exc), str(exc)), [str(x.message) for x in w]))
+            (ka, va, wa), (kb, vb, wb) = outs
+            assert ka == kb and wa == wb, (path, outs)
+            if ka == "exc":
+                assert va == vb, (path, va, vb)
+            else:
+                (A, na), (B, nb) = va, vb
+                assert na == nb and np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+                assert A.data.tobytes() == B.data.tobytes()
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_sharded_gzip_clean_and_corrupt(gpu, tmp_path):
+    import gzip
+    import zlib
+
+    import torch.multiprocessing as mp
+
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(20_000, 80_000, seed=23)
+    good = gzip.compress(data[:len(data) // 2]) + gzip.compress(data[len(data) // 2:])
+    paths = []
+    for name, blob in (("good.gfa.gz", good), ("trunc.gfa.gz", good[:len(good) * 3 // 4]),
+                       ("crc.gfa.gz", good[:-8] + (zlib.crc32(b"x") & 0xFFFFFFFF).to_bytes(4, "little") + good[-4:]),
+                       ("garbage.gfa.gz", good[:100] + bytes(range(256)) * 8 + good[2148:])):
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(str(p))
+    mp.spawn(_gz_worker, args=(2, _free_port(), paths, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert (tmp_path / f"ok{r}.npy").exists()

@@ -199,3 +199,140 @@ def test_file_line_ranges_match_in_memory_ranges(tmp_path):
         path.write_bytes(data)
         for g in (1, 2, 3, 7, 8):
             assert file_line_ranges(str(path), g, window=4096) == line_ranges(data, g)
+
+
+def test_scipy_index_dtype_past_int32():
+    """The gathered result's index dtype is scipy's (get_index_dtype with check_contents): int32 up
+    to 2^31 - 1 entries / nodes, int64 beyond (builders.py:281-283, utils.py:55)."""
+    from gfa2network_amd.shard import scipy_index_dtype
+
+    assert scipy_index_dtype(2**31 - 1, 10) == np.int32
+    assert scipy_index_dtype(2**31, 10) == np.int64
+    assert scipy_index_dtype(0, 2**31) == np.int64
+    assert scipy_index_dtype(5, 2**31 - 1) == np.int32
+
+
+def test_concat_indptr_past_int32():
+    """Slice indptrs (each from 0) whose entries total more than 2^31: the global indptr is int64
+    and exact — no int32 wrap (three slices of 1.0e9 / 0.9e9 / 0.4e9 entries)."""
+    from gfa2network_amd.shard import concat_indptr, scipy_index_dtype
+
+    parts = [np.array([0, 10**9 - 5, 10**9], dtype=np.int32), np.array([0, 9 * 10**8], dtype=np.int32),
+             np.array([0], dtype=np.int32), np.array([0, 1, 4 * 10**8], dtype=np.int32)]
+    total = 10**9 + 9 * 10**8 + 4 * 10**8
+    dt = scipy_index_dtype(total, 5)
+    assert dt == np.int64
+    ip = concat_indptr(parts, dt)
+    assert ip.dtype == np.int64
+    assert ip.tolist() == [0, 10**9 - 5, 10**9, 19 * 10**8, 19 * 10**8 + 1, total]
+    small = concat_indptr([np.array([0, 2, 3], dtype=np.int32), np.array([0, 4], dtype=np.int32)], np.int32)
+    assert small.dtype == np.int32 and small.tolist() == [0, 2, 3, 7]
+
+
+def _root_worker(rank, world, port, path, mode, root, outdir):
+    """parse_gfa_sharded(..., root=k): the result on rank k only, equal to the single-file one."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gfa2network_amd.api import finalize, parse_gfa_sharded
+        from oracle import oracle as orc
+        from shard_cpu_engine import CpuEngine
+
+        data = open(path, "rb").read()
+        full = orc.run(data, **mode)
+        for output in ("parse", "csr"):
+            got = parse_gfa_sharded(path, engine=CpuEngine(orc), return_node_list=output == "parse", output=output,
+                                    root=root, **mode)
+            if rank != root:
+                assert got is None
+                continue
+            if output == "parse":
+                A, nodes = got
+                B, bnodes = finalize(orc.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                                     return_node_list=True, raw_bytes_id=False, verbose=False)
+                assert nodes == bnodes
+            else:
+                A, B = got, orc.to_raw(full, "csr")
+            if A.format == "coo":
+                assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+            else:
+                assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+                assert A.indptr.dtype == np.int32
+            assert np.asarray(A.data).tobytes() == np.asarray(B.data).tobytes()
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,root", [("shuffled", 1), ("decimal", 2), ("undirected", 0)])
+def test_parse_gfa_sharded_to_root_only(oracle_lib, tmp_path, name, root):
+    import torch.multiprocessing as mp
+
+    data, mode = CASES[name]
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    mp.spawn(_root_worker, args=(3, _free_port(), str(path), mode, root, str(tmp_path)), nprocs=3, join=True)
+    for r in range(3):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def _want_worker(rank, world, port, paths, outdir):
+    """shard="auto" is decided collectively: rank 0's GPU has room, rank 1's does not -> both shard;
+    ranks naming different files -> ValueError on every rank (no rank enters the build alone)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gfa2network_amd import api
+
+        size = os.path.getsize(paths[0])
+        free = size * api.WORKING_SET_PER_INPUT_BYTE * (4 if rank == 0 else 0.5)
+        torch.cuda.mem_get_info = lambda device=None: (int(free), int(free))
+        assert api._want_shard(paths[0], "auto", 0) is True
+        assert api._want_shard(paths[0], "never", 0) is False
+        torch.cuda.mem_get_info = lambda device=None: (10**15, 10**15)
+        assert api._want_shard(paths[0], "auto", 0) is False  # fits everywhere
+        with pytest.raises(ValueError, match="same file"):
+            api._want_shard(paths[rank], "always", 0)
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_auto_is_decided_collectively(tmp_path):
+    import torch.multiprocessing as mp
+
+    paths = []
+    for k in range(2):
+        p = tmp_path / f"in{k}.gfa"
+        p.write_bytes(CASES["tiny"][0] * (k + 1))
+        paths.append(str(p))
+    mp.spawn(_want_worker, args=(2, _free_port(), paths, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+@pytest.mark.parametrize("bidirected", [False, True])
+def test_decimal_and_gathered_names(bidirected):
+    """The node-list helpers of the sharded build: decimal ids by arithmetic (builders.py:190-198
+    keys "k" / "k:+", "k:-") and names put in global id order (g2n_gather_names)."""
+    from gfa2network_amd import _native as nat
+
+    for n in (0, 2, 8, 10, 18, 20, 198, 200, 2002, 20000):
+        blob, offs = nat.decimal_names(n, bidirected)
+        want = ([f"{k // 2 + 1}:{'+-'[k & 1]}" for k in range(n)] if bidirected else [str(k + 1) for k in range(n)])
+        assert [bytes(blob[offs[i]:offs[i + 1]]).decode() for i in range(n)] == want
+    rng = np.random.default_rng(5)
+    keys = [bytes(rng.integers(33, 127, rng.integers(0, 40)).astype(np.uint8)) for _ in range(3000)]
+    offs = np.zeros(len(keys) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(k) for k in keys])
+    blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
+    order = rng.permutation(len(keys))
+    ob, oo = nat.gather_names(blob, offs, order)
+    assert [bytes(ob[oo[i]:oo[i + 1]]) for i in range(len(keys))] == [keys[k] for k in order]
