@@ -95,6 +95,47 @@ def algorithmic_bytes(input_bytes: int, n_nodes: int, nnz: int, w_dtype: int, w_
     return input_bytes + (n_nodes + 1) * w_idx + nnz * (w_idx + w_dtype)
 
 
+def config_leg(lib, nat, synth, wl, device: int, steps: int, warmup: int) -> dict:
+    """One more BASELINE config on this GPU, device-resident like the headline (C2 / C3 beside C4):
+    ms per build (host clock around g2n_build_device, which returns after its stream drained),
+    edge records/s, phase times (hipEvents) and the whole-path fraction of HBM peak."""
+    dev_in = synth.DeviceInput(wl.n_segments, wl.n_links, seed=0, rc_tag=wl.rc_tag, device=device)
+    ctx = lib.g2n_context_create(device)
+    mode = dict(wl.mode)
+    o = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=device,
+                         directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
+                         weight_tag=mode.get("weight_tag"))
+    res = nat.Result()
+    phases = []
+    try:
+        for k in range(warmup + steps):
+            if k == warmup:
+                t0 = time.perf_counter()
+            rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res))
+            if rc != 0:
+                raise RuntimeError(f"{wl.name}: {nat.status_name(rc)}: {nat.last_error()}")
+            if k >= warmup:
+                ph = {}
+                for j in range(res.n_phases):
+                    name = res.phase_names[j].decode()
+                    if not name.startswith("_"):
+                        ph[name] = ph.get(name, 0.0) + res.phase_ms[j]
+                phases.append(ph)
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        lib.g2n_context_destroy(ctx)
+        dev_in.free()
+    avg = {k: sum(p.get(k, 0.0) for p in phases) / len(phases) for k in phases[0]}
+    dev_ms = sum(avg.values())
+    b_alg = algorithmic_bytes(int(res.input_bytes), int(res.n_nodes), int(res.nnz), 8)
+    return {"workload": f"{wl.name}: {wl.note}", "ms_per_step": round(dt * 1e3, 3),
+            "m_edges_per_s": round(int(res.n_edges) / dt / 1e6, 2),
+            "gb_per_s_ingested": round(int(res.input_bytes) / dt / 1e9, 2), "nnz": int(res.nnz),
+            "device_ms_per_step": round(dev_ms, 3), "phase_ms": {k: round(v, 3) for k, v in avg.items()},
+            "pipeline_roofline": {"bound": "hbm", "b_alg_bytes": b_alg,
+                                  "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
 def cpu_baseline(workload, links: int) -> dict:
     """The oracle (C++ restatement of the reference, 1 thread) on a bounded sample of the
     same generator: segments scaled with the links so the S:L ratio is kept."""
@@ -585,6 +626,9 @@ def main():
         line["roofline"]["random_access"] = random_ceiling(probes, avg[dom])
     lib.g2n_context_destroy(ctx)
     dev_in.free()
+    if world == 1 and not args.no_alt and args.workload == "C4" and args.scale == 1:
+        line["other_configs"] = {w: config_leg(lib, nat, synth, synth.WORKLOADS[w], local, max(args.steps, 10),
+                                               max(args.warmup, 2)) for w in ("C2", "C3")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
     if rank == 0 and world == 1 and not args.no_e2e:

@@ -7,6 +7,6 @@ C-ABI in include/g2n.h (libg2n.so, loaded with ctypes).
 """
 from .api import convert_format, export_edge_list, parse_gfa, parse_gfa_sharded
 
-__version__ = "0.2.0"
+__version__ = "0.3.0"
 
 __all__ = ["parse_gfa", "parse_gfa_sharded", "convert_format", "export_edge_list", "__version__"]

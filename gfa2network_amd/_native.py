@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from dataclasses import dataclass, field
 from pathlib import Path
 
@@ -118,6 +119,36 @@ class NativeUnavailable(RuntimeError):
     """libg2n.so is missing or cannot be loaded (the path has no CPU fallback)."""
 
 
+def _torch_hip_runtime() -> str | None:
+    """Path of the HIP runtime bundled in the installed torch wheel, found without importing torch."""
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError, AttributeError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    p = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    return str(p) if p.exists() else None
+
+
+def _preload_hip_runtime() -> None:
+    """One HIP runtime per process: torch's wheel bundles a libamdhip64.so.7 of its own (same
+    SONAME as /opt/rocm's, which libg2n.so names), and whichever loads first serves both; torch
+    cannot initialise the device on /opt/rocm's.  So when torch is installed, its runtime is
+    loaded by path (RTLD_GLOBAL) before libg2n.so — without importing torch, which the
+    single-GPU path never needs; with no torch, libg2n.so resolves /opt/rocm's."""
+    if "torch" in sys.modules and sys.modules["torch"] is not None:
+        return  # torch loaded its runtime already
+    p = _torch_hip_runtime()
+    if p:
+        try:
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        except OSError:
+            pass
+
+
 def load() -> ctypes.CDLL:
     """Load libg2n.so once; raise NativeUnavailable when it is absent."""
     global _lib
@@ -128,13 +159,7 @@ def load() -> ctypes.CDLL:
         raise NativeUnavailable(
             f"{path} not found: build it with `make -C gfa2network_amd/csrc` "
             "(or __graft_entry__.build()); the GFA->CSR path has no CPU fallback")
-    try:
-        # One HIP runtime per process: torch's wheel bundles a libamdhip64.so.7 of its own (same
-        # SONAME as /opt/rocm's, which libg2n.so names), and whichever loads first serves both.
-        # torch cannot initialise the device on /opt/rocm's, so load torch's first when present.
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_hip_runtime()
     try:
         lib = ctypes.CDLL(path)
     except OSError as exc:  # pragma: no cover - depends on the image

@@ -30,6 +30,14 @@ import scipy.sparse as sp
 from . import _native as nat
 from ._native import RawResult
 
+try:  # the reference's verbose progress draws a tqdm bar when tqdm is importable (utils.py:8-14)
+    from tqdm.auto import tqdm
+
+    _HAS_TQDM = True
+except Exception:  # noqa: BLE001 - the same broad guard as the reference
+    tqdm = None  # type: ignore
+    _HAS_TQDM = False
+
 __all__ = ["parse_gfa", "parse_gfa_names", "parse_gfa_sharded", "convert_format", "finalize", "raise_for_status",
            "save_npz"]
 
@@ -576,9 +584,12 @@ def convert_format(A, fmt: str, *, verbose: bool = False):
         raise ValueError("matrix-format must be csr|csc|coo|dok")
     if fmt == "coo":
         return A
-    if verbose:
-        start = time.perf_counter()
-        print(f"[convert] -> {fmt} …", end="", file=sys.stderr, flush=True)
+    if verbose:  # utils.py:49-53
+        if _HAS_TQDM:
+            bar = tqdm(total=1, bar_format="{desc} …{elapsed}", desc=f"[convert→{fmt}")
+        else:
+            start = time.perf_counter()
+            print(f"[convert] -> {fmt} …", end="", file=sys.stderr, flush=True)
     if fmt == A.format:
         out = A
     elif fmt == "dok":
@@ -589,8 +600,12 @@ def convert_format(A, fmt: str, *, verbose: bool = False):
     else:
         coo = A if A.format == "coo" else A.tocoo()
         out = _native_tocsr(coo) if fmt == "csr" else _native_tocsc(coo)
-    if verbose:
-        print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
+    if verbose:  # utils.py:56-62
+        if _HAS_TQDM:
+            bar.update(1)
+            bar.close()
+        else:
+            print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
     return out
 
 
@@ -605,9 +620,13 @@ def save_matrix(A, dest: Path, *, verbose: bool = False, max_dense_gb: float = 5
             raise MemoryError(
                 f"dense export would allocate {nnz*itemsize/1e9:.1f} GB; choose a sparse .npz or write an edge list instead"
             )
-    if verbose:
-        start = time.perf_counter()
-        print(f"[save] {dest.suffix[1:]} → {dest}", "...", end="", file=sys.stderr, flush=True)
+    if verbose:  # utils.py:77-83
+        msg = f"[save] {dest.suffix[1:]} → {dest}"
+        if _HAS_TQDM:
+            bar = tqdm(total=1, bar_format="{desc} …{elapsed}", desc=msg)
+        else:
+            start = time.perf_counter()
+            print(msg, "...", end="", file=sys.stderr, flush=True)
     if dest.suffix == ".npz":
         save_npz(dest, A)
     elif dest.suffix == ".npy":
@@ -616,8 +635,12 @@ def save_matrix(A, dest: Path, *, verbose: bool = False, max_dense_gb: float = 5
         np.savetxt(dest, A.toarray() if sp.issparse(A) else A, delimiter=",", fmt="%.6g")
     else:
         raise ValueError("matrix path must end with .npz, .npy, or .csv")
-    if verbose:
-        print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
+    if verbose:  # utils.py:99-105
+        if _HAS_TQDM:
+            bar.update(1)
+            bar.close()
+        else:
+            print(f" done in {time.perf_counter() - start:,.1f}s", file=sys.stderr)
 
 
 def _npy_header(val: np.ndarray) -> bytes:

@@ -130,7 +130,7 @@ int guarded(const std::function<int()>& f) {
 
 extern "C" {
 
-const char* g2n_version(void) { return "gfa2network-amd 0.1.0 (gfx950)"; }
+const char* g2n_version(void) { return "gfa2network-amd " G2N_VERSION_STRING " (gfx950)"; }
 uint32_t g2n_abi_version(void) { return G2N_ABI_VERSION; }
 const char* g2n_last_error(void) { return g2n::t_last_error.c_str(); }
 

@@ -105,6 +105,9 @@ __global__ void __launch_bounds__(kInflTPB) k_inflate_members(const uint8_t* __r
                                                               unsigned int* __restrict__ n_bad) {
   __shared__ InflTables tabs[kInflTPB];
   __shared__ uint32_t crc_tab[256];
+  // 64 x 1056 B + 1 KB = 68.6 KB: needs gfx950's 160 KB of LDS per workgroup (the Makefile's
+  // ARCH is gfx950; older CDNA parts have 64 KB and would fail this launch)
+  static_assert(sizeof(tabs) + sizeof(crc_tab) <= 160 * 1024, "k_inflate_members LDS exceeds gfx950's 160 KB");
   for (uint32_t k = threadIdx.x; k < 256; k += kInflTPB) {
     uint32_t c = k;
     for (int j = 0; j < 8; j++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;

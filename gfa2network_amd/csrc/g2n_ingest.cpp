@@ -296,7 +296,20 @@ bool gunzip_parallel(const uint8_t* in, size_t n, Inflated& out) {
   if (nc > ((size_t)1 << 22)) return false;  // pathological; let the serial reader handle it
   // few member candidates in a large file: most likely one big member, which the member-level
   // speculation below would inflate on one thread — split its deflate stream instead
-  if (n >= ((size_t)64 << 20) && nc <= 64 && gunzip_chunked(in, n, 0, out)) return true;
+  if (n >= ((size_t)64 << 20) && nc <= 64) {
+    // the chunk-parallel decode holds ~15x the compressed size of buffers at once: when they
+    // cannot be had it declines, and the member-chain / exact readers below inflate the file
+    bool ok = false;
+    try {
+      ok = gunzip_chunked(in, n, 0, out);
+    } catch (const Failure& f) {
+      if (f.status != G2N_E_NOMEM) throw;
+      out = Inflated{};
+    } catch (const std::bad_alloc&) {
+      out = Inflated{};
+    }
+    if (ok) return true;
+  }
 
   // 2. speculative inflate of every candidate; the chain walker marks candidates that fall
   //    inside a resolved member as dead, which stops (or skips) their speculation

@@ -591,10 +591,9 @@ bool gunzip_chunked(const uint8_t* in, size_t n, size_t chunk_bytes, Inflated& o
   mark("sync");
   // 2. every present chunk decodes until it stands on a later chunk's start at a block boundary
   //    (a start that turns out false is stepped over), or to the stream's BFINAL block
-  std::atomic<bool> done{false};
   parallel_for(nch, T, [&](size_t k) {
     Chunk& c = ch[k];
-    if (!c.present || done.load(std::memory_order_relaxed)) return;
+    if (!c.present) return;
     const size_t guess = 5 * std::min(chunk_bytes, n) + ((size_t)1 << 20);  // GFA text deflates ~3.3:1
     c.out.reserve(guess);
     if (k) c.sh.reserve(kWin + guess);

@@ -41,6 +41,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#define G2N_VERSION_STRING "0.3.0" /* == gfa2network_amd.__version__ (tests check) */
+
 #ifdef __cplusplus
 extern "C" {
 #endif

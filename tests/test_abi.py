@@ -90,3 +90,26 @@ def test_join_names_matches_python():
         offs[1:] = np.cumsum([len(x) for x in names])
         blob = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8)
         assert bytes(_native.join_names(blob, offs)) == b"\n".join(names)
+
+
+def test_library_loads_without_importing_torch():
+    """libg2n.so loads without `import torch` (torch's bundled HIP runtime is preloaded by path
+    when torch is installed), and loads with torch not importable at all."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parent.parent)
+    for pre in ("", "sys.modules['torch'] = None\n"):
+        code = ("import sys\n" + pre + "from gfa2network_amd import _native, parse_gfa\n_native.load()\n"
+                "assert sys.modules.get('torch') is None, 'torch was imported'\nprint(_native.version())\n")
+        r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "gfa2network-amd" in r.stdout
+
+
+def test_library_version_matches_package():
+    import gfa2network_amd
+    from gfa2network_amd import _native
+
+    assert _native.version() == f"gfa2network-amd {gfa2network_amd.__version__} (gfx950)"

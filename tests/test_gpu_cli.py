@@ -129,3 +129,34 @@ def test_missing_file_raises_oserror(gpu, tmp_path):
 
     with pytest.raises(gzip.BadGzipFile):
         parse_gfa(bad, build_graph=False, build_matrix=True)
+
+
+def test_single_gpu_path_without_torch(gpu, tmp_path):
+    """The single-GPU path needs no torch: with torch unimportable, parse_gfa + convert_format run
+    on the GPU through libg2n.so alone and give what this (torch-importing) process gives."""
+    import subprocess
+    import sys
+
+    import numpy as np
+
+    from gfa2network_amd import convert_format, parse_gfa
+
+    gfa = Path(__file__).parent / "golden" / "inputs" / "DRB1-3123_unsorted.gfa"
+    code = (
+        "import sys; sys.modules['torch'] = None\n"
+        "import numpy as np\n"
+        "from gfa2network_amd import convert_format, parse_gfa\n"
+        f"A, nodes = parse_gfa({str(gfa)!r}, build_graph=False, build_matrix=True, return_node_list=True,"
+        " directed=False)\n"
+        "C = convert_format(A, 'csr')\n"
+        "assert 'torch' not in sys.modules or sys.modules['torch'] is None\n"
+        f"np.savez({str(tmp_path / 'out.npz')!r}, p=C.indptr, i=C.indices, d=C.data, n=np.array(nodes))\n"
+    )
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(Path(__file__).parent.parent), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(tmp_path / "out.npz")
+    A, nodes = parse_gfa(gfa, build_graph=False, build_matrix=True, return_node_list=True, directed=False)
+    C = convert_format(A, "csr")
+    assert np.array_equal(got["p"], C.indptr) and np.array_equal(got["i"], C.indices)
+    assert got["d"].tobytes() == C.data.tobytes() and got["n"].tolist() == nodes
