@@ -49,6 +49,7 @@ TEST_DICT_HASH = 8       # no decimal ids: the hash dictionary tiers
 TEST_DICT_GENERAL = 16   # no decimal ids, no S-first fast path: the general insert rounds
 TEST_NO_TILE_LOCAL = 32  # decimal ids: the lean parse after K1's tile bases, not the tile-local pass
 TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of the GPU inflate
+TEST_NO_GROUP = 128      # tile-local parse into per-tile slots + compaction (never group slots)
 TEST_FLAGS = 0
 
 
@@ -147,6 +148,16 @@ def _preload_hip_runtime() -> None:
             ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
         except OSError:
             pass
+
+
+def hip_runtime() -> ctypes.CDLL:
+    """The HIP runtime libg2n.so runs on (by its SONAME: whichever libamdhip64.so.7 the process
+    loaded — torch's when torch is installed), for callers that copy device memory themselves."""
+    load()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipMemcpy.restype = ctypes.c_int
+    return hip
 
 
 def load() -> ctypes.CDLL:

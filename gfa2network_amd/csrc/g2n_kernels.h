@@ -99,7 +99,13 @@ struct ParseOpts {
   // tile-local lean parse (no K1): tile t's COO goes to rows / cols from t * tile_pad * ktrip,
   // its counts to TileCnt and its premise evidence to TileLean; 0 = positions from K1's bases
   uint32_t tile_pad;
+  // tile-local lean parse into GROUP slots (k_tile_lean<true>): the kGroupTiles tiles of a group
+  // share one slot; a tile's entries go, in tile order inside, at a base it takes with one atomicAdd
+  // on its group's count (the group's order of tiles is arbitrary: only for consumers that do not
+  // need stream order — the unweighted bucket partition); rows / cols already point at the base
+  uint32_t grouped;
 };
+constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
 
 // per-tile evidence of the decimal-id premise in a tile-local parse: every S line's name value
 // minus (its S index within the tile + 1), min and max (equal, = the S lines before the tile, when

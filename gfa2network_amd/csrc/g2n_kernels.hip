@@ -954,7 +954,7 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
   }
   const uint32_t vm = (uint32_t)(a > b ? a : b);
   is.vmax = vm > is.vmax ? vm : is.vmax;
-  const uint64_t o = ((op.tile_pad ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
+  const uint64_t o = ((op.tile_pad && !op.grouped ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
   op.rows[o] = (int32_t)(a - 1);
   op.cols[o] = (int32_t)(b - 1);
   if (op.ktrip >= 2) {
@@ -993,6 +993,28 @@ constexpr uint32_t kTileLines = kTileChunks;            // line starts per windo
 constexpr uint32_t kLinesPer = kTileLines / kTPB;       // lines classified per thread
 static_assert(kChunkIters % 4 == 0 && kTile <= 32768, "tile layout: per-tile counts fit 16 bits");
 
+// Diagnostics build only (-DG2N_K2_STAMPS, tools/k2_stamps.py): per tile, the wall clock at the
+// block's phase boundaries (thread 0) and the hardware id of the CU it ran on.
+#ifdef G2N_K2_STAMPS
+constexpr int kK2Stamps = 10;
+__device__ unsigned long long* g2n_k2_stamps;
+#define K2_STAMP(k)                                                                               \
+  do {                                                                                            \
+    if (kLocal && threadIdx.x == 0) g2n_k2_stamps[blockIdx.x * kK2Stamps + (k)] = wall_clock64(); \
+  } while (0)
+#define K2_LEAN_STAMP(k)                                                                 \
+  do {                                                                                   \
+    if (threadIdx.x == 0) g2n_k2_stamps[blockIdx.x * kK2Stamps + (k)] = wall_clock64();  \
+  } while (0)
+#else
+#define K2_STAMP(k) \
+  do {              \
+  } while (0)
+#define K2_LEAN_STAMP(k) \
+  do {                   \
+  } while (0)
+#endif
+
 // kLocal: the tile-local lean parse (ParseOpts.tile_pad; lean, not bidirected, no weight tag, no
 // strip — fixed at compile time, so that instance carries none of the other paths' code)
 template <bool kLocal>
@@ -1019,6 +1041,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   uint16_t* const tabm = kDiet ? nullptr : tabm_s;
   const uint64_t tile = blockIdx.x;
   const uint64_t t0 = tile * kTile;
+  K2_STAMP(0);
   {
     TileRegs<kTileHalo> R;
     R.load(in, len, t0);
@@ -1036,6 +1059,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   }
   const TileCnt b = local ? TileCnt{} : base[tile];
   __syncthreads();
+  K2_STAMP(1);
   // the tile's tab bitmap (bytes past len: 0): the tile's own chunks come with pass (1), here the halo's
   if constexpr (!kDiet)
     for (uint32_t c = kTileChunks + threadIdx.x; c < kMaskChunks; c += kTPB)
@@ -1061,6 +1085,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     if constexpr (kLocal) n_nl += (uint32_t)__popc(m);
   }
   __syncthreads();
+  K2_STAMP(2);
   uint32_t n_starts;
   {  // kChunkIters consecutive chunk counts per thread (4-word vector accesses)
     uint32_t q[kChunkIters];
@@ -1110,6 +1135,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
   }
   const uint64_t idx0 = b.nl + (tile_prev_nl ? 0 : 1);  // index of the tile's first line
   __syncthreads();
+  K2_STAMP(3);
   uint32_t rank[kChunkIters];
 #pragma unroll
   for (uint32_t j = 0; j < kChunkIters; j++) rank[j] = kDiet ? (uint32_t)pre16[j * kTPB + threadIdx.x] : pre[j * kTPB + threadIdx.x];
@@ -1135,6 +1161,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       }
     }
     __syncthreads();
+    if (w0 == 0) K2_STAMP(4);
     // kinds of kLinesPer consecutive lines per thread; prefix counts of S and edge lines
     uint32_t cs = 0, ce = 0;
     uint8_t kk[kLinesPerW];
@@ -1161,6 +1188,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
       ex += ((uint32_t)(kk[q] == kS) << 16) | (uint32_t)(kk[q] == kEdge);
     }
     __syncthreads();
+    if (w0 == 0) K2_STAMP(5);
     // (4) parse: lane-parallel lines
 #if G2N_LEAN_ONLY
     if constexpr (kLocal) {  // the lean shapes only: any other line gives the tile-local parse up
@@ -1232,6 +1260,11 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     e_run += tot & 0xFFFF;
     s_run += tot >> 16;
   }
+#ifdef G2N_K2_STAMPS
+  K2_STAMP(6);  // thread 0's own lines parsed
+  __syncthreads();
+  K2_STAMP(7);  // every line of the block parsed
+#endif
   unk = wave_reduce_min(unk);
   if ((threadIdx.x & 63) == 0 && unk != ~0ull) atomicMin(&ctl->warn_line, unk);
   if constexpr (kLocal) {  // the tile's counts (K1's) and its premise evidence
@@ -1269,6 +1302,249 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
     }
   }
   if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+#ifdef G2N_K2_STAMPS
+  K2_STAMP(8);
+  if (kLocal && threadIdx.x == 0) {
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
+}
+
+// ============================ K2 lean: the tile-local decimal-id parse ========================
+// The tile-local lean parse (ParseOpts.tile_pad; S lines first named "1".."N", no bidirected, no
+// weight tag, no strip) as a kernel of its own.  One 256-thread block per 32 KiB tile (+ halo):
+//  (1) the tile is staged in LDS, every 16-byte load in flight before the first store; from the
+//      same registers (chunks 256 j + t: no LDS re-read) the tab and newline bitmaps of every
+//      chunk go to LDS, one u16 each;
+//  (2) thread t takes the line starts in ITS contiguous 128 bytes (chunks 8t..8t+7: one 16-byte
+//      LDS read of their newline bitmaps), classifies them (parser.py:117-134 first-byte
+//      dispatch) and counts starts, S and edge lines; ONE block scan of the packed counts ranks
+//      its lines in the tile, and it writes one 32-bit record per line (offset, kind, S / edge
+//      prefix) at that rank;
+//  (3) lane-parallel parse: line j goes to thread j mod 256 (balanced), its end is the next
+//      record's offset, the fields come from the tab bitmap (lean_line), the result goes to the
+//      tile's COO slot.
+// Same outputs as k_tile_parse<true> (tile counts, premise evidence, COO slot) with one block
+// scan instead of three.  Anything outside the lean shapes — an unsupported record (its warning
+// needs global line indices), a line running past the staged window — fails the tile-local parse
+// and the full parse runs (tile_local_parse).
+constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
+constexpr uint32_t kLeanLines = 2048;                                   // line records per tile
+static_assert(kTile <= 32768 && kChunkIters == 8, "records hold 15-bit offsets; one 16-byte read per region");
+
+__device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
+  return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
+}
+
+template <bool kGrouped>
+__global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
+                                                    Ctl* ctl, TileCnt* __restrict__ tcnt_out,
+                                                    TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
+                                                    uint64_t gcap) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
+  __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
+  __shared__ uint32_t rec[kLeanLines + 1];
+  __shared__ unsigned long long red64[kTPB / 64];
+  __shared__ uint32_t s_gbase;
+  const uint64_t tile = blockIdx.x;
+  const uint64_t t0 = tile * kTile;
+  op.grouped = kGrouped ? 1u : 0u;  // lean_line: positions relative to the tile's base in its group slot
+  K2_LEAN_STAMP(0);
+  {
+    TileRegs<kTileHalo> R;
+    R.load(in, len, t0);
+    R.store(buf);
+#pragma unroll
+    for (uint32_t j = 0; j < R.kPer; j++) {
+      const uint32_t c = j * kTPB + threadIdx.x;
+      if (c < kLeanChunks) {
+        tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
+        nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
+      }
+    }
+  }
+  if (threadIdx.x < 8) {  // tab_window reads up to 4 bitmaps past a chunk
+    tabm[kLeanChunks + threadIdx.x] = 0;
+    nlm[kLeanChunks + threadIdx.x] = 0;
+  }
+  const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
+  __syncthreads();
+  K2_LEAN_STAMP(1);
+  IntState is;
+  // (2) this thread's region: chunks c0 .. c0 + 7, its starts as a 128-bit mask (lo, hi)
+  const uint32_t c0 = kChunkIters * threadIdx.x;
+  unsigned long long nlo, nhi, slo, shi;
+  uint32_t n_nl;
+  {
+    const uint4 v = *(const uint4*)(nlm + c0);
+    nlo = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    nhi = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
+    const unsigned long long prev = c0 ? (unsigned long long)(nlm[c0 - 1] >> 15) : (tile_prev_nl ? 1ull : 0ull);
+    slo = (nlo << 1) | prev;
+    shi = (nhi << 1) | (nlo >> 63);
+    const uint64_t r0 = t0 + 16ull * c0;  // a start needs a byte: none at or past len
+    if (r0 + 128 > len) {
+      const uint64_t n = r0 >= len ? 0 : len - r0;
+      slo &= n >= 64 ? ~0ull : ((1ull << n) - 1);
+      shi &= n >= 128 ? ~0ull : (n <= 64 ? 0ull : ((1ull << (n - 64)) - 1));
+    }
+    n_nl = (uint32_t)(__popcll(nlo) + __popcll(nhi));
+  }
+  const uint32_t n_st = (uint32_t)(__popcll(slo) + __popcll(shi));
+  uint32_t n_s = 0, n_e = 0, n_po = 0;
+  {
+    unsigned long long lo = slo, hi = shi;
+#pragma unroll 1
+    for (uint32_t q = 0; q < n_st; q++) {
+      uint32_t b;
+      if (lo) {
+        b = (uint32_t)__builtin_ctzll(lo);
+        lo &= lo - 1;
+      } else {
+        b = 64 + (uint32_t)__builtin_ctzll(hi);
+        hi &= hi - 1;
+      }
+      const uint32_t o = 16 * c0 + b;
+      const uint8_t kd = kind_at(buf, o, t0 + o, len);
+      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
+      const uint32_t code = lean_code(kd);
+      n_s += code == 1;
+      n_e += code == 2;
+      n_po += code == 3;
+    }
+  }
+  unsigned long long tot;
+  const unsigned long long ex =
+      block_excl_scan_u64((unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40),
+                          &tot, red64);
+  const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
+                 e_tot = (uint32_t)(tot >> 40);
+  const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
+  if (kGrouped && threadIdx.x == 0 && n_lines == 0)
+    s_gbase = 0;  // no window below
+  if (kGrouped && threadIdx.x == 0 && n_lines)  // this tile's place in its group slot (published by the barrier below)
+    s_gbase = e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
+  // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
+  // records of its lines ranked in [w0, w0 + kLeanLines] (one past: the window's last line ends where
+  // the next one starts), then the window's lines are parsed
+  for (uint32_t w0 = 0; w0 < n_lines; w0 += kLeanLines) {
+    if (w0) __syncthreads();  // the previous window's records are read
+    {
+      uint32_t r = (uint32_t)(ex & 0xFFFFFu), sp = (uint32_t)((ex >> 20) & 0xFFFFFu), ep = (uint32_t)(ex >> 40);
+      unsigned long long lo = slo, hi = shi;
+#pragma unroll 1
+      for (uint32_t q = 0; q < n_st && r <= w0 + kLeanLines; q++, r++) {
+        uint32_t b;
+        if (lo) {
+          b = (uint32_t)__builtin_ctzll(lo);
+          lo &= lo - 1;
+        } else {
+          b = 64 + (uint32_t)__builtin_ctzll(hi);
+          hi &= hi - 1;
+        }
+        const uint32_t o = 16 * c0 + b;
+        const uint32_t code = lean_code(kind_at(buf, o, t0 + o, len));
+        if (w0 == 0 && code == 1 && ep) is.fail = 1;  // an S line after an edge line: not the decimal-id layout
+        if (r >= w0) rec[r - w0] = o | (code << 15) | ((code == 1 ? sp : ep) << 17);
+        sp += code == 1;
+        ep += code == 2;
+      }
+    }
+    __syncthreads();
+    if (w0 == 0) {
+      K2_LEAN_STAMP(2);
+      if (kGrouped) {
+        const uint64_t b = (tile >> kGroupShift) * gcap + s_gbase;
+        op.rows += b;
+        op.cols += b;
+      }
+    }
+    // (3) lane-parallel lines
+    const uint32_t n_win = n_lines - w0 < kLeanLines ? n_lines - w0 : kLeanLines;
+#pragma unroll 1
+    for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
+      const uint32_t x = rec[j];
+      const uint32_t code = (x >> 15) & 3u;
+      if (code == 0) continue;
+      const uint32_t o = x & 0x7FFFu, pref = x >> 17;
+      uint32_t next = 0;  // 1 + the line's '\n' (a virtual one at EOF), tile-local
+      if (w0 + j + 1 < n_lines) {
+        next = rec[j + 1] & 0x7FFFu;
+      } else {  // the tile's last line: its newline from the bitmaps
+        uint32_t c = o >> 4;
+        uint32_t m = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
+        const uint32_t ce = (lim + 15) / 16;
+        while (!m && ++c < ce) m = nlm[c];
+        if (m) next = 16 * c + (uint32_t)__builtin_ctz(m) + 1;
+        else if (lim == len - t0) next = lim + 1;
+      }
+      if (!next) {  // the line runs past the staged window
+        is.fail = 1;
+        continue;
+      }
+      if (code == 3) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
+        const uint32_t n = next - 1 - o, sh = o & 15;
+        const uint64_t w = tab_window(buf, tabm, o >> 4);
+        if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
+        continue;
+      }
+      // S line: tb = its S index (no edge precedes it); edge line: eb = its edge index
+      if (!lean_line(buf, tabm, o, next, code == 1 ? kS : kEdge, t0, code == 1 ? pref : 0ull,
+                     code == 1 ? 0ull : pref, op, TouchOut{}, is))
+        is.fail = 1;
+    }
+  }
+  K2_LEAN_STAMP(3);
+  // tile counts and premise evidence
+  if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
+  uint32_t vm = is.vmax;
+  int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
+  for (int o = 32; o > 0; o >>= 1) {
+    vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
+    dmn = min(dmn, (int32_t)__shfl_xor(dmn, o, 64));
+    dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
+  }
+  __shared__ uint32_t rv[kTPB / 64];
+  __shared__ int32_t rmn[kTPB / 64], rmx[kTPB / 64];
+  if ((threadIdx.x & 63) == 0) {
+    rv[threadIdx.x >> 6] = vm;
+    rmn[threadIdx.x >> 6] = dmn;
+    rmx[threadIdx.x >> 6] = dmx;
+  }
+  // P / O lines and newlines: per-tile totals (< 2^20 each)
+  const unsigned long long cnts = block_sum((unsigned long long)n_nl | ((unsigned long long)n_po << 20), red64);
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kTPB / 64; w++) {
+      vm = max(vm, rv[w]);
+      dmn = min(dmn, rmn[w]);
+      dmx = max(dmx, rmx[w]);
+    }
+    const uint32_t npo = (uint32_t)(cnts >> 20);
+    TileCnt c;
+    c.nl = cnts & 0xFFFFFu;
+    c.lines = n_lines;
+    c.segs = s_tot;
+    c.edges = e_tot;
+    c.touches = (uint64_t)s_tot + 2ull * e_tot;
+    c.recs = (uint64_t)s_tot + e_tot + npo;
+    tcnt_out[tile] = c;
+    tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
+  }
+  if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+  K2_LEAN_STAMP(4);
+#ifdef G2N_K2_STAMPS
+  if (threadIdx.x == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // Tile-local lean parse, afterwards: tile t's S lines must name (S lines before t) + their index

@@ -17,6 +17,12 @@
 
 #include "g2n_internal.h"
 #include "g2n_kernels.hip"
+#ifndef G2N_NO_GROUP_DEFAULT  // 1: never group slots (experiments)
+#define G2N_NO_GROUP_DEFAULT 0
+#endif
+#ifndef G2N_K2_OLD  // 1: the tile-local parse through k_tile_parse<true> (experiments)
+#define G2N_K2_OLD 0
+#endif
 #ifndef G2N_LOOKUP_BATCH  // touches per thread in the S-first lookup round (experiment builds vary it)
 #define G2N_LOOKUP_BATCH 2
 #endif
@@ -43,7 +49,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_NSLOTS
+  S_GCNT, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -52,11 +58,24 @@ constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean pars
 constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
 constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast path: the general rounds
 constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bases) instead of tile-local
+constexpr uint32_t kTestNoGroup = 128;      // tile-local parse into per-tile slots + compaction, never group slots
 
 
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+};
+
+// The tile-local lean parse's COO in GROUP slots (k_tile_lean<true>): group g's entries are
+// [g * gcap, g * gcap + gcount[g]) of rows / cols, its tiles in arbitrary order — for the
+// unweighted bucket partition only (csr_partition), which needs no stream order.
+struct GroupedCoo {
+  bool active = false;
+  bool failed = false;  // the partition could not take it: the build is redone without groups
+  const int32_t* rows = nullptr;
+  const int32_t* cols = nullptr;
+  const uint32_t* gcount = nullptr;
+  uint64_t gcap = 0, n_groups = 0;
 };
 
 }  // namespace g2n
@@ -66,6 +85,8 @@ struct g2n_context {
   int n_cu = 256;  // compute units: persistent launches size their grid from it
   uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
   uint64_t err_line_off = 0;  // byte offset of the last build's error line (edge-list prefix)
+  g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
+  bool no_group = false;      // redo of a build whose group-slot COO the partition refused
   hipStream_t stream = nullptr;
   std::vector<g2n::DevBuf> bufs;
   g2n::Ctl* ctl = nullptr;    // device
@@ -298,11 +319,13 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   const uint64_t n_buckets = 1ull << hb;                      // ids of the partition
   const uint64_t n_bk = (n_rows + (1ull << low) - 1) >> low;  // buckets holding rows
   const uint32_t shift1 = (uint32_t)(low + bits2);
-  PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, (sum || pair) ? 1u : 0u,
+  const bool grouped = c->gcoo.active && !pair;
+  PartSrc src{(const uint32_t*)(grouped ? c->gcoo.rows : rows), (const uint32_t*)(grouped ? c->gcoo.cols : cols),
+              grouped ? c->gcoo.n_groups * c->gcoo.gcap : n_trip, (sum || pair) ? 1u : 0u,
               (const uint32_t*)t_rows, (const uint32_t*)t_cols, pair ? n_t : 0, (uint32_t)row_base,
-              nullptr, nullptr, nullptr, 0};
-  // pass 1: over the COO entries, both sides
-  const uint64_t n_blk1 = (n_el + kPartTile - 1) / kPartTile;
+              nullptr, nullptr, nullptr, 0, grouped ? c->gcoo.gcount : nullptr, grouped ? c->gcoo.gcap : 0};
+  // pass 1: over the COO entries, both sides (grouped: one block per group slot)
+  const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + kPartTile - 1) / kPartTile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
@@ -318,10 +341,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                        (const uint32_t*)off1, n_blk1, (uint32_t)n_el, n_buckets, bst);
   } else {  // pass 2 inside each pass-1 group
     auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
-    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1};
+    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0};
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, n_blk1, n_dig1,
                        (uint32_t)n_el, grp, grp + n_dig1 + 1);
-    const uint64_t n_blk2 = n_blk1 + n_dig1;  // >= the blocks the groups need
+    // >= the blocks the groups need (sum of ceil(group / kPartTile) <= n_el / kPartTile + n_dig1)
+    const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
     auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
     auto* el2 = dget<uint2>(c, S_EL1, n_el);
@@ -372,6 +396,10 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
     if (n_trip && n_rows && (n_rows == n_cols || !maxsym) && !(c->test_flags & kTestNoBuckets) &&
         csr_partition<T>(c, rows, cols, n_trip, n_rows, !maxsym, R))
       return;
+  }
+  if (c->gcoo.active) {  // the group slots hold no stream order: redo the build without them
+    c->gcoo.failed = true;
+    return;
   }
   const T one = (T)1;
   RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0);
@@ -703,10 +731,23 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
 // slot): the caller then runs K1 and the classic parse, as if this had not run.
 constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge line is at least 12 bytes (2736 for 32 KiB)
 
+// grouped: the COO goes to group slots instead (k_tile_lean<true>, GroupedCoo) and is not compacted
+// — for builds whose only consumer is the unweighted bucket partition.
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
-                             TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out) {
-  auto* rows_p = dget<int32_t>(c, S_ROWSP, n_tiles * kTileEdgeCap * ktrip);
-  auto* cols_p = dget<int32_t>(c, S_COLSP, n_tiles * kTileEdgeCap * ktrip);
+                             TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped) {
+#if G2N_K2_OLD
+  grouped = false;  // k_tile_parse<true> writes per-tile slots only
+#endif
+  const uint64_t n_groups = (n_tiles + (1u << kGroupShift) - 1) >> kGroupShift;
+  const uint64_t gcap = ((uint64_t)kTileEdgeCap << kGroupShift) * ktrip;  // entries per group slot
+  const uint64_t slots = grouped ? n_groups * gcap : n_tiles * kTileEdgeCap * ktrip;
+  auto* rows_p = dget<int32_t>(c, S_ROWSP, slots);
+  auto* cols_p = dget<int32_t>(c, S_COLSP, slots);
+  uint32_t* gcount = nullptr;
+  if (grouped) {
+    gcount = dget<uint32_t>(c, S_GCNT, n_groups);
+    G2N_HIP(hipMemsetAsync(gcount, 0, n_groups * sizeof(uint32_t), c->stream));
+  }
   auto* tlean = dget<TileLean>(c, S_TLEAN, n_tiles);
   ParseOpts lo{};
   lo.rows = rows_p;
@@ -715,10 +756,36 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tile_pad = kTileEdgeCap;
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
+#ifdef G2N_K2_STAMPS
+  unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
+  G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));
+  G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_k2_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
+                                 c->stream));
+#endif
+#if G2N_K2_OLD  // experiment builds: the k_tile_parse<true> instance
   hipLaunchKernelGGL(k_tile_parse<true>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, (const TileCnt*)nullptr,
                      1u, 2u, lo, (uint64_t*)nullptr, (uint8_t*)nullptr, TouchOut{}, EdgeOut{}, c->ctl,
                      (uint64_t*)nullptr, (DeferredLine*)nullptr, n_tiles, tcnt, tlean);
+#else
+  if (grouped)
+    hipLaunchKernelGGL(k_tile_lean<true>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
+                       tlean, gcount, gcap);
+  else
+    hipLaunchKernelGGL(k_tile_lean<false>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, lo, c->ctl,
+                       tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0);
+#endif
   phase(c, "parse");
+#ifdef G2N_K2_STAMPS
+  if (const char* out = std::getenv("G2N_K2_STAMPS_OUT")) {  // diagnostics build only
+    std::vector<unsigned long long> h(n_tiles * kK2Stamps);
+    G2N_HIP(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(out, "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   sync_ctl(c);
   bool ok = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && c->h_ctl->warn_line == ~0ull;
   if (ok) {
@@ -734,6 +801,16 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                        (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, (uint64_t)tot.segs, c->ctl);
     sync_ctl(c);
     ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0x7FFFFFFFull;
+    if (ok && grouped) {
+      c->gcoo.active = true;
+      c->gcoo.rows = rows_p;
+      c->gcoo.cols = cols_p;
+      c->gcoo.gcount = gcount;
+      c->gcoo.gcap = gcap;
+      c->gcoo.n_groups = n_groups;
+      *tot_out = tot;
+      return true;
+    }
     if (ok) {
       const uint64_t n_trip = tot.edges * ktrip;
       auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
@@ -752,6 +829,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
 
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
+  c->gcoo = GroupedCoo{};
   c->test_flags = (uint32_t)o->reserved[1];
   R->input_bytes = len;
   c->n_ev = 0;
@@ -773,9 +851,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool shard_dec = (o->reserved[4] & 1) != 0;
   const bool first_one = !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
   // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
+  // group slots when the COO's only reader is the unweighted bucket partition (a CSR output)
+  const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
+  const bool grouped = !G2N_NO_GROUP_DEFAULT && !coo_wanted && !c->no_group &&
+                       !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
   const bool local_done = n_tiles && first_one && !shard_dec && !bidir && !(o->weight_tag && *o->weight_tag) &&
                           !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
-                          tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot);
+                          tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped);
   // ---- K1: per-tile counts -> tile bases
   if (n_tiles && !local_done) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
@@ -1023,6 +1105,20 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     case G2N_FLOAT32: assemble<float>(c, rows, cols, (const float*)data, n_trip, n_nodes, n_nodes, maxsym, uni, R); break;
     default: assemble<double>(c, rows, cols, (const double*)data, n_trip, n_nodes, n_nodes, maxsym, uni, R); break;
   }
+  if (c->gcoo.failed) {  // the partition refused the group-slot COO (an overfull bucket): once more without
+    c->gcoo = GroupedCoo{};
+    c->no_group = true;
+    int rc;
+    try {
+      rc = run_build(c, in, len, o, R);
+    } catch (...) {
+      c->no_group = false;
+      throw;
+    }
+    c->no_group = false;
+    return rc;
+  }
+  c->gcoo.active = false;
   finish_timings(c, R);
   return G2N_OK;
 }

@@ -84,6 +84,8 @@ struct PartSrc {
   const uint32_t* gstart; // n_groups + 1 element offsets of the groups
   const uint32_t* bstart; // n_groups + 1 first block of each group
   uint32_t n_groups;
+  const uint32_t* gcount; // pass 1 over group slots (GroupedCoo): block b = slot b, gcount[b] entries
+  uint64_t gcap;          //   from entry b * gcap
 };
 
 struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e0/2, e1/2))
@@ -93,6 +95,15 @@ struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e
 
 template <int kPass>
 __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) {
+  if (kPass == 1 && S.gcount) {
+    const uint64_t per = S.one_side ? 1 : 2;  // elements per entry
+    B.g = 0;
+    B.j = blk;
+    B.nb = 0;
+    B.e0 = (uint64_t)blk * S.gcap * per;
+    B.e1 = B.e0 + (uint64_t)S.gcount[blk] * per;
+    return true;
+  }
   if (kPass == 1) {
     B.g = 0;
     B.j = blk;

@@ -217,8 +217,7 @@ class HipEngine:
         self.ctx = self.lib.g2n_context_create(device)
         if not self.ctx:
             raise nat.NativeUnavailable(nat.last_error())
-        self._hip = ctypes.CDLL("libamdhip64.so")
-        self._hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        self._hip = nat.hip_runtime()
         self.ctx_b = None  # the fast path's build context: its COO is read in place by route / csr (on ctx)
 
     def close(self):

@@ -158,7 +158,7 @@ def test_c4_properties_on_device(gpu):
         assert res.n_edges == 200_000_000 and n == 50_000_000 and res.format == nat.FMT_CSR
         indptr = np.empty(n + 1, np.int32)
         indices = np.empty(nnz, np.int32)
-        hip = ctypes.CDLL("libamdhip64.so")
+        hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libg2n.so loaded (its SONAME)
         hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         assert hip.hipMemcpy(indptr.ctypes.data, res.indptr, indptr.nbytes, 2) == 0
         assert hip.hipMemcpy(indices.ctypes.data, res.indices, indices.nbytes, 2) == 0
@@ -381,8 +381,10 @@ TILE_LOCAL_CASES = {  # inputs of ~60 tiles: the premise checked ACROSS tiles af
 @pytest.mark.parametrize("case", sorted(TILE_LOCAL_CASES))
 def test_tile_local_parse_premise_across_tiles(gpu, oracle_lib, monkeypatch, case):
     """The decimal-id parse without K1 (tile-local positions; the premise checked per tile after one
-    scan, then the COO compacted) against the oracle and against the lean parse after K1
-    (TEST_NO_TILE_LOCAL); cases that break the premise only across tiles must fall back."""
+    scan, then the COO compacted — or, for a CSR output of an unweighted build, left in group slots
+    for the bucket partition) against the oracle, against the lean parse after K1
+    (TEST_NO_TILE_LOCAL) and against per-tile slots (TEST_NO_GROUP); cases that break the premise
+    only across tiles must fall back."""
     from gfa2network_amd import _native as nat
 
     data = "".join(TILE_LOCAL_CASES[case](_decimal_gfa(9, 20000, 80000))).encode()
@@ -390,15 +392,16 @@ def test_tile_local_parse_premise_across_tiles(gpu, oracle_lib, monkeypatch, cas
     for mode in MODES:
         st, ph = _phases(data, **mode)
         assert st == 0
-        local = "place" in ph and "tiles" not in ph
+        local = "parse" in ph and "tiles" not in ph
         eligible = not mode.get("bidirected") and not mode.get("strip_orientation")
         assert local == (eligible and case == "canonical"), (case, mode, sorted(ph))
         for dtype, wt in (("float64", None), ("int8", None), ("float64", "RC")):
             a = outcome(gpu_run(data, mode, dtype, wt))
             assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, wt)), (case, mode, dtype, wt)
-            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_TILE_LOCAL)
-            assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, dtype, wt)
-            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+            for flag in (nat.TEST_NO_TILE_LOCAL, nat.TEST_NO_GROUP):
+                monkeypatch.setattr(nat, "TEST_FLAGS", flag)
+                assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, dtype, wt, flag)
+                monkeypatch.setattr(nat, "TEST_FLAGS", 0)
 
 
 def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
@@ -437,16 +440,18 @@ def test_maxsym_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch):
     lines += [f"L\t{r.randint(1, 6000)}\t+\t{r.randint(1, 6000)}\t-\t0M\n" for _ in range(30000)]
     lines += ["L\t7\t+\t9\t+\t0M\n"] * 256 + ["L\t9\t+\t7\t+\t0M\n"] * 128 + ["L\t11\t+\t11\t+\t0M\n"] * 300
     hub = [f"L\t5000\t+\t{k}\t+\t0M\n" for k in range(1, 6001)]  # > one bucket's capacity
-    for extra in ([], hub):
+    for extra in ([], hub):  # the hub: the group-slot COO is refused, the build redone without it
         data = "".join(lines + extra).encode()
-        for dtype in ("bool", "int8", "int32", "float32", "float64"):
-            a = outcome(gpu_run(data, {}, dtype, None))
-            b = outcome(oracle_run(oracle_lib, data, {}, dtype, None))
-            assert a == b, (dtype, bool(extra))
-            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_BUCKETS)
-            c = outcome(gpu_run(data, {}, dtype, None))
-            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
-            assert a == c, (dtype, bool(extra))
+        for mode in ({}, {"directed": False}):
+            for dtype in ("bool", "int8", "int32", "float32", "float64"):
+                a = outcome(gpu_run(data, mode, dtype, None))
+                b = outcome(oracle_run(oracle_lib, data, mode, dtype, None))
+                assert a == b, (dtype, bool(extra), mode)
+                for flag in (nat.TEST_NO_BUCKETS, nat.TEST_NO_GROUP):
+                    monkeypatch.setattr(nat, "TEST_FLAGS", flag)
+                    c = outcome(gpu_run(data, mode, dtype, None))
+                    monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+                    assert a == c, (dtype, bool(extra), mode, flag)
 
 
 def test_maxsym_buckets_large(gpu, monkeypatch):

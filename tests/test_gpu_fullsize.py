@@ -34,7 +34,7 @@ def _digest(*arrays) -> str:
 
 
 def _hip():
-    hip = ctypes.CDLL("libamdhip64.so")
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libg2n.so loaded (its SONAME)
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     return hip
 
