@@ -1334,6 +1334,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 // and the full parse runs (tile_local_parse).
 constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
 constexpr uint32_t kLeanLines = 2048;                                   // line records per tile
+constexpr uint32_t kLeanBatch = 16;                                     // starts classified with loads batched
 static_assert(kTile <= 32768 && kChunkIters == 8, "records hold 15-bit offsets; one 16-byte read per region");
 
 __device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
@@ -1397,10 +1398,48 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
   }
   const uint32_t n_st = (uint32_t)(__popcll(slo) + __popcll(shi));
   uint32_t n_s = 0, n_e = 0, n_po = 0;
+  // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
+  // then the kinds (2-bit codes kept for the record pass); any further start one by one
+  uint32_t codes = 0;
   {
     unsigned long long lo = slo, hi = shi;
+    uint32_t off[kLeanBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      off[q] = 0xFFFFu;
+      if (lo | hi) {
+        uint32_t b;
+        if (lo) {
+          b = (uint32_t)__builtin_ctzll(lo);
+          lo &= lo - 1;
+        } else {
+          b = 64 + (uint32_t)__builtin_ctzll(hi);
+          hi &= hi - 1;
+        }
+        off[q] = 16 * c0 + b;
+      }
+    }
+    uint32_t x0[kLeanBatch], x1[kLeanBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      const uint32_t o = off[q] == 0xFFFFu ? 0u : off[q];
+      x0[q] = buf[o];
+      x1[q] = buf[o + 1];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      if (off[q] == 0xFFFFu) continue;
+      const bool exact = t0 + off[q] + 1 >= len || x0[q] == '\n' || x1[q] == '\t' || x1[q] == '\n';
+      const uint8_t kd = line_kind((uint8_t)x0[q], exact);
+      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
+      const uint32_t code = lean_code(kd);
+      codes |= code << (2 * q);
+      n_s += code == 1;
+      n_e += code == 2;
+      n_po += code == 3;
+    }
 #pragma unroll 1
-    for (uint32_t q = 0; q < n_st; q++) {
+    while (lo | hi) {  // more than kLeanBatch lines start in these 128 bytes
       uint32_t b;
       if (lo) {
         b = (uint32_t)__builtin_ctzll(lo);
@@ -1411,19 +1450,21 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
       }
       const uint32_t o = 16 * c0 + b;
       const uint8_t kd = kind_at(buf, o, t0 + o, len);
-      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
+      if (kd == kUnknown) is.fail = 1;
       const uint32_t code = lean_code(kd);
       n_s += code == 1;
       n_e += code == 2;
       n_po += code == 3;
     }
   }
+  K2_LEAN_STAMP(2);
   unsigned long long tot;
   const unsigned long long ex =
       block_excl_scan_u64((unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40),
                           &tot, red64);
   const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
                  e_tot = (uint32_t)(tot >> 40);
+  K2_LEAN_STAMP(3);
   const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
   if (kGrouped && threadIdx.x == 0 && n_lines == 0)
     s_gbase = 0;  // no window below
@@ -1448,7 +1489,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
           hi &= hi - 1;
         }
         const uint32_t o = 16 * c0 + b;
-        const uint32_t code = lean_code(kind_at(buf, o, t0 + o, len));
+        const uint32_t code = q < kLeanBatch ? (codes >> (2 * q)) & 3u : lean_code(kind_at(buf, o, t0 + o, len));
         if (w0 == 0 && code == 1 && ep) is.fail = 1;  // an S line after an edge line: not the decimal-id layout
         if (r >= w0) rec[r - w0] = o | (code << 15) | ((code == 1 ? sp : ep) << 17);
         sp += code == 1;
@@ -1457,7 +1498,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
     }
     __syncthreads();
     if (w0 == 0) {
-      K2_LEAN_STAMP(2);
+      K2_LEAN_STAMP(4);
       if (kGrouped) {
         const uint64_t b = (tile >> kGroupShift) * gcap + s_gbase;
         op.rows += b;
@@ -1499,7 +1540,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
         is.fail = 1;
     }
   }
-  K2_LEAN_STAMP(3);
+  K2_LEAN_STAMP(5);
   // tile counts and premise evidence
   if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
   uint32_t vm = is.vmax;
@@ -1536,7 +1577,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
     tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
   }
   if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
-  K2_LEAN_STAMP(4);
+  K2_LEAN_STAMP(6);
 #ifdef G2N_K2_STAMPS
   if (threadIdx.x == 0) {
     uint32_t hw, xcc;

@@ -16,14 +16,14 @@ NAMES = ["stage", "masks", "scan", "starts", "classify", "parse_t0", "parse_all"
 TICK_NS = 10.0  # wall_clock64 at 100 MHz
 
 
-LEAN_NAMES = ["stage_masks", "starts_scan_records", "parse", "finish"]
+LEAN_NAMES = ["stage_masks", "classify", "scan", "records", "parse", "finish"]
 
 
 def main():
     a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 10)
-    lean = bool((a[:, 5] == 0).all())  # k_tile_lean stamps 0..4 (and the hardware id in 9)
+    lean = bool((a[:, 7] == 0).all())  # k_tile_lean stamps 0..6 (and the hardware id in 9)
     names = LEAN_NAMES if lean else NAMES
-    last = 4 if lean else 8
+    last = 6 if lean else 8
     t = a[:, :last + 1].astype(np.int64)
     hw = a[:, 9]
     n = len(t)
