@@ -207,15 +207,15 @@ constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // chunks per thread
 // t + 256 j; all loads are issued before the first LDS write.  (A persistent variant that loads
 // tile i + G while parsing tile i measured slower on gfx950: the prefetch registers took K2 from
 // 80 to 212 VGPRs, 2 waves/SIMD, 6.3 -> 10.7 ms on C4.)
-template <uint32_t kHalo>
+template <uint32_t kHalo, uint32_t kT = kTPB>
 struct TileRegs {
   static constexpr uint32_t kChunks = (uint32_t)((kTile + kHalo) / 16);
-  static constexpr uint32_t kPer = (kChunks + kTPB - 1) / kTPB;
+  static constexpr uint32_t kPer = (kChunks + kT - 1) / kT;
   uint4 r[kPer];
   __device__ inline void load(const uint8_t* __restrict__ in, uint64_t len, uint64_t t0) {
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {  // every load in flight before any is used
-      const uint32_t c = j * kTPB + threadIdx.x;
+      const uint32_t c = j * kT + threadIdx.x;
       const uint64_t pos = t0 + (uint64_t)c * 16;
       r[j] = (c < kChunks && pos < len) ? load16(in, pos, len) : make_uint4(0, 0, 0, 0);
     }
@@ -223,7 +223,7 @@ struct TileRegs {
   __device__ inline void store(uint8_t* lds) const {
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {
-      const uint32_t c = j * kTPB + threadIdx.x;
+      const uint32_t c = j * kT + threadIdx.x;
       if (c < kChunks) *(uint4*)(lds + (uint64_t)c * 16) = r[j];
     }
   }
@@ -1316,53 +1316,80 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 
 // ============================ K2 lean: the tile-local decimal-id parse ========================
 // The tile-local lean parse (ParseOpts.tile_pad; S lines first named "1".."N", no bidirected, no
-// weight tag, no strip) as a kernel of its own.  One 256-thread block per 32 KiB tile (+ halo):
+// weight tag, no strip) as a kernel of its own.  One 512-thread block (8 waves) per 32 KiB tile
+// (+ halo):
 //  (1) the tile is staged in LDS, every 16-byte load in flight before the first store; from the
-//      same registers (chunks 256 j + t: no LDS re-read) the tab and newline bitmaps of every
+//      same registers (chunks 512 j + t: no LDS re-read) the tab and newline bitmaps of every
 //      chunk go to LDS, one u16 each;
-//  (2) thread t takes the line starts in ITS contiguous 128 bytes (chunks 8t..8t+7: one 16-byte
-//      LDS read of their newline bitmaps), classifies them (parser.py:117-134 first-byte
-//      dispatch) and counts starts, S and edge lines; ONE block scan of the packed counts ranks
-//      its lines in the tile, and it writes one 32-bit record per line (offset, kind, S / edge
-//      prefix) at that rank;
-//  (3) lane-parallel parse: line j goes to thread j mod 256 (balanced), its end is the next
+//  (2) thread t takes the line starts in ITS contiguous 64 bytes (chunks 4t..4t+3: one 8-byte
+//      LDS read of their newline bitmaps, one 64-bit start mask), classifies them (parser.py:
+//      117-134 first-byte dispatch) with every byte load in flight at once, and counts starts, S
+//      and edge lines; ONE block scan of the packed counts ranks its lines in the tile, and it
+//      writes one 32-bit record per line (offset, kind, S / edge prefix) at that rank;
+//  (3) lane-parallel parse: line j goes to thread j mod 512 (balanced), its end is the next
 //      record's offset, the fields come from the tab bitmap (lean_line), the result goes to the
 //      tile's COO slot.
+// 512 threads over the same 52 KB of LDS as 256 would use: 3 blocks and 6 waves per SIMD.
 // Same outputs as k_tile_parse<true> (tile counts, premise evidence, COO slot) with one block
 // scan instead of three.  Anything outside the lean shapes — an unsupported record (its warning
 // needs global line indices), a line running past the staged window — fails the tile-local parse
 // and the full parse runs (tile_local_parse).
+constexpr uint32_t kLeanTPB = 512;                                      // threads per tile
+constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
 constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
-constexpr uint32_t kLeanLines = 2048;                                   // line records per tile
-constexpr uint32_t kLeanBatch = 16;                                     // starts classified with loads batched
-static_assert(kTile <= 32768 && kChunkIters == 8, "records hold 15-bit offsets; one 16-byte read per region");
+constexpr uint32_t kLeanLines = 2048;                                   // line records per window
+constexpr uint32_t kLeanBatch = 8;                                      // starts classified with loads batched
+static_assert(kTile <= 32768 && kLeanRegion == 4, "records hold 15-bit offsets; a region is one 64-bit mask");
 
 __device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
   return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
 }
 
+template <uint32_t kN, class T>
+__device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) {  // exclusive; *tot = total
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  T wbase = 0, t = 0;
+#pragma unroll
+  for (int q = 0; q < (int)(kN / 64); q++) {
+    const T y = lds[q];
+    if (q < wid) wbase += y;
+    t += y;
+  }
+  __syncthreads();
+  *tot = t;
+  return wbase + x - v;
+}
+
 template <bool kGrouped>
-__global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
-                                                    Ctl* ctl, TileCnt* __restrict__ tcnt_out,
-                                                    TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
-                                                    uint64_t gcap) {
+__global__ void __launch_bounds__(kLeanTPB) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
+                                                        Ctl* ctl, TileCnt* __restrict__ tcnt_out,
+                                                        TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
+                                                        uint64_t gcap) {
+  constexpr uint32_t kW = kLeanTPB / 64;
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
   __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
   __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
   __shared__ uint32_t rec[kLeanLines + 1];
-  __shared__ unsigned long long red64[kTPB / 64];
+  __shared__ unsigned long long red64[kW];
   __shared__ uint32_t s_gbase;
   const uint64_t tile = blockIdx.x;
   const uint64_t t0 = tile * kTile;
   op.grouped = kGrouped ? 1u : 0u;  // lean_line: positions relative to the tile's base in its group slot
   K2_LEAN_STAMP(0);
   {
-    TileRegs<kTileHalo> R;
+    TileRegs<kTileHalo, kLeanTPB> R;
     R.load(in, len, t0);
     R.store(buf);
 #pragma unroll
     for (uint32_t j = 0; j < R.kPer; j++) {
-      const uint32_t c = j * kTPB + threadIdx.x;
+      const uint32_t c = j * kLeanTPB + threadIdx.x;
       if (c < kLeanChunks) {
         tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
         nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
@@ -1377,47 +1404,31 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
   __syncthreads();
   K2_LEAN_STAMP(1);
   IntState is;
-  // (2) this thread's region: chunks c0 .. c0 + 7, its starts as a 128-bit mask (lo, hi)
-  const uint32_t c0 = kChunkIters * threadIdx.x;
-  unsigned long long nlo, nhi, slo, shi;
+  // (2) this thread's region: chunks c0 .. c0 + 3, its starts as one 64-bit mask
+  const uint32_t c0 = kLeanRegion * threadIdx.x;
+  unsigned long long st;
   uint32_t n_nl;
   {
-    const uint4 v = *(const uint4*)(nlm + c0);
-    nlo = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
-    nhi = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
+    const uint2 v = *(const uint2*)(nlm + c0);
+    const unsigned long long nl = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
     const unsigned long long prev = c0 ? (unsigned long long)(nlm[c0 - 1] >> 15) : (tile_prev_nl ? 1ull : 0ull);
-    slo = (nlo << 1) | prev;
-    shi = (nhi << 1) | (nlo >> 63);
+    st = (nl << 1) | prev;
     const uint64_t r0 = t0 + 16ull * c0;  // a start needs a byte: none at or past len
-    if (r0 + 128 > len) {
-      const uint64_t n = r0 >= len ? 0 : len - r0;
-      slo &= n >= 64 ? ~0ull : ((1ull << n) - 1);
-      shi &= n >= 128 ? ~0ull : (n <= 64 ? 0ull : ((1ull << (n - 64)) - 1));
-    }
-    n_nl = (uint32_t)(__popcll(nlo) + __popcll(nhi));
+    if (r0 + 64 > len) st &= r0 >= len ? 0ull : ((1ull << (len - r0)) - 1);
+    n_nl = (uint32_t)__popcll(nl);
   }
-  const uint32_t n_st = (uint32_t)(__popcll(slo) + __popcll(shi));
+  const uint32_t n_st = (uint32_t)__popcll(st);
   uint32_t n_s = 0, n_e = 0, n_po = 0;
   // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
   // then the kinds (2-bit codes kept for the record pass); any further start one by one
   uint32_t codes = 0;
   {
-    unsigned long long lo = slo, hi = shi;
+    unsigned long long m = st;
     uint32_t off[kLeanBatch];
 #pragma unroll
     for (uint32_t q = 0; q < kLeanBatch; q++) {
-      off[q] = 0xFFFFu;
-      if (lo | hi) {
-        uint32_t b;
-        if (lo) {
-          b = (uint32_t)__builtin_ctzll(lo);
-          lo &= lo - 1;
-        } else {
-          b = 64 + (uint32_t)__builtin_ctzll(hi);
-          hi &= hi - 1;
-        }
-        off[q] = 16 * c0 + b;
-      }
+      off[q] = m ? 16 * c0 + (uint32_t)__builtin_ctzll(m) : 0xFFFFu;
+      m &= m - 1;
     }
     uint32_t x0[kLeanBatch], x1[kLeanBatch];
 #pragma unroll
@@ -1439,16 +1450,9 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
       n_po += code == 3;
     }
 #pragma unroll 1
-    while (lo | hi) {  // more than kLeanBatch lines start in these 128 bytes
-      uint32_t b;
-      if (lo) {
-        b = (uint32_t)__builtin_ctzll(lo);
-        lo &= lo - 1;
-      } else {
-        b = 64 + (uint32_t)__builtin_ctzll(hi);
-        hi &= hi - 1;
-      }
-      const uint32_t o = 16 * c0 + b;
+    while (m) {  // more than kLeanBatch lines start in these 64 bytes
+      const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
       const uint8_t kd = kind_at(buf, o, t0 + o, len);
       if (kd == kUnknown) is.fail = 1;
       const uint32_t code = lean_code(kd);
@@ -1459,17 +1463,14 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
   }
   K2_LEAN_STAMP(2);
   unsigned long long tot;
-  const unsigned long long ex =
-      block_excl_scan_u64((unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40),
-                          &tot, red64);
+  const unsigned long long ex = block_excl_scan_n64<kLeanTPB>(
+      (unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40), &tot, red64);
   const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
                  e_tot = (uint32_t)(tot >> 40);
   K2_LEAN_STAMP(3);
   const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
-  if (kGrouped && threadIdx.x == 0 && n_lines == 0)
-    s_gbase = 0;  // no window below
-  if (kGrouped && threadIdx.x == 0 && n_lines)  // this tile's place in its group slot (published by the barrier below)
-    s_gbase = e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
+  if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
+    s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
   // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
   // records of its lines ranked in [w0, w0 + kLeanLines] (one past: the window's last line ends where
   // the next one starts), then the window's lines are parsed
@@ -1477,18 +1478,11 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
     if (w0) __syncthreads();  // the previous window's records are read
     {
       uint32_t r = (uint32_t)(ex & 0xFFFFFu), sp = (uint32_t)((ex >> 20) & 0xFFFFFu), ep = (uint32_t)(ex >> 40);
-      unsigned long long lo = slo, hi = shi;
+      unsigned long long m = st;
 #pragma unroll 1
       for (uint32_t q = 0; q < n_st && r <= w0 + kLeanLines; q++, r++) {
-        uint32_t b;
-        if (lo) {
-          b = (uint32_t)__builtin_ctzll(lo);
-          lo &= lo - 1;
-        } else {
-          b = 64 + (uint32_t)__builtin_ctzll(hi);
-          hi &= hi - 1;
-        }
-        const uint32_t o = 16 * c0 + b;
+        const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
         const uint32_t code = q < kLeanBatch ? (codes >> (2 * q)) & 3u : lean_code(kind_at(buf, o, t0 + o, len));
         if (w0 == 0 && code == 1 && ep) is.fail = 1;  // an S line after an edge line: not the decimal-id layout
         if (r >= w0) rec[r - w0] = o | (code << 15) | ((code == 1 ? sp : ep) << 17);
@@ -1508,7 +1502,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
     // (3) lane-parallel lines
     const uint32_t n_win = n_lines - w0 < kLeanLines ? n_lines - w0 : kLeanLines;
 #pragma unroll 1
-    for (uint32_t j = threadIdx.x; j < n_win; j += kTPB) {
+    for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
       const uint32_t x = rec[j];
       const uint32_t code = (x >> 15) & 3u;
       if (code == 0) continue;
@@ -1518,10 +1512,10 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
         next = rec[j + 1] & 0x7FFFu;
       } else {  // the tile's last line: its newline from the bitmaps
         uint32_t c = o >> 4;
-        uint32_t m = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
+        uint32_t mm = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
         const uint32_t ce = (lim + 15) / 16;
-        while (!m && ++c < ce) m = nlm[c];
-        if (m) next = 16 * c + (uint32_t)__builtin_ctz(m) + 1;
+        while (!mm && ++c < ce) mm = nlm[c];
+        if (mm) next = 16 * c + (uint32_t)__builtin_ctz(mm) + 1;
         else if (lim == len - t0) next = lim + 1;
       }
       if (!next) {  // the line runs past the staged window
@@ -1545,29 +1539,34 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
   if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
   uint32_t vm = is.vmax;
   int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
+  unsigned long long cnt = (unsigned long long)n_nl | ((unsigned long long)n_po << 20);  // per tile < 2^20 each
   for (int o = 32; o > 0; o >>= 1) {
     vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
     dmn = min(dmn, (int32_t)__shfl_xor(dmn, o, 64));
     dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
+    cnt += __shfl_xor(cnt, o, 64);
   }
-  __shared__ uint32_t rv[kTPB / 64];
-  __shared__ int32_t rmn[kTPB / 64], rmx[kTPB / 64];
+  __shared__ uint32_t rv[kW];
+  __shared__ int32_t rmn[kW], rmx[kW];
+  __shared__ unsigned long long rc[kW];
   if ((threadIdx.x & 63) == 0) {
     rv[threadIdx.x >> 6] = vm;
     rmn[threadIdx.x >> 6] = dmn;
     rmx[threadIdx.x >> 6] = dmx;
+    rc[threadIdx.x >> 6] = cnt;
   }
-  // P / O lines and newlines: per-tile totals (< 2^20 each)
-  const unsigned long long cnts = block_sum((unsigned long long)n_nl | ((unsigned long long)n_po << 20), red64);
+  const unsigned long long failed = __ballot(is.fail);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < kTPB / 64; w++) {
+    for (int w = 1; w < (int)kW; w++) {
       vm = max(vm, rv[w]);
       dmn = min(dmn, rmn[w]);
       dmx = max(dmx, rmx[w]);
+      cnt += rc[w];
     }
-    const uint32_t npo = (uint32_t)(cnts >> 20);
+    const uint32_t npo = (uint32_t)(cnt >> 20);
     TileCnt c;
-    c.nl = cnts & 0xFFFFFu;
+    c.nl = cnt & 0xFFFFFu;
     c.lines = n_lines;
     c.segs = s_tot;
     c.edges = e_tot;
@@ -1576,7 +1575,7 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean(const uint8_t* __restrict__ 
     tcnt_out[tile] = c;
     tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
   }
-  if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+  if (failed && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
   K2_LEAN_STAMP(6);
 #ifdef G2N_K2_STAMPS
   if (threadIdx.x == 0) {

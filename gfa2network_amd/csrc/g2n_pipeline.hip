@@ -768,10 +768,10 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                      (uint64_t*)nullptr, (DeferredLine*)nullptr, n_tiles, tcnt, tlean);
 #else
   if (grouped)
-    hipLaunchKernelGGL(k_tile_lean<true>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
+    hipLaunchKernelGGL(k_tile_lean<true>, dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
                        tlean, gcount, gcap);
   else
-    hipLaunchKernelGGL(k_tile_lean<false>, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, lo, c->ctl,
+    hipLaunchKernelGGL(k_tile_lean<false>, dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl,
                        tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0);
 #endif
   phase(c, "parse");
