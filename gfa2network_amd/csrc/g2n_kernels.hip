@@ -1334,12 +1334,16 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 // scan instead of three.  Anything outside the lean shapes — an unsupported record (its warning
 // needs global line indices), a line running past the staged window — fails the tile-local parse
 // and the full parse runs (tile_local_parse).
-constexpr uint32_t kLeanTPB = 512;                                      // threads per tile
+#ifndef G2N_LEAN_TPB  // experiment builds: 1024 (32-byte regions)
+#define G2N_LEAN_TPB 512
+#endif
+constexpr uint32_t kLeanTPB = G2N_LEAN_TPB;                             // threads per tile
 constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
 constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
 constexpr uint32_t kLeanLines = 2048;                                   // line records per window
 constexpr uint32_t kLeanBatch = 8;                                      // starts classified with loads batched
-static_assert(kTile <= 32768 && kLeanRegion == 4, "records hold 15-bit offsets; a region is one 64-bit mask");
+static_assert(kTile <= 32768 && (kLeanRegion == 4 || kLeanRegion == 2),
+              "records hold 15-bit offsets; a region's starts fit one 64-bit mask");
 
 __device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
   return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
@@ -1368,7 +1372,7 @@ __device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) { 
 }
 
 template <bool kGrouped>
-__global__ void __launch_bounds__(kLeanTPB) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
+__global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
                                                         Ctl* ctl, TileCnt* __restrict__ tcnt_out,
                                                         TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
                                                         uint64_t gcap) {
@@ -1409,12 +1413,18 @@ __global__ void __launch_bounds__(kLeanTPB) k_tile_lean(const uint8_t* __restric
   unsigned long long st;
   uint32_t n_nl;
   {
-    const uint2 v = *(const uint2*)(nlm + c0);
-    const unsigned long long nl = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    unsigned long long nl;
+    if constexpr (kLeanRegion == 4) {
+      const uint2 v = *(const uint2*)(nlm + c0);
+      nl = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    } else {
+      nl = *(const uint32_t*)(nlm + c0);
+    }
     const unsigned long long prev = c0 ? (unsigned long long)(nlm[c0 - 1] >> 15) : (tile_prev_nl ? 1ull : 0ull);
     st = (nl << 1) | prev;
+    if constexpr (kLeanRegion == 2) st &= 0xFFFFFFFFull;
     const uint64_t r0 = t0 + 16ull * c0;  // a start needs a byte: none at or past len
-    if (r0 + 64 > len) st &= r0 >= len ? 0ull : ((1ull << (len - r0)) - 1);
+    if (r0 + 16 * kLeanRegion > len) st &= r0 >= len ? 0ull : ((1ull << (len - r0)) - 1);
     n_nl = (uint32_t)__popcll(nl);
   }
   const uint32_t n_st = (uint32_t)__popcll(st);
