@@ -355,7 +355,46 @@ __device__ inline void sym_sort_row(uint32_t* seg, uint32_t n) {
 // costs more than the extra 4.6 GB of staging traffic.)  A bucket over kSymCap elements sets
 // ctl->bucket_overflow (the host then takes the general path).
 constexpr uint32_t kShortRow = 16;
+constexpr uint32_t kMidRow = 64;  // rows of kShortRow + 1 .. kMidRow entries: sorted and merged by a whole wave
 constexpr uint32_t kStagedSkip = 0xFFFFFFFFu;
+
+// ascending bitonic sort of one u32 per lane across the wave
+__device__ inline uint32_t wave_sort64(uint32_t x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t y = (uint32_t)__shfl_xor((int)x, (int)j, 64);
+      const bool up = (lane & k) == 0;
+      const bool lower = (lane & j) == 0;
+      x = (lower == up) ? min(x, y) : max(x, y);
+    }
+  return x;
+}
+
+// One row of nr <= 64 sorted values (column << 1 | side), lane l holding entry l: for each column
+// run, the side-0 copies kx and side-1 copies ky; keep(kx, ky, kk) decides the entry.  Returns the
+// entries kept; emit(j, column, kk) for the j-th (lanes in order).
+template <class Keep, class Emit>
+__device__ inline uint32_t wave_merge(uint32_t x, uint32_t nr, Keep keep, Emit emit) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t col = x >> 1, sd = x & 1u;
+  const bool valid = lane < nr;
+  const uint32_t pcol = (uint32_t)__shfl_up((int)col, 1, 64), ncol = (uint32_t)__shfl_down((int)col, 1, 64);
+  const bool start = valid && (lane == 0 || pcol != col);
+  const bool last = valid && (lane + 1 == nr || ncol != col);
+  const unsigned long long smask = __ballot(start), s1 = __ballot(valid && sd);
+  const unsigned long long upto = (2ull << lane) - 1ull;  // lanes 0..lane (all 64 for lane 63)
+  const uint32_t sl = 63u - (uint32_t)__clzll((smask & upto) | 1ull);  // this lane's run start
+  const unsigned long long run = upto & ~((1ull << sl) - 1ull);
+  const uint32_t ky = (uint32_t)__popcll(s1 & run), kx = lane - sl + 1 - ky;
+  uint32_t kk = 0;
+  const bool kept = last && keep(kx, ky, kk);
+  const unsigned long long km = __ballot(kept);
+  if (kept) emit((uint32_t)__popcll(km & ((1ull << lane) - 1ull)), col, kk);
+  return (uint32_t)__popcll(km);
+}
 
 template <class T, bool kSum>
 __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
@@ -365,7 +404,11 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
   __shared__ uint32_t cnt[kTPB];
   __shared__ uint32_t red[kTPB / 64];
+  __shared__ uint16_t mlist[kTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
+  __shared__ uint32_t mval[kTPB];   // per such row: its entries kept, then its output offset
+  __shared__ uint32_t mcount;
   cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) mcount = 0;
   const uint64_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
   const bool over = n > kSymCap;  // block-uniform
@@ -410,7 +453,16 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   const uint64_t row = (b << low) + threadIdx.x;
   const bool live = threadIdx.x <= rmask && row < n_rows;
   const bool shortrow = my <= kShortRow;
+  const bool midrow = live && !shortrow && my <= kMidRow;
+  const bool longrow = live && my > kMidRow;
   uint32_t* sg = seg + rs;
+  // the rows of kShortRow + 1 .. kMidRow entries (about one per bucket): a whole wave sorts each
+  // (bitonic across lanes, in place in LDS) and counts its kept entries; a longer row is sorted by
+  // its own lane (Shell sort) — one row's lane-serial sort would hold its wave for microseconds
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (midrow) mlist[atomicAdd(&mcount, 1u)] = (uint16_t)threadIdx.x;
+  __syncthreads();
+  const uint32_t n_mid = mcount;  // block-uniform
   // short rows: registers; sorted ascending, padding sorts last
   uint32_t k[kShortRow];
 #pragma unroll
@@ -422,7 +474,7 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     else if (wm > 4) net_sort<8>(k);
     else if (wm > 1) net_sort<4>(k);
   }
-  if (live && !shortrow) sym_sort_row(sg, my);
+  if (longrow) sym_sort_row(sg, my);
   // merged entries: per column the side-0 copies (x) and side-1 copies (y); the value is
   // max(sum of x ones, sum of y ones) in dtype arithmetic, zeros dropped (csr_maximum_csr)
   auto keep = [&](uint32_t kx, uint32_t ky, uint32_t& kk) -> bool {
@@ -477,7 +529,18 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     return m;
   };
   auto none = [](uint32_t, uint32_t, uint32_t) {};
-  const uint32_t m = !live ? 0u : (shortrow ? short_merge(none, false) : long_merge(none));
+  if (n_mid) {
+    for (uint32_t i = wv; i < n_mid; i += kTPB / 64) {
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kTPB ? cnt[r + 1] : n) - s0;
+      uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
+      x = wave_sort64(x);
+      if (lane < nr) seg[s0 + lane] = x;
+      const uint32_t mm = wave_merge(x, nr, keep, none);
+      if (lane == 0) mval[r] = mm;
+    }
+    __syncthreads();
+  }
+  const uint32_t m = !live ? 0u : (shortrow ? short_merge(none, false) : midrow ? mval[threadIdx.x] : long_merge(none));
   uint32_t off;
   const uint32_t tot = block_excl_scan_u32(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
@@ -485,10 +548,19 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   if (live) {
     indptr[row] = (int32_t)off;  // local; k_sym_place adds the bucket's offset
     if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
-    if (!shortrow)  // straight out, before the staging below reuses the segments
+    if (longrow)  // straight out, before the staging below reuses the segments
       long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { out[off + j] = make_uint2(c, kk); });
+    if (midrow) mval[threadIdx.x] = off;
   }
   __syncthreads();
+  if (n_mid) {  // the wave-sorted rows, straight out (consecutive lanes write consecutive entries)
+    for (uint32_t i = wv; i < n_mid; i += kTPB / 64) {
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kTPB ? cnt[r + 1] : n) - s0, o = mval[r];
+      const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
+      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { out[o + j] = make_uint2(c, kk); });
+    }
+    __syncthreads();
+  }
   if (live) {
     if (shortrow) {
       short_merge([&](uint32_t j, uint32_t c, uint32_t kk) {

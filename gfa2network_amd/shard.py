@@ -768,13 +768,18 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
             out.names_blob, out.names_offsets = nat.gather_names(b_all, o_all, order)
         tm["names"] = (time.perf_counter() - t5) * 1e3
 
-    # 5. triplets to row owners (and the A.T stream for MAX-SYM); 6. this rank's CSR row slice
+    # 5. the range's triplets over global ids (one gather per coordinate; the routes below need no
+    #    map), to row owners (and the A.T stream for MAX-SYM); 6. this rank's CSR row slice
+    t6 = time.perf_counter()
     local.dtype_name = dtype
+    g = gmap.to(torch.int64)
+    local.rows = g[local.rows.to(torch.int64)].to(torch.int32)
+    local.cols = g[local.cols.to(torch.int64)].to(torch.int32)
+    del g
+    tm["remap"] = (time.perf_counter() - t6) * 1e3
     if keep_coo:
-        g = gmap.to(torch.int64)
-        out.coo = (g[local.rows.to(torch.int64)].to(torch.int32), g[local.cols.to(torch.int64)].to(torch.int32),
-                   local.data)
-    a, tstream = _route(engine, C, local, dtype, gmap.view(torch.int32), n_global, maxsym, not weight_tag, tm)
+        out.coo = (local.rows, local.cols, local.data)
+    a, tstream = _route(engine, C, local, dtype, None, n_global, maxsym, not weight_tag, tm)
     return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()))
 
 
