@@ -33,10 +33,16 @@
 
 namespace g2n {
 
-constexpr uint32_t kPartTPB = 1024;               // threads of a partition block
+#ifndef G2N_PART_TPB  // experiment builds vary the partition block shape
+#define G2N_PART_TPB 1024
+#endif
+#ifndef G2N_PART_PREFETCH
+#define G2N_PART_PREFETCH 1
+#endif
+constexpr uint32_t kPartTPB = G2N_PART_TPB;       // threads of a partition block
 constexpr uint32_t kSubPer = 8;                    // elements per thread in one sub-tile
 constexpr uint32_t kSub = kSubPer * kPartTPB;      // 8192 elements per sub-tile
-constexpr uint32_t kChunkSubs = 8;                 // sub-tiles per block
+constexpr uint32_t kChunkSubs = 8 * 1024 / kPartTPB;  // sub-tiles per block (65536 elements)
 constexpr uint32_t kPartTile = kSub * kChunkSubs;  // 65536 elements per partition block
 constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits
 constexpr uint32_t kSymCap = 4096;                 // elements one finish block holds
@@ -130,8 +136,8 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
 }
 
 // Sub-tile at element e (e multiple of kSub within the block's range): thread t's elements.
-// Pass 1: entries e/2 + t + 1024 k (k < 4), coalesced u32 loads of rows and cols; pass 2:
-// elements e + t + 1024 k (k < 8), coalesced 8-byte loads.
+// Pass 1: entries e/2 + t + kPartTPB k (k < 4), coalesced u32 loads of rows and cols; pass 2:
+// elements e + t + kPartTPB k (k < 8), coalesced 8-byte loads.
 template <int kPass>
 __device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint2 (&x)[kSubPer], uint32_t& valid) {
   valid = 0;
@@ -228,17 +234,30 @@ __global__ void __launch_bounds__(kPartTPB) k_part_scatter(PartSrc S, uint32_t s
   part_load<kPass>(S, B.e0, B.e1, x, valid);
   for (uint64_t e = B.e0; e < B.e1; e += kSub) {
     for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
-    if (e + kSub < B.e1) part_load<kPass>(S, e + kSub, B.e1, nx, nvalid);  // next sub-tile in flight
+    if (G2N_PART_PREFETCH && e + kSub < B.e1) part_load<kPass>(S, e + kSub, B.e1, nx, nvalid);  // next sub-tile in flight
     __syncthreads();
     uint32_t rk[kSubPer];
 #pragma unroll
     for (uint32_t k = 0; k < kSubPer; k++)
       rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(x[k].x >> shift) & dmask], 1u) : 0u;
     __syncthreads();
-    const uint32_t hv = threadIdx.x < n_dig ? hist[threadIdx.x] : 0u;  // n_dig <= 1024: one digit per thread
+    // digit starts: kDigPer consecutive digits per thread (n_dig <= 1024)
+    constexpr uint32_t kDigPer = (1u << kMaxDigitBits) / kPartTPB;
+    uint32_t hv[kDigPer], hsum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kDigPer; q++) {
+      const uint32_t d = threadIdx.x * kDigPer + q;
+      hv[q] = d < n_dig ? hist[d] : 0u;
+      hsum += hv[q];
+    }
     uint32_t ex;
-    const uint32_t tot = block_excl_scan_n<kPartTPB>(hv, &ex, red);
-    if (threadIdx.x < n_dig) hist[threadIdx.x] = ex;
+    const uint32_t tot = block_excl_scan_n<kPartTPB>(hsum, &ex, red);
+#pragma unroll
+    for (uint32_t q = 0; q < kDigPer; q++) {
+      const uint32_t d = threadIdx.x * kDigPer + q;
+      if (d < n_dig) hist[d] = ex;
+      ex += hv[q];
+    }
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kSubPer; k++)
@@ -250,10 +269,18 @@ __global__ void __launch_bounds__(kPartTPB) k_part_scatter(PartSrc S, uint32_t s
       out[cur[d] + (i - hist[d])] = y;
     }
     __syncthreads();
-    if (threadIdx.x < n_dig) cur[threadIdx.x] += hv;
 #pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++) x[k] = nx[k];
-    valid = nvalid;
+    for (uint32_t q = 0; q < kDigPer; q++) {
+      const uint32_t d = threadIdx.x * kDigPer + q;
+      if (d < n_dig) cur[d] += hv[q];
+    }
+    if (G2N_PART_PREFETCH) {
+#pragma unroll
+      for (uint32_t k = 0; k < kSubPer; k++) x[k] = nx[k];
+      valid = nvalid;
+    } else if (e + kSub < B.e1) {
+      part_load<kPass>(S, e + kSub, B.e1, x, valid);
+    }
   }
 }
 
