@@ -50,6 +50,7 @@ TEST_DICT_GENERAL = 16   # no decimal ids, no S-first fast path: the general ins
 TEST_NO_TILE_LOCAL = 32  # decimal ids: the lean parse after K1's tile bases, not the tile-local pass
 TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of the GPU inflate
 TEST_NO_GROUP = 128      # tile-local parse into per-tile slots + compaction (never group slots)
+TEST_NO_HASH_LEAN = 256  # names that are not decimal ids: the classic hash tiers, never the lean S-first one
 TEST_FLAGS = 0
 
 

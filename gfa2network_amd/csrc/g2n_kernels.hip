@@ -1314,289 +1314,6 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 #endif
 }
 
-// ============================ K2 lean: the tile-local decimal-id parse ========================
-// The tile-local lean parse (ParseOpts.tile_pad; S lines first named "1".."N", no bidirected, no
-// weight tag, no strip) as a kernel of its own.  One 512-thread block (8 waves) per 32 KiB tile
-// (+ halo):
-//  (1) the tile is staged in LDS, every 16-byte load in flight before the first store; from the
-//      same registers (chunks 512 j + t: no LDS re-read) the tab and newline bitmaps of every
-//      chunk go to LDS, one u16 each;
-//  (2) thread t takes the line starts in ITS contiguous 64 bytes (chunks 4t..4t+3: one 8-byte
-//      LDS read of their newline bitmaps, one 64-bit start mask), classifies them (parser.py:
-//      117-134 first-byte dispatch) with every byte load in flight at once, and counts starts, S
-//      and edge lines; ONE block scan of the packed counts ranks its lines in the tile, and it
-//      writes one 32-bit record per line (offset, kind, S / edge prefix) at that rank;
-//  (3) lane-parallel parse: line j goes to thread j mod 512 (balanced), its end is the next
-//      record's offset, the fields come from the tab bitmap (lean_line), the result goes to the
-//      tile's COO slot.
-// 512 threads over the same 52 KB of LDS as 256 would use: 3 blocks and 6 waves per SIMD.
-// Same outputs as k_tile_parse<true> (tile counts, premise evidence, COO slot) with one block
-// scan instead of three.  Anything outside the lean shapes — an unsupported record (its warning
-// needs global line indices), a line running past the staged window — fails the tile-local parse
-// and the full parse runs (tile_local_parse).
-#ifndef G2N_LEAN_TPB  // experiment builds: 1024 (32-byte regions)
-#define G2N_LEAN_TPB 512
-#endif
-constexpr uint32_t kLeanTPB = G2N_LEAN_TPB;                             // threads per tile
-constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
-constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
-constexpr uint32_t kLeanLines = 2048;                                   // line records per window
-constexpr uint32_t kLeanBatch = 8;                                      // starts classified with loads batched
-static_assert(kTile <= 32768 && (kLeanRegion == 4 || kLeanRegion == 2),
-              "records hold 15-bit offsets; a region's starts fit one 64-bit mask");
-
-__device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
-  return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
-}
-
-template <uint32_t kN, class T>
-__device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) {  // exclusive; *tot = total
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  T x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const T y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) lds[wid] = x;
-  __syncthreads();
-  T wbase = 0, t = 0;
-#pragma unroll
-  for (int q = 0; q < (int)(kN / 64); q++) {
-    const T y = lds[q];
-    if (q < wid) wbase += y;
-    t += y;
-  }
-  __syncthreads();
-  *tot = t;
-  return wbase + x - v;
-}
-
-template <bool kGrouped>
-__global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
-                                                        Ctl* ctl, TileCnt* __restrict__ tcnt_out,
-                                                        TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
-                                                        uint64_t gcap) {
-  constexpr uint32_t kW = kLeanTPB / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
-  __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
-  __shared__ uint32_t rec[kLeanLines + 1];
-  __shared__ unsigned long long red64[kW];
-  __shared__ uint32_t s_gbase;
-  const uint64_t tile = blockIdx.x;
-  const uint64_t t0 = tile * kTile;
-  op.grouped = kGrouped ? 1u : 0u;  // lean_line: positions relative to the tile's base in its group slot
-  K2_LEAN_STAMP(0);
-  {
-    TileRegs<kTileHalo, kLeanTPB> R;
-    R.load(in, len, t0);
-    R.store(buf);
-#pragma unroll
-    for (uint32_t j = 0; j < R.kPer; j++) {
-      const uint32_t c = j * kLeanTPB + threadIdx.x;
-      if (c < kLeanChunks) {
-        tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
-        nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
-      }
-    }
-  }
-  if (threadIdx.x < 8) {  // tab_window reads up to 4 bitmaps past a chunk
-    tabm[kLeanChunks + threadIdx.x] = 0;
-    nlm[kLeanChunks + threadIdx.x] = 0;
-  }
-  const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
-  __syncthreads();
-  K2_LEAN_STAMP(1);
-  IntState is;
-  // (2) this thread's region: chunks c0 .. c0 + 3, its starts as one 64-bit mask
-  const uint32_t c0 = kLeanRegion * threadIdx.x;
-  unsigned long long st;
-  uint32_t n_nl;
-  {
-    unsigned long long nl;
-    if constexpr (kLeanRegion == 4) {
-      const uint2 v = *(const uint2*)(nlm + c0);
-      nl = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
-    } else {
-      nl = *(const uint32_t*)(nlm + c0);
-    }
-    const unsigned long long prev = c0 ? (unsigned long long)(nlm[c0 - 1] >> 15) : (tile_prev_nl ? 1ull : 0ull);
-    st = (nl << 1) | prev;
-    if constexpr (kLeanRegion == 2) st &= 0xFFFFFFFFull;
-    const uint64_t r0 = t0 + 16ull * c0;  // a start needs a byte: none at or past len
-    if (r0 + 16 * kLeanRegion > len) st &= r0 >= len ? 0ull : ((1ull << (len - r0)) - 1);
-    n_nl = (uint32_t)__popcll(nl);
-  }
-  const uint32_t n_st = (uint32_t)__popcll(st);
-  uint32_t n_s = 0, n_e = 0, n_po = 0;
-  // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
-  // then the kinds (2-bit codes kept for the record pass); any further start one by one
-  uint32_t codes = 0;
-  {
-    unsigned long long m = st;
-    uint32_t off[kLeanBatch];
-#pragma unroll
-    for (uint32_t q = 0; q < kLeanBatch; q++) {
-      off[q] = m ? 16 * c0 + (uint32_t)__builtin_ctzll(m) : 0xFFFFu;
-      m &= m - 1;
-    }
-    uint32_t x0[kLeanBatch], x1[kLeanBatch];
-#pragma unroll
-    for (uint32_t q = 0; q < kLeanBatch; q++) {
-      const uint32_t o = off[q] == 0xFFFFu ? 0u : off[q];
-      x0[q] = buf[o];
-      x1[q] = buf[o + 1];
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kLeanBatch; q++) {
-      if (off[q] == 0xFFFFu) continue;
-      const bool exact = t0 + off[q] + 1 >= len || x0[q] == '\n' || x1[q] == '\t' || x1[q] == '\n';
-      const uint8_t kd = line_kind((uint8_t)x0[q], exact);
-      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
-      const uint32_t code = lean_code(kd);
-      codes |= code << (2 * q);
-      n_s += code == 1;
-      n_e += code == 2;
-      n_po += code == 3;
-    }
-#pragma unroll 1
-    while (m) {  // more than kLeanBatch lines start in these 64 bytes
-      const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
-      m &= m - 1;
-      const uint8_t kd = kind_at(buf, o, t0 + o, len);
-      if (kd == kUnknown) is.fail = 1;
-      const uint32_t code = lean_code(kd);
-      n_s += code == 1;
-      n_e += code == 2;
-      n_po += code == 3;
-    }
-  }
-  K2_LEAN_STAMP(2);
-  unsigned long long tot;
-  const unsigned long long ex = block_excl_scan_n64<kLeanTPB>(
-      (unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40), &tot, red64);
-  const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
-                 e_tot = (uint32_t)(tot >> 40);
-  K2_LEAN_STAMP(3);
-  const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
-  if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
-    s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
-  // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
-  // records of its lines ranked in [w0, w0 + kLeanLines] (one past: the window's last line ends where
-  // the next one starts), then the window's lines are parsed
-  for (uint32_t w0 = 0; w0 < n_lines; w0 += kLeanLines) {
-    if (w0) __syncthreads();  // the previous window's records are read
-    {
-      uint32_t r = (uint32_t)(ex & 0xFFFFFu), sp = (uint32_t)((ex >> 20) & 0xFFFFFu), ep = (uint32_t)(ex >> 40);
-      unsigned long long m = st;
-#pragma unroll 1
-      for (uint32_t q = 0; q < n_st && r <= w0 + kLeanLines; q++, r++) {
-        const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t code = q < kLeanBatch ? (codes >> (2 * q)) & 3u : lean_code(kind_at(buf, o, t0 + o, len));
-        if (w0 == 0 && code == 1 && ep) is.fail = 1;  // an S line after an edge line: not the decimal-id layout
-        if (r >= w0) rec[r - w0] = o | (code << 15) | ((code == 1 ? sp : ep) << 17);
-        sp += code == 1;
-        ep += code == 2;
-      }
-    }
-    __syncthreads();
-    if (w0 == 0) {
-      K2_LEAN_STAMP(4);
-      if (kGrouped) {
-        const uint64_t b = (tile >> kGroupShift) * gcap + s_gbase;
-        op.rows += b;
-        op.cols += b;
-      }
-    }
-    // (3) lane-parallel lines
-    const uint32_t n_win = n_lines - w0 < kLeanLines ? n_lines - w0 : kLeanLines;
-#pragma unroll 1
-    for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
-      const uint32_t x = rec[j];
-      const uint32_t code = (x >> 15) & 3u;
-      if (code == 0) continue;
-      const uint32_t o = x & 0x7FFFu, pref = x >> 17;
-      uint32_t next = 0;  // 1 + the line's '\n' (a virtual one at EOF), tile-local
-      if (w0 + j + 1 < n_lines) {
-        next = rec[j + 1] & 0x7FFFu;
-      } else {  // the tile's last line: its newline from the bitmaps
-        uint32_t c = o >> 4;
-        uint32_t mm = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
-        const uint32_t ce = (lim + 15) / 16;
-        while (!mm && ++c < ce) mm = nlm[c];
-        if (mm) next = 16 * c + (uint32_t)__builtin_ctz(mm) + 1;
-        else if (lim == len - t0) next = lim + 1;
-      }
-      if (!next) {  // the line runs past the staged window
-        is.fail = 1;
-        continue;
-      }
-      if (code == 3) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
-        const uint32_t n = next - 1 - o, sh = o & 15;
-        const uint64_t w = tab_window(buf, tabm, o >> 4);
-        if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
-        continue;
-      }
-      // S line: tb = its S index (no edge precedes it); edge line: eb = its edge index
-      if (!lean_line(buf, tabm, o, next, code == 1 ? kS : kEdge, t0, code == 1 ? pref : 0ull,
-                     code == 1 ? 0ull : pref, op, TouchOut{}, is))
-        is.fail = 1;
-    }
-  }
-  K2_LEAN_STAMP(5);
-  // tile counts and premise evidence
-  if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
-  uint32_t vm = is.vmax;
-  int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
-  unsigned long long cnt = (unsigned long long)n_nl | ((unsigned long long)n_po << 20);  // per tile < 2^20 each
-  for (int o = 32; o > 0; o >>= 1) {
-    vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
-    dmn = min(dmn, (int32_t)__shfl_xor(dmn, o, 64));
-    dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
-    cnt += __shfl_xor(cnt, o, 64);
-  }
-  __shared__ uint32_t rv[kW];
-  __shared__ int32_t rmn[kW], rmx[kW];
-  __shared__ unsigned long long rc[kW];
-  if ((threadIdx.x & 63) == 0) {
-    rv[threadIdx.x >> 6] = vm;
-    rmn[threadIdx.x >> 6] = dmn;
-    rmx[threadIdx.x >> 6] = dmx;
-    rc[threadIdx.x >> 6] = cnt;
-  }
-  const unsigned long long failed = __ballot(is.fail);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)kW; w++) {
-      vm = max(vm, rv[w]);
-      dmn = min(dmn, rmn[w]);
-      dmx = max(dmx, rmx[w]);
-      cnt += rc[w];
-    }
-    const uint32_t npo = (uint32_t)(cnt >> 20);
-    TileCnt c;
-    c.nl = cnt & 0xFFFFFu;
-    c.lines = n_lines;
-    c.segs = s_tot;
-    c.edges = e_tot;
-    c.touches = (uint64_t)s_tot + 2ull * e_tot;
-    c.recs = (uint64_t)s_tot + e_tot + npo;
-    tcnt_out[tile] = c;
-    tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
-  }
-  if (failed && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
-  K2_LEAN_STAMP(6);
-#ifdef G2N_K2_STAMPS
-  if (threadIdx.x == 0) {
-    uint32_t hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
-  }
-#endif
-}
-
 // Tile-local lean parse, afterwards: tile t's S lines must name (S lines before t) + their index
 // + 1 and no edge may precede them; every edge key at most the file's S count.
 __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restrict__ cnt,
@@ -1816,6 +1533,531 @@ __device__ inline bool tail_eq(const uint8_t* __restrict__ in, const TouchIn& T,
   for (uint64_t j = 16; j < len; j++)
     if (touch_byte(in, na, la, oa, j) != touch_byte(in, nb, lb, ob, j)) return false;
   return true;
+}
+
+// ============================ K2 lean: the tile-local decimal-id parse ========================
+// The tile-local lean parse (ParseOpts.tile_pad; S lines first named "1".."N", no bidirected, no
+// weight tag, no strip) as a kernel of its own.  One 512-thread block (8 waves) per 32 KiB tile
+// (+ halo):
+//  (1) the tile is staged in LDS, every 16-byte load in flight before the first store; from the
+//      same registers (chunks 512 j + t: no LDS re-read) the tab and newline bitmaps of every
+//      chunk go to LDS, one u16 each;
+//  (2) thread t takes the line starts in ITS contiguous 64 bytes (chunks 4t..4t+3: one 8-byte
+//      LDS read of their newline bitmaps, one 64-bit start mask), classifies them (parser.py:
+//      117-134 first-byte dispatch) with every byte load in flight at once, and counts starts, S
+//      and edge lines; ONE block scan of the packed counts ranks its lines in the tile, and it
+//      writes one 32-bit record per line (offset, kind, S / edge prefix) at that rank;
+//  (3) lane-parallel parse: line j goes to thread j mod 512 (balanced), its end is the next
+//      record's offset, the fields come from the tab bitmap (lean_line), the result goes to the
+//      tile's COO slot.
+// 512 threads over the same 52 KB of LDS as 256 would use: 3 blocks and 6 waves per SIMD.
+// Same outputs as k_tile_parse<true> (tile counts, premise evidence, COO slot) with one block
+// scan instead of three.  Anything outside the lean shapes — an unsupported record (its warning
+// needs global line indices), a line running past the staged window — fails the tile-local parse
+// and the full parse runs (tile_local_parse).
+#ifndef G2N_LEAN_TPB  // experiment builds: 1024 (32-byte regions)
+#define G2N_LEAN_TPB 512
+#endif
+constexpr uint32_t kLeanTPB = G2N_LEAN_TPB;                             // threads per tile
+constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
+constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
+constexpr uint32_t kLeanLines = 2048;                                   // line records per window
+constexpr uint32_t kLeanBatch = 8;                                      // starts classified with loads batched
+static_assert(kTile <= 32768 && (kLeanRegion == 4 || kLeanRegion == 2),
+              "records hold 15-bit offsets; a region's starts fit one 64-bit mask");
+
+__device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
+  return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
+}
+
+template <uint32_t kN, class T>
+__device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) {  // exclusive; *tot = total
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  T wbase = 0, t = 0;
+#pragma unroll
+  for (int q = 0; q < (int)(kN / 64); q++) {
+    const T y = lds[q];
+    if (q < wid) wbase += y;
+    t += y;
+  }
+  __syncthreads();
+  *tot = t;
+  return wbase + x - v;
+}
+
+// ---- the S-first hash dictionary on the lean front end (modes kLeanClaim / kLeanEdges) --------
+// For inputs whose S lines come first with unique names that are not the decimal ids (any names):
+// after K1's tile bases, kLeanClaim claims every S name in a table of 32-byte entries (hdr = hash
+// tag << 32 | node id = the S line's index, meta = key length << 40 | the name's input offset,
+// the first 16 key bytes inline) and records each node's name (noff / nlen); kLeanEdges parses
+// every edge line's two names from the staged tile, finds them (one random 32-byte read each) and
+// writes the stream-order COO.  builders.py:190-198: with every S line before every other line and
+// no repeated S name, a key's first touch is its S line, so node id = S index.  Anything else — a
+// repeated name (or a 32-bit tag shared by two S names), an edge key that is no S name, an S line
+// after an edge line, a line outside the lean shapes — fails the pass and the classic hash tiers
+// (full parse + dictionary rounds) run instead.
+enum : int { kLeanDecimal = 0, kLeanClaim = 1, kLeanEdges = 2 };
+#ifndef G2N_HL_LINES  // edge lines per thread per step in kLeanEdges (2, four probes in flight: 105 VGPRs, slower)
+#define G2N_HL_LINES 1
+#endif
+
+struct HashLeanArgs {
+  const TileCnt* tbase;  // K1's tile bases (exclusive scan of tcnt)
+  const TileCnt* tcnt;   // K1's tile counts
+  DictEntry* table;
+  uint64_t mask;         // table slots - 1
+  uint64_t max_probes;
+  uint64_t* noff;        // kLeanClaim: node id -> input offset of its name
+  uint32_t* nlen;        //             node id -> name length
+  int32_t* rows;         // kLeanEdges: stream-order COO, ktrip entries per edge line
+  int32_t* cols;
+  uint32_t ktrip;
+};
+
+// The first min(l, 16) bytes at tile offset x of the staged tile, little-endian, zero padded
+// (aligned 8-byte LDS reads; never past x + l rounded up to 8)
+__device__ inline u128 lds_span16(const uint8_t* buf, uint32_t x, uint32_t l) {
+  if (l == 0) return 0;
+  const uint32_t m = l < 16 ? l : 16, a = x & ~7u, end = x + m, sh = (x & 7u) * 8;
+  const uint64_t w0 = *(const uint64_t*)(buf + a);
+  const uint64_t w1 = a + 8 < end ? *(const uint64_t*)(buf + a + 8) : 0ull;
+  const uint64_t w2 = a + 16 < end ? *(const uint64_t*)(buf + a + 16) : 0ull;
+  const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  u128 k = ((u128)hi << 64) | lo;
+  if (m < 16) k &= (((u128)1) << (8 * m)) - 1;
+  return k;
+}
+
+__device__ inline bool tail_eq_in(const uint8_t* __restrict__ in, uint64_t a, uint64_t b, uint32_t len) {
+  for (uint32_t j = 16; j < len; j++)
+    if (in[a + j] != in[b + j]) return false;
+  return true;
+}
+
+// S line at tile offset so (its '\n' at next - 1): the name's tile offset and length (fields[1],
+// parser.py:133-163), false when the name is not in the 48-byte tab view (the classic parse decides)
+__device__ inline bool lean_s_name(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next,
+                                   uint32_t& x, uint32_t& l) {
+  const uint32_t n = next - 1 - so;
+  const uint64_t w = tab_window(buf, tabm, so >> 4);
+  uint64_t m = (w >> (so & 15)) & ((1ull << (n > 48 ? 48 : n)) - 1);
+  if (!m) return false;
+  const uint32_t t1 = (uint32_t)__builtin_ctzll(m);
+  m &= m - 1;
+  if (!m && n > 48) return false;
+  const uint32_t t2 = m ? (uint32_t)__builtin_ctzll(m) : n;
+  x = so + t1 + 1;
+  l = t2 - t1 - 1;
+  return true;
+}
+
+// L / E / C line in the link_fast shape (lean_line's): the two names' tile offsets and lengths
+__device__ inline bool lean_edge_names(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next,
+                                       uint32_t& xa, uint32_t& la, uint32_t& xb, uint32_t& lb) {
+  const uint32_t n = next - 1 - so;
+  if (n > 48) return false;
+  const uint64_t w = tab_window(buf, tabm, so >> 4);
+  uint64_t m = (w >> (so & 15)) & ((1ull << n) - 1);
+  if (__popcll(m) < 5) return false;
+  uint32_t p[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    p[j] = m ? (uint32_t)__builtin_ctzll(m) : n;
+    m &= m - 1;
+  }
+  if (p[2] - p[1] != 2 || p[4] - p[3] != 2) return false;
+  const uint32_t c2 = buf[so + p[1] + 1], c4 = buf[so + p[3] + 1];
+  if ((c2 != '+' && c2 != '-') || (c4 != '+' && c4 != '-')) return false;
+  xa = so + p[0] + 1;
+  la = p[1] - p[0] - 1;
+  xb = so + p[2] + 1;
+  lb = p[3] - p[2] - 1;
+  return true;
+}
+
+// key head + hash of the name at tile offset x (input offset t0 + x), the classic tiers' key_hash
+__device__ inline uint64_t lean_key(const uint8_t* __restrict__ in, const uint8_t* buf, uint64_t t0, uint32_t x,
+                                    uint32_t l, KeyHead& kh) {
+  kh.k = lds_span16(buf, x, l);
+  kh.len = l;
+  return key_hash(in, kh, t0 + x, l, 0);
+}
+
+// the node id of the name at input offset no (head kh, hash h), or ~0u when no S line names it;
+// (a0, b0): the first probed entry, already loaded by the caller (so several probes are in flight)
+__device__ inline uint32_t lean_find(const uint8_t* __restrict__ in, const HashLeanArgs& H, const KeyHead& kh,
+                                     uint64_t h, uint64_t no, uint4 a0, uint4 b0) {
+  const uint32_t tag = (uint32_t)(h >> 32);
+  const uint64_t k0 = (uint64_t)kh.k, k1 = (uint64_t)(kh.k >> 64);
+  uint64_t idx = h & H.mask;
+  for (uint64_t probe = 0; probe < H.max_probes; probe++) {
+    uint4 a = a0, b = b0;
+    if (probe) {
+      const DictEntry* e = H.table + idx;
+      a = ((const uint4*)e)[0];
+      b = ((const uint4*)e)[1];
+    }
+    const unsigned long long hdr = ((unsigned long long)a.y << 32) | a.x;
+    if (hdr == kEmptySlot) return ~0u;
+    const unsigned long long meta = ((unsigned long long)a.w << 32) | a.z;
+    if ((uint32_t)(hdr >> 32) == tag && (uint32_t)(meta >> 40) == kh.len &&
+        (((uint64_t)b.y << 32) | b.x) == k0 && (((uint64_t)b.w << 32) | b.z) == k1 &&
+        (kh.len <= 16 || tail_eq_in(in, no, meta & ((1ull << 40) - 1), kh.len)))
+      return (uint32_t)hdr;
+    idx = (idx + 1) & H.mask;
+  }
+  return ~0u;
+}
+
+template <int kMode, bool kGrouped>
+__global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
+                                                        Ctl* ctl, TileCnt* __restrict__ tcnt_out,
+                                                        TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
+                                                        uint64_t gcap, HashLeanArgs H) {
+  constexpr uint32_t kW = kLeanTPB / 64;
+  if constexpr (kMode == kLeanClaim) {  // tiles with S or P / O lines (block-uniform)
+    const TileCnt c = H.tcnt[blockIdx.x];
+    if (c.segs == 0 && c.recs == c.segs + c.edges) return;
+    if (c.segs && H.tbase[blockIdx.x].edges) {  // an edge line before this tile's S lines
+      if (threadIdx.x == 0) ctl->int_fail = 1;
+      return;
+    }
+  } else if constexpr (kMode == kLeanEdges) {  // tiles with edge lines
+    if (H.tcnt[blockIdx.x].edges == 0) return;
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
+  __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
+  __shared__ uint32_t rec[kLeanLines + 1];
+  __shared__ unsigned long long red64[kW];
+  __shared__ uint32_t s_gbase;
+  const uint64_t tile = blockIdx.x;
+  const uint64_t t0 = tile * kTile;
+  op.grouped = kGrouped ? 1u : 0u;  // lean_line: positions relative to the tile's base in its group slot
+  uint64_t sbase = 0, ebase = 0;     // hash modes: S lines / edge lines before this tile (K1's bases)
+  if constexpr (kMode != kLeanDecimal) {
+    sbase = H.tbase[tile].segs;
+    ebase = H.tbase[tile].edges;
+  }
+  K2_LEAN_STAMP(0);
+  {
+    TileRegs<kTileHalo, kLeanTPB> R;
+    R.load(in, len, t0);
+    R.store(buf);
+#pragma unroll
+    for (uint32_t j = 0; j < R.kPer; j++) {
+      const uint32_t c = j * kLeanTPB + threadIdx.x;
+      if (c < kLeanChunks) {
+        tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
+        nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
+      }
+    }
+  }
+  if (threadIdx.x < 8) {  // tab_window reads up to 4 bitmaps past a chunk
+    tabm[kLeanChunks + threadIdx.x] = 0;
+    nlm[kLeanChunks + threadIdx.x] = 0;
+  }
+  const bool tile_prev_nl = t0 == 0 || in[t0 - 1] == '\n';
+  __syncthreads();
+  K2_LEAN_STAMP(1);
+  IntState is;
+  // (2) this thread's region: chunks c0 .. c0 + 3, its starts as one 64-bit mask
+  const uint32_t c0 = kLeanRegion * threadIdx.x;
+  unsigned long long st;
+  uint32_t n_nl;
+  {
+    unsigned long long nl;
+    if constexpr (kLeanRegion == 4) {
+      const uint2 v = *(const uint2*)(nlm + c0);
+      nl = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    } else {
+      nl = *(const uint32_t*)(nlm + c0);
+    }
+    const unsigned long long prev = c0 ? (unsigned long long)(nlm[c0 - 1] >> 15) : (tile_prev_nl ? 1ull : 0ull);
+    st = (nl << 1) | prev;
+    if constexpr (kLeanRegion == 2) st &= 0xFFFFFFFFull;
+    const uint64_t r0 = t0 + 16ull * c0;  // a start needs a byte: none at or past len
+    if (r0 + 16 * kLeanRegion > len) st &= r0 >= len ? 0ull : ((1ull << (len - r0)) - 1);
+    n_nl = (uint32_t)__popcll(nl);
+  }
+  const uint32_t n_st = (uint32_t)__popcll(st);
+  uint32_t n_s = 0, n_e = 0, n_po = 0;
+  // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
+  // then the kinds (2-bit codes kept for the record pass); any further start one by one
+  uint32_t codes = 0;
+  {
+    unsigned long long m = st;
+    uint32_t off[kLeanBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      off[q] = m ? 16 * c0 + (uint32_t)__builtin_ctzll(m) : 0xFFFFu;
+      m &= m - 1;
+    }
+    uint32_t x0[kLeanBatch], x1[kLeanBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      const uint32_t o = off[q] == 0xFFFFu ? 0u : off[q];
+      x0[q] = buf[o];
+      x1[q] = buf[o + 1];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      if (off[q] == 0xFFFFu) continue;
+      const bool exact = t0 + off[q] + 1 >= len || x0[q] == '\n' || x1[q] == '\t' || x1[q] == '\n';
+      const uint8_t kd = line_kind((uint8_t)x0[q], exact);
+      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
+      const uint32_t code = lean_code(kd);
+      codes |= code << (2 * q);
+      n_s += code == 1;
+      n_e += code == 2;
+      n_po += code == 3;
+    }
+#pragma unroll 1
+    while (m) {  // more than kLeanBatch lines start in these 64 bytes
+      const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const uint8_t kd = kind_at(buf, o, t0 + o, len);
+      if (kd == kUnknown) is.fail = 1;
+      const uint32_t code = lean_code(kd);
+      n_s += code == 1;
+      n_e += code == 2;
+      n_po += code == 3;
+    }
+  }
+  K2_LEAN_STAMP(2);
+  unsigned long long tot;
+  const unsigned long long ex = block_excl_scan_n64<kLeanTPB>(
+      (unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40), &tot, red64);
+  const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
+                 e_tot = (uint32_t)(tot >> 40);
+  K2_LEAN_STAMP(3);
+  const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
+  if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
+    s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
+  // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
+  // records of its lines ranked in [w0, w0 + kLeanLines] (one past: the window's last line ends where
+  // the next one starts), then the window's lines are parsed
+  for (uint32_t w0 = 0; w0 < n_lines; w0 += kLeanLines) {
+    if (w0) __syncthreads();  // the previous window's records are read
+    {
+      uint32_t r = (uint32_t)(ex & 0xFFFFFu), sp = (uint32_t)((ex >> 20) & 0xFFFFFu), ep = (uint32_t)(ex >> 40);
+      unsigned long long m = st;
+#pragma unroll 1
+      for (uint32_t q = 0; q < n_st && r <= w0 + kLeanLines; q++, r++) {
+        const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t code = q < kLeanBatch ? (codes >> (2 * q)) & 3u : lean_code(kind_at(buf, o, t0 + o, len));
+        if (w0 == 0 && code == 1 && ep) is.fail = 1;  // an S line after an edge line: not the decimal-id layout
+        if (r >= w0) rec[r - w0] = o | (code << 15) | ((code == 1 ? sp : ep) << 17);
+        sp += code == 1;
+        ep += code == 2;
+      }
+    }
+    __syncthreads();
+    if (w0 == 0) {
+      K2_LEAN_STAMP(4);
+      if (kGrouped) {
+        const uint64_t b = (tile >> kGroupShift) * gcap + s_gbase;
+        op.rows += b;
+        op.cols += b;
+      }
+    }
+    // (3) lane-parallel lines
+    const uint32_t n_win = n_lines - w0 < kLeanLines ? n_lines - w0 : kLeanLines;
+    // line j's end: 1 + its '\n' (a virtual one at EOF), tile-local; 0 = past the staged window
+    auto line_next = [&](uint32_t j, uint32_t o) -> uint32_t {
+      if (w0 + j + 1 < n_lines) return rec[j + 1] & 0x7FFFu;
+      uint32_t c = o >> 4;
+      uint32_t mm = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
+      const uint32_t ce = (lim + 15) / 16;
+      while (!mm && ++c < ce) mm = nlm[c];
+      if (mm) return 16 * c + (uint32_t)__builtin_ctz(mm) + 1;
+      return lim == len - t0 ? lim + 1 : 0u;
+    };
+    if constexpr (kMode == kLeanEdges) {
+      // kHL lines per thread per step: their names' first probes are all in flight at once
+      constexpr int kHL = G2N_HL_LINES;
+#pragma unroll 1
+      for (uint32_t j0 = threadIdx.x; j0 < n_win; j0 += kHL * kLeanTPB) {
+        bool act[kHL];
+        uint32_t xs[2 * kHL], ls[2 * kHL];
+        uint64_t ebs[kHL];
+#pragma unroll
+        for (int q = 0; q < kHL; q++) {
+          const uint32_t j = j0 + q * kLeanTPB;
+          act[q] = false;
+          ebs[q] = 0;
+          xs[2 * q] = xs[2 * q + 1] = 0;
+          ls[2 * q] = ls[2 * q + 1] = 0;
+          if (j >= n_win) continue;
+          const uint32_t x = rec[j];
+          if (((x >> 15) & 3u) != 2u) continue;
+          const uint32_t o = x & 0x7FFFu;
+          const uint32_t next = line_next(j, o);
+          if (!next || !lean_edge_names(buf, tabm, o, next, xs[2 * q], ls[2 * q], xs[2 * q + 1], ls[2 * q + 1])) {
+            is.fail = 1;
+            continue;
+          }
+          act[q] = true;
+          ebs[q] = (ebase + (x >> 17)) * H.ktrip;
+        }
+        KeyHead kh[2 * kHL];
+        uint64_t h[2 * kHL];
+        uint4 ea[2 * kHL], eb[2 * kHL];
+#pragma unroll
+        for (int k = 0; k < 2 * kHL; k++) {
+          h[k] = lean_key(in, buf, t0, xs[k], ls[k], kh[k]);
+          if (act[k >> 1]) {
+            const DictEntry* e = H.table + (h[k] & H.mask);
+            ea[k] = ((const uint4*)e)[0];
+            eb[k] = ((const uint4*)e)[1];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kHL; q++) {
+          if (!act[q]) continue;
+          const uint32_t ida = lean_find(in, H, kh[2 * q], h[2 * q], t0 + xs[2 * q], ea[2 * q], eb[2 * q]);
+          const uint32_t idb =
+              lean_find(in, H, kh[2 * q + 1], h[2 * q + 1], t0 + xs[2 * q + 1], ea[2 * q + 1], eb[2 * q + 1]);
+          if (ida == ~0u || idb == ~0u) {  // a key no S line defined: a new node (not S-first)
+            is.fail = 1;
+            continue;
+          }
+          H.rows[ebs[q]] = (int32_t)ida;
+          H.cols[ebs[q]] = (int32_t)idb;
+          if (H.ktrip >= 2) {
+            H.rows[ebs[q] + 1] = (int32_t)idb;
+            H.cols[ebs[q] + 1] = (int32_t)ida;
+          }
+        }
+      }
+      continue;  // next window
+    }
+#pragma unroll 1
+    for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
+      const uint32_t x = rec[j];
+      const uint32_t code = (x >> 15) & 3u;
+      if (code == 0) continue;
+      const uint32_t o = x & 0x7FFFu, pref = x >> 17;
+      const uint32_t next = line_next(j, o);
+      if (!next) {  // the line runs past the staged window
+        is.fail = 1;
+        continue;
+      }
+      if (code == 3) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
+        const uint32_t n = next - 1 - o, sh = o & 15;
+        const uint64_t w = tab_window(buf, tabm, o >> 4);
+        if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
+        continue;
+      }
+      if constexpr (kMode == kLeanClaim) {  // S line: claim its name for node id (S lines before) + pref
+        if (code != 1) continue;
+        uint32_t x, l;
+        if (!lean_s_name(buf, tabm, o, next, x, l)) {
+          is.fail = 1;
+          continue;
+        }
+        KeyHead kh;
+        const uint64_t h = lean_key(in, buf, t0, x, l, kh);
+        const uint32_t id = (uint32_t)(sbase + pref), tag = (uint32_t)(h >> 32);
+        const unsigned long long mine = ((unsigned long long)tag << 32) | id;
+        uint64_t idx = h & H.mask;
+        bool done = false;
+        for (uint64_t probe = 0; probe < H.max_probes && !done; probe++) {
+          DictEntry* e = H.table + idx;
+          unsigned long long cur = e->hdr;
+          if (cur == kEmptySlot) {
+            cur = atomicCAS(&e->hdr, kEmptySlot, mine);
+            if (cur == kEmptySlot) {  // claimed: the key is published for the edge pass (a later launch)
+              e->meta = ((unsigned long long)l << 40) | (t0 + x);
+              e->k0 = (uint64_t)kh.k;
+              e->k1 = (uint64_t)(kh.k >> 64);
+              H.noff[id] = t0 + x;
+              H.nlen[id] = l;
+              done = true;
+              break;
+            }
+          }
+          if ((uint32_t)(cur >> 32) == tag) {  // a repeated S name (or a shared tag): the classic tiers decide
+            is.fail = 1;
+            done = true;
+            break;
+          }
+          idx = (idx + 1) & H.mask;
+        }
+        if (!done) is.fail = 1;  // no free slot within the probe bound
+        continue;
+      } else {
+        // S line: tb = its S index (no edge precedes it); edge line: eb = its edge index
+        if (!lean_line(buf, tabm, o, next, code == 1 ? kS : kEdge, t0, code == 1 ? pref : 0ull,
+                       code == 1 ? 0ull : pref, op, TouchOut{}, is))
+          is.fail = 1;
+      }
+    }
+  }
+  K2_LEAN_STAMP(5);
+  if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
+    if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+    return;
+  }
+  // tile counts and premise evidence
+  if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
+  uint32_t vm = is.vmax;
+  int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
+  unsigned long long cnt = (unsigned long long)n_nl | ((unsigned long long)n_po << 20);  // per tile < 2^20 each
+  for (int o = 32; o > 0; o >>= 1) {
+    vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
+    dmn = min(dmn, (int32_t)__shfl_xor(dmn, o, 64));
+    dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
+    cnt += __shfl_xor(cnt, o, 64);
+  }
+  __shared__ uint32_t rv[kW];
+  __shared__ int32_t rmn[kW], rmx[kW];
+  __shared__ unsigned long long rc[kW];
+  if ((threadIdx.x & 63) == 0) {
+    rv[threadIdx.x >> 6] = vm;
+    rmn[threadIdx.x >> 6] = dmn;
+    rmx[threadIdx.x >> 6] = dmx;
+    rc[threadIdx.x >> 6] = cnt;
+  }
+  const unsigned long long failed = __ballot(is.fail);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)kW; w++) {
+      vm = max(vm, rv[w]);
+      dmn = min(dmn, rmn[w]);
+      dmx = max(dmx, rmx[w]);
+      cnt += rc[w];
+    }
+    const uint32_t npo = (uint32_t)(cnt >> 20);
+    TileCnt c;
+    c.nl = cnt & 0xFFFFFu;
+    c.lines = n_lines;
+    c.segs = s_tot;
+    c.edges = e_tot;
+    c.touches = (uint64_t)s_tot + 2ull * e_tot;
+    c.recs = (uint64_t)s_tot + e_tot + npo;
+    tcnt_out[tile] = c;
+    tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
+  }
+  if (failed && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+  K2_LEAN_STAMP(6);
+#ifdef G2N_K2_STAMPS
+  if (threadIdx.x == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // Open-addressing dictionary, 32-byte entries: hdr = (hash tag << 32 | first touch),

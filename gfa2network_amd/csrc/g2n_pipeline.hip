@@ -59,6 +59,7 @@ constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictiona
 constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast path: the general rounds
 constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bases) instead of tile-local
 constexpr uint32_t kTestNoGroup = 128;      // tile-local parse into per-tile slots + compaction, never group slots
+constexpr uint32_t kTestNoHashLean = 256;   // names that are not decimal ids: the classic hash tiers, never the lean one
 
 
 struct DevBuf {
@@ -768,11 +769,11 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                      (uint64_t*)nullptr, (DeferredLine*)nullptr, n_tiles, tcnt, tlean);
 #else
   if (grouped)
-    hipLaunchKernelGGL(k_tile_lean<true>, dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
-                       tlean, gcount, gcap);
+    hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                       len, lo, c->ctl, tcnt, tlean, gcount, gcap, HashLeanArgs{});
   else
-    hipLaunchKernelGGL(k_tile_lean<false>, dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl,
-                       tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0);
+    hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                       len, lo, c->ctl, tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0, HashLeanArgs{});
 #endif
   phase(c, "parse");
 #ifdef G2N_K2_STAMPS
@@ -825,6 +826,43 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   }
   reset_ctl(c);  // the classic path starts from a clean slate
   return false;
+}
+
+// The S-first hash dictionary on the lean front end (k_tile_lean kLeanClaim / kLeanEdges, after K1):
+// S names claimed with node id = S index, then every edge line's names found straight from its
+// staged tile and the stream-order COO written.  False (and a clean slate) when the input is not
+// S-first with unique names in the lean shapes: the classic parse + dictionary tiers run instead.
+static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
+                            const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
+                            uint64_t** noff_out, uint32_t** nlen_out) {
+  if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
+  uint64_t cap = 1024;
+  while (cap < n_s + n_s / 2) cap <<= 1;  // load <= 2/3: probe sequences stay short
+  auto* table = dget<DictEntry>(c, S_TABLE, cap);
+  G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
+  auto* noff = dget<uint64_t>(c, S_NOFF, n_s);
+  auto* nlen = dget<uint32_t>(c, S_NLEN, n_s);
+  const HashLeanArgs H{tbase, tcnt, table, cap - 1, cap, noff, nlen, rows, cols, ktrip};
+  phase(c, "table_init");
+  hipLaunchKernelGGL((k_tile_lean<kLeanClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
+                     ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  phase(c, "insert_claim");
+  sync_ctl(c);
+  if (c->h_ctl->int_fail) {
+    reset_ctl(c);
+    return false;
+  }
+  hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
+                     ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  phase(c, "insert_lookup");
+  sync_ctl(c);
+  if (c->h_ctl->int_fail) {
+    reset_ctl(c);
+    return false;
+  }
+  *noff_out = noff;
+  *nlen_out = nlen;
+  return true;
 }
 
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
@@ -935,7 +973,14 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     phase(c, "parse");
     sync_ctl(c);
   };
-  bool lean_done = local_done;  // rows / cols hold the stream-order COO already
+  // names that are not the decimal ids: the S-first hash dictionary on the lean front end first
+  uint64_t* hl_noff = nullptr;
+  uint32_t* hl_nlen = nullptr;
+  const bool hash_done = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
+                         !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s &&
+                         hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, &hl_noff,
+                                         &hl_nlen);
+  bool lean_done = local_done || hash_done;  // rows / cols hold the stream-order COO already
   if (lean && !local_done) {
     ParseOpts lo = op;
     lo.rows = rows;
@@ -1024,7 +1069,20 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");
-  if (o->want_node_names && lean_done) {
+  if (o->want_node_names && hash_done) {  // node k's name: S line k's (noff / nlen from the claims)
+    auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
+    scan_excl<uint32_t, int64_t>(c, hl_nlen, offs, n_nodes);
+    hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)hl_nlen, n_nodes, offs, c->ctl);
+    const uint64_t names_len = read_dev(c, &c->ctl->names_len);
+    auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
+    if (n_nodes)
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in,
+                         TouchIn{hl_noff, hl_nlen, nullptr, nullptr}, n_nodes, (const uint32_t*)nullptr, offs, 0, blob);
+    R->names_bytes = names_len;
+    R->names_blob = blob;
+    R->names_offsets = offs;
+    phase(c, "names");
+  } else if (o->want_node_names && lean_done) {
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     const uint64_t names_len = dec_name_off(n_nodes, (int)bidir);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
