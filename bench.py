@@ -658,7 +658,7 @@ class _DevBytes:
 
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
     "tiles": "g2n::k_tile_count",
-    "parse": "g2n::k_tile_parse<true>",  # the tile-local lean parse (decimal ids, no K1); <false> after K1
+    "parse": "g2n::k_tile_lean<0, true>",  # the tile-local lean parse (decimal ids, no K1, group slots)
     "insert_claim": "g2n::k_insert_round<0>",
     "insert_lookup": "g2n::k_lookup_fast<2>",
     "triplets": "g2n::k_triplets<double>",
@@ -713,7 +713,7 @@ def random_ceiling(records: int, ms: float):
             "source": "profiles/r01/randread_ceiling.jsonl"}
 
 
-PMC_SUMMARY = ROOT / "profiles" / "r02" / "pmc_c4.json"
+PMC_SUMMARY = ROOT / "profiles" / "r03" / "pmc_c4.json"
 
 
 def measured_traffic(kernel: str):
