@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
-    "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    "g2n_build_device", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
@@ -208,6 +208,8 @@ def load() -> ctypes.CDLL:
     P, U64, I32, U32, I64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64
     lib.g2n_partition_keys.argtypes = [P, P, U64, P, U64, U32, P, P, P, P]
     lib.g2n_dedup_keys.argtypes = [P, P, U64, P, U64, P, P, ctypes.POINTER(U64)]
+    lib.g2n_gather_keys.argtypes = [P, P, P, P, U64, P, U64, P, ctypes.POINTER(U64)]
+    lib.g2n_remap_pairs.argtypes = [P, P, U64, P, P, U64]
     lib.g2n_route_triplets.argtypes = [P, P, P, P, U64, I32, P, U64, U32, I32, P, P, P, P]
     lib.g2n_csr_from_coo_pair.argtypes = [P, P, P, P, U64, P, P, P, U64, I32, I64, U64, U64, I32, I32, I32,
                                           ctypes.POINTER(Result)]
@@ -238,7 +240,7 @@ def load() -> ctypes.CDLL:
     lib.g2n_first_bad_utf8.restype = I64
     lib.g2n_upload_file_range.argtypes = [ctypes.c_char_p, U64, U64, P, I32]
     lib.g2n_count_device.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(I64)]
-    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
               "g2n_upload_file_range", "g2n_count_device"):
         getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:

@@ -78,6 +78,7 @@ struct Ctl {
   unsigned long long n_deferred;      // lines parsed from global memory after k_tile_parse
   unsigned long long int_fail;        // the decimal-id dictionary (k_int_ids) does not apply
   unsigned long long bucket_overflow; // k_sym_finish met a bucket over its LDS capacity
+  unsigned long long bad_id;          // k_remap_pairs met an id outside its map
 };
 
 struct ParseOpts {

@@ -3191,15 +3191,19 @@ __global__ void __launch_bounds__(kTPB) k_keys_to_touches(const int64_t* __restr
 }
 
 // node id of every touch, whichever dictionary path ran: the claimers and (general path) every
-// touch through its table slot, the other touches of the S-first paths through tid
+// touch through its table slot, the other touches of the S-first paths through tid.
+// s_ident: the S-prefix path (every touch an S touch, ids = claimer indices) — a claimer's id
+// is its own index, no table read.
 __global__ void __launch_bounds__(kTPB) k_touch_ids(uint64_t n, const uint8_t* __restrict__ first,
                                                     const uint32_t* __restrict__ slot,
                                                     const DictEntry* __restrict__ table,
-                                                    const uint32_t* __restrict__ tid, int general,
+                                                    const uint32_t* __restrict__ tid, int general, int s_ident,
                                                     uint32_t* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (t >= n) return;
-  out[t] = (general || first[t]) ? (uint32_t)table[slot[t]].hdr : tid[t];
+  if (general) out[t] = (uint32_t)table[slot[t]].hdr;
+  else if (first[t]) out[t] = s_ident ? (uint32_t)t : (uint32_t)table[slot[t]].hdr;
+  else out[t] = tid[t];
 }
 
 __global__ void __launch_bounds__(kTPB) k_first_of(uint64_t n_nodes, const uint32_t* __restrict__ inv,
@@ -3235,6 +3239,41 @@ __global__ void __launch_bounds__(kTPB) k_copy_keys(const uint8_t* __restrict__ 
   if (j >= n) return;
   const int64_t s = offs[perm[j]], l = offs[perm[j] + 1] - s, o = ooffs[j];
   for (int64_t b = 0; b < l; b++) oblob[o + b] = blob[s + b];
+}
+
+// rows / cols through a local -> global id map, in place (g2n_remap_pairs).  kVec: 4 pairs per
+// thread with 16-byte accesses (both arrays 16-byte aligned, checked by the host), the last
+// n % 4 pairs by the scalar branch; else one pair per thread.
+template <bool kVec>
+__global__ void __launch_bounds__(kTPB) k_remap_pairs(const uint32_t* __restrict__ map, uint64_t n_map,
+                                                      int32_t* __restrict__ rows, int32_t* __restrict__ cols,
+                                                      uint64_t n, Ctl* __restrict__ ctl) {
+  const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  auto one = [&](uint32_t x) -> int32_t {
+    if (x >= n_map) {
+      atomicAdd(&ctl->bad_id, 1ull);
+      return -1;
+    }
+    return (int32_t)map[x];
+  };
+  if (!kVec) {
+    if (q < n) {
+      rows[q] = one((uint32_t)rows[q]);
+      cols[q] = one((uint32_t)cols[q]);
+    }
+  } else if (4 * q + 4 <= n) {
+    const int4 r = reinterpret_cast<const int4*>(rows)[q];
+    const int4 c = reinterpret_cast<const int4*>(cols)[q];
+    const int4 ro{one((uint32_t)r.x), one((uint32_t)r.y), one((uint32_t)r.z), one((uint32_t)r.w)};
+    const int4 co{one((uint32_t)c.x), one((uint32_t)c.y), one((uint32_t)c.z), one((uint32_t)c.w)};
+    reinterpret_cast<int4*>(rows)[q] = ro;
+    reinterpret_cast<int4*>(cols)[q] = co;
+  } else if (4 * q < n) {
+    for (uint64_t i = 4 * q; i < n; i++) {
+      rows[i] = one((uint32_t)rows[i]);
+      cols[i] = one((uint32_t)cols[i]);
+    }
+  }
 }
 
 // owner rank of each triplet's (remapped) row; the sort payload is the triplet index

@@ -1514,7 +1514,7 @@ uint64_t dedup_keys(g2n_context* c, const uint8_t* blob, uint64_t blob_len, cons
   hipLaunchKernelGGL(k_keys_to_touches, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, offs, n, T.noff, T.nlen, T.tkind);
   const DictOut D = build_dictionary(c, blob, blob_len, T, n, n, n, false, kIntFailed);
   hipLaunchKernelGGL(k_touch_ids, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, n, D.first, D.slot, D.table, D.tid,
-                     (int)D.general, ids);
+                     (int)D.general, (int)(!D.general && D.inv == nullptr), ids);
   if (D.n_nodes)
     hipLaunchKernelGGL(k_first_of, dim3(grid_for(D.n_nodes)), dim3(kTPB), 0, c->stream, D.n_nodes, D.inv, first_of);
   G2N_HIP(hipStreamSynchronize(c->stream));
@@ -1545,6 +1545,38 @@ void partition_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, ui
   hipLaunchKernelGGL(k_row_start, dim3(grid_for((uint64_t)n_ranks + 1)), dim3(kTPB), 0, c->stream, owner_s, n,
                      (uint64_t)n_ranks, starts, (const Ctl*)c->ctl);
   G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+uint64_t gather_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, const uint32_t* index, uint64_t n,
+                     uint8_t* oblob, uint64_t oblob_cap, int64_t* ooffs) {
+  begin_call(c);
+  if (n >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 keys");
+  auto* lens = dget<int64_t>(c, S_FOFF64, n + 1);
+  if (n) hipLaunchKernelGGL(k_key_lens, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, offs, index, n, lens);
+  G2N_HIP(hipMemsetAsync(lens + n, 0, sizeof(int64_t), c->stream));
+  excl_scan<int64_t>(c, lens, ooffs, n + 1);
+  int64_t total = 0;
+  G2N_HIP(hipMemcpyAsync(&total, ooffs + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  if ((uint64_t)total > oblob_cap) throw Failure(G2N_E_ARG, "output blob smaller than the gathered keys");
+  if (n && total)
+    hipLaunchKernelGGL(k_copy_keys, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, blob, offs, index, n, ooffs, oblob);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  return (uint64_t)total;
+}
+
+void remap_pairs(g2n_context* c, const uint32_t* map, uint64_t n_map, int32_t* rows, int32_t* cols, uint64_t n) {
+  begin_call(c);
+  if (n) {
+    if (((uintptr_t)rows | (uintptr_t)cols) & 15)
+      hipLaunchKernelGGL(k_remap_pairs<false>, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, map, n_map, rows, cols, n,
+                         c->ctl);
+    else
+      hipLaunchKernelGGL(k_remap_pairs<true>, dim3(grid_for((n + 3) / 4)), dim3(kTPB), 0, c->stream, map, n_map, rows,
+                         cols, n, c->ctl);
+  }
+  sync_ctl(c);
+  if (c->h_ctl->bad_id) throw Failure(G2N_E_ARG, "an id outside the map");
 }
 
 void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, const void* data, uint64_t nnz,
@@ -1732,6 +1764,21 @@ int g2n_partition_keys(g2n_context* ctx, const uint8_t* d_blob, uint64_t blob_le
     return G2N_E_ARG;
   G2N_CTX_CALL(ctx, g2n::partition_keys(ctx, d_blob, d_offsets, n, n_ranks, d_out_blob, d_out_offsets, d_out_index,
                                         d_starts));
+  return G2N_OK;
+}
+
+int g2n_gather_keys(g2n_context* ctx, const uint8_t* d_blob, const int64_t* d_offsets, const uint32_t* d_index,
+                    uint64_t n, uint8_t* d_out_blob, uint64_t out_cap, int64_t* d_out_offsets, uint64_t* out_len) {
+  if (!out_len || !d_out_offsets || (n && (!d_offsets || !d_index || (out_cap && !d_out_blob)))) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, *out_len = g2n::gather_keys(ctx, d_blob, d_offsets, d_index, n, d_out_blob, out_cap,
+                                                d_out_offsets));
+  return G2N_OK;
+}
+
+int g2n_remap_pairs(g2n_context* ctx, const uint32_t* d_map, uint64_t n_map, int32_t* d_rows, int32_t* d_cols,
+                    uint64_t n) {
+  if (n && (!d_map || !d_rows || !d_cols)) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::remap_pairs(ctx, d_map, n_map, d_rows, d_cols, n));
   return G2N_OK;
 }
 

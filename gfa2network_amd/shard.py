@@ -205,7 +205,10 @@ class DevArray:
 
 
 class HipEngine:
-    """The product engine: libg2n.so on one GPU; buffers are torch device tensors."""
+    """The product engine: libg2n.so on one GPU; buffers are torch device tensors (or DevArray
+    views of a context's arena)."""
+
+    supports_views = True
 
     def __init__(self, device: int = 0):
         import torch
@@ -245,13 +248,23 @@ class HipEngine:
         return self.torch.empty(n, dtype=getattr(self.torch, dtype) if isinstance(dtype, str) else dtype,
                                 device=self.device)
 
-    def local_build(self, buf, opts: dict, unknown_warned: bool = False) -> LocalShard:
+    def _build_ctx(self):
+        if self.ctx_b is None:
+            self.ctx_b = self.lib.g2n_context_create(self.device_index)
+            if not self.ctx_b:
+                raise nat.NativeUnavailable(nat.last_error())
+        return self.ctx_b
+
+    def local_build(self, buf, opts: dict, unknown_warned: bool = False, view: bool = False) -> LocalShard:
+        """The range on its own (local ids, names).  view: the COO as DevArray views of the build
+        context (valid until its next build; remap_pairs rewrites them in place), the names copied."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=True, device=self.device_index, **opts)
         o.reserved[0] = int(unknown_warned)
         res = nat.Result()
+        ctx = self._build_ctx() if view else self.ctx
         self._sync()
-        rc = self.lib.g2n_build_device(self.ctx, buf.data_ptr() if buf.numel() else None, buf.numel(),
+        rc = self.lib.g2n_build_device(ctx, buf.data_ptr() if buf.numel() else None, buf.numel(),
                                        ctypes.byref(o), ctypes.byref(res))
         if rc not in (0,) and not (1 <= rc <= 12):
             self._check(rc, "g2n_build_device")
@@ -265,9 +278,14 @@ class HipEngine:
         if rc != 0:
             return sh
         n = res.nnz
-        sh.rows = self._copy_out(res.rows, n, torch.int32)
-        sh.cols = self._copy_out(res.cols, n, torch.int32)
-        sh.data = self._copy_out(res.data, n, getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")]))
+        tdt = getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")])
+        if view:
+            sh.rows, sh.cols = DevArray(res.rows or 0, n, 4), DevArray(res.cols or 0, n, 4)
+            sh.data = DevArray(res.data or 0, n, torch.empty(0, dtype=tdt).element_size())
+        else:
+            sh.rows = self._copy_out(res.rows, n, torch.int32)
+            sh.cols = self._copy_out(res.cols, n, torch.int32)
+            sh.data = self._copy_out(res.data, n, tdt)
         sh.names_offsets = self._copy_out(res.names_offsets, res.n_nodes + 1, torch.int64)
         sh.names_blob = self._copy_out(res.names_blob, int(res.names_bytes), torch.uint8)
         return sh
@@ -298,10 +316,7 @@ class HipEngine:
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
         o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1
         res = nat.Result()
-        if self.ctx_b is None:
-            self.ctx_b = self.lib.g2n_context_create(self.device_index)
-            if not self.ctx_b:
-                raise nat.NativeUnavailable(nat.last_error())
+        self._build_ctx()
         self._sync()
         rc = self.lib.g2n_build_device(self.ctx_b, buf.data_ptr() if buf.numel() else None, buf.numel(),
                                        ctypes.byref(o), ctypes.byref(res))
@@ -350,6 +365,29 @@ class HipEngine:
                                             offsets.data_ptr(), n, ids.data_ptr(), first.data_ptr(),
                                             ctypes.byref(nd)), "g2n_dedup_keys")
         return ids[:n], first[:nd.value], nd.value
+
+    def gather_keys(self, blob, offsets, index, nbytes: int):
+        """Keys index[j] of the blob in that order: (blob of nbytes, offsets)."""
+        torch = self.torch
+        n = index.numel()
+        oblob = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        ooffs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        got = ctypes.c_uint64(0)
+        self._sync()
+        self._check(self.lib.g2n_gather_keys(self.ctx, blob.data_ptr() if blob.numel() else None,
+                                             offsets.data_ptr(), index.data_ptr() if n else None, n,
+                                             oblob.data_ptr(), nbytes, ooffs.data_ptr(), ctypes.byref(got)),
+                    "g2n_gather_keys")
+        return oblob[:got.value], ooffs
+
+    def remap_pairs(self, rows, cols, gmap):
+        """rows / cols (int32) through the local -> global id map, in place."""
+        n = rows.numel()
+        self._sync()
+        self._check(self.lib.g2n_remap_pairs(self.ctx, gmap.data_ptr() if gmap.numel() else None, gmap.numel(),
+                                             rows.data_ptr() if n else None, cols.data_ptr() if n else None, n),
+                    "g2n_remap_pairs")
+        return rows, cols
 
     def route_triplets(self, rows, cols, data, dtype: str, gmap, n_global: int, n_ranks: int, transposed: bool):
         torch = self.torch
@@ -645,7 +683,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     t0 = time.perf_counter()
 
     # 1. local build; 2. stream-order resolution of errors and the one-shot warning
-    local = engine.local_build(buf, opts)
+    view = not keep_coo and getattr(engine, "supports_views", False)
+    local = engine.local_build(buf, opts, view=view) if view else engine.local_build(buf, opts)
 
     def stats(sh):
         return [sh.status, sh.err_line, sh.warn_line, sh.n_lines, sh.n_records, sh.n_records_before_error,
@@ -656,7 +695,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     if first_unk is not None and rank > first_unk and local.warn_line >= 0:
         # an earlier range already warned: this range's unsupported records are silent
         if local.status == 8 and local.err_line == local.warn_line:
-            local = engine.local_build(buf, opts, unknown_warned=True)
+            local = (engine.local_build(buf, opts, unknown_warned=True, view=True) if view
+                     else engine.local_build(buf, opts, unknown_warned=True))
         local.has_warning = False
     allst = C.allgather_list(stats(local))
     line_base = np.concatenate([[0], np.cumsum([int(s[3]) for s in allst])])
@@ -710,6 +750,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     # 3. names to owners, owner dedup in arrival (= global first-touch) order
     t1 = time.perf_counter()
     pb, po, pidx, pst = engine.partition_keys(local.names_blob, local.names_offsets, world)
+    tm["partition_keys"] = (time.perf_counter() - t1) * 1e3
     pst_l = pst.tolist()
     po_l = po[pst.to(torch.int64)].tolist() if local.n_local_nodes else [0] * (world + 1)
     key_counts = [pst_l[k + 1] - pst_l[k] for k in range(world)]
@@ -717,15 +758,17 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     lens = (po[1:] - po[:-1]) if local.n_local_nodes else torch.zeros(0, dtype=torch.int64, device=dev)
     r_blob, _ = C.a2av(pb[:int(po_l[-1])] if local.n_local_nodes else pb[:0], byte_counts)
     (r_lens, r_idx), r_kc = C.a2av_multi([lens, pidx.to(torch.int64)], key_counts)
-    r_src = torch.repeat_interleave(torch.arange(world, dtype=torch.int64, device=dev),
-                                    torch.tensor(r_kc, dtype=torch.int64, device=dev))
     r_off = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
     if r_lens.numel():
         r_off[1:] = torch.cumsum(r_lens, 0)
+    tm["key_exchange"] = (time.perf_counter() - t1) * 1e3 - tm["partition_keys"]
+    t7 = time.perf_counter()
     ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
-    okey = (r_src << 32) | r_idx  # (source rank, local id): global first-touch order
+    tm["dedup_keys"] = (time.perf_counter() - t7) * 1e3
+    # order key (source rank, local id) of each distinct key: global first-touch order
     fo = first_of.to(torch.int64)
-    dkey = okey[fo] if nd else okey[:0]
+    k_end = torch.tensor(np.cumsum(r_kc), dtype=torch.int64, device=dev)
+    dkey = (torch.searchsorted(k_end, fo, right=True) << 32) | r_idx[fo] if nd else r_idx[:0]
     tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
 
     # 4. global ids: rank of each distinct key's order key among all owners'
@@ -738,9 +781,11 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
             gid += torch.searchsorted(other, dkey)
     del all_dkey
     back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
-    gmap = torch.empty(local.n_local_nodes, dtype=torch.int32, device=dev)
-    if local.n_local_nodes:
-        gmap[pidx.to(torch.int64)] = back
+    gmap = None
+    if rank > 0:  # rank 0's map is the identity (step 5)
+        gmap = torch.empty(local.n_local_nodes, dtype=torch.int32, device=dev)
+        if local.n_local_nodes:
+            gmap[pidx.to(torch.int64)] = back
     tm["global_ids"] = (time.perf_counter() - t2) * 1e3
     out.n_nodes = n_global
     if gather_names:
@@ -751,9 +796,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         d_off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
         if nd:
             d_off[1:] = torch.cumsum(d_lens, 0)
-        tot = int(d_off[-1].item())
-        src = torch.repeat_interleave(r_off[fo] - d_off[:-1], d_lens) if nd else d_off[:0]
-        d_blob = r_blob[src + torch.arange(tot, dtype=torch.int64, device=dev)] if tot else r_blob[:0]
+        d_blob, _ = engine.gather_keys(r_blob, r_off, first_of, int(d_off[-1].item()))
         p_gid = list(C.parts(gid, root=names_root))
         p_len = list(C.parts(d_lens, root=names_root))
         p_blob = list(C.parts(d_blob, root=names_root))
@@ -772,10 +815,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     #    map), to row owners (and the A.T stream for MAX-SYM); 6. this rank's CSR row slice
     t6 = time.perf_counter()
     local.dtype_name = dtype
-    g = gmap.to(torch.int64)
-    local.rows = g[local.rows.to(torch.int64)].to(torch.int32)
-    local.cols = g[local.cols.to(torch.int64)].to(torch.int32)
-    del g
+    if rank > 0:  # rank 0's keys are the first n0 distinct keys in its own first-touch order: identity map
+        local.rows, local.cols = engine.remap_pairs(local.rows, local.cols, gmap)
     tm["remap"] = (time.perf_counter() - t6) * 1e3
     if keep_coo:
         out.coo = (local.rows, local.cols, local.data)

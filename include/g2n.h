@@ -279,7 +279,18 @@ int g2n_partition_keys(g2n_context *ctx, const uint8_t *d_blob, uint64_t blob_le
                        uint64_t n, uint32_t n_ranks, uint8_t *d_out_blob, int64_t *d_out_offsets,
                        uint32_t *d_out_index, uint32_t *d_starts);
 
-/* Triplet i = (d_map[d_rows[i]], d_map[d_cols[i]], d_data[i]) (transposed: row and column
+/* Keys d_index[j] (j < n) of a names blob, in that order, to d_out_blob (out_cap bytes) and
+ * d_out_offsets (n + 1); *out_len = bytes written.  G2N_E_ARG if they exceed out_cap (nothing
+ * written to d_out_blob then).  The owner's distinct keys for the names gather. */
+int g2n_gather_keys(g2n_context *ctx, const uint8_t *d_blob, const int64_t *d_offsets, const uint32_t *d_index,
+                    uint64_t n, uint8_t *d_out_blob, uint64_t out_cap, int64_t *d_out_offsets, uint64_t *out_len);
+
+/* d_rows[i] = d_map[d_rows[i]], d_cols[i] = d_map[d_cols[i]] in place (i < n): a range's COO
+ * from local to global ids.  G2N_E_ARG if an id is >= n_map (those entries become -1). */
+int g2n_remap_pairs(g2n_context *ctx, const uint32_t *d_map, uint64_t n_map, int32_t *d_rows, int32_t *d_cols,
+                    uint64_t n);
+
+/* Triplet i = (d_map[d_rows[i]],d_map[d_cols[i]], d_data[i]) (transposed: row and column
  * swapped) goes to rank floor(row * n_ranks / n_global); the output holds them grouped by
  * rank, stream order kept within a rank; d_starts[r] = first output of rank r
  * (d_starts[n_ranks] = nnz).  Outputs sized nnz (data: nnz elements of dtype).  d_map may be

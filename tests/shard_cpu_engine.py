@@ -118,6 +118,18 @@ class CpuEngine:
             ids.append(seen[k])
         return (torch.tensor(ids, dtype=torch.int32), torch.tensor(first, dtype=torch.int32), len(first))
 
+    def gather_keys(self, blob, offsets, index, nbytes):
+        b, off = blob.numpy().tobytes(), offsets.numpy()
+        keys = [b[off[i]:off[i + 1]] for i in index.numpy().astype(np.int64)]
+        ooff = np.zeros(len(keys) + 1, dtype=np.int64)
+        ooff[1:] = np.cumsum([len(k) for k in keys])
+        assert ooff[-1] == nbytes
+        return torch.from_numpy(np.frombuffer(b"".join(keys), dtype=np.uint8).copy()), torch.from_numpy(ooff)
+
+    def remap_pairs(self, rows, cols, gmap):
+        m = gmap.numpy().astype(np.int64)
+        return (torch.from_numpy(m[rows.numpy()].astype(np.int32)), torch.from_numpy(m[cols.numpy()].astype(np.int32)))
+
     def route_triplets(self, rows, cols, data, dtype, gmap, n_global, n_ranks, transposed):
         if gmap is None:  # ids are global already (decimal fast path)
             r, c = rows.numpy().astype(np.int64), cols.numpy().astype(np.int64)
