@@ -2006,6 +2006,15 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
   K2_LEAN_STAMP(5);
   if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
     if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+#ifdef G2N_K2_STAMPS
+    K2_LEAN_STAMP(6);
+    if (threadIdx.x == 0) {
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+    }
+#endif
     return;
   }
   // tile counts and premise evidence

@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -89,6 +90,10 @@ struct g2n_context {
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
   bool no_group = false;      // redo of a build whose group-slot COO the partition refused
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
+  hipEvent_t side_ev[2] = {nullptr, nullptr};  // main -> side fork, side -> main join
+  bool side_pending = false;    // the main stream has not joined the side stream's last work yet
+  std::function<void()> side_work;  // launches deferred to the assembly's latency-bound finish (F1)
   std::vector<g2n::DevBuf> bufs;
   g2n::Ctl* ctl = nullptr;    // device
   g2n::Ctl* h_ctl = nullptr;  // pinned host mirror
@@ -136,6 +141,24 @@ static void phase(g2n_context* c, const char* name) {
 static void sync_ctl(g2n_context* c) {
   G2N_HIP(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
   G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+// the deferred side-stream launches (run_build's decimal names), forked from the main stream here
+static void fork_side(g2n_context* c) {
+  if (!c->side_work) return;
+  G2N_HIP(hipEventRecord(c->side_ev[0], c->stream));
+  G2N_HIP(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+  c->side_work();
+  c->side_work = nullptr;
+  G2N_HIP(hipEventRecord(c->side_ev[1], c->side));
+  c->side_pending = true;
+}
+
+static void join_side(g2n_context* c) {
+  fork_side(c);
+  if (!c->side_pending) return;
+  G2N_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+  c->side_pending = false;
 }
 
 template <class T>
@@ -365,20 +388,24 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   T* odata = dget<T>(c, S_ODATA, n_el);
   auto* btot = dget<uint32_t>(c, S_BTOT, n_bk);
   uint2* tmp = el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1;  // the pass-1 output is dead by now
+  // staged entries (F1 -> F2): columns (u32) then copies (u16) in tmp's 8 bytes per element
+  auto* tcol = (uint32_t*)tmp;
+  auto* tcn = (uint16_t*)(tcol + n_el);
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
+  fork_side(c);  // F1 leaves HBM bandwidth to spare
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tmp, indptr, c->ctl);
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tmp, indptr, c->ctl);
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
   hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, (const uint32_t*)bst,
-                     (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint2*)tmp,
-                     indptr, indices, odata);
+                     (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint32_t*)tcol,
+                     (const uint16_t*)tcn, indptr, indices, odata);
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
   R->nnz = (int64_t)read_dev(c, indptr + n_rows);
@@ -538,6 +565,7 @@ static void reset_ctl(g2n_context* c) {
 }
 
 static void finish_timings(g2n_context* c, g2n_result* R) {
+  join_side(c);
   G2N_HIP(hipStreamSynchronize(c->stream));
   R->n_phases = c->n_ev;
   for (int k = 0; k < c->n_ev; k++) {
@@ -838,12 +866,20 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
   while (cap < n_s + n_s / 2) cap <<= 1;  // load <= 2/3: probe sequences stay short
+#ifdef G2N_HL_CAP_SHIFT  // experiment builds: table footprint vs probe cost
+  cap <<= G2N_HL_CAP_SHIFT;
+#endif
   auto* table = dget<DictEntry>(c, S_TABLE, cap);
   G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
   auto* noff = dget<uint64_t>(c, S_NOFF, n_s);
   auto* nlen = dget<uint32_t>(c, S_NLEN, n_s);
   const HashLeanArgs H{tbase, tcnt, table, cap - 1, cap, noff, nlen, rows, cols, ktrip};
   phase(c, "table_init");
+#ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
+  unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
+  G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_k2_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
+                                 c->stream));
+#endif
   hipLaunchKernelGGL((k_tile_lean<kLeanClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
                      ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "insert_claim");
@@ -852,9 +888,23 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
     reset_ctl(c);
     return false;
   }
+#ifdef G2N_K2_STAMPS
+  G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));  // the claim pass stamped too
+#endif
   hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
                      ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "insert_lookup");
+#ifdef G2N_K2_STAMPS
+  if (const char* out = std::getenv("G2N_HL_STAMPS_OUT")) {  // diagnostics build only: the edge pass
+    std::vector<unsigned long long> h(n_tiles * kK2Stamps);
+    G2N_HIP(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(out, "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   sync_ctl(c);
   if (c->h_ctl->int_fail) {
     reset_ctl(c);
@@ -867,6 +917,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
+  c->side_work = nullptr;  // a launch deferred by a build that threw: its buffers are not this build's
   c->gcoo = GroupedCoo{};
   c->test_flags = (uint32_t)o->reserved[1];
   R->input_bytes = len;
@@ -1086,8 +1137,12 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     const uint64_t names_len = dec_name_off(n_nodes, (int)bidir);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
-    hipLaunchKernelGGL(k_names_dec, dim3(grid_for(n_nodes + 1)), dim3(kTPB), 0, c->stream, n_nodes, (int)bidir, offs,
-                       blob);
+    // no input but n_nodes: on the side stream, overlapping the assembly's finish (fork_side in
+    // csr_partition; joined in finish_timings)
+    const int bd = (int)bidir;
+    c->side_work = [c, n_nodes, bd, offs, blob]() {
+      hipLaunchKernelGGL(k_names_dec, dim3(grid_for(n_nodes + 1)), dim3(kTPB), 0, c->side, n_nodes, bd, offs, blob);
+    };
     R->names_bytes = names_len;
     R->names_blob = blob;
     R->names_offsets = offs;
@@ -1285,6 +1340,8 @@ static g2n_context* context_create(int device) {
   c->device = device;
   G2N_HIP(hipSetDevice(device));
   G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  G2N_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  for (auto& e : c->side_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   G2N_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
   if (c->n_cu <= 0) c->n_cu = 1;
   c->bufs.resize(S_NSLOTS);
@@ -1298,12 +1355,16 @@ static void context_destroy(g2n_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   for (auto& b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   if (c->ctl) (void)hipFree(c->ctl);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
   for (int k = 0; k <= G2N_MAX_PHASES; k++)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  for (auto& e : c->side_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

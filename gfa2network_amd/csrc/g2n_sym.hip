@@ -426,7 +426,8 @@ __device__ inline uint32_t wave_merge(uint32_t x, uint32_t nr, Keep keep, Emit e
 template <class T, bool kSum>
 __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
-                                                     uint2* __restrict__ tmp, int32_t* __restrict__ indptr, Ctl* ctl) {
+                                                     uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
+                                                     int32_t* __restrict__ indptr, Ctl* ctl) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
   __shared__ uint32_t cnt[kTPB];
@@ -518,10 +519,13 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
       return kk != 0;
     }
   };
-  // short row, unrolled and branch-free except for the emit: emit(j, col, copies) for each kept
-  // column in order (padding 0xFFFFFFFF never ends a run of a real column: columns < 2^31 - 1)
-  auto short_merge = [&](auto emit, bool emits) -> uint32_t {
-    uint32_t m = 0, kx = 0, ky = 0;
+  // short row, unrolled and branch-free: the kept columns' positions (bit q: k[q] ends a kept
+  // column run) and copies (byte q of kq: <= kShortRow) in registers, emitted after the offsets
+  // are known (padding 0xFFFFFFFF never ends a run of a real column: columns < 2^31 - 1)
+  uint32_t kmask = 0;
+  uint64_t kq[kShortRow / 8] = {};
+  auto short_merge = [&]() -> uint32_t {
+    uint32_t kx = 0, ky = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kShortRow; q++) {
       const bool valid = q < my;
@@ -531,14 +535,12 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
       const bool last = valid && (q + 1 == kShortRow || (k[q + 1] >> 1) != (k[q] >> 1));
       uint32_t kk;
       const bool kept = keep(kx, ky, kk);
-      if (emits) {
-        if (last && kept) emit(m, k[q] >> 1, kk);
-      }
-      m += (last && kept) ? 1u : 0u;
+      kmask |= (last && kept) ? 1u << q : 0u;
+      kq[q / 8] |= (uint64_t)(kk & 0xFFu) << (8 * (q % 8));
       kx = last ? 0u : kx;
       ky = last ? 0u : ky;
     }
-    return m;
+    return (uint32_t)__builtin_popcount(kmask);
   };
   auto long_merge = [&](auto emit) -> uint32_t {
     uint32_t i = 0, m = 0;
@@ -567,16 +569,21 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     }
     __syncthreads();
   }
-  const uint32_t m = !live ? 0u : (shortrow ? short_merge(none, false) : midrow ? mval[threadIdx.x] : long_merge(none));
+  const uint32_t m = !live ? 0u : (shortrow ? short_merge() : midrow ? mval[threadIdx.x] : long_merge(none));
   uint32_t off;
   const uint32_t tot = block_excl_scan_u32(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
-  uint2* out = tmp + e0;  // tot <= n: the bucket's staged entries stay inside its input range
+  // tot <= n: the bucket's staged entries stay inside its input range
+  uint32_t* ocol = tcol + e0;
+  uint16_t* ocn = tcn + e0;
   if (live) {
     indptr[row] = (int32_t)off;  // local; k_sym_place adds the bucket's offset
     if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
     if (longrow)  // straight out, before the staging below reuses the segments
-      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { out[off + j] = make_uint2(c, kk); });
+      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
+        ocol[off + j] = c;
+        ocn[off + j] = (uint16_t)kk;
+      });
     if (midrow) mval[threadIdx.x] = off;
   }
   __syncthreads();
@@ -584,16 +591,23 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     for (uint32_t i = wv; i < n_mid; i += kTPB / 64) {
       const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kTPB ? cnt[r + 1] : n) - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
-      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { out[o + j] = make_uint2(c, kk); });
+      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) {
+        ocol[o + j] = c;
+        ocn[o + j] = (uint16_t)kk;
+      });
     }
     __syncthreads();
   }
   if (live) {
     if (shortrow) {
-      short_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
-        seg[off + j] = c;
-        ocnt[off + j] = (uint8_t)kk;
-      }, true);
+      uint32_t j = off;
+#pragma unroll
+      for (uint32_t q = 0; q < kShortRow; q++)
+        if (kmask >> q & 1u) {
+          seg[j] = k[q] >> 1;
+          ocnt[j] = (uint8_t)(kq[q / 8] >> (8 * (q % 8)));
+          j++;
+        }
     } else {
       for (uint32_t j = 0; j < m; j++) seg[off + j] = kStagedSkip;
     }
@@ -601,7 +615,10 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
     const uint32_t c = seg[i];
-    if (c != kStagedSkip) out[i] = make_uint2(c, ocnt[i]);
+    if (c != kStagedSkip) {
+      ocol[i] = c;
+      ocn[i] = ocnt[i];
+    }
   }
 }
 
@@ -609,14 +626,14 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
 template <class T>
 __global__ void __launch_bounds__(kTPB) k_sym_place(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ btot,
                                                     const uint32_t* __restrict__ boff, uint32_t low, uint64_t n_rows,
-                                                    T one, const uint2* __restrict__ tmp, int32_t* __restrict__ indptr,
+                                                    T one, const uint32_t* __restrict__ tcol,
+                                                    const uint16_t* __restrict__ tcn, int32_t* __restrict__ indptr,
                                                     int32_t* __restrict__ indices, T* __restrict__ data) {
   const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
   for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
-    const uint2 x = tmp[e0 + i];
-    indices[base + i] = (int32_t)x.x;
-    data[base + i] = sum_copies<T>(one, x.y);
+    indices[base + i] = (int32_t)tcol[e0 + i];
+    data[base + i] = sum_copies<T>(one, tcn[e0 + i]);
   }
   const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
   if (threadIdx.x < (1u << low) && row < n_rows) {

@@ -21,6 +21,7 @@ LEAN_NAMES = ["stage_masks", "classify", "scan", "records", "parse", "finish"]
 
 def main():
     a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 10)
+    a = a[a[:, 0] != 0]  # tiles that returned before the first stamp (the hash passes skip some)
     lean = bool((a[:, 7] == 0).all())  # k_tile_lean stamps 0..6 (and the hardware id in 9)
     names = LEAN_NAMES if lean else NAMES
     last = 6 if lean else 8
