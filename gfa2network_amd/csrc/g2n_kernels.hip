@@ -1769,6 +1769,7 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
   __syncthreads();
   K2_LEAN_STAMP(1);
   IntState is;
+  uint32_t claimed_bytes = 0;  // kLeanClaim: name bytes of the S lines this thread claimed (names blob size)
   // (2) this thread's region: chunks c0 .. c0 + 3, its starts as one 64-bit mask
   const uint32_t c0 = kLeanRegion * threadIdx.x;
   unsigned long long st;
@@ -1982,6 +1983,7 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
               e->k1 = (uint64_t)(kh.k >> 64);
               H.noff[id] = t0 + x;
               H.nlen[id] = l;
+              claimed_bytes += l;
               done = true;
               break;
             }
@@ -2006,6 +2008,11 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
   K2_LEAN_STAMP(5);
   if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
     if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+    if constexpr (kMode == kLeanClaim) {
+      unsigned long long nb = claimed_bytes;
+      for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
+      if ((threadIdx.x & 63) == 0 && nb) atomicAdd(&ctl->names_len, nb);
+    }
 #ifdef G2N_K2_STAMPS
     K2_LEAN_STAMP(6);
     if (threadIdx.x == 0) {

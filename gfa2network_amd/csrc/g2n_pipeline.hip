@@ -862,7 +862,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
 // S-first with unique names in the lean shapes: the classic parse + dictionary tiers run instead.
 static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
                             const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
-                            uint64_t** noff_out, uint32_t** nlen_out) {
+                            uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
   while (cap < n_s + n_s / 2) cap <<= 1;  // load <= 2/3: probe sequences stay short
@@ -888,6 +888,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
     reset_ctl(c);
     return false;
   }
+  *names_len = c->h_ctl->names_len;  // the claimed names' bytes: the names blob needs no later sync
 #ifdef G2N_K2_STAMPS
   G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));  // the claim pass stamped too
 #endif
@@ -1027,10 +1028,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   // names that are not the decimal ids: the S-first hash dictionary on the lean front end first
   uint64_t* hl_noff = nullptr;
   uint32_t* hl_nlen = nullptr;
+  uint64_t hl_names_len = 0;
   const bool hash_done = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
                          !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s &&
                          hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, &hl_noff,
-                                         &hl_nlen);
+                                         &hl_nlen, &hl_names_len);
   bool lean_done = local_done || hash_done;  // rows / cols hold the stream-order COO already
   if (lean && !local_done) {
     ParseOpts lo = op;
@@ -1124,11 +1126,17 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     scan_excl<uint32_t, int64_t>(c, hl_nlen, offs, n_nodes);
     hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)hl_nlen, n_nodes, offs, c->ctl);
-    const uint64_t names_len = read_dev(c, &c->ctl->names_len);
+    const uint64_t names_len = hl_names_len;
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
-    if (n_nodes)
-      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in,
-                         TouchIn{hl_noff, hl_nlen, nullptr, nullptr}, n_nodes, (const uint32_t*)nullptr, offs, 0, blob);
+    if (n_nodes) {  // the copy on the side stream, overlapping the assembly's finish (fork_side)
+      const uint64_t* no = hl_noff;
+      const uint32_t* nl = hl_nlen;
+      c->side_work = [c, in, no, nl, n_nodes, offs, blob]() {
+        hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->side, in,
+                           TouchIn{(uint64_t*)no, (uint32_t*)nl, nullptr, nullptr}, n_nodes, (const uint32_t*)nullptr,
+                           (const int64_t*)offs, 0, blob);
+      };
+    }
     R->names_bytes = names_len;
     R->names_blob = blob;
     R->names_offsets = offs;
