@@ -331,8 +331,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   const int bits = bits_for(n_rows);
   const double per_row =
       (double)(pair ? n_trip + n_t : (sum ? 1 : 2) * n_trip) / (double)(n_rows ? n_rows : 1);
-  int low = 8;  // rows per bucket 2^low: about 2048 elements per bucket on average (capacity 4096)
-  while (low > 1 && (double)(1u << low) * per_row > 2048.0) low--;
+  // rows per bucket 2^low <= kFinTPB (one finish thread per row): about half the finish block's
+  // capacity on average (kSymCap / 2 elements)
+  int low = 0;
+  while ((1u << (low + 1)) <= kFinTPB) low++;
+  while (low > 1 && (double)(1u << low) * per_row > (double)(kSymCap / 2)) low--;
   if (low > bits) low = bits;
   const int hb = bits - low;  // bucket id bits
   if (hb > 2 * (int)kMaxDigitBits) return false;
@@ -394,16 +397,16 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
   fork_side(c);  // F1 leaves HBM bandwidth to spare
   if (sum)
-    hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
+    hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
   else
-    hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, el,
+    hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
-  hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kTPB), 0, c->stream, (const uint32_t*)bst,
+  hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, (const uint32_t*)bst,
                      (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint32_t*)tcol,
                      (const uint16_t*)tcn, indptr, indices, odata);
   R->format = G2N_FMT_CSR;

@@ -45,8 +45,12 @@ constexpr uint32_t kSub = kSubPer * kPartTPB;      // 8192 elements per sub-tile
 constexpr uint32_t kChunkSubs = 8 * 1024 / kPartTPB;  // sub-tiles per block (65536 elements)
 constexpr uint32_t kPartTile = kSub * kChunkSubs;  // 65536 elements per partition block
 constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits
-constexpr uint32_t kSymCap = 4096;                 // elements one finish block holds
-constexpr uint32_t kSymPer = kSymCap / kTPB;       // 16 per thread
+#ifndef G2N_FIN_TPB  // experiment builds vary the finish block (one row per thread)
+#define G2N_FIN_TPB 512
+#endif
+constexpr uint32_t kFinTPB = G2N_FIN_TPB;          // threads (= rows) of a finish block
+constexpr uint32_t kSymCap = 16 * kFinTPB;         // elements one finish block holds
+constexpr uint32_t kSymPer = kSymCap / kFinTPB;    // 16 per thread
 
 // exclusive scan of one u32 per thread over a kN-thread block; returns the block total
 template <uint32_t kN>
@@ -424,16 +428,16 @@ __device__ inline uint32_t wave_merge(uint32_t x, uint32_t nr, Keep keep, Emit e
 }
 
 template <class T, bool kSum>
-__global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
+__global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
                                                      uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
                                                      int32_t* __restrict__ indptr, Ctl* ctl) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
-  __shared__ uint32_t cnt[kTPB];
-  __shared__ uint32_t red[kTPB / 64];
-  __shared__ uint16_t mlist[kTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
-  __shared__ uint32_t mval[kTPB];   // per such row: its entries kept, then its output offset
+  __shared__ uint32_t cnt[kFinTPB];
+  __shared__ uint32_t red[kFinTPB / 64];
+  __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
+  __shared__ uint32_t mval[kFinTPB];   // per such row: its entries kept, then its output offset
   __shared__ uint32_t mcount;
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
@@ -455,7 +459,7 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     {
 #pragma unroll
       for (uint32_t k = 0; k < kSymPer; k++) {
-        const uint32_t i = threadIdx.x + k * kTPB;
+        const uint32_t i = threadIdx.x + k * kFinTPB;
         if (i < n) {
           const uint2 x = el[e0 + i];
           rr[k] = x.x & rmask;
@@ -464,17 +468,17 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
       }
 #pragma unroll
       for (uint32_t k = 0; k < kSymPer; k++)
-        if (threadIdx.x + k * kTPB < n) rr[k] |= atomicAdd(&cnt[rr[k]], 1u) << 16;  // rank within the row
+        if (threadIdx.x + k * kFinTPB < n) rr[k] |= atomicAdd(&cnt[rr[k]], 1u) << 16;  // rank within the row
     }
     __syncthreads();
     my = cnt[threadIdx.x];
-    block_excl_scan_u32(my, &rs, red);
+    block_excl_scan_n<kFinTPB>(my, &rs, red);
     cnt[threadIdx.x] = rs;  // row starts
     __syncthreads();
     {
 #pragma unroll
       for (uint32_t k = 0; k < kSymPer; k++)
-        if (threadIdx.x + k * kTPB < n) seg[cnt[rr[k] & 0xFFFFu] + (rr[k] >> 16)] = vv[k];
+        if (threadIdx.x + k * kFinTPB < n) seg[cnt[rr[k] & 0xFFFFu] + (rr[k] >> 16)] = vv[k];
     }
     __syncthreads();
   }
@@ -559,8 +563,8 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   };
   auto none = [](uint32_t, uint32_t, uint32_t) {};
   if (n_mid) {
-    for (uint32_t i = wv; i < n_mid; i += kTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kTPB ? cnt[r + 1] : n) - s0;
+    for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : n) - s0;
       uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       x = wave_sort64(x);
       if (lane < nr) seg[s0 + lane] = x;
@@ -571,7 +575,7 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   }
   const uint32_t m = !live ? 0u : (shortrow ? short_merge() : midrow ? mval[threadIdx.x] : long_merge(none));
   uint32_t off;
-  const uint32_t tot = block_excl_scan_u32(m, &off, red);
+  const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
   // tot <= n: the bucket's staged entries stay inside its input range
   uint32_t* ocol = tcol + e0;
@@ -588,8 +592,8 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
   }
   __syncthreads();
   if (n_mid) {  // the wave-sorted rows, straight out (consecutive lanes write consecutive entries)
-    for (uint32_t i = wv; i < n_mid; i += kTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kTPB ? cnt[r + 1] : n) - s0, o = mval[r];
+    for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : n) - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) {
         ocol[o + j] = c;
@@ -613,7 +617,7 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
+  for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
     const uint32_t c = seg[i];
     if (c != kStagedSkip) {
       ocol[i] = c;
@@ -624,14 +628,14 @@ __global__ void __launch_bounds__(kTPB) k_sym_finish(const uint2* __restrict__ e
 
 // F2: bucket b's staged entries to their CSR place (boff = exclusive scan of btot), indptr rebased.
 template <class T>
-__global__ void __launch_bounds__(kTPB) k_sym_place(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ btot,
+__global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ btot,
                                                     const uint32_t* __restrict__ boff, uint32_t low, uint64_t n_rows,
                                                     T one, const uint32_t* __restrict__ tcol,
                                                     const uint16_t* __restrict__ tcn, int32_t* __restrict__ indptr,
                                                     int32_t* __restrict__ indices, T* __restrict__ data) {
   const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
-  for (uint32_t i = threadIdx.x; i < tot; i += kTPB) {
+  for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
     indices[base + i] = (int32_t)tcol[e0 + i];
     data[base + i] = sum_copies<T>(one, tcn[e0 + i]);
   }
