@@ -48,6 +48,11 @@ constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1
 #ifndef G2N_FIN_TPB  // experiment builds vary the finish block (one row per thread)
 #define G2N_FIN_TPB 512
 #endif
+#ifdef G2N_FIN_W8  // experiment: 8 waves per SIMD (VGPRs <= 64, some spilled)
+#define G2N_FIN_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define G2N_FIN_WAVES
+#endif
 constexpr uint32_t kFinTPB = G2N_FIN_TPB;          // threads (= rows) of a finish block
 constexpr uint32_t kSymCap = 16 * kFinTPB;         // elements one finish block holds
 constexpr uint32_t kSymPer = kSymCap / kFinTPB;    // 16 per thread
@@ -388,6 +393,7 @@ __device__ inline void sym_sort_row(uint32_t* seg, uint32_t n) {
 constexpr uint32_t kShortRow = 16;
 constexpr uint32_t kMidRow = 64;  // rows of kShortRow + 1 .. kMidRow entries: sorted and merged by a whole wave
 constexpr uint32_t kStagedSkip = 0xFFFFFFFFu;
+constexpr uint32_t kMultiCopy = 0x80000000u;  // staged entry flag: its copies are in tcn
 
 // ascending bitonic sort of one u32 per lane across the wave
 __device__ inline uint32_t wave_sort64(uint32_t x) {
@@ -428,12 +434,11 @@ __device__ inline uint32_t wave_merge(uint32_t x, uint32_t nr, Keep keep, Emit e
 }
 
 template <class T, bool kSum>
-__global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
+__global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
                                                      uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
                                                      int32_t* __restrict__ indptr, Ctl* ctl) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
-  __shared__ uint8_t ocnt[kSymCap];  // staged entries: copies their value sums
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t red[kFinTPB / 64];
   __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
@@ -577,17 +582,20 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict_
   uint32_t off;
   const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
-  // tot <= n: the bucket's staged entries stay inside its input range
+  // tot <= n: the bucket's staged entries stay inside its input range.  A staged entry is its
+  // column with bit 31 set when its value sums more than one copy (columns < 2^31 - 2); only
+  // then are the copies written (ocn), so the common single copy costs no bytes
   uint32_t* ocol = tcol + e0;
   uint16_t* ocn = tcn + e0;
+  auto stage = [&](uint32_t j, uint32_t c, uint32_t kk) -> uint32_t {
+    if (kk > 1u) ocn[j] = (uint16_t)kk;
+    return kk > 1u ? (c | kMultiCopy) : c;
+  };
   if (live) {
     indptr[row] = (int32_t)off;  // local; k_sym_place adds the bucket's offset
     if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
     if (longrow)  // straight out, before the staging below reuses the segments
-      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) {
-        ocol[off + j] = c;
-        ocn[off + j] = (uint16_t)kk;
-      });
+      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { ocol[off + j] = stage(off + j, c, kk); });
     if (midrow) mval[threadIdx.x] = off;
   }
   __syncthreads();
@@ -595,10 +603,7 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict_
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
       const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : n) - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
-      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) {
-        ocol[o + j] = c;
-        ocn[o + j] = (uint16_t)kk;
-      });
+      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { ocol[o + j] = stage(o + j, c, kk); });
     }
     __syncthreads();
   }
@@ -608,8 +613,7 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict_
 #pragma unroll
       for (uint32_t q = 0; q < kShortRow; q++)
         if (kmask >> q & 1u) {
-          seg[j] = k[q] >> 1;
-          ocnt[j] = (uint8_t)(kq[q / 8] >> (8 * (q % 8)));
+          seg[j] = stage(j, k[q] >> 1, (uint32_t)(kq[q / 8] >> (8 * (q % 8))) & 0xFFu);
           j++;
         }
     } else {
@@ -619,10 +623,7 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_finish(const uint2* __restrict_
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
     const uint32_t c = seg[i];
-    if (c != kStagedSkip) {
-      ocol[i] = c;
-      ocn[i] = ocnt[i];
-    }
+    if (c != kStagedSkip) ocol[i] = c;
   }
 }
 
@@ -636,8 +637,9 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
   const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
   for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
-    indices[base + i] = (int32_t)tcol[e0 + i];
-    data[base + i] = sum_copies<T>(one, tcn[e0 + i]);
+    const uint32_t c = tcol[e0 + i];
+    indices[base + i] = (int32_t)(c & ~kMultiCopy);
+    data[base + i] = sum_copies<T>(one, (c & kMultiCopy) ? (uint32_t)tcn[e0 + i] : 1u);
   }
   const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
   if (threadIdx.x < (1u << low) && row < n_rows) {
