@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_NSLOTS
+  S_GCNT, S_TCN, S_NSLOTS
 };
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
@@ -350,7 +350,8 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   PartSrc src{(const uint32_t*)(grouped ? c->gcoo.rows : rows), (const uint32_t*)(grouped ? c->gcoo.cols : cols),
               grouped ? c->gcoo.n_groups * c->gcoo.gcap : n_trip, (sum || pair) ? 1u : 0u,
               (const uint32_t*)t_rows, (const uint32_t*)t_cols, pair ? n_t : 0, (uint32_t)row_base,
-              nullptr, nullptr, nullptr, 0, grouped ? c->gcoo.gcount : nullptr, grouped ? c->gcoo.gcap : 0};
+              nullptr, nullptr, nullptr, 0, grouped ? c->gcoo.gcount : nullptr, grouped ? c->gcoo.gcap : 0,
+              (sum || pair) ? 0u : (uint32_t)low + 1u};
   // pass 1: over the COO entries, both sides (grouped: one block per group slot)
   const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + kPartTile - 1) / kPartTile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
@@ -365,12 +366,12 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   const uint2* el = el1;
   if (bits2 == 0) {
     hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                       (const uint32_t*)off1, n_blk1, (uint32_t)n_el, n_buckets, bst);
+                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst);
   } else {  // pass 2 inside each pass-1 group
     auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
-    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0};
-    hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, n_blk1, n_dig1,
-                       (uint32_t)n_el, grp, grp + n_dig1 + 1);
+    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0};
+    hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
+                       n_blk1, n_dig1, grp, grp + n_dig1 + 1);
     // >= the blocks the groups need (sum of ceil(group / kPartTile) <= n_el / kPartTile + n_dig1)
     const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
@@ -382,7 +383,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     hipLaunchKernelGGL(k_part_scatter<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low, n_dig2,
                        (const uint32_t*)off2, n_blk2, el2);
     hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                       (const uint32_t*)off2, s2, n_dig2, (uint32_t)n_el, n_buckets, bst);
+                       (const uint32_t*)off2, s2, n_dig2, n_buckets, bst);
     el = el2;
   }
   phase(c, "sum");
@@ -391,9 +392,10 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   T* odata = dget<T>(c, S_ODATA, n_el);
   auto* btot = dget<uint32_t>(c, S_BTOT, n_bk);
   uint2* tmp = el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1;  // the pass-1 output is dead by now
-  // staged entries (F1 -> F2): columns (u32) then copies (u16) in tmp's 8 bytes per element
+  // staged entries (F1 -> F2): up to two per stored element (kElPair) — columns (u32) in tmp's 8 bytes
+  // per element, the copies (u16, written only for sums of several copies) beside them
   auto* tcol = (uint32_t*)tmp;
-  auto* tcn = (uint16_t*)(tcol + n_el);
+  auto* tcn = dget<uint16_t>(c, S_TCN, 2 * n_el);
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
   fork_side(c);  // F1 leaves HBM bandwidth to spare
   if (sum)

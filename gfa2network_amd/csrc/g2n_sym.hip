@@ -80,8 +80,12 @@ __device__ inline uint32_t block_excl_scan_n(uint32_t v, uint32_t* excl, uint32_
   return tot;
 }
 
-// element: x = row, y = column << 1 | side  (columns < 2^31)
-__device__ inline uint2 sym_elem(uint32_t row, uint32_t col, uint32_t side) { return make_uint2(row, (col << 1) | side); }
+// element: x = row, y = column << 2 | kind (columns < 2^30).  kind 0: the A entry (row, column);
+// 1: the A.T entry of A's (column, row); 2: BOTH entries of A's (row, column), whose two rows share a
+// bucket — P1 emits one such element instead of two when the entry's rows fall in the same bucket
+// (graphs whose edges join nearby ids: half the partition and finish traffic), F1 expands it.
+constexpr uint32_t kElSide1 = 1, kElPair = 2;
+__device__ inline uint2 sym_elem(uint32_t row, uint32_t col, uint32_t kind) { return make_uint2(row, (col << 2) | kind); }
 
 // Where a partition block's elements come from.  Pass 1: the COO entries, each giving two
 // elements (row a, side 0) and (row b, side 1) for A.maximum(A.T), or one (row a, side 0) for the
@@ -101,6 +105,8 @@ struct PartSrc {
   uint32_t n_groups;
   const uint32_t* gcount; // pass 1 over group slots (GroupedCoo): block b = slot b, gcount[b] entries
   uint64_t gcap;          //   from entry b * gcap
+  uint32_t pair_bits;     // pass 1, two per entry: 0, or low + 1 — an entry whose rows agree above bit
+                          //   low (one bucket) is one kElPair element
 };
 
 struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e0/2, e1/2))
@@ -167,13 +173,15 @@ __device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint
     for (uint32_t k = 0; k < kSubPer / 2; k++) {
       const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
       uint32_t a = 0, b = 0;
+      bool pr = false;
       if (2 * i < e1) {
         a = S.rows[i];
         b = S.cols[i];
-        valid |= 3u << (2 * k);
+        pr = S.pair_bits && ((a ^ b) >> (S.pair_bits - 1)) == 0;
+        valid |= (pr ? 1u : 3u) << (2 * k);
       }
-      x[2 * k] = sym_elem(a, b, 0);
-      x[2 * k + 1] = sym_elem(b, a, 1);
+      x[2 * k] = sym_elem(a, b, pr ? kElPair : 0u);
+      x[2 * k + 1] = sym_elem(b, a, kElSide1);
     }
   } else {
 #pragma unroll
@@ -226,8 +234,13 @@ __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shif
 // Scatter: per sub-tile, elements ranked in LDS (unstable), staged in digit order and written
 // as runs at each digit's cursor; the cursors advance sub-tile by sub-tile, so one block fills
 // each of its runs front to back (whole cache lines from one L2).
+#ifdef G2N_PART_WAVES  // experiment: cap VGPRs so more partition blocks share a CU
+#define G2N_PART_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(G2N_PART_WAVES, G2N_PART_WAVES)))
+#else
+#define G2N_PART_WAVES_ATTR
+#endif
 template <int kPass>
-__global__ void __launch_bounds__(kPartTPB) k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
+__global__ void __launch_bounds__(kPartTPB) G2N_PART_WAVES_ATTR k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                        const uint32_t* __restrict__ offs, uint64_t n_blk,
                                                        uint2* __restrict__ out) {
   __shared__ uint32_t hist[1u << kMaxDigitBits];  // sub-tile counts, then its digit starts
@@ -293,13 +306,20 @@ __global__ void __launch_bounds__(kPartTPB) k_part_scatter(PartSrc S, uint32_t s
   }
 }
 
+// the elements pass 1 wrote (kElPair elements make it data-dependent): the end of the scanned count matrix
+__device__ inline uint32_t part_total(const uint32_t* offs, const uint32_t* counts, uint64_t n) {
+  return n ? offs[n - 1] + counts[n - 1] : 0u;
+}
+
 // pass-1 groups -> pass-2 block map: gstart[g] = offs[g * n_blk1] (the scan at digit g, block 0),
 // bstart = scan of the groups' block counts.  One block of 1024 threads (n_groups <= 1024).
-__global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs1, uint64_t n_blk1,
-                                                      uint32_t n_groups, uint32_t total, uint32_t* __restrict__ gstart,
+__global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs1,
+                                                      const uint32_t* __restrict__ cnt1, uint64_t n_blk1,
+                                                      uint32_t n_groups, uint32_t* __restrict__ gstart,
                                                       uint32_t* __restrict__ bstart) {
   __shared__ uint32_t red[16];
   const uint32_t g = threadIdx.x;
+  const uint32_t total = part_total(offs1, cnt1, (uint64_t)n_groups * n_blk1);
   const uint32_t s = g < n_groups ? offs1[(uint64_t)g * n_blk1] : total;
   const uint32_t e = g + 1 < n_groups ? offs1[(uint64_t)(g + 1) * n_blk1] : total;
   const uint32_t nb = g < n_groups ? (e - s + kPartTile - 1) / kPartTile : 0u;
@@ -329,12 +349,12 @@ __global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict
 
 // bucket starts after the last pass: bucket q = (g << bits2) | d
 __global__ void __launch_bounds__(kTPB) k_part_bucket_starts(const uint32_t* __restrict__ offs2, PartSrc m,
-                                                             uint32_t n_dig2, uint32_t total, uint64_t n_buckets,
+                                                             uint32_t n_dig2, uint64_t n_buckets,
                                                              uint32_t* __restrict__ bstart_out) {
   const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (q > n_buckets) return;
   if (q == n_buckets) {
-    bstart_out[q] = total;
+    bstart_out[q] = m.gstart[m.n_groups];  // the total
     return;
   }
   const uint32_t g = (uint32_t)(q / n_dig2), d = (uint32_t)(q % n_dig2);
@@ -343,12 +363,12 @@ __global__ void __launch_bounds__(kTPB) k_part_bucket_starts(const uint32_t* __r
 }
 
 // single pass: bucket q = digit q, start = offs1[q * n_blk1]
-__global__ void __launch_bounds__(kTPB) k_part_bucket_starts1(const uint32_t* __restrict__ offs1, uint64_t n_blk1,
-                                                              uint32_t total, uint64_t n_buckets,
-                                                              uint32_t* __restrict__ bstart_out) {
+__global__ void __launch_bounds__(kTPB) k_part_bucket_starts1(const uint32_t* __restrict__ offs1,
+                                                              const uint32_t* __restrict__ cnt1, uint64_t n_blk1,
+                                                              uint64_t n_buckets, uint32_t* __restrict__ bstart_out) {
   const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (q > n_buckets) return;
-  bstart_out[q] = q == n_buckets ? total : offs1[q * n_blk1];
+  bstart_out[q] = q == n_buckets ? part_total(offs1, cnt1, n_buckets * n_blk1) : offs1[q * n_blk1];
 }
 
 // ---- F: bucket finish --------------------------------------------------------------------
@@ -440,6 +460,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
                                                      int32_t* __restrict__ indptr, Ctl* ctl) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
+  __shared__ uint32_t cur[kFinTPB];    // placement cursors
   __shared__ uint32_t red[kFinTPB / 64];
   __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
   __shared__ uint32_t mval[kFinTPB];   // per such row: its entries kept, then its output offset
@@ -447,44 +468,50 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
   const uint64_t b = blockIdx.x;
-  const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
-  const bool over = n > kSymCap;  // block-uniform
-  if (over) {  // the build's sums go through the general path
+  const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;  // stored elements (a kElPair one is two entries)
+  auto overflow = [&]() {  // the build's sums go through the general path
     if (threadIdx.x == 0) {
       ctl->bucket_overflow = 1;
       btot[b] = 0;
     }
+  };
+  if (n > kSymCap) {  // block-uniform
+    overflow();
     return;
   }
   __syncthreads();
   const uint32_t rmask = (1u << low) - 1u;
-  uint32_t my, rs;
+  uint32_t my, rs, nx;  // nx: the bucket's entries, kElPair elements expanded
   {
-    uint32_t rr[kSymPer], vv[kSymPer];
-    {
+    uint2 xs[kSymPer];
 #pragma unroll
-      for (uint32_t k = 0; k < kSymPer; k++) {
-        const uint32_t i = threadIdx.x + k * kFinTPB;
-        if (i < n) {
-          const uint2 x = el[e0 + i];
-          rr[k] = x.x & rmask;
-          vv[k] = x.y;
-        }
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < kSymPer; k++)
-        if (threadIdx.x + k * kFinTPB < n) rr[k] |= atomicAdd(&cnt[rr[k]], 1u) << 16;  // rank within the row
+    for (uint32_t k = 0; k < kSymPer; k++) {  // every load in flight before the first count
+      const uint32_t i = threadIdx.x + k * kFinTPB;
+      if (i < n) xs[k] = el[e0 + i];
     }
+#pragma unroll
+    for (uint32_t k = 0; k < kSymPer; k++)
+      if (threadIdx.x + k * kFinTPB < n) {
+        atomicAdd(&cnt[xs[k].x & rmask], 1u);
+        if ((xs[k].y & 3u) == kElPair) atomicAdd(&cnt[(xs[k].y >> 2) & rmask], 1u);
+      }
     __syncthreads();
     my = cnt[threadIdx.x];
-    block_excl_scan_n<kFinTPB>(my, &rs, red);
-    cnt[threadIdx.x] = rs;  // row starts
-    __syncthreads();
-    {
-#pragma unroll
-      for (uint32_t k = 0; k < kSymPer; k++)
-        if (threadIdx.x + k * kFinTPB < n) seg[cnt[rr[k] & 0xFFFFu] + (rr[k] >> 16)] = vv[k];
+    nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
+    if (nx > kSymCap) {  // block-uniform
+      overflow();
+      return;
     }
+    cnt[threadIdx.x] = rs;  // row starts
+    cur[threadIdx.x] = rs;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kSymPer; k++)
+      if (threadIdx.x + k * kFinTPB < n) {
+        const uint32_t kind = xs[k].y & 3u, col = xs[k].y >> 2;
+        seg[atomicAdd(&cur[xs[k].x & rmask], 1u)] = (col << 1) | (kind & 1u);
+        if (kind == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = (xs[k].x << 1) | 1u;  // the A.T entry
+      }
     __syncthreads();
   }
   const uint64_t row = (b << low) + threadIdx.x;
@@ -569,7 +596,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   auto none = [](uint32_t, uint32_t, uint32_t) {};
   if (n_mid) {
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : n) - s0;
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : nx) - s0;
       uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       x = wave_sort64(x);
       if (lane < nr) seg[s0 + lane] = x;
@@ -582,11 +609,11 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   uint32_t off;
   const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
-  // tot <= n: the bucket's staged entries stay inside its input range.  A staged entry is its
-  // column with bit 31 set when its value sums more than one copy (columns < 2^31 - 2); only
-  // then are the copies written (ocn), so the common single copy costs no bytes
-  uint32_t* ocol = tcol + e0;
-  uint16_t* ocn = tcn + e0;
+  // tot <= nx <= 2 n: the bucket's staged entries stay inside [2 e0, 2 e0 + 2 n).  A staged entry is
+  // its column with bit 31 set when its value sums more than one copy (columns < 2^30); only then
+  // are the copies written (ocn), so the common single copy costs no bytes
+  uint32_t* ocol = tcol + 2 * (uint64_t)e0;
+  uint16_t* ocn = tcn + 2 * (uint64_t)e0;
   auto stage = [&](uint32_t j, uint32_t c, uint32_t kk) -> uint32_t {
     if (kk > 1u) ocn[j] = (uint16_t)kk;
     return kk > 1u ? (c | kMultiCopy) : c;
@@ -601,7 +628,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   __syncthreads();
   if (n_mid) {  // the wave-sorted rows, straight out (consecutive lanes write consecutive entries)
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : n) - s0, o = mval[r];
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : nx) - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { ocol[o + j] = stage(o + j, c, kk); });
     }
@@ -636,10 +663,21 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
                                                     int32_t* __restrict__ indices, T* __restrict__ data) {
   const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
-  for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
-    const uint32_t c = tcol[e0 + i];
-    indices[base + i] = (int32_t)(c & ~kMultiCopy);
-    data[base + i] = sum_copies<T>(one, (c & kMultiCopy) ? (uint32_t)tcn[e0 + i] : 1u);
+  const uint32_t* src = tcol + 2 * (uint64_t)e0;
+  const uint16_t* scn = tcn + 2 * (uint64_t)e0;
+  constexpr uint32_t kU = 4;  // loads in flight per thread (a bucket averages ~3000 entries)
+  for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += kU * kFinTPB) {
+    uint32_t c[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) c[u] = i0 + u * kFinTPB < tot ? src[i0 + u * kFinTPB] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t i = i0 + u * kFinTPB;
+      if (i < tot) {
+        indices[base + i] = (int32_t)(c[u] & ~kMultiCopy);
+        data[base + i] = sum_copies<T>(one, (c[u] & kMultiCopy) ? (uint32_t)scn[i] : 1u);
+      }
+    }
   }
   const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
   if (threadIdx.x < (1u << low) && row < n_rows) {
