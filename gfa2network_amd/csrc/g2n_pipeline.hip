@@ -357,11 +357,19 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
-  hipLaunchKernelGGL(k_part_hist<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1, cnt1,
-                     n_blk1);
-  scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
-  hipLaunchKernelGGL(k_part_scatter<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
-                     (const uint32_t*)off1, n_blk1, el1);
+  if (sum || pair) {  // one element per entry
+    hipLaunchKernelGGL(k_part_hist<3>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       cnt1, n_blk1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+    hipLaunchKernelGGL(k_part_scatter<3>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       (const uint32_t*)off1, n_blk1, el1);
+  } else {
+    hipLaunchKernelGGL(k_part_hist<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       cnt1, n_blk1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+    hipLaunchKernelGGL(k_part_scatter<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       (const uint32_t*)off1, n_blk1, el1);
+  }
   auto* bst = dget<uint32_t>(c, S_BSTART, n_buckets + 1);
   const uint2* el = el1;
   if (bits2 == 0) {

@@ -114,10 +114,12 @@ struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e
   uint32_t g, j, nb;
 };
 
+// kPass: 1 = pass 1 over A entries, two elements each (or one kElPair); 3 = pass 1 with one element
+// per entry (one_side: the SUM CSR, a sharded slice's pair streams); 2 = pass 2 over pass-1 groups
 template <int kPass>
 __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) {
-  if (kPass == 1 && S.gcount) {
-    const uint64_t per = S.one_side ? 1 : 2;  // elements per entry
+  if (kPass != 2 && S.gcount) {
+    const uint64_t per = kPass == 3 ? 1 : 2;  // elements per entry
     B.g = 0;
     B.j = blk;
     B.nb = 0;
@@ -125,12 +127,12 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
     B.e1 = B.e0 + (uint64_t)S.gcount[blk] * per;
     return true;
   }
-  if (kPass == 1) {
+  if (kPass != 2) {
     B.g = 0;
     B.j = blk;
     B.nb = 0;
     B.e0 = (uint64_t)blk * kPartTile;
-    const uint64_t n_el = S.one_side ? S.n_entries + S.n_t : 2 * S.n_entries;
+    const uint64_t n_el = kPass == 3 ? S.n_entries + S.n_t : 2 * S.n_entries;
     B.e1 = B.e0 + kPartTile < n_el ? B.e0 + kPartTile : n_el;
     return true;
   }
@@ -150,50 +152,87 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
   return true;
 }
 
-// Sub-tile at element e (e multiple of kSub within the block's range): thread t's elements.
-// Pass 1: entries e/2 + t + kPartTPB k (k < 4), coalesced u32 loads of rows and cols; pass 2:
-// elements e + t + kPartTPB k (k < 8), coalesced 8-byte loads.
+// Element slots per thread in one sub-tile: pass 1 loads kSubPer entries (a, b), each one or two
+// elements (kElPair) — up to 16 K elements per sub-tile, staged in 128 KB of LDS (pass 1 runs one
+// block per CU) — and expands them only when ranked, so the next sub-tile's prefetch holds the
+// entries, not the elements; the other passes load kSubPer elements.
 template <int kPass>
-__device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint2 (&x)[kSubPer], uint32_t& valid) {
-  valid = 0;
-  if (kPass == 1 && S.one_side) {
+constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : kSubPer;
+template <int kPass>
+constexpr uint32_t kSubEl = kElPer<kPass> * kPartTPB;  // element slots per sub-tile
+
+template <int kPass>
+struct PartRaw {
+  static constexpr uint32_t kN = kSubPer;
+  uint2 v[kN];
+  uint32_t valid;  // bit k: v[k] holds an entry / element
+};
+
+// Sub-tile at element slot e (a multiple of kSubEl within the block's range): thread t's entries
+// or elements.  Pass 1: entries e/2 + t + kPartTPB k (k < 8), coalesced u32 loads of rows and cols;
+// otherwise elements e + t + kPartTPB k (k < 8).
+template <int kPass>
+__device__ inline void part_fetch(const PartSrc& S, uint64_t e, uint64_t e1, PartRaw<kPass>& r) {
+  r.valid = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++) {
+  for (uint32_t k = 0; k < PartRaw<kPass>::kN; k++) {
+    r.v[k] = make_uint2(0, 0);
+    if (kPass == 1) {
+      const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
+      if (2 * i < e1) {
+        r.v[k] = make_uint2(S.rows[i], S.cols[i]);
+        r.valid |= 1u << k;
+      }
+    } else if (kPass == 3) {
       const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
-      x[k] = make_uint2(0, 0);
       if (i < e1) {
         const bool t = i >= S.n_entries;
         const uint64_t j = t ? i - S.n_entries : i;
-        x[k] = sym_elem((t ? S.rows_t[j] : S.rows[j]) - S.row_base, t ? S.cols_t[j] : S.cols[j], t ? 1u : 0u);
-        valid |= 1u << k;
+        r.v[k] = sym_elem((t ? S.rows_t[j] : S.rows[j]) - S.row_base, t ? S.cols_t[j] : S.cols[j], t ? 1u : 0u);
+        r.valid |= 1u << k;
       }
-    }
-  } else if (kPass == 1) {
-#pragma unroll
-    for (uint32_t k = 0; k < kSubPer / 2; k++) {
-      const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
-      uint32_t a = 0, b = 0;
-      bool pr = false;
-      if (2 * i < e1) {
-        a = S.rows[i];
-        b = S.cols[i];
-        pr = S.pair_bits && ((a ^ b) >> (S.pair_bits - 1)) == 0;
-        valid |= (pr ? 1u : 3u) << (2 * k);
-      }
-      x[2 * k] = sym_elem(a, b, pr ? kElPair : 0u);
-      x[2 * k + 1] = sym_elem(b, a, kElSide1);
-    }
-  } else {
-#pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++) {
+    } else {
       const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
-      x[k] = make_uint2(0, 0);
       if (i < e1) {
-        x[k] = S.in[i];
-        valid |= 1u << k;
+        r.v[k] = S.in[i];
+        r.valid |= 1u << k;
       }
     }
   }
+}
+
+// The sub-tile's elements, derived from what was loaded (no second copy in registers): pass 1
+// turns entry (a, b) into (a, b, side 0) and (b, a, side 1), or one (a, b, kElPair) when both rows
+// fall in one bucket.
+template <int kPass>
+__device__ inline bool part_pair(const PartSrc& S, uint2 v) {
+  return S.pair_bits && ((v.x ^ v.y) >> (S.pair_bits - 1)) == 0;
+}
+template <int kPass>
+__device__ inline uint32_t part_valid(const PartSrc& S, const PartRaw<kPass>& r) {
+  if constexpr (kPass == 1) {
+    uint32_t valid = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSubPer; k++)
+      valid |= (r.valid >> k & 1u) ? (part_pair<kPass>(S, r.v[k]) ? 1u : 3u) << (2 * k) : 0u;
+    return valid;
+  } else {
+    return r.valid;
+  }
+}
+template <int kPass>
+__device__ inline uint2 part_elem(const PartSrc& S, const PartRaw<kPass>& r, uint32_t k) {
+  if constexpr (kPass == 1) {
+    const uint2 v = r.v[k / 2];
+    return (k & 1) ? sym_elem(v.y, v.x, kElSide1) : sym_elem(v.x, v.y, part_pair<kPass>(S, v) ? kElPair : 0u);
+  } else {
+    return r.v[k];
+  }
+}
+template <int kPass>
+__device__ inline uint32_t part_row(const PartRaw<kPass>& r, uint32_t k) {
+  if constexpr (kPass == 1) return (k & 1) ? r.v[k / 2].y : r.v[k / 2].x;
+  else return r.v[k].x;
 }
 
 // index of the block's count for digit d in the count matrix: pass 1 digit-major over blocks,
@@ -201,7 +240,7 @@ __device__ inline void part_load(const PartSrc& S, uint64_t e, uint64_t e1, uint
 // gives every (block, digit) run its output position)
 template <int kPass>
 __device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint32_t d, uint32_t n_dig, uint64_t n_blk) {
-  if (kPass == 1) return (uint64_t)d * n_blk + B.j;
+  if (kPass != 2) return (uint64_t)d * n_blk + B.j;
   return (uint64_t)S.bstart[B.g] * n_dig + (uint64_t)d * B.nb + B.j;
 }
 
@@ -219,13 +258,13 @@ __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shif
   __syncthreads();
   const uint32_t dmask = n_dig - 1;
 #pragma unroll 2
-  for (uint64_t e = B.e0; e < B.e1; e += kSub) {
-    uint2 x[kSubPer];
-    uint32_t valid;
-    part_load<kPass>(S, e, B.e1, x, valid);
+  for (uint64_t e = B.e0; e < B.e1; e += kSubEl<kPass>) {
+    PartRaw<kPass> r;
+    part_fetch<kPass>(S, e, B.e1, r);
+    const uint32_t valid = part_valid<kPass>(S, r);
 #pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++)
-      if (valid >> k & 1) atomicAdd(&hist[(x[k].x >> shift) & dmask], 1u);
+    for (uint32_t k = 0; k < kElPer<kPass>; k++)
+      if (valid >> k & 1) atomicAdd(&hist[(part_row<kPass>(r, k) >> shift) & dmask], 1u);
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) counts[part_slot<kPass>(S, B, d, n_dig, n_blk)] = hist[d];
@@ -234,34 +273,40 @@ __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shif
 // Scatter: per sub-tile, elements ranked in LDS (unstable), staged in digit order and written
 // as runs at each digit's cursor; the cursors advance sub-tile by sub-tile, so one block fills
 // each of its runs front to back (whole cache lines from one L2).
-#ifdef G2N_PART_WAVES  // experiment: cap VGPRs so more partition blocks share a CU
-#define G2N_PART_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(G2N_PART_WAVES, G2N_PART_WAVES)))
-#else
-#define G2N_PART_WAVES_ATTR
+// waves per SIMD the scatter is compiled for: one 1024-thread block per CU (pass 1's stage is 128 KB;
+// two blocks per CU at 64 VGPRs spill and measured slower: 10.0 vs 9.6 ms per C4 build)
+#ifndef G2N_PART1_WAVES
+#define G2N_PART1_WAVES 4
+#endif
+#ifndef G2N_PART2_WAVES
+#define G2N_PART2_WAVES 4
 #endif
 template <int kPass>
-__global__ void __launch_bounds__(kPartTPB) G2N_PART_WAVES_ATTR k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
+__global__ void __launch_bounds__(kPartTPB)
+    __attribute__((amdgpu_waves_per_eu(kPass == 1 ? G2N_PART1_WAVES : G2N_PART2_WAVES)))
+    k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                        const uint32_t* __restrict__ offs, uint64_t n_blk,
                                                        uint2* __restrict__ out) {
   __shared__ uint32_t hist[1u << kMaxDigitBits];  // sub-tile counts, then its digit starts
   __shared__ uint32_t cur[1u << kMaxDigitBits];   // output position of the next element of digit d
-  __shared__ uint2 stage[kSub];
+  __shared__ uint2 stage[kSubEl<kPass>];
   __shared__ uint32_t red[kPartTPB / 64];
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) return;
   for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)];
   const uint32_t dmask = n_dig - 1;
-  uint2 x[kSubPer], nx[kSubPer];
-  uint32_t valid, nvalid = 0;
-  part_load<kPass>(S, B.e0, B.e1, x, valid);
-  for (uint64_t e = B.e0; e < B.e1; e += kSub) {
+  PartRaw<kPass> raw, nraw;
+  part_fetch<kPass>(S, B.e0, B.e1, raw);
+  constexpr uint64_t kStep = kSubEl<kPass>;
+  for (uint64_t e = B.e0; e < B.e1; e += kStep) {
     for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
-    if (G2N_PART_PREFETCH && e + kSub < B.e1) part_load<kPass>(S, e + kSub, B.e1, nx, nvalid);  // next sub-tile in flight
+    if (G2N_PART_PREFETCH && e + kStep < B.e1) part_fetch<kPass>(S, e + kStep, B.e1, nraw);  // next sub-tile in flight
+    const uint32_t valid = part_valid<kPass>(S, raw);
     __syncthreads();
-    uint32_t rk[kSubPer];
+    uint32_t rk[kElPer<kPass>];
 #pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++)
-      rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(x[k].x >> shift) & dmask], 1u) : 0u;
+    for (uint32_t k = 0; k < kElPer<kPass>; k++)
+      rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(part_row<kPass>(raw, k) >> shift) & dmask], 1u) : 0u;
     __syncthreads();
     // digit starts: kDigPer consecutive digits per thread (n_dig <= 1024)
     constexpr uint32_t kDigPer = (1u << kMaxDigitBits) / kPartTPB;
@@ -282,8 +327,8 @@ __global__ void __launch_bounds__(kPartTPB) G2N_PART_WAVES_ATTR k_part_scatter(P
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < kSubPer; k++)
-      if (valid >> k & 1) stage[hist[(x[k].x >> shift) & dmask] + rk[k]] = x[k];
+    for (uint32_t k = 0; k < kElPer<kPass>; k++)
+      if (valid >> k & 1) stage[hist[(part_row<kPass>(raw, k) >> shift) & dmask] + rk[k]] = part_elem<kPass>(S, raw, k);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kPartTPB) {
       const uint2 y = stage[i];
@@ -296,13 +341,8 @@ __global__ void __launch_bounds__(kPartTPB) G2N_PART_WAVES_ATTR k_part_scatter(P
       const uint32_t d = threadIdx.x * kDigPer + q;
       if (d < n_dig) cur[d] += hv[q];
     }
-    if (G2N_PART_PREFETCH) {
-#pragma unroll
-      for (uint32_t k = 0; k < kSubPer; k++) x[k] = nx[k];
-      valid = nvalid;
-    } else if (e + kSub < B.e1) {
-      part_load<kPass>(S, e + kSub, B.e1, x, valid);
-    }
+    if (G2N_PART_PREFETCH) raw = nraw;
+    else if (e + kStep < B.e1) part_fetch<kPass>(S, e + kStep, B.e1, raw);
   }
 }
 
