@@ -25,6 +25,10 @@ struct InflTables {
   uint16_t dcount[16], dsym[32];
   uint16_t offs[16];
 };
+// k_inflate_members' LDS (kInflTPB tables + the 1 KB CRC table, ~68.6 KB) is sized for gfx950's
+// 160 KB per CU; a 64 KB-LDS target would fail at launch, not here
+static_assert(kInflTPB * sizeof(InflTables) + 256 * sizeof(uint32_t) <= 160 * 1024,
+              "k_inflate_members: LDS tables exceed gfx950's 160 KB");
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};

@@ -405,6 +405,12 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   auto* tcol = (uint32_t*)tmp;
   auto* tcn = dget<uint16_t>(c, S_TCN, 2 * n_el);
   G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
+#ifdef G2N_F1_STAMPS
+  unsigned long long* f1st = dget<unsigned long long>(c, S_TEMP, n_bk * kF1Stamps);
+  G2N_HIP(hipMemsetAsync(f1st, 0, n_bk * kF1Stamps * 8, c->stream));
+  G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_f1_stamps), &f1st, sizeof(f1st), 0, hipMemcpyHostToDevice,
+                                 c->stream));
+#endif
   fork_side(c);  // F1 leaves HBM bandwidth to spare
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
@@ -412,6 +418,17 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   else
     hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
+#ifdef G2N_F1_STAMPS
+  if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
+    std::vector<unsigned long long> h(n_bk * kF1Stamps);
+    G2N_HIP(hipMemcpyAsync(h.data(), f1st, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(out, "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
   sync_ctl(c);

@@ -56,6 +56,10 @@ constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1
 constexpr uint32_t kFinTPB = G2N_FIN_TPB;          // threads (= rows) of a finish block
 constexpr uint32_t kSymCap = 16 * kFinTPB;         // elements one finish block holds
 constexpr uint32_t kSymPer = kSymCap / kFinTPB;    // 16 per thread
+#ifndef G2N_FIN_REG
+#define G2N_FIN_REG 8
+#endif
+constexpr uint32_t kSymReg = G2N_FIN_REG;         // stored elements per thread kept in registers
 
 // exclusive scan of one u32 per thread over a kN-thread block; returns the block total
 template <uint32_t kN>
@@ -155,15 +159,18 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
 // Element slots per thread in one sub-tile: pass 1 loads kSubPer entries (a, b), each one or two
 // elements (kElPair) — up to 16 K elements per sub-tile, staged in 128 KB of LDS (pass 1 runs one
 // block per CU) — and expands them only when ranked, so the next sub-tile's prefetch holds the
-// entries, not the elements; the other passes load kSubPer elements.
+// entries, not the elements; the other passes load G2N_PART_EL2 elements per thread.
+#ifndef G2N_PART_EL2
+#define G2N_PART_EL2 16
+#endif
 template <int kPass>
-constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : kSubPer;
+constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : G2N_PART_EL2;
 template <int kPass>
 constexpr uint32_t kSubEl = kElPer<kPass> * kPartTPB;  // element slots per sub-tile
 
 template <int kPass>
 struct PartRaw {
-  static constexpr uint32_t kN = kSubPer;
+  static constexpr uint32_t kN = kPass == 1 ? kSubPer : kElPer<kPass>;
   uint2 v[kN];
   uint32_t valid;  // bit k: v[k] holds an entry / element
 };
@@ -493,6 +500,21 @@ __device__ inline uint32_t wave_merge(uint32_t x, uint32_t nr, Keep keep, Emit e
   return (uint32_t)__popcll(km);
 }
 
+// Diagnostics build only (-DG2N_F1_STAMPS, tools/k2_stamps.py ... f1): per bucket, the wall clock
+// at F1's phase boundaries (thread 0) and the hardware id of the CU it ran on.
+#ifdef G2N_F1_STAMPS
+constexpr int kF1Stamps = 10;
+__device__ unsigned long long* g2n_f1_stamps;
+#define F1_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0) g2n_f1_stamps[blockIdx.x * kF1Stamps + (k)] = wall_clock64();      \
+  } while (0)
+#else
+#define F1_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 template <class T, bool kSum>
 __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
@@ -505,6 +527,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
   __shared__ uint32_t mval[kFinTPB];   // per such row: its entries kept, then its output offset
   __shared__ uint32_t mcount;
+  F1_STAMP(0);
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
   const uint64_t b = blockIdx.x;
@@ -523,19 +546,30 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   const uint32_t rmask = (1u << low) - 1u;
   uint32_t my, rs, nx;  // nx: the bucket's entries, kElPair elements expanded
   {
-    uint2 xs[kSymPer];
+    // the first kSymReg elements per thread stay in registers from the count to the placement;
+    // a bucket of more stored elements (rare: a skewed bucket) reads the rest again, so F1 keeps
+    // to 64 VGPRs — 4 blocks per CU
+    uint2 xs[kSymReg];
 #pragma unroll
-    for (uint32_t k = 0; k < kSymPer; k++) {  // every load in flight before the first count
+    for (uint32_t k = 0; k < kSymReg; k++) {  // every load in flight before the first count
       const uint32_t i = threadIdx.x + k * kFinTPB;
       if (i < n) xs[k] = el[e0 + i];
     }
+    auto count = [&](uint2 x) {
+      atomicAdd(&cnt[x.x & rmask], 1u);
+      if ((x.y & 3u) == kElPair) atomicAdd(&cnt[(x.y >> 2) & rmask], 1u);
+    };
+    auto place = [&](uint2 x) {
+      const uint32_t kind = x.y & 3u, col = x.y >> 2;
+      seg[atomicAdd(&cur[x.x & rmask], 1u)] = (col << 1) | (kind & 1u);
+      if (kind == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = (x.x << 1) | 1u;  // the A.T entry
+    };
 #pragma unroll
-    for (uint32_t k = 0; k < kSymPer; k++)
-      if (threadIdx.x + k * kFinTPB < n) {
-        atomicAdd(&cnt[xs[k].x & rmask], 1u);
-        if ((xs[k].y & 3u) == kElPair) atomicAdd(&cnt[(xs[k].y >> 2) & rmask], 1u);
-      }
+    for (uint32_t k = 0; k < kSymReg; k++)
+      if (threadIdx.x + k * kFinTPB < n) count(xs[k]);
+    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < n; i += kFinTPB) count(el[e0 + i]);
     __syncthreads();
+    F1_STAMP(1);
     my = cnt[threadIdx.x];
     nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
     if (nx > kSymCap) {  // block-uniform
@@ -546,13 +580,11 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     cur[threadIdx.x] = rs;
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < kSymPer; k++)
-      if (threadIdx.x + k * kFinTPB < n) {
-        const uint32_t kind = xs[k].y & 3u, col = xs[k].y >> 2;
-        seg[atomicAdd(&cur[xs[k].x & rmask], 1u)] = (col << 1) | (kind & 1u);
-        if (kind == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = (xs[k].x << 1) | 1u;  // the A.T entry
-      }
+    for (uint32_t k = 0; k < kSymReg; k++)
+      if (threadIdx.x + k * kFinTPB < n) place(xs[k]);
+    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < n; i += kFinTPB) place(el[e0 + i]);
     __syncthreads();
+    F1_STAMP(2);
   }
   const uint64_t row = (b << low) + threadIdx.x;
   const bool live = threadIdx.x <= rmask && row < n_rows;
@@ -645,9 +677,11 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     }
     __syncthreads();
   }
+  F1_STAMP(3);
   const uint32_t m = !live ? 0u : (shortrow ? short_merge() : midrow ? mval[threadIdx.x] : long_merge(none));
   uint32_t off;
   const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
+  F1_STAMP(4);
   if (threadIdx.x == 0) btot[b] = tot;
   // tot <= nx <= 2 n: the bucket's staged entries stay inside [2 e0, 2 e0 + 2 n).  A staged entry is
   // its column with bit 31 set when its value sums more than one copy (columns < 2^30); only then
@@ -688,10 +722,20 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     }
   }
   __syncthreads();
+  F1_STAMP(5);
   for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
     const uint32_t c = seg[i];
     if (c != kStagedSkip) ocol[i] = c;
   }
+#ifdef G2N_F1_STAMPS
+  F1_STAMP(6);
+  if (threadIdx.x == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g2n_f1_stamps[blockIdx.x * kF1Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // F2: bucket b's staged entries to their CSR place (boff = exclusive scan of btot), indptr rebased.

@@ -1,6 +1,8 @@
 """Analyse the K2 (k_tile_parse<true>) phase stamps of a -DG2N_K2_STAMPS build.
 
-usage: python tools/k2_stamps.py stamps.bin [out.json]
+usage: python tools/k2_stamps.py stamps.bin [out.json] [f1]
+(f1: the bucket-finish stamps of a -DG2N_F1_STAMPS build: 0 entry, 1 loaded + counted, 2 placed,
+3 rows sorted, 4 merged + offsets, 5 staged, 6 end; 9 = hardware id)
 stamps.bin: n_tiles x 10 u64 — wall clock (100 MHz) at: 0 entry, 1 staged, 2 chunk masks,
 3 chunk-rank scan, 4 start list, 5 kinds + line prefixes, 6 thread 0's lines parsed, 7 all lines
 parsed (barrier), 8 end; 9 = XCC id << 32 | HW_ID.
@@ -17,6 +19,7 @@ TICK_NS = 10.0  # wall_clock64 at 100 MHz
 
 
 LEAN_NAMES = ["stage_masks", "classify", "scan", "records", "parse", "finish"]
+F1_NAMES = ["load_count", "place", "sort", "merge_scan", "stage", "write"]
 
 
 def main():
@@ -25,6 +28,8 @@ def main():
     lean = bool((a[:, 7] == 0).all())  # k_tile_lean stamps 0..6 (and the hardware id in 9)
     names = LEAN_NAMES if lean else NAMES
     last = 6 if lean else 8
+    if len(sys.argv) > 3 and sys.argv[3] == "f1":
+        names, last = F1_NAMES, 6
     t = a[:, :last + 1].astype(np.int64)
     hw = a[:, 9]
     n = len(t)
@@ -64,7 +69,7 @@ def main():
         gaps.append(idle * TICK_NS / 1e3)
     out["cu_idle_us_mean"] = round(float(np.mean(gaps)), 2)
     print(json.dumps(out, indent=1))
-    if len(sys.argv) > 2:
+    if len(sys.argv) > 2 and sys.argv[2] != "-":
         with open(sys.argv[2], "w") as fh:
             json.dump(out, fh, indent=1)
 
