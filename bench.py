@@ -619,6 +619,31 @@ def main():
             "note": "export --format edge-list (cli.py:264-281): the same parse with a stream-order COO, "
                     "then per-edge lengths, a scan and the rendered u\\tv lines in HBM (device-resident; "
                     "edge_text_gbs = (text bytes + 8 B ids per edge) / edge_text phase)"}
+    if not args.no_alt and world == 1:
+        # the same dimensions with no id locality (an L line's second segment uniform over all
+        # segments): every entry's two rows fall in different CSR buckets, so none travels as one
+        # pair element through the partition (g2n_sym.hip) — the assembly's worst case
+        far = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local, names=args.names,
+                                far_links=True)
+        try:
+            far_ph = []
+            for i in range(1 + max(2, min(args.steps, 5))):
+                rc = lib.g2n_build_device(ctx, far.ptr, far.len, ctypes.byref(opts), ctypes.byref(res))
+                if rc != 0:
+                    raise RuntimeError(f"{nat.status_name(rc)}: {nat.last_error()}")
+                if i:
+                    far_ph.append({res.phase_names[k].decode(): res.phase_ms[k] for k in range(res.n_phases)
+                                   if not res.phase_names[k].decode().startswith("_")})
+            far_avg = {k: sum(p.get(k, 0.0) for p in far_ph) / len(far_ph) for k in far_ph[0]}
+            line.setdefault("alt_paths", {})["far_links"] = {
+                "device_ms_per_step": round(sum(far_avg.values()), 3),
+                "m_edges_per_s": round(int(res.n_edges) / (sum(far_avg.values()) / 1e3) / 1e6, 2),
+                "nnz": int(res.nnz), "phase_ms": {k: round(v, 3) for k, v in far_avg.items()},
+                "note": "same dimensions and flags, L lines' second segment uniform over all segments (no id "
+                        "locality: no pair elements in the CSR partition); device time from the phase events"}
+        finally:
+            far.free()
+        step()  # leaves res describing the headline build again
     if dom in ("insert_claim", "insert_lookup"):
         tps = 2 if mode.get("bidirected") else 1
         tpe = 4 if (mode.get("bidirected") and not mode.get("keep_directed_bidir")) else 2

@@ -50,8 +50,12 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_NSLOTS
 };
+
+#ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
+#define G2N_FIN_DIRECT 0
+#endif
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
 constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-sum path
@@ -412,12 +416,40 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                                  c->stream));
 #endif
   fork_side(c);  // F1 leaves HBM bandwidth to spare
+#if G2N_FIN_DIRECT
+  // F1 places every bucket's entries itself, its offset from a decoupled look-back over the buckets
+  auto* lbst = dget<uint64_t>(c, S_FINLB, n_bk);
+  G2N_HIP(hipMemsetAsync(lbst, 0, n_bk * sizeof(uint64_t), c->stream));
   if (sum)
-    hipLaunchKernelGGL((k_sym_finish<T, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
+    hipLaunchKernelGGL((k_sym_finish<T, true, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
+                       indices, odata);
   else
-    hipLaunchKernelGGL((k_sym_finish<T, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
-                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl);
+    hipLaunchKernelGGL((k_sym_finish<T, false, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
+                       indices, odata);
+#ifdef G2N_F1_STAMPS
+  if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
+    std::vector<unsigned long long> h(n_bk * kF1Stamps);
+    G2N_HIP(hipMemcpyAsync(h.data(), f1st, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(out, "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
+  sync_ctl(c);
+  if (c->h_ctl->bucket_overflow) return false;
+#else
+  if (sum)
+    hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
+  else
+    hipLaunchKernelGGL((k_sym_finish<T, false, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
+                       (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -436,6 +468,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, (const uint32_t*)bst,
                      (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint32_t*)tcol,
                      (const uint16_t*)tcn, indptr, indices, odata);
+#endif
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
   R->nnz = (int64_t)read_dev(c, indptr + n_rows);

@@ -515,11 +515,55 @@ __device__ unsigned long long* g2n_f1_stamps;
   } while (0)
 #endif
 
-template <class T, bool kSum>
+// Decoupled look-back over the buckets' status words (kDirect F1): a word holds the bucket's merged
+// entry count (kLbAgg) or the inclusive prefix through it (kLbIncl).  Written with one relaxed
+// agent-scope 8-byte store, polled with relaxed agent-scope loads (sc1: L2-served, the store drops
+// the line from its XCD's L2 — MI355X_MICROARCH.md's flag hand-off).  Every thread of the block
+// reads one predecessor per round, so a round covers kFinTPB buckets: the inclusive frontier moves
+// faster than blocks are dispatched, and a block rarely needs a second round.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+__device__ inline uint64_t fin_lookback(uint64_t* lbst, uint64_t b, uint32_t* lb /* 4 */, uint64_t* red64 /* kFinTPB / 64 */) {
+  uint64_t acc = 0;
+  int64_t hi = (int64_t)b;
+  for (uint32_t it = 0;; it++) {
+    uint32_t* w = lb + 2 * (it & 1);  // parity-double-buffered: a thread may still read the other pair
+    if (threadIdx.x == 0) w[0] = w[1] = kFinTPB;
+    __syncthreads();
+    const int64_t j = hi - 1 - (int64_t)threadIdx.x;
+    const uint64_t st = j >= 0 ? __hip_atomic_load(lbst + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    const uint64_t f = st >> 62;
+    if (f == 2) atomicMin(&w[0], threadIdx.x);
+    if (f == 0) atomicMin(&w[1], threadIdx.x);
+    __syncthreads();
+    const uint32_t p = w[0], z = w[1];  // nearest inclusive predecessor, nearest unpublished one
+    if (z < p) {  // block-uniform: a needed predecessor has not published yet
+      __builtin_amdgcn_s_sleep(4);
+      continue;
+    }
+    uint64_t v = threadIdx.x <= p ? (st & kLbVal) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = v;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kFinTPB / 64; q++) acc += red64[q];
+    __syncthreads();  // red64 is reused by the next round
+    if (p < kFinTPB) return acc;
+    hi -= kFinTPB;
+  }
+}
+
+// kDirect: the bucket's offset comes from the look-back above, and F1 writes indptr / indices /
+// data at their final place (no staging, no F2).  Otherwise F1 stages (tcol / tcn) and F2 places.
+// Measured on C4 (G2N_FIN_DIRECT, F1 stamps): the look-back costs ~10 us per block (merge + offsets
+// 1.8 -> 11.9 us: a block's window waits on predecessors dispatched to other XCDs), F1 3.56 ms
+// against 1.94 + 1.12 ms for F1 + F2 — so the staged form is the default.
+template <class T, bool kSum, bool kDirect>
 __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ bstart,
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
                                                      uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
-                                                     int32_t* __restrict__ indptr, Ctl* ctl) {
+                                                     int32_t* __restrict__ indptr, Ctl* ctl, uint64_t* __restrict__ lbst,
+                                                     int32_t* __restrict__ indices, T* __restrict__ data) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];    // placement cursors
@@ -527,6 +571,8 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kShortRow + 1 .. kMidRow entries
   __shared__ uint32_t mval[kFinTPB];   // per such row: its entries kept, then its output offset
   __shared__ uint32_t mcount;
+  __shared__ uint32_t lb[4];
+  __shared__ uint64_t red64[kFinTPB / 64];
   F1_STAMP(0);
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
@@ -535,7 +581,8 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   auto overflow = [&]() {  // the build's sums go through the general path
     if (threadIdx.x == 0) {
       ctl->bucket_overflow = 1;
-      btot[b] = 0;
+      if constexpr (kDirect) __hip_atomic_store(lbst + b, kLbIncl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else btot[b] = 0;
     }
   };
   if (n > kSymCap) {  // block-uniform
@@ -679,32 +726,61 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   }
   F1_STAMP(3);
   const uint32_t m = !live ? 0u : (shortrow ? short_merge() : midrow ? mval[threadIdx.x] : long_merge(none));
+  // kDirect: a short row's sorted values go back to its own segment (nobody else reads or writes it
+  // before the staging below), so k[] need not stay in registers across the look-back
+  if (kDirect && live && shortrow) {
+#pragma unroll
+    for (uint32_t q = 0; q < kShortRow; q++)
+      if (q < my) sg[q] = k[q];
+  }
   uint32_t off;
   const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
+  uint64_t base = 0;  // kDirect: the bucket's first CSR entry
+  if constexpr (kDirect) {
+    if (threadIdx.x == 0) __hip_atomic_store(lbst + b, kLbAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = fin_lookback(lbst, b, lb, red64);
+    if (threadIdx.x == 0) __hip_atomic_store(lbst + b, kLbIncl | (base + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) btot[b] = tot;
+  }
   F1_STAMP(4);
-  if (threadIdx.x == 0) btot[b] = tot;
   // tot <= nx <= 2 n: the bucket's staged entries stay inside [2 e0, 2 e0 + 2 n).  A staged entry is
   // its column with bit 31 set when its value sums more than one copy (columns < 2^30); only then
   // are the copies written (ocn), so the common single copy costs no bytes
   uint32_t* ocol = tcol + 2 * (uint64_t)e0;
   uint16_t* ocn = tcn + 2 * (uint64_t)e0;
-  auto stage = [&](uint32_t j, uint32_t c, uint32_t kk) -> uint32_t {
-    if (kk > 1u) ocn[j] = (uint16_t)kk;
+  auto stage = [&](uint32_t j, uint32_t c, uint32_t kk) -> uint32_t {  // entry j of the bucket, staged
+    if (kk > 1u) {
+      if constexpr (kDirect) data[base + j] = sum_copies<T>(one, kk);
+      else ocn[j] = (uint16_t)kk;
+    }
     return kk > 1u ? (c | kMultiCopy) : c;
   };
+  auto out = [&](uint32_t j, uint32_t c, uint32_t kk) {  // entry j of the bucket, straight out
+    if constexpr (kDirect) {
+      indices[base + j] = (int32_t)c;
+      data[base + j] = sum_copies<T>(one, kk);
+    } else {
+      ocol[j] = stage(j, c, kk);
+    }
+  };
   if (live) {
-    indptr[row] = (int32_t)off;  // local; k_sym_place adds the bucket's offset
-    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
+    indptr[row] = (int32_t)(base + off);  // !kDirect: local, k_sym_place adds the bucket's offset
+    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(base + off + m);
     if (longrow)  // straight out, before the staging below reuses the segments
-      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { ocol[off + j] = stage(off + j, c, kk); });
+      long_merge([&](uint32_t j, uint32_t c, uint32_t kk) { out(off + j, c, kk); });
     if (midrow) mval[threadIdx.x] = off;
   }
-  __syncthreads();
+  if constexpr (kDirect) {
+#pragma unroll
+    for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
+  }
+  __syncthreads();  // every segment read before the staging below overwrites them
   if (n_mid) {  // the wave-sorted rows, straight out (consecutive lanes write consecutive entries)
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
       const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : nx) - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
-      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { ocol[o + j] = stage(o + j, c, kk); });
+      wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { out(o + j, c, kk); });
     }
     __syncthreads();
   }
@@ -725,7 +801,13 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   F1_STAMP(5);
   for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
     const uint32_t c = seg[i];
-    if (c != kStagedSkip) ocol[i] = c;
+    if (c == kStagedSkip) continue;
+    if constexpr (kDirect) {
+      indices[base + i] = (int32_t)(c & ~kMultiCopy);
+      if (!(c & kMultiCopy)) data[base + i] = sum_copies<T>(one, 1u);
+    } else {
+      ocol[i] = c;
+    }
   }
 #ifdef G2N_F1_STAMPS
   F1_STAMP(6);

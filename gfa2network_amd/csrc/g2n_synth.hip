@@ -32,6 +32,7 @@ static SynthSpec to_spec(const g2n_synth_spec* p) {
   s.seed = p->seed;
   s.rc = p->rc_tag;
   s.names = p->names;
+  s.far = p->far_links;
   return s;
 }
 

@@ -7,7 +7,7 @@
 //   S lines i=1..N_S:  S\t{name(i)}\t{seq}  |seq| ~ Geometric(1/8) over ACGT;
 //                      name(i) = "i", or (names = 1) "s" + 8 hex digits of a u32 bijection of i
 //   L lines j:         L\t{name(src)}\t{o1}\t{name(dst)}\t{o2}\t0M[\tRC:i:{k}]
-//                      src ~ U[1,N_S], dst = min(src + Geometric(5/16), N_S),
+//                      src ~ U[1,N_S], dst = min(src + Geometric(5/16), N_S) (far = 1: dst ~ U[1,N_S]),
 //                      o = '+' with probability 922/1024, k ~ U[1,99]
 // Integer-only draws (splitmix64 of (seed, stream, index, chunk)) keep host == device.
 #pragma once
@@ -25,6 +25,7 @@ struct SynthSpec {
   uint64_t n_s, n_l, seed;
   int32_t rc;
   int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32)
+  int32_t far;    // 1: dst ~ U[1, N_S] instead of src + Geometric(5/16)
 };
 
 G2N_HD inline uint64_t smix64(uint64_t x) {
@@ -76,6 +77,7 @@ G2N_HD inline SynthLink synth_link(const SynthSpec& s, uint64_t j) {
     if (done) break;
   }
   L.dst = L.src + g > s.n_s ? s.n_s : L.src + g;
+  if (s.far) L.dst = synth_rnd(s.seed, 7, j, 0) % s.n_s + 1;
   uint64_t h = synth_rnd(s.seed, 5, j, 0);
   L.o1 = (h & 1023) < 922 ? '+' : '-';
   L.o2 = ((h >> 10) & 1023) < 922 ? '+' : '-';

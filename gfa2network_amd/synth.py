@@ -16,7 +16,7 @@ from . import _native
 
 class Spec(ctypes.Structure):
     _fields_ = [("n_segments", ctypes.c_uint64), ("n_links", ctypes.c_uint64), ("seed", ctypes.c_uint64),
-                ("rc_tag", ctypes.c_int32), ("names", ctypes.c_int32)]
+                ("rc_tag", ctypes.c_int32), ("names", ctypes.c_int32), ("far_links", ctypes.c_int32)]
 
 
 @dataclass(frozen=True)
@@ -63,11 +63,12 @@ NAME_MODES = {"decimal": 0, "hashed": 1}
 
 
 def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, threads: int = 0,
-               names: str = "decimal") -> bytes:
+               names: str = "decimal", far_links: bool = False) -> bytes:
     """The synthetic GFA as bytes, generated on the CPU.  names="hashed": segment i is named
-    "s" + 8 hex digits of a bijection of i (unique, not the decimal ids "1".."N")."""
+    "s" + 8 hex digits of a bijection of i (unique, not the decimal ids "1".."N").  far_links: an L
+    line's second segment is uniform over all segments (no id locality)."""
     lib = _lib()
-    spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names])
+    spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names], int(far_links))
     ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
     rc = lib.g2n_synth_host(ctypes.byref(spec), threads, ctypes.byref(ptr), ctypes.byref(n))
     if rc:
@@ -82,9 +83,9 @@ class DeviceInput:
     """Synthetic GFA generated directly in HBM; owns the device buffer."""
 
     def __init__(self, n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, device: int = 0,
-                 names: str = "decimal"):
+                 names: str = "decimal", far_links: bool = False):
         lib = _lib()
-        spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names])
+        spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names], int(far_links))
         ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
         rc = lib.g2n_synth_device(device, ctypes.byref(spec), ctypes.byref(ptr), ctypes.byref(n))
         if rc:

@@ -21,6 +21,8 @@ typedef struct g2n_synth_spec {
   int32_t rc_tag;      /* append RC:i:k to every L line */
   int32_t names;       /* 0: segment i is "i"; 1: "s" + 8 hex digits of a bijection of i
                           (unique, not decimal: the hash-dictionary / general sharded paths) */
+  int32_t far_links;   /* 1: an L line's second segment is uniform over all segments (no id
+                          locality: every edge's two rows fall in different CSR buckets) */
 } g2n_synth_spec;
 
 /* host: malloc'd buffer of the whole file (free with g2n_synth_free_host) */
