@@ -46,7 +46,7 @@ constexpr uint32_t kChunkSubs = 8 * 1024 / kPartTPB;  // sub-tiles per block (65
 constexpr uint32_t kPartTile = kSub * kChunkSubs;  // 65536 elements per partition block
 constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits
 #ifndef G2N_FIN_TPB  // experiment builds vary the finish block (one row per thread)
-#define G2N_FIN_TPB 512
+#define G2N_FIN_TPB 256
 #endif
 #ifdef G2N_FIN_W8  // experiment: 8 waves per SIMD (VGPRs <= 64, some spilled)
 #define G2N_FIN_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
