@@ -343,7 +343,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (low > bits) low = bits;
   const int hb = bits - low;  // bucket id bits
   if (hb > 2 * (int)kMaxDigitBits) return false;
-  const int bits2 = hb > (int)kMaxDigitBits ? hb / 2 : 0, bits1 = hb - bits2;
+  // two passes: at most 8 bits in pass 1 (its sub-tiles rank 8192 COO entries: longer runs per
+  // digit), the rest in pass 2 (C4, hb = 18: 8 + 10 measured 9.07 ms per build against 9.19 for 9 + 9
+  // and 9.39 for 10 + 8)
+  const int bits1 = hb > (int)kMaxDigitBits ? std::max(hb - (int)kMaxDigitBits, std::min(8, (hb + 1) / 2)) : hb;
+  const int bits2 = hb - bits1;
   const uint32_t n_dig1 = 1u << bits1, n_dig2 = 1u << bits2;
   const uint64_t n_el = pair ? n_trip + n_t : (sum ? 1 : 2) * n_trip;
   if (n_el >= 0xFFFFFFFFull) return false;

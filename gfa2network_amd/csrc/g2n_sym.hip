@@ -831,7 +831,10 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
   const uint32_t* src = tcol + 2 * (uint64_t)e0;
   const uint16_t* scn = tcn + 2 * (uint64_t)e0;
-  constexpr uint32_t kU = 4;  // loads in flight per thread (a bucket averages ~3000 entries)
+#ifndef G2N_PLACE_U
+#define G2N_PLACE_U 8
+#endif
+  constexpr uint32_t kU = G2N_PLACE_U;  // loads in flight per thread (a bucket averages ~1500 entries)
   for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += kU * kFinTPB) {
     uint32_t c[kU];
 #pragma unroll
