@@ -113,3 +113,21 @@ def test_library_version_matches_package():
     from gfa2network_amd import _native
 
     assert _native.version() == f"gfa2network-amd {gfa2network_amd.__version__} (gfx950)"
+
+
+def test_synthetic_far_links_mode():
+    """The benchmark generator's far_links mode (include/g2n_synth.h): the same S lines and L sources,
+    the second segment uniform over all segments instead of a few ids after the source."""
+    from gfa2network_amd import synth
+
+    near = synth.host_bytes(1000, 5000, seed=3).decode().splitlines()
+    far = synth.host_bytes(1000, 5000, seed=3, far_links=True).decode().splitlines()
+    assert [x for x in near if x[0] != "L"] == [x for x in far if x[0] != "L"]
+    ln = [x.split("\t") for x in near if x[0] == "L"]
+    lf = [x.split("\t") for x in far if x[0] == "L"]
+    assert len(ln) == len(lf) == 5000
+    assert [x[1:3] + x[4:] for x in ln] == [x[1:3] + x[4:] for x in lf]  # source, orientations, overlap
+    gap_near = [int(x[3]) - int(x[1]) for x in ln]
+    gap_far = [abs(int(x[3]) - int(x[1])) for x in lf]
+    assert all(0 <= g <= 64 for g in gap_near)
+    assert sum(g > 64 for g in gap_far) > 4000

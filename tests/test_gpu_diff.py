@@ -102,14 +102,18 @@ def test_fuzz_convert_format_equals_oracle(gpu, oracle_lib):
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("n_s,n_l,rc", [(1000, 4000, True), (100_000, 400_000, True), (1_000_000, 4_000_000, False)])
-def test_synthetic_gpu_equals_oracle(gpu, oracle_lib, n_s, n_l, rc):
+@pytest.mark.parametrize("n_s,n_l,rc,far", [(1000, 4000, True, False), (100_000, 400_000, True, False),
+                                             (1_000_000, 4_000_000, False, False), (100_000, 400_000, False, True),
+                                             (1_000_000, 4_000_000, False, True)])
+def test_synthetic_gpu_equals_oracle(gpu, oracle_lib, n_s, n_l, rc, far):
+    """far: L lines' second segment uniform over all segments — no entry's two rows share a finish
+    bucket, so the partition carries no pair elements (g2n_sym.hip); otherwise nearly all do."""
     from gfa2network_amd import synth
 
-    data = synth.host_bytes(n_s, n_l, seed=11, rc_tag=rc)
+    data = synth.host_bytes(n_s, n_l, seed=11, rc_tag=rc, far_links=far)
     modes = MODES if n_l <= 400_000 else [{}, {"directed": False}, {"bidirected": True}]
     for mode in modes:
-        for dtype in (["float64", "float32", "int32"] if n_l <= 400_000 else ["float64"]):
+        for dtype in (["float64", "float32", "int32", "int8"] if n_l <= 400_000 else ["float64"]):
             wt = "RC" if rc else None
             a = outcome(gpu_run(data, mode, dtype, wt))
             b = outcome(oracle_run(oracle_lib, data, mode, dtype, wt))
