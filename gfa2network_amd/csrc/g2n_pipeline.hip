@@ -365,7 +365,14 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
-  if (sum || pair) {  // one element per entry
+  if (sum && !t_rows) {  // the SUM CSR: one element per entry, adjacent transposed twins as one
+    src.pair_bits = (uint32_t)low + 1u;
+    hipLaunchKernelGGL(k_part_hist<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       cnt1, n_blk1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+    hipLaunchKernelGGL(k_part_scatter<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                       (const uint32_t*)off1, n_blk1, el1);
+  } else if (sum || pair) {  // one element per entry
     hipLaunchKernelGGL(k_part_hist<3>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
     scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
@@ -427,11 +434,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata);
+                       indices, odata, (uint32_t)row_base);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata);
+                       indices, odata, (uint32_t)row_base);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -449,11 +456,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
-                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
-                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr);
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -932,7 +939,10 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
                             uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
-  while (cap < n_s + n_s / 2) cap <<= 1;  // load <= 2/3: probe sequences stay short
+#ifndef G2N_HL_LOAD_PCT  // experiment builds: the lean table's maximum load, percent
+#define G2N_HL_LOAD_PCT 67
+#endif
+  while (cap * G2N_HL_LOAD_PCT < n_s * 100) cap <<= 1;  // load <= 2/3: probe sequences stay short
 #ifdef G2N_HL_CAP_SHIFT  // experiment builds: table footprint vs probe cost
   cap <<= G2N_HL_CAP_SHIFT;
 #endif

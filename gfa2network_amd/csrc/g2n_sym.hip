@@ -10,16 +10,18 @@
 // partition need not be stable.
 //
 //   P1 (one or two passes, MSD): elements are partitioned by the high bits of their row into
-//      buckets of 2^low rows — per 1024-thread block of 65536 elements, an LDS histogram
-//      (written to a digit-major count matrix), a device scan of that matrix (g2n_scan.hip),
-//      then the same block re-ranks each 8192-element sub-tile with per-digit cursors in LDS and
-//      writes each digit's run contiguously.  Pass 1 reads the COO coordinates themselves (both
-//      sides generated on the fly); pass 2 works inside each pass-1 group, blocks mapped to
-//      (group, chunk) on the device.  The SUM CSR (coo.tocsr of an unweighted undirected build)
-//      and a sharded rank's row slice (pair streams, row base) use the same partition.
-//   F1 one block per bucket (<= kSymCap elements): count rows in LDS, scatter by row, sort each
-//      row (registers, or Shell sort for long rows), merge the two sides per column, stage the
-//      merged entries in LDS and write them, coalesced, at the bucket's input offset;
+//      buckets of 2^low rows — per 1024-thread block, an LDS histogram (written to a digit-major
+//      count matrix), a device scan of that matrix (g2n_scan.hip), then the same block re-ranks
+//      each sub-tile with per-digit cursors in LDS and writes each digit's run contiguously.
+//      Pass 1 reads the COO coordinates themselves (both sides generated on the fly; an entry
+//      whose two rows share a bucket is ONE kElPair element); pass 2 works inside each pass-1
+//      group, blocks mapped to (group, chunk) on the device.  The SUM CSR (coo.tocsr of an
+//      unweighted undirected build: adjacent (a, b), (b, a) twins in one bucket are one kElPair
+//      element) and a sharded rank's row slice (pair streams, row base) use the same partition.
+//   F1 one block per bucket (<= kSymCap entries): count rows in LDS (kElPair elements expanded),
+//      scatter by row, sort each row (registers, a whole wave, or a lane's Shell sort), merge the
+//      two sides per column, stage the merged entries in LDS and write them, coalesced, at twice
+//      the bucket's input offset;
 //   F2 after a scan of the buckets' entry counts, one block per bucket copies them to their CSR
 //      place (indices, data) and rebases the bucket's indptr.
 #pragma once
@@ -119,11 +121,14 @@ struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e
 };
 
 // kPass: 1 = pass 1 over A entries, two elements each (or one kElPair); 3 = pass 1 with one element
-// per entry (one_side: the SUM CSR, a sharded slice's pair streams); 2 = pass 2 over pass-1 groups
+// per entry (a sharded MAX-SYM slice's two streams); 4 = pass 1 of the SUM CSR (coo.tocsr of an
+// undirected build, one stream): one element per entry, or one kElPair for two adjacent entries
+// that are each other's transpose in one bucket (the (a, b), (b, a) twins an undirected build writes
+// for every edge); 2 = pass 2 over pass-1 groups
 template <int kPass>
 __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) {
   if (kPass != 2 && S.gcount) {
-    const uint64_t per = kPass == 3 ? 1 : 2;  // elements per entry
+    const uint64_t per = kPass == 1 ? 2 : 1;  // element slots per entry
     B.g = 0;
     B.j = blk;
     B.nb = 0;
@@ -136,7 +141,7 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
     B.j = blk;
     B.nb = 0;
     B.e0 = (uint64_t)blk * kPartTile;
-    const uint64_t n_el = kPass == 3 ? S.n_entries + S.n_t : 2 * S.n_entries;
+    const uint64_t n_el = kPass == 1 ? 2 * S.n_entries : S.n_entries + S.n_t;
     B.e1 = B.e0 + kPartTile < n_el ? B.e0 + kPartTile : n_el;
     return true;
   }
@@ -163,8 +168,11 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
 #ifndef G2N_PART_EL2
 #define G2N_PART_EL2 16
 #endif
+#ifndef G2N_PART_EL4  // pass 4 (SUM twins): 16 per thread spills 124 B per lane
+#define G2N_PART_EL4 8
+#endif
 template <int kPass>
-constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : G2N_PART_EL2;
+constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : kPass == 4 ? G2N_PART_EL4 : G2N_PART_EL2;
 template <int kPass>
 constexpr uint32_t kSubEl = kElPer<kPass> * kPartTPB;  // element slots per sub-tile
 
@@ -188,6 +196,12 @@ __device__ inline void part_fetch(const PartSrc& S, uint64_t e, uint64_t e1, Par
       const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
       if (2 * i < e1) {
         r.v[k] = make_uint2(S.rows[i], S.cols[i]);
+        r.valid |= 1u << k;
+      }
+    } else if (kPass == 4) {  // adjacent entries per thread: item k / 2 = entries i0, i0 + 1
+      const uint64_t i = e + 2 * (threadIdx.x + (uint64_t)(k / 2) * kPartTPB) + (k & 1);
+      if (i < e1) {
+        r.v[k] = make_uint2(S.rows[i] - S.row_base, S.cols[i]);
         r.valid |= 1u << k;
       }
     } else if (kPass == 3) {
@@ -215,6 +229,11 @@ template <int kPass>
 __device__ inline bool part_pair(const PartSrc& S, uint2 v) {
   return S.pair_bits && ((v.x ^ v.y) >> (S.pair_bits - 1)) == 0;
 }
+// kPass 4: entries u = (row - row_base, col) and w, adjacent, are one kElPair element
+__device__ inline bool part_twins(const PartSrc& S, uint2 u, uint2 w) {
+  const uint32_t b = u.y - S.row_base;  // u's column as a slice row
+  return S.pair_bits && w.x == b && w.y == u.x + S.row_base && ((u.x ^ b) >> (S.pair_bits - 1)) == 0;
+}
 template <int kPass>
 __device__ inline uint32_t part_valid(const PartSrc& S, const PartRaw<kPass>& r) {
   if constexpr (kPass == 1) {
@@ -222,6 +241,12 @@ __device__ inline uint32_t part_valid(const PartSrc& S, const PartRaw<kPass>& r)
 #pragma unroll
     for (uint32_t k = 0; k < kSubPer; k++)
       valid |= (r.valid >> k & 1u) ? (part_pair<kPass>(S, r.v[k]) ? 1u : 3u) << (2 * k) : 0u;
+    return valid;
+  } else if constexpr (kPass == 4) {
+    uint32_t valid = r.valid;
+#pragma unroll
+    for (uint32_t k = 0; k < kElPer<kPass>; k += 2)
+      if ((r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1])) valid &= ~(2u << k);
     return valid;
   } else {
     return r.valid;
@@ -232,6 +257,9 @@ __device__ inline uint2 part_elem(const PartSrc& S, const PartRaw<kPass>& r, uin
   if constexpr (kPass == 1) {
     const uint2 v = r.v[k / 2];
     return (k & 1) ? sym_elem(v.y, v.x, kElSide1) : sym_elem(v.x, v.y, part_pair<kPass>(S, v) ? kElPair : 0u);
+  } else if constexpr (kPass == 4) {
+    const bool tw = !(k & 1) && (r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1]);
+    return sym_elem(r.v[k].x, r.v[k].y, tw ? kElPair : 0u);
   } else {
     return r.v[k];
   }
@@ -563,7 +591,8 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
                                                      uint32_t low, uint64_t n_rows, T one, uint32_t* __restrict__ btot,
                                                      uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
                                                      int32_t* __restrict__ indptr, Ctl* ctl, uint64_t* __restrict__ lbst,
-                                                     int32_t* __restrict__ indices, T* __restrict__ data) {
+                                                     int32_t* __restrict__ indices, T* __restrict__ data,
+                                                     uint32_t row_base) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];    // placement cursors
@@ -602,14 +631,17 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
       const uint32_t i = threadIdx.x + k * kFinTPB;
       if (i < n) xs[k] = el[e0 + i];
     }
+    // a kElPair element (x.x, column b) is also the entry (b, x.x): the A.T entry of MAX-SYM (side
+    // 1), or the SUM CSR's twin (side 0); rows are slice rows (row - row_base), columns global
     auto count = [&](uint2 x) {
       atomicAdd(&cnt[x.x & rmask], 1u);
-      if ((x.y & 3u) == kElPair) atomicAdd(&cnt[(x.y >> 2) & rmask], 1u);
+      if ((x.y & 3u) == kElPair) atomicAdd(&cnt[((x.y >> 2) - row_base) & rmask], 1u);
     };
     auto place = [&](uint2 x) {
       const uint32_t kind = x.y & 3u, col = x.y >> 2;
       seg[atomicAdd(&cur[x.x & rmask], 1u)] = (col << 1) | (kind & 1u);
-      if (kind == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = (x.x << 1) | 1u;  // the A.T entry
+      if (kind == kElPair)
+        seg[atomicAdd(&cur[(col - row_base) & rmask], 1u)] = ((x.x + row_base) << 1) | (kSum ? 0u : 1u);
     };
 #pragma unroll
     for (uint32_t k = 0; k < kSymReg; k++)
