@@ -1319,13 +1319,13 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restrict__ cnt,
                                                           const TileCnt* __restrict__ tbase,
                                                           const TileLean* __restrict__ tlean, uint64_t n_tiles,
-                                                          uint64_t n_seg, Ctl* ctl) {
+                                                          uint64_t n_seg, uint64_t s_base, Ctl* ctl) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (t >= n_tiles) return;
   const TileLean e = tlean[t];
-  bool bad = e.vmax > n_seg;
+  bool bad = e.vmax > n_seg;  // (s_base: S lines before this byte range of a sharded file)
   if (cnt[t].segs)
-    bad |= tbase[t].edges != 0 || e.dmin != e.dmax || e.dmin != (long long)tbase[t].segs;
+    bad |= tbase[t].edges != 0 || e.dmin != e.dmax || e.dmin != (long long)(s_base + tbase[t].segs);
   if (bad) ctl->int_fail = 1;
 }
 

@@ -836,8 +836,11 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 
 // grouped: the COO goes to group slots instead (k_tile_lean<true>, GroupedCoo) and is not compacted
 // — for builds whose only consumer is the unweighted bucket partition.
+// s_base / n_seg_all: a byte range of a sharded file with global decimal ids (options.reserved[2..3]):
+// the S lines before the range and in the whole file; 0 / 0 for a whole file.
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
-                             TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped) {
+                             TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
+                             uint64_t n_seg_all = 0) {
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
 #endif
@@ -901,7 +904,8 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
     const TileCnt tot = read_dev(c, part + n_parts);
     hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
-                       (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, (uint64_t)tot.segs, c->ctl);
+                       (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles,
+                       n_seg_all ? n_seg_all : (uint64_t)tot.segs, s_base, c->ctl);
     sync_ctl(c);
     ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0x7FFFFFFFull;
     if (ok && grouped) {
@@ -1022,9 +1026,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   const bool grouped = !G2N_NO_GROUP_DEFAULT && !coo_wanted && !c->no_group &&
                        !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
-  const bool local_done = n_tiles && first_one && !shard_dec && !bidir && !(o->weight_tag && *o->weight_tag) &&
-                          !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
-                          tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped);
+  // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
+  const bool local_done =
+      n_tiles && (first_one || (shard_dec && o->reserved[2] >= 0 && o->reserved[3] > 0)) && !bidir &&
+      !(o->weight_tag && *o->weight_tag) && !o->strip_orientation &&
+      !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
+      tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped,
+                       shard_dec ? (uint64_t)o->reserved[2] : 0, shard_dec ? (uint64_t)o->reserved[3] : 0);
   // ---- K1: per-tile counts -> tile bases
   if (n_tiles && !local_done) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
