@@ -321,6 +321,7 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
             assert C.format == "csr" and len(nodes) == raw.n_nodes
             dev_ms = sum(v for k, v in raw.phase_ms.items() if not k.startswith("_"))
             wall = t2 - t0
+            ok = _digest_ok(wl.name, n_s, n_l, C, nodes)  # after the timed region
             out[name] = {
                 "wall_s": round(wall, 3), "m_edges_per_s": round(raw.n_edges / wall / 1e6, 2),
                 "gb_per_s_ingested": round(raw.input_bytes / wall / 1e9, 2),
@@ -329,7 +330,7 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
                               "native_total": round((t1 - t0) * 1e3, 1),
                               "gpu_inflate": round(raw.phase_ms.get("gz_inflate", 0.0), 1),
                               "python_objects": round((t2 - t1) * 1e3, 1)},
-                "nnz": int(C.nnz), "n_nodes": len(nodes)}
+                "nnz": int(C.nnz), "n_nodes": len(nodes), "digest_ok": ok}
             del A, C, nodes, raw
         # the convert CLI end to end (cli.py:193-250): gzip file -> .npz + .nodes.tsv on disk
         from gfa2network_amd.cli import main as cli_main
@@ -350,6 +351,12 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
             "wall_s": round(wall, 3), "m_edges_per_s": round(n_l / wall / 1e6, 2),
             "npz_bytes": os.path.getsize(npz), "nodes_tsv_bytes": os.path.getsize(npz + ".nodes.tsv"),
             "writers": "native (g2n_write_npz / g2n_write_node_map, host threads)"}
+        import scipy.sparse as sp
+
+        with open(npz + ".nodes.tsv", "rb") as fh:  # utils.py:108-114: "<index>\t<name>\n" per node
+            names = [ln.split(b"\t", 1)[1].decode() for ln in fh.read().splitlines()]
+        out["cli_convert_gzip"]["digest_ok"] = _digest_ok(wl.name, n_s, n_l, sp.load_npz(npz).tocsr(), names)
+        del names
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     ref = {"C4": 1295.5}.get(wl.name)  # reference parse_gfa+convert_format, gzip C4, 1 core
@@ -366,6 +373,26 @@ def end_to_end(wl, n_s: int, n_l: int, device: int) -> dict:
                 "speedup": round(same["total_s"] / out["gzip_64MiB_members"]["wall_s"], 1),
                 "note": "identical .gz bytes (64 MiB members); timed on the 8-vCPU build container"}
     return out
+
+
+def _digest_ok(workload: str, n_s: int, n_l: int, C, nodes):
+    """The end-to-end result against the oracle's digest of the same generator bytes
+    (tests/golden/expected/synth_digests.json, tests/golden/make_synth_digests.py): sha256 of the
+    int32 indptr | indices | data of the CSR parse_gfa + convert_format return, and of the names in
+    id order.  None when the workload has no digest (scaled runs)."""
+    import hashlib
+
+    import numpy as np
+
+    doc = json.loads((ROOT / "tests" / "golden" / "expected" / "synth_digests.json").read_text()).get(workload)
+    if not doc or (doc["n_segments"], doc["n_links"]) != (n_s, n_l):
+        return None
+    want = doc["parse"] if doc["parse"]["format"] == "csr" else doc["csr"]  # what convert_format(A, "csr") gives
+    h = hashlib.sha256()
+    for a in (C.indptr.astype(np.int32, copy=False), C.indices.astype(np.int32, copy=False), C.data):
+        h.update(np.ascontiguousarray(a).tobytes())
+    names = hashlib.sha256("".join(nodes).encode()).hexdigest()
+    return h.hexdigest() == want["digest"] and names == doc["names"]
 
 
 def _line_start_device(ptr: int, length: int, nominal: int) -> int:

@@ -51,6 +51,7 @@ TEST_NO_TILE_LOCAL = 32  # decimal ids: the lean parse after K1's tile bases, no
 TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of the GPU inflate
 TEST_NO_GROUP = 128      # tile-local parse into per-tile slots + compaction (never group slots)
 TEST_NO_HASH_LEAN = 256  # names that are not decimal ids: the classic hash tiers, never the lean S-first one
+TEST_THROW_AFTER_IDS = 512  # the build throws (G2N_E_DEVICE) once its ids and names are set up: call-state tests
 TEST_FLAGS = 0
 
 

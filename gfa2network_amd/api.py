@@ -210,7 +210,7 @@ def parse_gfa(
         return parse_gfa_sharded(path, directed=directed, weight_tag=weight_tag, strip_orientation=strip_orientation,
                                  verbose=verbose, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
                                  dtype=dt.name, asymmetric=asymmetric, raw_bytes_id=raw_bytes_id,
-                                 return_node_list=return_node_list)
+                                 return_node_list=return_node_list, device=device)
     opts = nat.make_options(
         directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
         asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
@@ -388,7 +388,7 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
                       strip_orientation: bool = False, verbose: bool = False, bidirected: bool = False,
                       keep_directed_bidir: bool = False, dtype="float64", asymmetric: bool = False,
                       raw_bytes_id: bool = False, return_node_list: bool = False, output: str = "parse",
-                      group=None, engine=None, root=None):
+                      group=None, engine=None, root=None, device=None):
     """``parse_gfa(path, build_graph=False, build_matrix=True, ...)`` with the file split over the
     ranks of a torch.distributed group — a collective: every rank calls it with
     the same path.  Each rank preads only its line-aligned byte range (``file_line_ranges``) into
@@ -396,7 +396,8 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     protocol, gfa2network_amd/shard.py) and route triplets to row owners.  The result — what
     parse_gfa returns (the MAX-SYM CSR, or the stream-order COO), or with ``output="csr"`` what
     ``convert_format(parse_gfa(...), "csr")`` returns — is assembled on every rank (``root=None``)
-    or on rank ``root`` only (the other ranks return None).  Index dtypes follow scipy (int64 once
+    or on rank ``root`` only (the other ranks return None; a failed build raises on every rank).
+    ``device``: this rank's GPU (default: torch's current device) — the one ``shard="auto"`` measured.  Index dtypes follow scipy (int64 once
     the entries pass 2^31 - 1).  Exceptions, the one-shot warning and the verbose strings are the
     reference's (builders.py:95-299).  A ``.gz`` file is inflated by every rank (its byte ranges
     are not seekable); one that does not inflate cleanly is built by every rank on its own GPU
@@ -409,6 +410,12 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     if output not in ("parse", "csr"):
         raise ValueError("output must be 'parse' or 'csr'")
     import torch.distributed as dist
+
+    def dev() -> int:  # this rank's GPU, resolved only where a GPU is used (CPU engines have none)
+        if device is not None:
+            return device
+        d = getattr(engine, "device_index", None)
+        return torch.cuda.current_device() if d is None else d
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -425,9 +432,7 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
             opts = nat.make_options(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
                                     asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
                                     weight_tag=weight_tag or None, output=nat.OUT_CSR if output == "csr" else nat.OUT_PARSE,
-                                    want_node_names=bool(return_node_list),
-                                    device=getattr(engine, "device_index", 0) if engine is not None
-                                    else torch.cuda.current_device())
+                                    want_node_names=bool(return_node_list), device=dev())
             raw = _run(p, opts)  # the exact reader raises gzip.py's error after the prefix's lines
             out = finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
                            verbose=verbose, path=path)
@@ -435,12 +440,12 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
         del blob
         from .shard import line_ranges
 
-        eng = engine or HipEngine(torch.cuda.current_device())
+        eng = engine or HipEngine(dev())
         lo, hi = line_ranges(data, world)[rank]
         buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
         del data
     else:
-        eng = engine or HipEngine(torch.cuda.current_device())
+        eng = engine or HipEngine(dev())
         lo, hi = file_line_ranges(p, world)[rank]
         buf = eng.read_range(p, lo, hi - lo)
     res = build_sharded(buf, engine=eng, group=group, directed=directed, bidirected=bidirected,
@@ -471,7 +476,14 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
         if return_node_list:
             raw.names_blob, raw.names_offsets = res.names_blob, res.names_offsets
     elif root is not None and rank != root:
-        return None
+        # a failed build (every rank agrees on its status) raises on every rank, not only on the
+        # root: None means success.  The warnings and verbose strings stay the root's.
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            finalize(raw, dtype=dt, return_node_list=False, raw_bytes_id=raw_bytes_id, verbose=False, path=path)
+        raise AssertionError(f"sharded build status {res.status} did not raise")  # finalize raises on any error
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=verbose,
                     path=path)
 

@@ -65,6 +65,7 @@ constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast p
 constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bases) instead of tile-local
 constexpr uint32_t kTestNoGroup = 128;      // tile-local parse into per-tile slots + compaction, never group slots
 constexpr uint32_t kTestNoHashLean = 256;   // names that are not decimal ids: the classic hash tiers, never the lean one
+constexpr uint32_t kTestThrowAfterIds = 512;  // a build that throws once its ids and names are set up (call-state tests)
 
 
 struct DevBuf {
@@ -163,6 +164,19 @@ static void join_side(g2n_context* c) {
   if (!c->side_pending) return;
   G2N_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
   c->side_pending = false;
+}
+
+// Every entry point starts here: a build that threw may have left a deferred side launch (its
+// buffers are not this call's), an unjoined side stream, or an active group-slot COO behind on
+// this context.  The deferred launch is dropped, the side stream joined (its buffers may be
+// reused by this call), the group slots forgotten.
+static void clear_call_state(g2n_context* c) {
+  c->side_work = nullptr;
+  if (c->side_pending) {
+    G2N_HIP(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+    c->side_pending = false;
+  }
+  c->gcoo = GroupedCoo{};
 }
 
 template <class T>
@@ -999,8 +1013,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
-  c->side_work = nullptr;  // a launch deferred by a build that threw: its buffers are not this build's
-  c->gcoo = GroupedCoo{};
+  clear_call_state(c);
   c->test_flags = (uint32_t)o->reserved[1];
   R->input_bytes = len;
   c->n_ev = 0;
@@ -1207,6 +1220,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");
+  const bool throw_after_ids = (c->test_flags & kTestThrowAfterIds) != 0;
   if (o->want_node_names && hash_done) {  // node k's name: S line k's (noff / nlen from the claims)
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     scan_excl<uint32_t, int64_t>(c, hl_nlen, offs, n_nodes);
@@ -1254,6 +1268,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     R->names_offsets = offs;
     phase(c, "names");
   }
+  if (throw_after_ids) throw Failure(G2N_E_DEVICE, "test: injected failure after the ids");
 
   // ---- triplets (K6): stream-order COO with the dtype cast
   void* data = dbuf(c, S_DATA, n_trip * dtype_size(dt));
@@ -1615,6 +1630,7 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   g2n_context* c = shared_context(device);
   std::lock_guard<std::mutex> lk(c->mu);
   G2N_HIP(hipSetDevice(c->device));
+  clear_call_state(c);
   const size_t w = dtype_size(dtype);
   auto* dr = dget<int32_t>(c, S_ROWS, (uint64_t)nnz);
   auto* dc = dget<int32_t>(c, S_COLS, (uint64_t)nnz);
@@ -1653,6 +1669,7 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
 
 // --------------------------------------------------------- sharded build steps ------
 static void begin_call(g2n_context* c) {
+  clear_call_state(c);
   c->n_ev = 0;
   G2N_HIP(hipEventRecord(c->ev[0], c->stream));
   reset_ctl(c);

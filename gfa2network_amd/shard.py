@@ -72,6 +72,7 @@ class LocalShard:
     names_blob: object = None  # torch uint8
     names_offsets: object = None  # torch int64, n_local_nodes + 1
     n_cast_overflow: int = 0
+    parse_path: str = ""  # build_decimal: "tile_local" (the one-pass lean parse) or "k1" (tile counts first)
 
 
 @dataclass
@@ -102,6 +103,7 @@ class ShardResult:
     n_cast_overflow: int = 0
     timings_ms: dict = field(default_factory=dict)
     fast_path: bool = False  # the decimal-id fast path built it
+    parse_path: str = ""  # fast path: how this rank's range was parsed ("tile_local" or "k1")
     coo: tuple | None = None  # keep_coo: this range's stream-order triplets over global ids
 
     @property
@@ -337,6 +339,7 @@ class HipEngine:
             sh.rows = self._copy_out(res.rows, n, torch.int32)
             sh.cols = self._copy_out(res.cols, n, torch.int32)
             sh.data = self._copy_out(res.data, n, tdt)
+        sh.parse_path = "k1" if any(res.phase_names[k] == b"tiles" for k in range(res.n_phases)) else "tile_local"
         return sh
 
     def partition_keys(self, blob, offsets, n_ranks: int):
@@ -647,6 +650,7 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
         out.names_blob, out.names_offsets = nat.decimal_names(n_global, bool(opts.get("bidirected")))
     out.timings_ms = tm
     out.fast_path = True
+    out.parse_path = getattr(local, "parse_path", "")
     if keep_coo:
         out.coo = (local.rows, local.cols, local.data)
     return out
@@ -806,8 +810,14 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
             b_all = np.concatenate([x.cpu().numpy() for _, x in p_blob])
             o_all = np.zeros(len(l_all) + 1, dtype=np.int64)
             np.cumsum(l_all, out=o_all[1:])
-            order = np.empty(n_global, dtype=np.int64)
-            order[g_all] = np.arange(n_global, dtype=np.int64)  # the key holding global id i
+            # the key holding global id i; every id must be covered exactly once, or the protocol
+            # is broken — raise here rather than hand g2n_gather_names an unchecked index
+            if len(g_all) != n_global or (n_global and (g_all.min() < 0 or g_all.max() >= n_global)):
+                raise RuntimeError(f"sharded names: {len(g_all)} ids gathered for {n_global} nodes")
+            order = np.full(n_global, -1, dtype=np.int64)
+            order[g_all] = np.arange(n_global, dtype=np.int64)
+            if n_global and order.min() < 0:
+                raise RuntimeError("sharded names: a global id was not gathered")
             out.names_blob, out.names_offsets = nat.gather_names(b_all, o_all, order)
         tm["names"] = (time.perf_counter() - t5) * 1e3
 

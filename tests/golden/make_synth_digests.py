@@ -11,7 +11,7 @@ digest = sha256(int32 indptr | int32 indices | data bytes) for a CSR answer,
          names blob (id order) — what parse_gfa(..., return_node_list=True) and
          convert_format(A, "csr") return (builders.py:278-299, utils.py:40-63).
 
-usage: python tests/golden/make_synth_digests.py C3 C4
+usage: python tests/golden/make_synth_digests.py C2 C3 C4
 """
 import hashlib
 import json
@@ -26,6 +26,7 @@ sys.path.insert(0, str(ROOT))
 OUT = ROOT / "tests" / "golden" / "expected" / "synth_digests.json"
 
 CASES = {  # name -> (n_segments, n_links, rc_tag, seed, mode)
+    "C2": (1_000_000, 4_000_000, False, 0, {"directed": False}),
     "C3": (1_000_000, 4_000_000, True, 0, {"bidirected": True, "weight_tag": "RC"}),
     "C4": (50_000_000, 200_000_000, False, 0, {}),
 }

@@ -525,3 +525,30 @@ def test_csr_output_equals_oracle(gpu, oracle_lib, case):
                         and raw.data.tobytes() == R.data.tobytes()):
                     bad.append((mode, dtype, wt))
     assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"bidirected": True}])
+def test_failed_build_leaves_no_call_state(gpu, oracle_lib, mode):
+    """A build that throws after its parse and ids (TEST_THROW_AFTER_IDS: the group-slot COO active, the
+    names launch deferred to the side stream) must leave nothing behind on the device's shared context:
+    the next convert_format and the next build on it equal the oracle."""
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(20_000, 80_000, seed=5)
+    with pytest.raises(RuntimeError, match="injected"):
+        nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, want_node_names=True,
+                                                     test_flags=nat.TEST_THROW_AFTER_IDS, **mode))
+    o = oracle_lib.run(data, **mode)
+    R = oracle_lib.to_raw(o, "csr")
+    got = nat.coo_to_csr(o.rows, o.cols, o.data, int(o.n_nodes), int(o.n_nodes))
+    assert got.indptr.tobytes() == R.indptr.tobytes() and got.indices.tobytes() == R.indices.tobytes()
+    assert got.data.tobytes() == R.data.tobytes()
+    with pytest.raises(RuntimeError, match="injected"):
+        nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, want_node_names=True,
+                                                     test_flags=nat.TEST_THROW_AFTER_IDS, **mode))
+    raw = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, want_node_names=True, **mode))
+    assert raw.status == 0
+    assert raw.indptr.tobytes() == R.indptr.tobytes() and raw.indices.tobytes() == R.indices.tobytes()
+    assert raw.data.tobytes() == R.data.tobytes()
+    assert raw.names_blob.tobytes() == o.names_blob.tobytes()

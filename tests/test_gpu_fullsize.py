@@ -46,14 +46,14 @@ def _down(hip, ptr, n, dtype):
     return out
 
 
-def _device_build(n_s, n_l, **opts):
+def _device_build(n_s, n_l, names="decimal", **opts):
     """g2n_build_device on generator bytes in HBM; the result's arrays downloaded."""
     from gfa2network_amd import _native as nat
     from gfa2network_amd import synth
 
     lib = nat.load()
     hip = _hip()
-    dev = synth.DeviceInput(n_s, n_l, seed=0)
+    dev = synth.DeviceInput(n_s, n_l, seed=0, names=names)
     ctx = lib.g2n_context_create(0)
     try:
         o = nat.make_options(**opts)
@@ -98,6 +98,35 @@ def test_c3_full_size_equals_oracle(gpu):
     # the same CSR straight from the build (G2N_OUT_CSR)
     raw = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, bidirected=True, weight_tag="RC"))
     assert raw.status == 0 and _digest(raw.indptr, raw.indices, raw.data) == d["csr"]["digest"]
+
+
+def test_c2_full_size_equals_oracle(gpu):
+    """C2 (1M S / 4M L, ``directed=False``) as configured: the stream-order COO parse_gfa returns and
+    its ``convert_format(A, "csr")`` (utils.py:55 ``coo.tocsr``: the SUM CSR whose partition pairs
+    adjacent mutually transposed entries, g2n_sym.hip pass 4), through parse_gfa + convert_format,
+    through G2N_OUT_CSR from a host buffer, and device-resident (g2n_build_device, the bench's
+    C2 leg) on the decimal and the hash dictionary tiers."""
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import convert_format, parse_gfa, synth
+
+    d = DIGESTS["C2"]
+    data = synth.host_bytes(d["n_segments"], d["n_links"], seed=d["seed"], rc_tag=d["rc_tag"])
+    assert len(data) == d["input_bytes"]
+    A, nodes = parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, return_node_list=True,
+                         **d["mode"])
+    assert A.format == d["parse"]["format"] == "coo" and A.shape == (d["n_nodes"], d["n_nodes"])
+    assert _digest(A.row.astype(np.int32), A.col.astype(np.int32), A.data) == d["parse"]["digest"]
+    assert hashlib.sha256("".join(nodes).encode()).hexdigest() == d["names"]
+    C = convert_format(A, "csr")
+    assert C.nnz == d["csr"]["nnz"]
+    assert _digest(C.indptr, C.indices, C.data) == d["csr"]["digest"]
+    raw = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, directed=False))
+    assert raw.status == 0 and _digest(raw.indptr, raw.indices, raw.data) == d["csr"]["digest"]
+    for flags in (0, nat.TEST_DICT_HASH):
+        out = _device_build(d["n_segments"], d["n_links"], output=nat.OUT_CSR, directed=False, test_flags=flags)
+        assert out["format"] == nat.FMT_CSR and out["n"] == d["n_nodes"] and out["nnz"] == d["csr"]["nnz"]
+        assert _digest(out["indptr"], out["indices"], out["data"]) == d["csr"]["digest"], flags
+        assert hashlib.sha256(out["blob"].tobytes()).hexdigest() == d["names"], flags
 
 
 @pytest.mark.parametrize("flags", ["decimal", "hash"])

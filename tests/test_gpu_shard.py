@@ -241,3 +241,92 @@ def test_gpu_sharded_gzip_clean_and_corrupt(gpu, tmp_path):
     mp.spawn(_gz_worker, args=(2, _free_port(), paths, str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def _range_cases(world):
+    """Decimal-id inputs whose S section spans more than one byte range (S lines before a range,
+    S lines inside a later range), each range many 32 KiB tiles, and premise breaks that only the
+    range offset (s_base) or the whole file's S count (N) can see: the sharded tile-local lean parse
+    (k_tile_lean + k_tile_lean_check with s_base / n_seg_all) must take exactly the canonical ones."""
+    from gfa2network_amd.shard import line_ranges
+
+    r = random.Random(21)
+    n_s, n_l = 60_000, 100_000
+    S = [f"S\t{k}\t{'ACGT' * r.randint(5, 15)}\n" for k in range(1, n_s + 1)]
+    L = [f"L\t{r.randint(1, n_s)}\t{r.choice('+-')}\t{r.randint(1, n_s)}\t{r.choice('+-')}\t0M\n" for _ in range(n_l)]
+    base = "".join(S + L).encode()
+    lo1, hi1 = line_ranges(base, world)[1]
+    # S lines whose bytes start inside range 1
+    pos, in_r1 = 0, []
+    for i, x in enumerate(S):
+        if lo1 <= pos < hi1:
+            in_r1.append(i)
+        pos += len(x)
+    assert in_r1 and in_r1[0] > 0, "range 1 must start inside the S section"
+    shifted = list(S)
+    for i in in_r1:  # range 1's S names all one too high: consistent inside the range, wrong for its s_base
+        shifted[i] = f"S\t{i + 2}\t{S[i].split(chr(9))[2]}"
+    assert sum(map(len, shifted)) == sum(map(len, S))
+    renamed = list(S)
+    renamed[in_r1[len(in_r1) // 2]] = f"S\t{in_r1[len(in_r1) // 2] + 1}x\t*\n"
+    half = len(L) // 10
+    return {  # name -> (bytes, fast path expected)
+        "canonical": (base, True),
+        "edge_names_n_last_range": (base + f"L\t{n_s}\t+\t1\t-\t0M\n".encode(), True),
+        "s_names_off_by_range_base": ("".join(shifted + L).encode(), False),
+        "s_renamed_in_range1": ("".join(renamed + L).encode(), False),
+        "edge_beyond_n_last_range": (base + f"L\t{n_s + 1}\t+\t1\t-\t0M\n".encode(), False),
+        "s_after_edges": ("".join(S[:n_s // 2] + L[:half] + S[n_s // 2:] + L[half:]).encode(), False),
+    }
+
+
+def _range_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        from gfa2network_amd.shard import HipEngine, build_sharded, gather_csr, line_ranges
+        from oracle import oracle as orc
+
+        eng = HipEngine(0)
+        for name, (data, fast) in _range_cases(world).items():
+            lo, hi = line_ranges(data, world)[rank]
+            assert hi - lo > 8 * 32768, (name, rank, hi - lo)
+            buf = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy()).to(eng.device)
+            for mode in ({}, {"directed": False}, {"dtype": "int8"}):
+                res = build_sharded(buf, engine=eng, gather_names=rank == 0, names_root=0, **mode)
+                assert res.status == 0, (name, mode, res.status)
+                assert res.fast_path == fast, (name, mode, rank)
+                if fast:  # the one-pass lean parse, not K1 + the tile parse
+                    assert res.parse_path == "tile_local", (name, mode, rank, res.parse_path)
+                indptr, indices, vals = gather_csr(res)
+                if rank != 0:
+                    continue
+                full = orc.run(data, **mode)
+                want = [bytes(full.names_blob[full.names_offsets[i]:full.names_offsets[i + 1]])
+                        for i in range(full.n_nodes)]
+                assert res.names == want, (name, mode)
+                wp, wi, wd = ((full.ms_indptr, full.ms_indices, full.ms_data) if full.maxsym
+                              else (full.sum_indptr, full.sum_indices, full.sum_data))
+                assert np.array_equal(indptr, wp) and np.array_equal(indices, wi), (name, mode)
+                assert vals.tobytes() == np.ascontiguousarray(wd).tobytes(), (name, mode)
+        eng.close()
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_tile_local_range_premise(gpu, oracle_lib, tmp_path, world):
+    """Sharded decimal-id ranges take the tile-local lean parse; premise breaks visible only through
+    the range's S offset or the file's S count fall back to the general protocol.  Always the oracle's
+    single-file answer."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_range_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()

@@ -243,6 +243,27 @@ def _root_worker(rank, world, port, path, mode, root, outdir):
 
         data = open(path, "rb").read()
         full = orc.run(data, **mode)
+        if full.status:  # a failed build raises on EVERY rank (None would read as success)
+            import warnings
+
+            try:
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore")
+                    finalize(orc.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                             return_node_list=False, raw_bytes_id=False, verbose=False)
+            except Exception as e:  # noqa: BLE001 - the reference's exception, whatever it is
+                want = (type(e), str(e))
+            for output in ("parse", "csr"):
+                try:
+                    with warnings.catch_warnings():
+                        warnings.simplefilter("ignore")
+                        parse_gfa_sharded(path, engine=CpuEngine(orc), output=output, root=root, **mode)
+                except Exception as e:  # noqa: BLE001
+                    assert (type(e), str(e)) == want, (rank, e, want)
+                else:
+                    raise AssertionError(f"rank {rank}: no exception")
+            np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+            return
         for output in ("parse", "csr"):
             got = parse_gfa_sharded(path, engine=CpuEngine(orc), return_node_list=output == "parse", output=output,
                                     root=root, **mode)
@@ -267,7 +288,7 @@ def _root_worker(rank, world, port, path, mode, root, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,root", [("shuffled", 1), ("decimal", 2), ("undirected", 0)])
+@pytest.mark.parametrize("name,root", [("shuffled", 1), ("decimal", 2), ("undirected", 0), ("error", 1)])
 def test_parse_gfa_sharded_to_root_only(oracle_lib, tmp_path, name, root):
     import torch.multiprocessing as mp
 
