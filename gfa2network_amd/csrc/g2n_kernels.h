@@ -79,6 +79,8 @@ struct Ctl {
   unsigned long long int_fail;        // the decimal-id dictionary (k_int_ids) does not apply
   unsigned long long bucket_overflow; // k_sym_finish met a bucket over its LDS capacity
   unsigned long long bad_id;          // k_remap_pairs met an id outside its map
+  unsigned long long ev_dmin, ev_dmax;  // k_tile_lean_evidence: a range's S-name offsets (+ 2^62)
+  unsigned long long ev_vmax;           //   and its largest edge key
 };
 
 struct ParseOpts {

@@ -1329,6 +1329,43 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restr
   if (bad) ctl->int_fail = 1;
 }
 
+// The same evidence for one byte range of a sharded file whose S lines before the range are not
+// known yet (g2n_build_decimal_range): each S tile's offset d = dmin - (S lines before it in the
+// range) must be one value for the whole range (the caller checks d == the S lines before the range
+// once the ranges' counts are exchanged); no edge may precede an S line inside the range; the
+// range's largest edge key goes to the caller too (checked against the file's S count).  d is
+// biased by 2^62 for the unsigned atomics.
+__global__ void __launch_bounds__(kTPB) k_tile_lean_evidence(const TileCnt* __restrict__ cnt,
+                                                             const TileCnt* __restrict__ tbase,
+                                                             const TileLean* __restrict__ tlean, uint64_t n_tiles,
+                                                             Ctl* ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  unsigned long long vm = 0, dmn = ~0ull, dmx = 0;
+  bool bad = false;
+  if (t < n_tiles) {
+    const TileLean e = tlean[t];
+    vm = e.vmax;
+    if (cnt[t].segs) {
+      bad = tbase[t].edges != 0 || e.dmin != e.dmax;
+      dmn = dmx = (unsigned long long)(e.dmin - (long long)tbase[t].segs + (1ll << 62));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    vm = max(vm, (unsigned long long)__shfl_xor(vm, o, 64));
+    dmn = min(dmn, (unsigned long long)__shfl_xor(dmn, o, 64));
+    dmx = max(dmx, (unsigned long long)__shfl_xor(dmx, o, 64));
+  }
+  const bool any_bad = __ballot(bad) != 0;
+  if ((threadIdx.x & 63) == 0) {
+    if (any_bad) ctl->int_fail = 1;
+    if (vm) atomicMax(&ctl->ev_vmax, vm);
+    if (dmn != ~0ull) {
+      atomicMin(&ctl->ev_dmin, dmn);
+      atomicMax(&ctl->ev_dmax, dmx);
+    }
+  }
+}
+
 // Tile-local lean parse, last: each tile's COO slot to its stream-order place.
 __global__ void __launch_bounds__(kTPB) k_tile_compact(const int32_t* __restrict__ rows_p,
                                                        const int32_t* __restrict__ cols_p, uint32_t pad,

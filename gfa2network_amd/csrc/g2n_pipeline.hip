@@ -98,6 +98,10 @@ struct g2n_context {
   hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
   hipEvent_t side_ev[2] = {nullptr, nullptr};  // main -> side fork, side -> main join
   bool side_pending = false;    // the main stream has not joined the side stream's last work yet
+  bool range_has_s = false;     // g2n_build_decimal_range: the range's evidence (k_tile_lean_evidence)
+  int64_t range_d = -1;
+  uint64_t range_vmax = 0;
+  uint64_t range_nseg = 0;
   std::function<void()> side_work;  // launches deferred to the assembly's latency-bound finish (F1)
   std::vector<g2n::DevBuf> bufs;
   g2n::Ctl* ctl = nullptr;    // device
@@ -649,6 +653,7 @@ static void reset_ctl(g2n_context* c) {
   c->h_ctl->err_key = ~0ull;
   c->h_ctl->warn_line = ~0ull;
   c->h_ctl->cast_key = ~0ull;
+  c->h_ctl->ev_dmin = ~0ull;
   G2N_HIP(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
 }
 
@@ -854,7 +859,7 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 // the S lines before the range and in the whole file; 0 / 0 for a whole file.
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
-                             uint64_t n_seg_all = 0) {
+                             uint64_t n_seg_all = 0, bool deferred = false) {
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
 #endif
@@ -917,11 +922,23 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
     const TileCnt tot = read_dev(c, part + n_parts);
-    hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
-                       (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles,
-                       n_seg_all ? n_seg_all : (uint64_t)tot.segs, s_base, c->ctl);
+    if (deferred)  // the range's offset evidence, checked by the caller across ranges
+      hipLaunchKernelGGL(k_tile_lean_evidence, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream,
+                         (const TileCnt*)tcnt, (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, c->ctl);
+    else
+      hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
+                         (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles,
+                         n_seg_all ? n_seg_all : (uint64_t)tot.segs, s_base, c->ctl);
     sync_ctl(c);
     ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0x7FFFFFFFull;
+    if (deferred) {
+      const Ctl& h = *c->h_ctl;
+      ok = ok && (h.ev_dmin == ~0ull || h.ev_dmin == h.ev_dmax);
+      c->range_has_s = h.ev_dmin != ~0ull;
+      c->range_d = c->range_has_s ? (int64_t)(h.ev_dmin - (1ull << 62)) : -1;
+      c->range_vmax = h.ev_vmax;
+      c->range_nseg = tot.segs;
+    }
     if (ok && grouped) {
       c->gcoo.active = true;
       c->gcoo.rows = rows_p;
@@ -1033,7 +1050,15 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto* tbase = dget<TileCnt>(c, S_TILE_BASE, n_tiles + 1);
   TileCnt tot{};
   const bool shard_dec = (o->reserved[4] & 1) != 0;
-  const bool first_one = !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
+  // g2n_build_decimal_range: the S lines before the range are not known yet — the one-pass parse
+  // reports the range's offset evidence instead of checking it (the caller checks across ranges)
+  const bool shard_deferred = shard_dec && (o->reserved[4] & 2) != 0;
+  c->range_has_s = false;
+  c->range_d = -1;
+  c->range_vmax = 0;
+  c->range_nseg = 0;
+  const bool first_one =
+      !shard_dec && !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
   // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
   // group slots when the COO's only reader is the unweighted bucket partition (a CSR output)
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
@@ -1041,11 +1066,14 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
                        !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
   // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
   const bool local_done =
-      n_tiles && (first_one || (shard_dec && o->reserved[2] >= 0 && o->reserved[3] > 0)) && !bidir &&
-      !(o->weight_tag && *o->weight_tag) && !o->strip_orientation &&
+      n_tiles && (first_one || (shard_dec && (shard_deferred || (o->reserved[2] >= 0 && o->reserved[3] > 0)))) &&
+      !bidir && !(o->weight_tag && *o->weight_tag) && !o->strip_orientation &&
       !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
       tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped,
-                       shard_dec ? (uint64_t)o->reserved[2] : 0, shard_dec ? (uint64_t)o->reserved[3] : 0);
+                       shard_dec ? (uint64_t)o->reserved[2] : 0, shard_dec ? (uint64_t)o->reserved[3] : 0,
+                       shard_deferred);
+  if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
+    throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
   // ---- K1: per-tile counts -> tile bases
   if (n_tiles && !local_done) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
@@ -1885,6 +1913,33 @@ int g2n_build_device(g2n_context* ctx, const void* d_input, size_t len, const g2
     out->status = G2N_E_DEVICE;
     return G2N_E_DEVICE;
   }
+}
+
+int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, const g2n_options* opts,
+                            int64_t* ev6, g2n_result* out) {
+  if (!ctx || !opts || !out || !ev6 || (len && !d_input)) {
+    g2n::set_last_error("g2n_build_decimal_range: null argument");
+    return G2N_E_ARG;
+  }
+  if (opts->output != G2N_OUT_COO || opts->want_node_names || opts->bidirected || opts->strip_orientation ||
+      (opts->weight_tag && *opts->weight_tag)) {
+    g2n::set_last_error("g2n_build_decimal_range: COO output, no names, not bidirected, no weights, no strip");
+    return G2N_E_ARG;
+  }
+  g2n_options o = *opts;
+  o.reserved[2] = 0;
+  o.reserved[3] = 0;
+  o.reserved[4] = 3;  // sharded decimal ids, offset evidence instead of the check
+  const int rc = g2n_build_device(ctx, d_input, len, &o, out);
+  if (rc == G2N_OK) {
+    ev6[0] = out->n_lines;
+    ev6[1] = (int64_t)ctx->range_nseg;
+    ev6[2] = out->n_edges;
+    ev6[3] = out->n_records;
+    ev6[4] = ctx->range_d;
+    ev6[5] = (int64_t)ctx->range_vmax;
+  }
+  return rc;
 }
 
 int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows,

@@ -326,6 +326,28 @@ class HipEngine:
             if rc not in (nat.E_UNSUPPORTED,) and not (1 <= rc <= 12):
                 self._check(rc, "g2n_build_device")
             return None
+        return self._decimal_shard(res, opts, view)
+
+    def build_decimal_range(self, buf, opts: dict, view: bool = False):
+        """The range parsed into GLOBAL decimal ids before the ranges' counts are known (one pass, no
+        count: g2n_build_decimal_range): (LocalShard, evidence [lines, S lines, edges, records, d,
+        largest edge key]) — the caller checks d against the S lines before the range and the key
+        against the file's S count — or None when the one pass declines (count + build_decimal then)."""
+        o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
+        res = nat.Result()
+        ev = (ctypes.c_int64 * 6)()
+        self._build_ctx()
+        self._sync()
+        rc = self.lib.g2n_build_decimal_range(self.ctx_b, buf.data_ptr() if buf.numel() else None, buf.numel(),
+                                              ctypes.byref(o), ev, ctypes.byref(res))
+        if rc != 0:
+            if rc not in (nat.E_UNSUPPORTED,) and not (1 <= rc <= 12):
+                self._check(rc, "g2n_build_decimal_range")
+            return None
+        return self._decimal_shard(res, opts, view), [int(v) for v in ev]
+
+    def _decimal_shard(self, res, opts: dict, view: bool) -> LocalShard:
+        torch = self.torch
         n = res.nnz
         sh = LocalShard(status=0, err_line=-1, err_index=-1, err_value=0.0, err_detail=b"", warn_line=-1,
                         has_warning=False, warn_byte=0, n_lines=res.n_lines, n_records=res.n_records,
@@ -616,25 +638,51 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
 
     world, rank = C.world, C.rank
     t0 = time.perf_counter()
-    cnt = engine.count(buf)  # [lines, S lines, edges, records]
-    allc = C.allgather_list(cnt)
-    seen_edge, ok = False, True
-    for k in range(world):  # no edge line may precede an S line (ids = S order)
-        if allc[k][1] and seen_edge:
-            ok = False
-        seen_edge = seen_edge or allc[k][2] > 0
-    n_seg = int(sum(c[1] for c in allc))
     tps = 2 if opts.get("bidirected") else 1
-    if not ok or n_seg == 0 or n_seg * tps >= 2**31 - 1:
-        return None
-    s_base = int(sum(allc[k][1] for k in range(rank)))
-    tm["count"] = (time.perf_counter() - t0) * 1e3
-    local = engine.build_decimal(buf, opts, s_base, n_seg, view=not keep_coo)
-    # every range's ids are global decimals (the id map needs no exchange) — or nobody's are
-    verdict = torch.tensor([0 if local is None else 1], dtype=torch.int64, device=engine.device)
-    if int(C.allreduce_min(verdict).item()) == 0:
-        return None
-    tm["build"] = (time.perf_counter() - t0) * 1e3 - tm["count"]
+
+    def premise(allc):  # no edge line may precede an S line (ids = S order); the file's S count
+        seen_edge, ok = False, True
+        for k in range(world):
+            if allc[k][1] and seen_edge:
+                ok = False
+            seen_edge = seen_edge or allc[k][2] > 0
+        n = int(sum(c[1] for c in allc))
+        return ok and 0 < n and n * tps < 2**31 - 1, n
+
+    local, allc = None, None
+    if (hasattr(engine, "build_decimal_range") and not opts.get("bidirected") and not opts.get("weight_tag")
+            and not opts.get("strip_orientation")):
+        # one pass, no count: every range parses into global ids first and reports its evidence; one
+        # all-gather decides for every rank at once (g2n_build_decimal_range)
+        got = engine.build_decimal_range(buf, opts, view=not keep_coo)
+        alle = C.allgather_list(got[1] if got is not None else [-1] * 6)
+        tm["count"] = 0.0
+        if all(e[0] >= 0 for e in alle):
+            allc = [e[:4] for e in alle]
+            ok, n_seg = premise(allc)
+            s_bases = np.cumsum([0] + [c[1] for c in allc])
+            ok = ok and all(e[1] == 0 or e[4] == s_bases[k] for k, e in enumerate(alle)) and \
+                max(e[5] for e in alle) <= n_seg
+            if not ok:
+                return None
+            local = got[0]
+            tm["build"] = (time.perf_counter() - t0) * 1e3
+        # else some range declined the one pass: count and build with the range offsets known
+    if local is None:
+        t0 = time.perf_counter()
+        cnt = engine.count(buf)  # [lines, S lines, edges, records]
+        allc = C.allgather_list(cnt)
+        ok, n_seg = premise(allc)
+        if not ok:
+            return None
+        s_base = int(sum(allc[k][1] for k in range(rank)))
+        tm["count"] = (time.perf_counter() - t0) * 1e3
+        local = engine.build_decimal(buf, opts, s_base, n_seg, view=not keep_coo)
+        # every range's ids are global decimals (the id map needs no exchange) — or nobody's are
+        verdict = torch.tensor([0 if local is None else 1], dtype=torch.int64, device=engine.device)
+        if int(C.allreduce_min(verdict).item()) == 0:
+            return None
+        tm["build"] = (time.perf_counter() - t0) * 1e3 - tm["count"]
     n_global = n_seg * tps
     local.dtype_name = opts.get("dtype", "float64")
     a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"), tm)

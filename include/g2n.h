@@ -322,6 +322,23 @@ int g2n_upload_file_range(const char *path, uint64_t offset, uint64_t len, void 
  * build exchange first): out4 = {lines, S lines, edge records (L/E/C), records (S/L/E/C/P/O)}. */
 int g2n_count_device(g2n_context *ctx, const void *d_input, size_t len, int64_t *out4);
 
+/* One byte range of a sharded decimal-id build (S lines named "1".."N" in order), built BEFORE the
+ * ranges' record counts are exchanged: one pass of the tile-local lean parse writes the range's
+ * stream-order COO over GLOBAL ids (name value - 1; builders.py:190-198 first-touch order when the
+ * premise holds) and reports the evidence the caller checks across ranges (shard.py):
+ *   ev6 = {lines, S lines, edge records, records,
+ *          d: the range's first S line names d + 1 and every later one continues it (-1: no S line;
+ *             the premise needs d == the S lines of the ranges before),
+ *          the largest edge key value (the premise needs it <= the file's S lines)}.
+ * Options: output G2N_OUT_COO, no names, not bidirected, no weight tag, no strip (else G2N_E_ARG);
+ * reserved[2..4] are set by the call.  G2N_E_UNSUPPORTED when the one pass declines (a line past
+ * its tile window, a record outside the lean shapes, S names that are not one decimal run, an S
+ * line after an edge line in the range): the caller then counts the ranges (g2n_count_device) and
+ * builds with reserved[2..4] (g2n_build_device), whose check decides.  Replaces the count pass of
+ * the sharded build for the common layout; results as g2n_build_device's (device pointers). */
+int g2n_build_decimal_range(g2n_context *ctx, const void *d_input, size_t len, const g2n_options *opts,
+                            int64_t *ev6, g2n_result *out);
+
 #ifdef __cplusplus
 }
 #endif

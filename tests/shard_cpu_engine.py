@@ -94,6 +94,43 @@ class CpuEngine:
         sh.n_local_nodes = n_seg * (2 if bidir else 1)
         return sh
 
+    def build_decimal_range(self, buf, opts, view=False):
+        """g2n_build_decimal_range's contract on the oracle: the range's COO over global decimal ids
+        and its evidence [lines, S lines, edges, records, d, largest edge key], or None when the one
+        pass would decline (not one run of canonical decimal S names, an S line after an edge line,
+        an edge key that is no canonical decimal, an error or warning in the range)."""
+        b = bytes(buf.numpy())
+        o = self.oracle.run(b, **opts)
+        if o.status != 0 or o.has_warning:
+            return None
+        recs = [ln.split(b"\t") for ln in b.split(b"\n") if ln[:2] in (b"S\t", b"L\t", b"E\t", b"C\t")]
+        canon = lambda k: k.isdigit() and k[:1] != b"0"  # noqa: E731 - str(v) is v's only spelling
+        s_names, seen_edge, vmax = [], False, 0
+        for f in recs:
+            if f[0] == b"S":
+                if seen_edge or len(f) < 2 or not canon(f[1]):
+                    return None
+                s_names.append(int(f[1]))
+            else:
+                seen_edge = True
+        d = s_names[0] - 1 if s_names else -1
+        if s_names != list(range(d + 1, d + 1 + len(s_names))):
+            return None
+        blob, off = o.names_blob.tobytes(), o.names_offsets
+        gid = np.empty(o.n_nodes, dtype=np.int64)
+        for i in range(o.n_nodes):
+            k = blob[off[i]:off[i + 1]]
+            if not canon(k) or int(k) > 2**31 - 2:
+                return None
+            gid[i] = int(k) - 1
+        sh = self.local_build(buf, opts)
+        if sh.rows.numel():
+            vmax = int(max(gid[sh.rows.numpy()].max(), gid[sh.cols.numpy()].max())) + 1
+        sh.rows = torch.from_numpy(gid[sh.rows.numpy()].astype(np.int32))
+        sh.cols = torch.from_numpy(gid[sh.cols.numpy()].astype(np.int32))
+        c = self.count(buf)
+        return sh, [c[0], c[1], c[2], c[3], d, vmax]
+
     def partition_keys(self, blob, offsets, n_ranks):
         b, off = blob.numpy().tobytes(), offsets.numpy()
         n = len(off) - 1
