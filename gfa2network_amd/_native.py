@@ -52,6 +52,7 @@ TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of
 TEST_NO_GROUP = 128      # tile-local parse into per-tile slots + compaction (never group slots)
 TEST_NO_HASH_LEAN = 256  # names that are not decimal ids: the classic hash tiers, never the lean S-first one
 TEST_THROW_AFTER_IDS = 512  # the build throws (G2N_E_DEVICE) once its ids and names are set up: call-state tests
+TEST_INDEX64 = 1024      # unweighted CSR results in int64 indptr / indices (the > 2^31 - 1 entries path)
 TEST_FLAGS = 0
 
 

@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_NSLOTS
 };
 
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
@@ -66,6 +66,7 @@ constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bas
 constexpr uint32_t kTestNoGroup = 128;      // tile-local parse into per-tile slots + compaction, never group slots
 constexpr uint32_t kTestNoHashLean = 256;   // names that are not decimal ids: the classic hash tiers, never the lean one
 constexpr uint32_t kTestThrowAfterIds = 512;  // a build that throws once its ids and names are set up (call-state tests)
+constexpr uint32_t kTestIndex64 = 1024;     // CSR results with int64 indptr / indices (the > 2^31 - 1 entries path)
 
 
 struct DevBuf {
@@ -490,13 +491,37 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     }
   }
 #endif
-  auto* boff = dget<uint32_t>(c, S_MOFF, n_bk);
-  scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk);
+  auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
+  scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk, boff + n_bk);
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
-  hipLaunchKernelGGL((k_sym_place<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, (const uint32_t*)bst,
-                     (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1, (const uint32_t*)tcol,
-                     (const uint16_t*)tcn, indptr, indices, odata);
+  // scipy's index dtype (get_index_dtype(maxval=nnz)): int64 indptr / indices once the result holds
+  // more than 2^31 - 1 entries (utils.py:55 coo.tocsr, builders.py:283 maximum) — only possible when
+  // the partition's upper bound passes it, so the total is read only then
+  // (a bucket's merged entries never outnumber its expanded input: the result holds <= n_el entries)
+  const bool wide = (c->test_flags & kTestIndex64) ||
+                    (n_el > 0x7FFFFFFFull && (uint64_t)read_dev(c, boff + n_bk) > 0x7FFFFFFFull);
+  if (wide) {
+    if (pair) throw Failure(G2N_E_UNSUPPORTED, "a sharded row slice of more than 2^31-1 entries");
+    auto* indptr64 = dget<int64_t>(c, S_INDPTR64, n_rows + 1);
+    auto* indices64 = dget<int64_t>(c, S_INDICES64, n_el);
+    hipLaunchKernelGGL((k_sym_place<T, int64_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
+                       (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
+                       (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices64, odata, indptr64);
+    R->format = G2N_FMT_CSR;
+    R->index_width = 8;
+    R->indptr = indptr64;
+    R->nnz = read_dev(c, indptr64 + n_rows);
+    R->indices = indices64;
+    R->data = odata;
+    R->sum_sorted = -1;
+    R->sum_t_sorted = -1;
+    phase(c, sum ? "csr" : "maxsym");
+    return true;
+  }
+  hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
+                     (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
+                     (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr);
 #endif
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
@@ -521,6 +546,8 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
     c->gcoo.failed = true;
     return;
   }
+  // the row-sum path (weighted / float sums, or a partition that declined) keeps int32 positions
+  if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 weighted matrix entries");
   const T one = (T)1;
   RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0);
   R->sum_sorted = A.unsorted ? 0 : 1;
@@ -930,7 +957,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                          (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles,
                          n_seg_all ? n_seg_all : (uint64_t)tot.segs, s_base, c->ctl);
     sync_ctl(c);
-    ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0x7FFFFFFFull;
+    ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0xFFFFFFFFull;
     if (deferred) {
       const Ctl& h = *c->h_ctl;
       ok = ok && (h.ev_dmin == ~0ull || h.ev_dmin == h.ev_dmax);
@@ -1117,7 +1144,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
   const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
   const uint64_t n_trip = n_e * (uint64_t)ktrip;
-  if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 matrix entries");
+  // the stream-order COO holds int32 node ids (< 2^31 - 1, checked below) at 64-bit positions; the
+  // partition counts its elements in 32 bits (more than 2^31 - 1 entries: int64 CSR indices, F2)
+  if (n_trip >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 matrix entries");
   auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
   auto* cols = dget<int32_t>(c, S_COLS, n_trip);
   // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
@@ -1553,8 +1582,9 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
       R.rows = download(c, H->rows, D.rows, (size_t)D.nnz * 4);
       R.cols = download(c, H->cols, D.cols, (size_t)D.nnz * 4);
     } else {
-      R.indptr = download(c, H->indptr, D.indptr, (size_t)(D.n_nodes + 1) * 4);
-      R.indices = download(c, H->indices, D.indices, (size_t)D.nnz * 4);
+      const size_t iw = D.index_width == 8 ? 8 : 4;
+      R.indptr = download(c, H->indptr, D.indptr, (size_t)(D.n_nodes + 1) * iw);
+      R.indices = download(c, H->indices, D.indices, (size_t)D.nnz * iw);
     }
     if (D.format != G2N_FMT_TEXT) R.data = download(c, H->data, D.data, (size_t)D.nnz * w);
   }

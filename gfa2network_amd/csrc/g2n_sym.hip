@@ -853,12 +853,15 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
 }
 
 // F2: bucket b's staged entries to their CSR place (boff = exclusive scan of btot), indptr rebased.
-template <class T>
+// I = int64_t: scipy's int64 index arrays (more than 2^31 - 1 entries): indices widened, and indptr64
+// = base + F1's local offsets (indptr holds those; every offset stays below 2^32 — elements < 2^32).
+template <class T, class I>
 __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ btot,
                                                     const uint32_t* __restrict__ boff, uint32_t low, uint64_t n_rows,
                                                     T one, const uint32_t* __restrict__ tcol,
                                                     const uint16_t* __restrict__ tcn, int32_t* __restrict__ indptr,
-                                                    int32_t* __restrict__ indices, T* __restrict__ data) {
+                                                    I* __restrict__ indices, T* __restrict__ data,
+                                                    int64_t* __restrict__ indptr64) {
   const uint32_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
   const uint32_t* src = tcol + 2 * (uint64_t)e0;
@@ -875,15 +878,20 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
     for (uint32_t u = 0; u < kU; u++) {
       const uint32_t i = i0 + u * kFinTPB;
       if (i < tot) {
-        indices[base + i] = (int32_t)(c[u] & ~kMultiCopy);
-        data[base + i] = sum_copies<T>(one, (c[u] & kMultiCopy) ? (uint32_t)scn[i] : 1u);
+        indices[(uint64_t)base + i] = (I)(c[u] & ~kMultiCopy);
+        data[(uint64_t)base + i] = sum_copies<T>(one, (c[u] & kMultiCopy) ? (uint32_t)scn[i] : 1u);
       }
     }
   }
   const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
   if (threadIdx.x < (1u << low) && row < n_rows) {
-    indptr[row] += (int32_t)base;
-    if (row == n_rows - 1) indptr[n_rows] += (int32_t)base;
+    if constexpr (sizeof(I) == 8) {
+      indptr64[row] = (int64_t)base + (int64_t)(uint32_t)indptr[row];
+      if (row == n_rows - 1) indptr64[n_rows] = (int64_t)base + (int64_t)(uint32_t)indptr[n_rows];
+    } else {
+      indptr[row] += (int32_t)base;
+      if (row == n_rows - 1) indptr[n_rows] += (int32_t)base;
+    }
   }
 }
 

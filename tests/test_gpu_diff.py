@@ -552,3 +552,32 @@ def test_failed_build_leaves_no_call_state(gpu, oracle_lib, mode):
     assert raw.indptr.tobytes() == R.indptr.tobytes() and raw.indices.tobytes() == R.indices.tobytes()
     assert raw.data.tobytes() == R.data.tobytes()
     assert raw.names_blob.tobytes() == o.names_blob.tobytes()
+
+
+@pytest.mark.parametrize("case", ["dups", "synth"])
+def test_int64_index_path_equals_oracle(gpu, oracle_lib, case):
+    """TEST_INDEX64 forces the CSR results of unweighted builds through the int64 index path (what a
+    result of more than 2^31 - 1 entries takes: scipy's get_index_dtype, utils.py:55, builders.py:283):
+    int64 indptr / indices holding exactly the oracle's values, in every mode (MAX-SYM, SUM twins,
+    bidirected) and dtype family."""
+    from gfa2network_amd import _native as nat
+
+    data = _csr_cases()[case]
+    bad = []
+    for mode in MODES:
+        for dtype in ("float64", "int8", "bool"):
+            for out in (nat.OUT_CSR, nat.OUT_PARSE):
+                o = oracle_lib.run(data, dtype=dtype, **mode)
+                raw = nat.build_from_buffer(data, nat.make_options(output=out, dtype=dtype,
+                                                                   test_flags=nat.TEST_INDEX64, **mode))
+                assert raw.status == o.status == 0
+                if raw.format != "csr":
+                    continue  # a COO parse result (stream order) has no index path of its own
+                R = oracle_lib.to_raw(o, "csr" if out == nat.OUT_CSR else "parse")
+                if raw.indptr.dtype != np.int64 or raw.indices.dtype != np.int64:
+                    bad.append((mode, dtype, out, "dtype", raw.indptr.dtype))
+                    continue
+                if not (np.array_equal(raw.indptr, R.indptr) and np.array_equal(raw.indices, R.indices)
+                        and raw.data.tobytes() == R.data.tobytes()):
+                    bad.append((mode, dtype, out))
+    assert not bad, bad[:4]

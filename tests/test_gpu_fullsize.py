@@ -190,3 +190,52 @@ def test_c5_single_gpu_properties(gpu):
     r, c = coo["rows"], coo["cols"]
     assert np.array_equal(r[0::2], c[1::2]) and np.array_equal(c[0::2], r[1::2])
     assert np.all(coo["data"] == 1.0)
+
+
+def test_int64_indices_past_2_31_entries(gpu):
+    """One GPU, more than 2^31 - 1 result entries: 275M S / 1.1G L undirected (40 GB in HBM, 2.2G SUM
+    entries), the CSR convert_format returns (utils.py:55 coo.tocsr) in scipy's int64 index dtype —
+    checked on the device with torch: indptr int64, starts at 0, ends at nnz, non-decreasing; every
+    row's columns strictly increasing and < n; the values sum to 2 x edges (each L line adds (u, v)
+    and (v, u) with value 1; exact in float64).  Parity beyond these properties is the forced int64
+    path's (test_gpu_diff.py::test_int64_index_path_equals_oracle) and the int32 builds'."""
+    import torch
+
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    n_s, n_l = 275_000_000, 1_100_000_000
+    lib = nat.load()
+    hip = nat.hip_runtime()
+    dev = synth.DeviceInput(n_s, n_l, seed=0)
+    ctx = lib.g2n_context_create(0)
+    try:
+        o = nat.make_options(output=nat.OUT_CSR, directed=False, want_node_names=False)
+        res = nat.Result()
+        rc = lib.g2n_build_device(ctx, dev.ptr, dev.len, ctypes.byref(o), ctypes.byref(res))
+        assert rc == 0, (nat.status_name(rc), nat.last_error())
+        n, nnz = int(res.n_nodes), int(res.nnz)
+        assert n == n_s and int(res.n_edges) == n_l and res.index_width == 8 and nnz > 2**31 - 1
+
+        def copy(ptr, count, dtype):
+            t = torch.empty(count, dtype=dtype, device="cuda")
+            assert hip.hipMemcpy(t.data_ptr(), ptr, t.numel() * t.element_size(), 3) == 0
+            return t
+
+        indptr = copy(res.indptr, n + 1, torch.int64)
+        assert int(indptr[0]) == 0 and int(indptr[-1]) == nnz
+        assert bool((indptr[1:] >= indptr[:-1]).all())
+        data = copy(res.data, nnz, torch.float64)
+        assert float(data.sum()) == 2.0 * n_l and bool((data >= 1).all())
+        del data
+        torch.cuda.empty_cache()
+        indices = copy(res.indices, nnz, torch.int64)
+        assert int(indices.min()) >= 0 and int(indices.max()) < n
+        starts = torch.zeros(nnz, dtype=torch.bool, device="cuda")
+        rs = indptr[1:-1]
+        starts[rs[rs < nnz]] = True
+        inc = indices[1:] > indices[:-1]
+        assert bool((inc | starts[1:]).all())
+    finally:
+        lib.g2n_context_destroy(ctx)
+        dev.free()
