@@ -107,6 +107,9 @@ struct ParseOpts {
   // on its group's count (the group's order of tiles is arbitrary: only for consumers that do not
   // need stream order — the unweighted bucket partition); rows / cols already point at the base
   uint32_t grouped;
+  // experiment (G2N_K2_PREFETCH): the one-tile-per-block lean parse warms the cache with tile
+  // blockIdx + pf_dist (0: off)
+  uint32_t pf_dist;
 };
 constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
 

@@ -899,6 +899,29 @@ __device__ inline bool dec_lds(const uint8_t* buf, uint32_t x, uint32_t l, uint6
   return true;
 }
 
+// dec_lds's 1-8 digit case on words already loaded: w0 / w1 = the aligned 8-byte LDS words at
+// (x & ~7) and (x & ~7) + 8.  false for anything else (the caller takes dec_lds for 9-10 digits).
+__device__ inline bool dec_words(uint64_t w0, uint64_t w1, uint32_t x, uint32_t l, uint64_t* v) {
+  if (l == 0 || l > 8) return false;
+  const uint32_t sh = (x & 7u) * 8;
+  uint64_t w = w0 >> sh;
+  if (sh && (x & 7u) + l > 8) w |= w1 << (64 - sh);
+  const uint64_t keep = l == 8 ? ~0ull : ((1ull << (8 * l)) - 1);
+  w &= keep;
+  const uint64_t zeros = 0x3030303030303030ull & keep;
+  if ((w & 0xF0F0F0F0F0F0F0F0ull & keep) != zeros ||
+      (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) != 0 ||
+      (w & 0xFF) == '0')
+    return false;
+  const uint64_t d = (w - zeros) << (8 * (8 - l));
+  auto four = [](uint32_t y) {
+    y = ((y << 3) + (y << 1) + (y >> 8)) & 0x00FF00FFu;
+    return ((y << 6) + (y << 5) + (y << 2) + (y >> 16)) & 0xFFFFu;
+  };
+  *v = (uint64_t)(four((uint32_t)d) * 10000u + four((uint32_t)(d >> 32)));
+  return true;
+}
+
 // tab bits of the 64 staged bytes from chunk q: from the tile's tab bitmap, or (tabm == nullptr)
 // recomputed from the staged bytes (the LDS-lean instance keeps no bitmap)
 __device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, uint32_t q) {
@@ -1004,7 +1027,7 @@ __device__ unsigned long long* g2n_k2_stamps;
   } while (0)
 #define K2_LEAN_STAMP(k)                                                                 \
   do {                                                                                   \
-    if (threadIdx.x == 0) g2n_k2_stamps[blockIdx.x * kK2Stamps + (k)] = wall_clock64();  \
+    if (threadIdx.x == 0) g2n_k2_stamps[tile * kK2Stamps + (k)] = wall_clock64();        \
   } while (0)
 #else
 #define K2_STAMP(k) \
@@ -1599,7 +1622,13 @@ constexpr uint32_t kLeanTPB = G2N_LEAN_TPB;                             // threa
 constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
 constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
 constexpr uint32_t kLeanLines = 2048;                                   // line records per window
-constexpr uint32_t kLeanBatch = 8;                                      // starts classified with loads batched
+#ifndef G2N_LEAN_PAIR  // experiment builds: the decimal parse two lines per lane per step
+#define G2N_LEAN_PAIR 0
+#endif
+#ifndef G2N_LEAN_BATCH  // experiment builds: starts classified per region with their loads batched
+#define G2N_LEAN_BATCH 4
+#endif
+constexpr uint32_t kLeanBatch = G2N_LEAN_BATCH;                         // starts classified with loads batched
 static_assert(kTile <= 32768 && (kLeanRegion == 4 || kLeanRegion == 2),
               "records hold 15-bit offsets; a region's starts fit one 64-bit mask");
 
@@ -1754,50 +1783,49 @@ __device__ inline uint32_t lean_find(const uint8_t* __restrict__ in, const HashL
   return ~0u;
 }
 
+using LeanRegs = TileRegs<kTileHalo, kLeanTPB>;
+#ifndef G2N_K2_PREFETCH
+#define G2N_K2_PREFETCH 0
+#endif
+
+// One tile of the lean front end.  R holds the tile's staged bytes on entry (loaded by the caller);
+// after they are in LDS, R is refilled with tile next_tile's bytes (next_tile < n_tiles), which stay
+// in flight through this tile's parse — the persistent decimal kernel's prefetch.
 template <int kMode, bool kGrouped>
-__global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op,
-                                                        Ctl* ctl, TileCnt* __restrict__ tcnt_out,
-                                                        TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount,
-                                                        uint64_t gcap, HashLeanArgs H) {
+__device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl,
+                                          TileCnt* __restrict__ tcnt_out, TileLean* __restrict__ tlean,
+                                          uint32_t* __restrict__ gcount, uint64_t gcap, const HashLeanArgs& H,
+                                          const uint64_t tile, LeanRegs& R, uint64_t next_tile, uint64_t n_tiles) {
   constexpr uint32_t kW = kLeanTPB / 64;
-  if constexpr (kMode == kLeanClaim) {  // tiles with S or P / O lines (block-uniform)
-    const TileCnt c = H.tcnt[blockIdx.x];
-    if (c.segs == 0 && c.recs == c.segs + c.edges) return;
-    if (c.segs && H.tbase[blockIdx.x].edges) {  // an edge line before this tile's S lines
-      if (threadIdx.x == 0) ctl->int_fail = 1;
-      return;
-    }
-  } else if constexpr (kMode == kLeanEdges) {  // tiles with edge lines
-    if (H.tcnt[blockIdx.x].edges == 0) return;
-  }
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
   __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
   __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
   __shared__ uint32_t rec[kLeanLines + 1];
   __shared__ unsigned long long red64[kW];
   __shared__ uint32_t s_gbase;
-  const uint64_t tile = blockIdx.x;
   const uint64_t t0 = tile * kTile;
-  op.grouped = kGrouped ? 1u : 0u;  // lean_line: positions relative to the tile's base in its group slot
+  if (!kGrouped && op.tile_pad) {  // this tile's slot (positions relative to it, as in a group slot)
+    const uint64_t b = tile * (uint64_t)op.tile_pad * op.ktrip;
+    op.rows += b;
+    op.cols += b;
+  }
+  op.grouped = op.tile_pad ? 1u : 0u;  // lean_line: positions relative to the tile's base in its slot
   uint64_t sbase = 0, ebase = 0;     // hash modes: S lines / edge lines before this tile (K1's bases)
   if constexpr (kMode != kLeanDecimal) {
     sbase = H.tbase[tile].segs;
     ebase = H.tbase[tile].edges;
   }
   K2_LEAN_STAMP(0);
-  {
-    TileRegs<kTileHalo, kLeanTPB> R;
-    R.load(in, len, t0);
-    R.store(buf);
+  R.store(buf);
 #pragma unroll
-    for (uint32_t j = 0; j < R.kPer; j++) {
-      const uint32_t c = j * kLeanTPB + threadIdx.x;
-      if (c < kLeanChunks) {
-        tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
-        nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
-      }
+  for (uint32_t j = 0; j < R.kPer; j++) {
+    const uint32_t c = j * kLeanTPB + threadIdx.x;
+    if (c < kLeanChunks) {
+      tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
+      nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
     }
   }
+  if (next_tile < n_tiles) R.load(in, len, next_tile * kTile);  // in flight through this tile's parse
   if (threadIdx.x < 8) {  // tab_window reads up to 4 bitmaps past a chunk
     tabm[kLeanChunks + threadIdx.x] = 0;
     nlm[kLeanChunks + threadIdx.x] = 0;
@@ -1979,6 +2007,102 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
       }
       continue;  // next window
     }
+#if G2N_LEAN_PAIR
+    // decimal ids: two lines per lane per step, every stage's LDS loads for both lines issued
+    // together (rec -> tab window -> name words), the checks branch-free (lean_line's rules)
+    if constexpr (kMode == kLeanDecimal) {
+#pragma unroll 1
+      for (uint32_t j0 = threadIdx.x; j0 < n_win; j0 += 2 * kLeanTPB) {
+        uint32_t o[2], nx[2], cd[2], pf[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t j = j0 + (uint32_t)q * kLeanTPB;
+          const uint32_t x = j < n_win ? rec[j] : 0u;
+          cd[q] = (x >> 15) & 3u;
+          o[q] = x & 0x7FFFu;
+          pf[q] = x >> 17;
+          nx[q] = cd[q] ? line_next(j, o[q]) : 0u;
+        }
+        uint64_t w[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) w[q] = tab_window(buf, tabm, o[q] >> 4);
+        uint32_t xa[2], la[2], xb[2], lb[2], oa[2], ob[2];
+        bool good[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t n = nx[q] - 1 - o[q];
+          uint64_t m = (w[q] >> (o[q] & 15)) & ((1ull << (n > 48 ? 48 : n)) - 1);
+          const uint32_t pc = (uint32_t)__popcll(m);
+          uint32_t p[6];
+#pragma unroll
+          for (int k = 0; k < 6; k++) {
+            p[k] = m ? (uint32_t)__builtin_ctzll(m) : n;
+            m &= m - 1;
+          }
+          const bool s_ok = pc >= 1 && (pc >= 2 || n <= 48);
+          const bool e_ok = n <= 48 && pc >= 5 && p[2] - p[1] == 2 && p[4] - p[3] == 2;
+          const bool po_ok = pc >= 2;
+          good[q] = cd[q] == 0 || (nx[q] != 0 && (cd[q] == 1 ? s_ok : cd[q] == 2 ? e_ok : po_ok));
+          const bool s = cd[q] == 1 && good[q], e = cd[q] == 2 && good[q];
+          xa[q] = s || e ? o[q] + p[0] + 1 : 0u;
+          la[q] = s || e ? p[1] - p[0] - 1 : 0u;
+          xb[q] = e ? o[q] + p[2] + 1 : 0u;
+          lb[q] = e ? p[3] - p[2] - 1 : 0u;
+          oa[q] = e ? o[q] + p[1] + 1 : 0u;  // the orientation bytes
+          ob[q] = e ? o[q] + p[3] + 1 : 0u;
+        }
+        uint64_t wa0[2], wa1[2], wb0[2], wb1[2];
+        uint32_t c2[2], c4[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t a = xa[q] & ~7u, b = xb[q] & ~7u;
+          wa0[q] = *(const uint64_t*)(buf + a);
+          wa1[q] = *(const uint64_t*)(buf + a + 8);
+          wb0[q] = *(const uint64_t*)(buf + b);
+          wb1[q] = *(const uint64_t*)(buf + b + 8);
+          c2[q] = buf[oa[q]];
+          c4[q] = buf[ob[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          if (!good[q]) {
+            is.fail = 1;
+            continue;
+          }
+          if (cd[q] == 1) {  // S line: its S index pf (no edge precedes it in the tile)
+            if (is.fail) continue;
+            uint64_t v;
+            const bool dok = la[q] <= 8 ? dec_words(wa0[q], wa1[q], xa[q], la[q], &v) : dec_lds(buf, xa[q], la[q], &v);
+            if (!dok) is.fail = 1;
+            else is.s_name(op, v, pf[q]);
+          } else if (cd[q] == 2) {
+            if ((c2[q] != '+' && c2[q] != '-') || (c4[q] != '+' && c4[q] != '-') || pf[q] >= op.tile_pad) {
+              is.fail = 1;
+              continue;
+            }
+            if (is.fail) continue;
+            uint64_t a, b;
+            const bool aok = la[q] <= 8 ? dec_words(wa0[q], wa1[q], xa[q], la[q], &a) : dec_lds(buf, xa[q], la[q], &a);
+            const bool bok = lb[q] <= 8 ? dec_words(wb0[q], wb1[q], xb[q], lb[q], &b) : dec_lds(buf, xb[q], lb[q], &b);
+            if (!aok || !bok || a > op.n_seg || b > op.n_seg) {
+              is.fail = 1;
+              continue;
+            }
+            const uint32_t vm = (uint32_t)(a > b ? a : b);
+            is.vmax = vm > is.vmax ? vm : is.vmax;
+            const uint64_t eo = (uint64_t)pf[q] * op.ktrip;
+            op.rows[eo] = (int32_t)(a - 1);
+            op.cols[eo] = (int32_t)(b - 1);
+            if (op.ktrip >= 2) {
+              op.rows[eo + 1] = (int32_t)(b - 1);
+              op.cols[eo + 1] = (int32_t)(a - 1);
+            }
+          }
+        }
+      }
+      continue;  // next window
+    }
+#endif
 #pragma unroll 1
     for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
       const uint32_t x = rec[j];
@@ -2056,7 +2180,7 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
       uint32_t hw, xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+      g2n_k2_stamps[tile * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
     }
 #endif
     return;
@@ -2108,9 +2232,68 @@ __global__ void __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1) k_tile_lea
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g2n_k2_stamps[blockIdx.x * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+    g2n_k2_stamps[tile * kK2Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
   }
 #endif
+}
+
+// One block per tile (the hash modes skip the tiles they have nothing to do in before loading them).
+#if G2N_LEAN_PAIR  // the LDS allows 3 blocks (6 waves per SIMD): keep the VGPRs to 80
+#define G2N_LEAN_ATTR __attribute__((amdgpu_flat_work_group_size(kLeanTPB, kLeanTPB), amdgpu_waves_per_eu(6, 6)))
+#else
+#define G2N_LEAN_ATTR __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1)
+#endif
+template <int kMode, bool kGrouped>
+__global__ void G2N_LEAN_ATTR
+    k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl, TileCnt* __restrict__ tcnt_out,
+                TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount, uint64_t gcap, HashLeanArgs H) {
+  const uint64_t tile = blockIdx.x;
+  if constexpr (kMode == kLeanClaim) {  // tiles with S or P / O lines (block-uniform)
+    const TileCnt c = H.tcnt[tile];
+    if (c.segs == 0 && c.recs == c.segs + c.edges) return;
+    if (c.segs && H.tbase[tile].edges) {  // an edge line before this tile's S lines
+      if (threadIdx.x == 0) ctl->int_fail = 1;
+      return;
+    }
+  } else if constexpr (kMode == kLeanEdges) {  // tiles with edge lines
+    if (H.tcnt[tile].edges == 0) return;
+  }
+  LeanRegs R;
+  R.load(in, len, tile * kTile);
+#if G2N_K2_PREFETCH
+  // experiment: warm the L2 / Infinity Cache with the tile the block G tiles on will stage (G = the
+  // blocks resident at once, a multiple of the 8 XCDs: the same XCD's L2) — one dword per 128-byte
+  // line, into a sink register kept live (and drained) to the end, so no later value shares it
+  uint32_t sink = 0;
+  const uint64_t pf = (tile + op.pf_dist) * kTile + 128ull * threadIdx.x;
+  const bool do_pf = op.pf_dist && threadIdx.x < (kTile + kTileHalo) / 128 && pf < len;
+  if (do_pf) asm volatile("global_load_dword %0, %1, off" : "=v"(sink) : "v"(in + pf) : "memory");
+#endif
+  lean_tile<kMode, kGrouped>(in, len, op, ctl, tcnt_out, tlean, gcount, gcap, H, tile, R, ~0ull, 0);
+#if G2N_K2_PREFETCH
+  asm volatile("s_waitcnt vmcnt(0)" : : "v"(sink) : "memory");
+#endif
+}
+
+// The decimal-id parse persistent: a block walks tiles blockIdx.x, + gridDim.x, ... and loads the
+// next one's bytes into registers while it parses the current one (the staged loads' HBM latency
+// was a quarter of a block's time with one tile per block: stamps).
+#ifndef G2N_K2P_WAVES  // waves per SIMD the persistent parse is compiled for (LDS allows 6: VGPRs <= 80)
+#define G2N_K2P_WAVES 6
+#endif
+template <bool kGrouped>
+__global__ void __attribute__((amdgpu_flat_work_group_size(kLeanTPB, kLeanTPB), amdgpu_waves_per_eu(G2N_K2P_WAVES, G2N_K2P_WAVES)))
+    k_tile_lean_p(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl, TileCnt* __restrict__ tcnt_out,
+                  TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount, uint64_t gcap, uint64_t n_tiles) {
+  LeanRegs R;
+  uint64_t tile = blockIdx.x;
+  if (tile < n_tiles) R.load(in, len, tile * kTile);
+#pragma unroll 1
+  for (; tile < n_tiles; tile += gridDim.x) {
+    if (tile != blockIdx.x) __syncthreads();  // the previous tile's LDS fully read
+    lean_tile<kLeanDecimal, kGrouped>(in, len, op, ctl, tcnt_out, tlean, gcount, gcap, HashLeanArgs{}, tile, R,
+                                      tile + gridDim.x, n_tiles);
+  }
 }
 
 // Open-addressing dictionary, 32-byte entries: hdr = (hash tag << 32 | first touch),

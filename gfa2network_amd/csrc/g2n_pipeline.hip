@@ -58,6 +58,9 @@ enum Slot {
 #endif
 
 // options.reserved[1] bits (tests only): take a path that is normally rare, same results
+#ifndef G2N_K2_PERSIST  // experiment builds: 1 = the persistent parse, next tile in registers (k_tile_lean_p)
+#define G2N_K2_PERSIST 0
+#endif
 constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-sum path
 constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean parse (ids per touch, k_triplets)
 constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
@@ -99,6 +102,7 @@ struct g2n_context {
   hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
   hipEvent_t side_ev[2] = {nullptr, nullptr};  // main -> side fork, side -> main join
   bool side_pending = false;    // the main stream has not joined the side stream's last work yet
+  uint64_t lean_blocks = 0;     // k_tile_lean_p blocks resident on the device at once (its grid)
   bool range_has_s = false;     // g2n_build_decimal_range: the range's evidence (k_tile_lean_evidence)
   int64_t range_d = -1;
   uint64_t range_vmax = 0;
@@ -603,6 +607,14 @@ static void assemble_pair_t(g2n_context* c, const int32_t* ar, const int32_t* ac
                             const int32_t* tr, const int32_t* tc, const T* td, uint64_t tn, bool maxsym, int64_t base,
                             uint64_t n_rows, int force_unsorted, g2n_result* R) {
   if constexpr (kU) {  // unweighted: the bucket partition (the slice's sums cannot depend on order)
+    // one rank that routed nothing passes A's own arrays swapped as the A.T stream: the whole-matrix
+    // MAX-SYM partition then reads each entry once and pairs its two sides (kElPair) like one GPU
+    const bool self_t = maxsym && tn == an && tr == ac && tc == ar && base == 0;
+    if (self_t && an && n_rows && !(c->test_flags & kTestNoBuckets) &&
+        csr_partition<T>(c, ar, ac, an, n_rows, false, R)) {
+      R->sum_sorted = R->sum_t_sorted = 1;
+      return;
+    }
     if (an + tn && n_rows && base >= 0 && base < 0xFFFFFFFFll && !(c->test_flags & kTestNoBuckets) &&
         csr_partition<T>(c, ar, ac, an, n_rows, !maxsym, R, maxsym ? (tr ? tr : ar) : nullptr,
                          maxsym ? tc : nullptr, maxsym ? tn : 0, base ? base : 0)) {
@@ -908,6 +920,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tile_pad = kTileEdgeCap;
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
+  lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
 #ifdef G2N_K2_STAMPS
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
   G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));
@@ -919,12 +932,23 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                      1u, 2u, lo, (uint64_t*)nullptr, (uint8_t*)nullptr, TouchOut{}, EdgeOut{}, c->ctl,
                      (uint64_t*)nullptr, (DeferredLine*)nullptr, n_tiles, tcnt, tlean);
 #else
+#if G2N_K2_PERSIST
+  // persistent: as many blocks as fit on the device at once, each prefetching its next tile
+  const unsigned grid = (unsigned)std::min<uint64_t>(n_tiles, (uint64_t)c->lean_blocks);
+  if (grouped)
+    hipLaunchKernelGGL((k_tile_lean_p<true>), dim3(grid), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
+                       tlean, gcount, gcap, n_tiles);
+  else
+    hipLaunchKernelGGL((k_tile_lean_p<false>), dim3(grid), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
+                       tlean, (uint32_t*)nullptr, (uint64_t)0, n_tiles);
+#else
   if (grouped)
     hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
                        len, lo, c->ctl, tcnt, tlean, gcount, gcap, HashLeanArgs{});
   else
     hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
                        len, lo, c->ctl, tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0, HashLeanArgs{});
+#endif
 #endif
   phase(c, "parse");
 #ifdef G2N_K2_STAMPS
@@ -1509,6 +1533,15 @@ static g2n_context* context_create(int device) {
   for (auto& e : c->side_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   G2N_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
   if (c->n_cu <= 0) c->n_cu = 1;
+  {  // the persistent decimal parse's grid: every block resident at once (LDS-limited: 3 per CU)
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tile_lean_p<true>, kLeanTPB, 0) != hipSuccess ||
+        per_cu <= 0) {
+      (void)hipGetLastError();
+      per_cu = 1;
+    }
+    c->lean_blocks = (uint64_t)per_cu * (uint64_t)c->n_cu;
+  }
   c->bufs.resize(S_NSLOTS);
   G2N_HIP(hipMalloc(&c->ctl, sizeof(Ctl)));
   G2N_HIP(hipHostMalloc(&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
@@ -1689,6 +1722,7 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   std::lock_guard<std::mutex> lk(c->mu);
   G2N_HIP(hipSetDevice(c->device));
   clear_call_state(c);
+  c->test_flags = 0;  // a build's test flags are not this conversion's
   const size_t w = dtype_size(dtype);
   auto* dr = dget<int32_t>(c, S_ROWS, (uint64_t)nnz);
   auto* dc = dget<int32_t>(c, S_COLS, (uint64_t)nnz);
