@@ -924,7 +924,17 @@ __device__ inline bool dec_words(uint64_t w0, uint64_t w1, uint32_t x, uint32_t 
 
 // tab bits of the 64 staged bytes from chunk q: from the tile's tab bitmap, or (tabm == nullptr)
 // recomputed from the staged bytes (the LDS-lean instance keeps no bitmap)
+#ifndef G2N_TAB_B64  // experiment builds: 1 = the window from two aligned 8-byte LDS reads
+#define G2N_TAB_B64 0
+#endif
 __device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, uint32_t q) {
+#if G2N_TAB_B64
+  if (tabm) {  // tabm is 16-byte aligned with 8 entries of padding past its last window
+    const uint32_t a = q & ~3u, sh = (q & 3u) * 16;
+    const uint64_t lo = *(const uint64_t*)(tabm + a), hi = *(const uint64_t*)(tabm + a + 4);
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  }
+#endif
   if (tabm)
     return (uint64_t)tabm[q] | ((uint64_t)tabm[q + 1] << 16) | ((uint64_t)tabm[q + 2] << 32) |
            ((uint64_t)tabm[q + 3] << 48);

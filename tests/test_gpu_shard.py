@@ -298,7 +298,7 @@ def _range_worker(rank, world, port, outdir):
             assert hi - lo > 8 * 32768, (name, rank, hi - lo)
             buf = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy()).to(eng.device)
             for mode in ({}, {"directed": False}, {"dtype": "int8"}):
-                res = build_sharded(buf, engine=eng, gather_names=rank == 0, names_root=0, **mode)
+                res = build_sharded(buf, engine=eng, gather_names=True, names_root=0, **mode)
                 assert res.status == 0, (name, mode, res.status)
                 assert res.fast_path == fast, (name, mode, rank)
                 if fast:  # the one-pass lean parse, not K1 + the tile parse

@@ -357,3 +357,44 @@ def test_decimal_and_gathered_names(bidirected):
     order = rng.permutation(len(keys))
     ob, oo = nat.gather_names(blob, offs, order)
     assert [bytes(ob[oo[i]:oo[i + 1]]) for i in range(len(keys))] == [keys[k] for k in order]
+
+
+def _range_worker(rank, world, port, outdir):
+    """The one-pass decimal protocol on the CPU engine over the range-premise inputs of
+    tests/test_gpu_shard.py (S sections spanning ranges, breaks only the range offset or the file's
+    S count reveal): every rank takes the same branch, the result is the single-file one."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        from gfa2network_amd.shard import build_sharded, gather_csr, line_ranges
+        from oracle import oracle as orc
+        from shard_cpu_engine import CpuEngine
+        from test_gpu_shard import _range_cases
+
+        for name, (data, fast) in _range_cases(world).items():
+            lo, hi = line_ranges(data, world)[rank]
+            buf = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy())
+            res = build_sharded(buf, engine=CpuEngine(orc), gather_names=True, names_root=0)
+            assert res.status == 0 and res.fast_path == fast, (name, rank)
+            indptr, indices, vals = gather_csr(res)
+            if rank == 0:
+                full = orc.run(data)
+                assert np.array_equal(indptr, full.ms_indptr) and np.array_equal(indices, full.ms_indices), name
+                assert res.n_nodes == full.n_nodes, name
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_range_premise_one_pass(oracle_lib, tmp_path, world):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_range_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()
