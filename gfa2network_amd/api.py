@@ -314,15 +314,19 @@ def _parse_gfa_split(path, *, build_matrix: bool, directed: bool, weight_tag, st
         if return_node_list:
             gb = raw.names_blob if raw.names_blob is not None else np.zeros(0, dtype=np.uint8)
             go = raw.names_offsets if raw.names_offsets is not None else np.zeros(1, dtype=np.int64)
-            pieces = [None] * n_fin
+            # final node p: the next interval segment name (host blob, in order) where no GPU node
+            # lands, else GPU node g with gmap[g] = p — one gather over the two blobs (no per-name
+            # Python objects)
             is_gpu = np.zeros(n_fin, dtype=bool)
             is_gpu[gmap] = True
-            for dst, i in zip(np.flatnonzero(~is_gpu), range(m)):
-                pieces[dst] = blob[offs[i]:offs[i + 1]].tobytes()
-            for g in range(n_gpu):
-                pieces[gmap[g]] = gb[go[g]:go[g + 1]].tobytes()
-            raw.names_blob = np.frombuffer(b"".join(pieces), dtype=np.uint8)
-            raw.names_offsets = np.concatenate([[0], np.cumsum([len(x) for x in pieces])]).astype(np.int64)
+            order = np.empty(n_fin, dtype=np.int64)
+            order[~is_gpu] = np.arange(m, dtype=np.int64)
+            order[gmap] = m + np.arange(n_gpu, dtype=np.int64)
+            hb = np.asarray(blob, dtype=np.uint8)[:int(offs[m])] if m else np.zeros(0, dtype=np.uint8)
+            src = np.concatenate([hb, np.asarray(gb, dtype=np.uint8)])
+            src_offs = np.concatenate([np.asarray(offs[:m + 1], dtype=np.int64),
+                                       np.asarray(go[1:], dtype=np.int64) + int(offs[m])])
+            raw.names_blob, raw.names_offsets = nat.gather_names(src, src_offs, order)
         raw.n_nodes = n_fin
     elif not bidirected and return_node_list and raw.status == nat.OK and raw.names_offsets is None:
         raw.names_blob, raw.names_offsets = np.zeros(0, dtype=np.uint8), np.zeros(1, dtype=np.int64)
