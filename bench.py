@@ -438,8 +438,11 @@ def main_sharded(args, wl):
     starts = [_line_start_device(dev_in.ptr, dev_in.len, r * dev_in.len // world) for r in range(world)] + [dev_in.len]
     lo, hi = starts[rank], starts[rank + 1]
     mode = dict(wl.mode)
+    # copy_out=False: each rank's CSR slice stays in its engine's HBM arena, as the one-GPU build's
+    # result stays in its context (no device-to-device copy into torch tensors)
     kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
-              weight_tag=mode.get("weight_tag"), dtype="float64", force_protocol=args.force_protocol)
+              weight_tag=mode.get("weight_tag"), dtype="float64", force_protocol=args.force_protocol,
+              copy_out=False)
     one = None
     lib = nat.load()
     if rank == 0:  # the whole file on one GPU: the scaling reference

@@ -365,11 +365,14 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   while (low > 1 && (double)(1u << low) * per_row > (double)(kSymCap / 2)) low--;
   if (low > bits) low = bits;
   const int hb = bits - low;  // bucket id bits
-  if (hb > 2 * (int)kMaxDigitBits) return false;
+  // pass 2 takes up to kWideDigitBits only past 2^20 buckets (more than 2^31 elements at most 2^11 per
+  // bucket): the tuned 10-bit kernels otherwise; pass 1's groups stay <= 1024 (k_part_groups)
+  const int max2 = hb > 2 * (int)kMaxDigitBits ? (int)kWideDigitBits : (int)kMaxDigitBits;
+  if (hb > (int)kMaxDigitBits + max2) return false;
   // two passes: at most 8 bits in pass 1 (its sub-tiles rank 8192 COO entries: longer runs per
   // digit), the rest in pass 2 (C4, hb = 18: 8 + 10 measured 9.07 ms per build against 9.19 for 9 + 9
   // and 9.39 for 10 + 8)
-  const int bits1 = hb > (int)kMaxDigitBits ? std::max(hb - (int)kMaxDigitBits, std::min(8, (hb + 1) / 2)) : hb;
+  const int bits1 = hb > max2 ? std::max(hb - max2, std::min(8, (hb + 1) / 2)) : hb;
   const int bits2 = hb - bits1;
   const uint32_t n_dig1 = 1u << bits1, n_dig2 = 1u << bits2;
   const uint64_t n_el = pair ? n_trip + n_t : (sum ? 1 : 2) * n_trip;
@@ -423,11 +426,19 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
     auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
     auto* el2 = dget<uint2>(c, S_EL1, n_el);
-    hipLaunchKernelGGL(k_part_hist<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low, n_dig2,
-                       cnt2, n_blk2);
-    scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
-    hipLaunchKernelGGL(k_part_scatter<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low, n_dig2,
-                       (const uint32_t*)off2, n_blk2, el2);
+    if (bits2 > (int)kMaxDigitBits) {
+      hipLaunchKernelGGL((k_part_hist<2, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2,
+                         (uint32_t)low, n_dig2, cnt2, n_blk2);
+      scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+      hipLaunchKernelGGL((k_part_scatter<2, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2,
+                         (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, el2);
+    } else {
+      hipLaunchKernelGGL(k_part_hist<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
+                         n_dig2, cnt2, n_blk2);
+      scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+      hipLaunchKernelGGL(k_part_scatter<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
+                         n_dig2, (const uint32_t*)off2, n_blk2, el2);
+    }
     hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
                        (const uint32_t*)off2, s2, n_dig2, n_buckets, bst);
     el = el2;
@@ -1357,8 +1368,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
+  // options.reserved[4] bit 2: a sharded decimal range whose caller routes coordinates only
+  // (uniform values, no COO result): the values array is left unwritten
+  const bool no_values = shard_dec && uni && (o->reserved[4] & 4) != 0;
   if (coords_done) {  // values only, and only when the output or the sums read them
-    if (n_e && (coo_out || !uni)) {
+    if (n_e && (coo_out || !uni) && !no_values) {
 #define G2N_VALUES(T) \
   hipLaunchKernelGGL(k_values<T>, dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E.w, n_e, ktrip, (int)uni, (T*)data, c->ctl)
       switch (dt) {
@@ -1993,7 +2007,7 @@ int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, c
   g2n_options o = *opts;
   o.reserved[2] = 0;
   o.reserved[3] = 0;
-  o.reserved[4] = 3;  // sharded decimal ids, offset evidence instead of the check
+  o.reserved[4] = 3 | (opts->reserved[4] & 4);  // sharded decimal ids, offset evidence instead of the check
   const int rc = g2n_build_device(ctx, d_input, len, &o, out);
   if (rc == G2N_OK) {
     ev6[0] = out->n_lines;

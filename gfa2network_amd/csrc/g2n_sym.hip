@@ -46,7 +46,8 @@ constexpr uint32_t kSubPer = 8;                    // elements per thread in one
 constexpr uint32_t kSub = kSubPer * kPartTPB;      // 8192 elements per sub-tile
 constexpr uint32_t kChunkSubs = 8 * 1024 / kPartTPB;  // sub-tiles per block (65536 elements)
 constexpr uint32_t kPartTile = kSub * kChunkSubs;  // 65536 elements per partition block
-constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits
+constexpr uint32_t kMaxDigitBits = 10;             // LDS histogram of at most 1024 digits (the tuned shape)
+constexpr uint32_t kWideDigitBits = 11;            // pass 2 of a partition past 2^20 buckets (> 2^31 elements)
 #ifndef G2N_FIN_TPB  // experiment builds vary the finish block (one row per thread)
 #define G2N_FIN_TPB 256
 #endif
@@ -280,10 +281,10 @@ __device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint3
 }
 
 // Histogram of the block's digits (row >> shift) & (n_dig - 1) over its whole range.
-template <int kPass>
+template <int kPass, uint32_t kDB = kMaxDigitBits>
 __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                     uint32_t* __restrict__ counts, uint64_t n_blk) {
-  __shared__ uint32_t hist[1u << kMaxDigitBits];
+  __shared__ uint32_t hist[1u << kDB];
   for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) {  // block-uniform: past the last group's blocks
@@ -316,14 +317,14 @@ __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shif
 #ifndef G2N_PART2_WAVES
 #define G2N_PART2_WAVES 4
 #endif
-template <int kPass>
+template <int kPass, uint32_t kDB = kMaxDigitBits>
 __global__ void __launch_bounds__(kPartTPB)
     __attribute__((amdgpu_waves_per_eu(kPass == 1 ? G2N_PART1_WAVES : G2N_PART2_WAVES)))
     k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                        const uint32_t* __restrict__ offs, uint64_t n_blk,
                                                        uint2* __restrict__ out) {
-  __shared__ uint32_t hist[1u << kMaxDigitBits];  // sub-tile counts, then its digit starts
-  __shared__ uint32_t cur[1u << kMaxDigitBits];   // output position of the next element of digit d
+  __shared__ uint32_t hist[1u << kDB];  // sub-tile counts, then its digit starts
+  __shared__ uint32_t cur[1u << kDB];   // output position of the next element of digit d
   __shared__ uint2 stage[kSubEl<kPass>];
   __shared__ uint32_t red[kPartTPB / 64];
   PartBlock B;
@@ -344,7 +345,7 @@ __global__ void __launch_bounds__(kPartTPB)
       rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(part_row<kPass>(raw, k) >> shift) & dmask], 1u) : 0u;
     __syncthreads();
     // digit starts: kDigPer consecutive digits per thread (n_dig <= 1024)
-    constexpr uint32_t kDigPer = (1u << kMaxDigitBits) / kPartTPB;
+    constexpr uint32_t kDigPer = (1u << kDB) / kPartTPB;
     uint32_t hv[kDigPer], hsum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kDigPer; q++) {

@@ -310,13 +310,13 @@ class HipEngine:
                     "g2n_count_device")
         return [int(v) for v in out]
 
-    def build_decimal(self, buf, opts: dict, s_base: int, n_seg: int, view: bool = False):
+    def build_decimal(self, buf, opts: dict, s_base: int, n_seg: int, view: bool = False, values: bool = True):
         """The range parsed straight into GLOBAL decimal ids (S lines s_base.. of n_seg), or None when
         it needs the general protocol (ids that are not decimal, errors, warnings, slow weights).
         view: the COO as DevArray views of the build context (valid until the next build_decimal)."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
-        o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1
+        o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1 | (0 if values else 4)
         res = nat.Result()
         self._build_ctx()
         self._sync()
@@ -328,12 +328,13 @@ class HipEngine:
             return None
         return self._decimal_shard(res, opts, view)
 
-    def build_decimal_range(self, buf, opts: dict, view: bool = False):
+    def build_decimal_range(self, buf, opts: dict, view: bool = False, values: bool = True):
         """The range parsed into GLOBAL decimal ids before the ranges' counts are known (one pass, no
         count: g2n_build_decimal_range): (LocalShard, evidence [lines, S lines, edges, records, d,
         largest edge key]) — the caller checks d against the S lines before the range and the key
         against the file's S count — or None when the one pass declines (count + build_decimal then)."""
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
+        o.reserved[4] = 0 if values else 4  # values: the caller reads them (a COO result, weights)
         res = nat.Result()
         ev = (ctypes.c_int64 * 6)()
         self._build_ctx()
@@ -433,7 +434,9 @@ class HipEngine:
         return orows, ocols, odata, starts
 
     def csr_pair(self, a, t, maxsym: bool, row_base: int, n_rows: int, n_cols: int, dtype: str, uniform: bool,
-                 force_unsorted: int):
+                 force_unsorted: int, copy: bool = True):
+        """The slice's CSR; copy=False: DevArray views of the context's result (valid until its next
+        call — what a caller that reads the slice right away, or never, needs: no device copy)."""
         torch = self.torch
         res = nat.Result()
         t = t if t is not None else (a[0][:0], a[1][:0], None)
@@ -446,9 +449,14 @@ class HipEngine:
                                                    p(t[1]), p(t[2]), t[0].numel(), int(maxsym), row_base, n_rows,
                                                    n_cols, nat.DTYPE_CODES[dtype], int(uniform), force_unsorted,
                                                    ctypes.byref(res)), "g2n_csr_from_coo_pair")
+        tdt = getattr(torch, TORCH_DTYPES[dtype])
+        if not copy:
+            w = torch.empty(0, dtype=tdt).element_size()
+            return (DevArray(res.indptr or 0, n_rows + 1, 4), DevArray(res.indices or 0, res.nnz, 4),
+                    DevArray(res.data or 0, res.nnz, w), not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted)
         indptr = self._copy_out(res.indptr, n_rows + 1, torch.int32)
         indices = self._copy_out(res.indices, res.nnz, torch.int32)
-        vals = self._copy_out(res.data, res.nnz, getattr(torch, TORCH_DTYPES[dtype]))
+        vals = self._copy_out(res.data, res.nnz, tdt)
         return indptr, indices, vals, not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted
 
 
@@ -583,7 +591,7 @@ class Comm:
         return xc.to(dev)
 
 
-def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm):
+def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm, copy_out=True):
     """Step 6: this rank's CSR row slice (rows [row_lo, row_hi) of n_global)."""
     import time
 
@@ -600,8 +608,9 @@ def _slice(engine, C, a, tstream, maxsym, n_global, dtype, weight_tag, tm):
         _, _, _, ua, ut = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype, uniform, -1)
         flags = C.allreduce_max(torch.tensor([int(ua), int(ut)], dtype=torch.int64, device=engine.device))
         force = int(flags[0].item()) | (int(flags[1].item()) << 1)
+    kw = {} if copy_out else {"copy": False}  # (engines without views always copy)
     indptr, indices, vals, _, _ = engine.csr_pair(a, tstream, maxsym, row_lo, row_hi - row_lo, n_global, dtype,
-                                                  uniform, force)
+                                                  uniform, force, **kw)
     tm["csr"] = (time.perf_counter() - t4) * 1e3
     return row_lo, row_hi, indptr, indices, vals
 
@@ -630,7 +639,8 @@ def _route(engine, C, local, dtype, gmap, n_global, maxsym, uniform, tm):
     return a, tstream
 
 
-def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo=False, names_root=None):
+def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, keep_coo=False, names_root=None,
+                           copy_out=True):
     """The decimal-id fast path (module docstring), or None when a range breaks its premise."""
     import time
 
@@ -654,7 +664,7 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
             and not opts.get("strip_orientation")):
         # one pass, no count: every range parses into global ids first and reports its evidence; one
         # all-gather decides for every rank at once (g2n_build_decimal_range)
-        got = engine.build_decimal_range(buf, opts, view=not keep_coo)
+        got = engine.build_decimal_range(buf, opts, view=not keep_coo, values=keep_coo)
         alle = C.allgather_list(got[1] if got is not None else [-1] * 6)
         tm["count"] = 0.0
         if all(e[0] >= 0 for e in alle):
@@ -677,7 +687,8 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
             return None
         s_base = int(sum(allc[k][1] for k in range(rank)))
         tm["count"] = (time.perf_counter() - t0) * 1e3
-        local = engine.build_decimal(buf, opts, s_base, n_seg, view=not keep_coo)
+        local = engine.build_decimal(buf, opts, s_base, n_seg, view=not keep_coo,
+                                     values=keep_coo or bool(opts.get("weight_tag")))
         # every range's ids are global decimals (the id map needs no exchange) — or nobody's are
         verdict = torch.tensor([0 if local is None else 1], dtype=torch.int64, device=engine.device)
         if int(C.allreduce_min(verdict).item()) == 0:
@@ -687,7 +698,7 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     local.dtype_name = opts.get("dtype", "float64")
     a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"), tm)
     row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
-                                                   opts.get("weight_tag"), tm)
+                                                   opts.get("weight_tag"), tm, copy_out)
     sums = C.allreduce_sum([local.n_cast_overflow, int(indices.numel()), int(local.rows.numel())], engine.device)
     out = ShardResult(status=0, n_lines=int(sum(c[0] for c in allc)), n_records=int(sum(c[3] for c in allc)),
                       n_edges=int(sum(c[2] for c in allc)), n_nodes=n_global, row_lo=row_lo, row_hi=row_hi,
@@ -706,13 +717,16 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
 
 def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, keep_directed_bidir=False,
                   asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None,
-                  gather_names=False, keep_coo=False, names_root=None, force_protocol=False) -> ShardResult:
+                  gather_names=False, keep_coo=False, names_root=None, force_protocol=False,
+                  copy_out=True) -> ShardResult:
     """Build this rank's byte range `buf` (uint8 tensor on the engine's device) as part of one
     file split over `group` in rank order; returns this rank's CSR row slice (and, keep_coo, the
     range's stream-order triplets over global ids: res.coo = (rows, cols, data)).
     gather_names: the node names in id order (res.names_blob / names_offsets) on every rank, or
     on rank `names_root` only.  force_protocol: run the general exchange even on one rank (whose
-    local ids are the global ones; measurement of the protocol's cost only)."""
+    local ids are the global ones; measurement of the protocol's cost only).  copy_out=False: the slice's
+    indptr / indices / data are views of the engine's context (no device copy; valid until the engine's
+    next call) — the bench's timed steps, which never read them."""
     import time
 
     import torch
@@ -729,7 +743,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     ktrip = 4 if tpe == 4 else (1 if gd else 2)
     tm = {}
     fast = None if force_protocol else _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm,
-                                                               keep_coo, names_root)
+                                                               keep_coo, names_root, copy_out)
     if fast is not None:
         return fast
     t0 = time.perf_counter()
@@ -797,7 +811,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         if keep_coo:
             out.coo = (local.rows, local.cols, local.data)
         a, tstream = _route(engine, C, local, dtype, None, out.n_nodes, maxsym, not weight_tag, tm)
-        return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()))
+        return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()), copy_out)
 
     # 3. names to owners, owner dedup in arrival (= global first-touch) order
     t1 = time.perf_counter()
@@ -879,12 +893,13 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     if keep_coo:
         out.coo = (local.rows, local.cols, local.data)
     a, tstream = _route(engine, C, local, dtype, None, n_global, maxsym, not weight_tag, tm)
-    return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()))
+    return _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, int(local.rows.numel()), copy_out)
 
 
-def _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, n_trip):
+def _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, n_trip, copy_out=True):
     """Step 6 and the result's index-dtype count (scipy_index_dtype)."""
-    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, out.n_nodes, dtype, weight_tag, tm)
+    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, out.n_nodes, dtype, weight_tag, tm,
+                                                   copy_out)
     out.row_lo, out.row_hi = row_lo, row_hi
     out.indptr, out.indices, out.data = indptr, indices, vals
     nnz, trip = C.allreduce_sum([int(indices.numel()), n_trip], engine.device)

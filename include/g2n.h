@@ -104,6 +104,8 @@ typedef struct g2n_options {
                                   [3] = S lines in the file (output G2N_OUT_COO, no names; returns
                                   G2N_E_UNSUPPORTED when the range needs the general protocol:
                                   ids that are not decimal, errors, warnings, slow weights);
+                                  [4] bit 2: no weight tag and the caller reads coordinates only —
+                                  the result's values are left unwritten;
                                   [5] = 0 */
 } g2n_options;
 
@@ -331,7 +333,7 @@ int g2n_count_device(g2n_context *ctx, const void *d_input, size_t len, int64_t 
  *             the premise needs d == the S lines of the ranges before),
  *          the largest edge key value (the premise needs it <= the file's S lines)}.
  * Options: output G2N_OUT_COO, no names, not bidirected, no weight tag, no strip (else G2N_E_ARG);
- * reserved[2..4] are set by the call.  G2N_E_UNSUPPORTED when the one pass declines (a line past
+ * reserved[2..4] are set by the call (reserved[4] bit 2 is kept: values left unwritten).  G2N_E_UNSUPPORTED when the one pass declines (a line past
  * its tile window, a record outside the lean shapes, S names that are not one decimal run, an S
  * line after an edge line in the range): the caller then counts the ranges (g2n_count_device) and
  * builds with reserved[2..4] (g2n_build_device), whose check decides.  Replaces the count pass of

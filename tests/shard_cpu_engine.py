@@ -66,7 +66,7 @@ class CpuEngine:
         po = sum(k in (b"P", b"O") for k in kind)
         return [len(lines), segs, edges, segs + edges + po]
 
-    def build_decimal(self, buf, opts, s_base, n_seg, view=False):
+    def build_decimal(self, buf, opts, s_base, n_seg, view=False, values=True):
         """The oracle's range build with its local ids mapped to GLOBAL decimal ids, or None when a
         key is not the canonical decimal of a segment (or the range has a warning / error)."""
         o = self.oracle.run(bytes(buf.numpy()), **opts)
@@ -94,7 +94,7 @@ class CpuEngine:
         sh.n_local_nodes = n_seg * (2 if bidir else 1)
         return sh
 
-    def build_decimal_range(self, buf, opts, view=False):
+    def build_decimal_range(self, buf, opts, view=False, values=True):
         """g2n_build_decimal_range's contract on the oracle: the range's COO over global decimal ids
         and its evidence [lines, S lines, edges, records, d, largest edge key], or None when the one
         pass would decline (not one run of canonical decimal S names, an S line after an edge line,
