@@ -1159,8 +1159,12 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (!local_done) phase(c, "tiles");
 
   // ---- K2: parse every line from its tile's LDS window
-  auto* ls = dget<uint64_t>(c, S_LS, n_lines + 1);
-  auto* kind = dget<uint8_t>(c, S_KIND, n_lines);
+  // A tile-local build (local_done) is parsed already: none of the full parse's per-line / per-touch /
+  // per-edge buffers is read, so none is allocated (C5-size inputs: ~100 GB of HBM).  z(n): a buffer
+  // size that is 1 for such a build.
+  auto z = [&](uint64_t n) -> uint64_t { return local_done ? 1 : n; };
+  auto* ls = dget<uint64_t>(c, S_LS, z(n_lines + 1));
+  auto* kind = dget<uint8_t>(c, S_KIND, z(n_lines));
   ParseOpts op{};
   op.bidir = bidir;
   op.keep = keep;
@@ -1173,17 +1177,20 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     G2N_HIP(hipMemcpyAsync(wt, o->weight_tag, wtl, hipMemcpyHostToDevice, c->stream));
     op.wt = wt;
   }
-  TouchOut T{dget<uint64_t>(c, S_NOFF, n_t), dget<uint32_t>(c, S_NLEN, n_t),
-             bidir ? dget<uint64_t>(c, S_OOFF, n_t) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, n_t) : nullptr,
-             dget<uint8_t>(c, S_TKIND, n_t)};
-  EdgeOut E{dget<double>(c, S_EW, n_e), dget<uint32_t>(c, S_ETB, n_e)};
+  TouchOut T{dget<uint64_t>(c, S_NOFF, z(n_t)), dget<uint32_t>(c, S_NLEN, z(n_t)),
+             bidir ? dget<uint64_t>(c, S_OOFF, z(n_t)) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, z(n_t)) : nullptr,
+             dget<uint8_t>(c, S_TKIND, z(n_t))};
+  // (E.w is read by k_values only for weights: a tile-local build has none)
+  EdgeOut E{dget<double>(c, S_EW, z(n_e)), dget<uint32_t>(c, S_ETB, z(n_e))};
   const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
   const uint64_t n_trip = n_e * (uint64_t)ktrip;
   // the stream-order COO holds int32 node ids (< 2^31 - 1, checked below) at 64-bit positions; the
   // partition counts its elements in 32 bits (more than 2^31 - 1 entries: int64 CSR indices, F2)
   if (n_trip >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 matrix entries");
-  auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
-  auto* cols = dget<int32_t>(c, S_COLS, n_trip);
+  // the group slots hold a grouped tile-local build's COO (GroupedCoo): rows / cols only for a rebuild
+  const bool in_groups = local_done && c->gcoo.active;
+  auto* rows = dget<int32_t>(c, S_ROWS, in_groups ? 1 : n_trip);
+  auto* cols = dget<int32_t>(c, S_COLS, in_groups ? 1 : n_trip);
   // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
   // the first S line names "1" (a cheap guess: a wrong one costs one extra parse)
   // options.reserved[4] bit 0: one byte range of a sharded build whose node ids are decimal and
@@ -1194,13 +1201,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool int_ids = n_t && (shard_dec || first_one);
   const bool lean = int_ids && (shard_dec || !(c->test_flags & kTestNoLean));
   if (int_ids) {
-    op.tid = dget<uint32_t>(c, S_TID, n_t);
+    op.tid = dget<uint32_t>(c, S_TID, z(n_t));
     op.n_seg = shard_dec ? (uint64_t)o->reserved[3] : n_s;
     op.s_base = shard_dec ? (uint64_t)o->reserved[2] : 0;
   }
-  auto* wl = dget<uint64_t>(c, S_WL, 2 * n_e);
+  auto* wl = dget<uint64_t>(c, S_WL, z(2 * n_e));
   auto* deferred = dget<DeferredLine>(c, S_DEFER, n_tiles + 1);
-  G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  if (!local_done) G2N_HIP(hipMemcpyAsync(ls + n_lines, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   phase(c, "_prep");
   auto parse = [&](const ParseOpts& po) {
     if (n_tiles)
@@ -1363,7 +1370,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (throw_after_ids) throw Failure(G2N_E_DEVICE, "test: injected failure after the ids");
 
   // ---- triplets (K6): stream-order COO with the dtype cast
-  void* data = dbuf(c, S_DATA, n_trip * dtype_size(dt));
+  // values: not for a grouped build whose every value is dtype(1) (the partition reads none)
+  void* data = dbuf(c, S_DATA, (in_groups && !o->weight_tag) ? 16 : n_trip * dtype_size(dt));
   const bool uni = !op.has_wt;  // no weight tag: every entry is dtype(1.0)
   const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
