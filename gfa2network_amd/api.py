@@ -143,6 +143,10 @@ def finalize(raw: RawResult, *, dtype: np.dtype, return_node_list: bool, raw_byt
         A = sp.coo_matrix((raw.data, (raw.rows, raw.cols)), shape=(n, n), dtype=dtype)
     else:
         A = sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=(n, n), dtype=dtype)
+        if raw.indptr.dtype == np.int64 and A.indptr.dtype != np.int64:
+            # scipy's own result keeps int64 here (coo.tocsr of more than 2^31 - 1 triplets sizes its
+            # arrays by the triplets; the constructor's content check would narrow them)
+            A.indices, A.indptr = raw.indices, raw.indptr
     if return_node_list:
         return A, _node_list(raw, raw_bytes_id)
     return A

@@ -513,9 +513,12 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   // scipy's index dtype (get_index_dtype(maxval=nnz)): int64 indptr / indices once the result holds
   // more than 2^31 - 1 entries (utils.py:55 coo.tocsr, builders.py:283 maximum) — only possible when
   // the partition's upper bound passes it, so the total is read only then
-  // (a bucket's merged entries never outnumber its expanded input: the result holds <= n_el entries)
-  const bool wide = (c->test_flags & kTestIndex64) ||
-                    (n_el > 0x7FFFFFFFull && (uint64_t)read_dev(c, boff + n_bk) > 0x7FFFFFFFull);
+  // coo.tocsr() (the SUM CSR) sizes its index dtype by the COO's entries, duplicates included
+  // (scipy _coo_to_compressed: maxval = coo.nnz; sum_duplicates keeps the dtype); A.maximum(A.T) by
+  // the result's entries (_binopt's arrays, then the constructor's check_contents downcast).  A
+  // bucket's merged entries never outnumber its expanded input: the result holds <= n_el entries.
+  const bool wide = (c->test_flags & kTestIndex64) || (sum && !pair && n_trip > 0x7FFFFFFFull) ||
+                    (!sum && n_el > 0x7FFFFFFFull && (uint64_t)read_dev(c, boff + n_bk) > 0x7FFFFFFFull);
   if (wide) {
     if (pair) throw Failure(G2N_E_UNSUPPORTED, "a sharded row slice of more than 2^31-1 entries");
     auto* indptr64 = dget<int64_t>(c, S_INDPTR64, n_rows + 1);
