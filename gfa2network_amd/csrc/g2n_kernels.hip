@@ -924,8 +924,8 @@ __device__ inline bool dec_words(uint64_t w0, uint64_t w1, uint32_t x, uint32_t 
 
 // tab bits of the 64 staged bytes from chunk q: from the tile's tab bitmap, or (tabm == nullptr)
 // recomputed from the staged bytes (the LDS-lean instance keeps no bitmap)
-#ifndef G2N_TAB_B64  // experiment builds: 1 = the window from two aligned 8-byte LDS reads
-#define G2N_TAB_B64 0
+#ifndef G2N_TAB_B64  // 1: the window from two aligned 8-byte LDS reads (C4 parse 3.47 -> 3.43 ms); 0: four u16 reads
+#define G2N_TAB_B64 1
 #endif
 __device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, uint32_t q) {
 #if G2N_TAB_B64
