@@ -36,7 +36,7 @@ EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
-    "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
@@ -244,8 +244,11 @@ def load() -> ctypes.CDLL:
     lib.g2n_count_device.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(I64)]
     lib.g2n_build_decimal_range.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(Options), ctypes.POINTER(I64),
                                             ctypes.POINTER(Result)]
+    lib.g2n_order_keys.argtypes = [P, P, P, U64, P, U32, P]
+    lib.g2n_rank_keys.argtypes = [P, P, U64, P, P, U32, U32, P]
     for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
-              "g2n_upload_file_range", "g2n_count_device", "g2n_build_decimal_range"):
+              "g2n_upload_file_range", "g2n_count_device", "g2n_build_decimal_range", "g2n_order_keys",
+              "g2n_rank_keys"):
         getattr(lib, f).restype = ctypes.c_int
     if lib.g2n_abi_version() != ABI_VERSION:
         raise NativeUnavailable("libg2n.so ABI version mismatch; rebuild it")

@@ -1853,6 +1853,30 @@ uint64_t gather_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, c
   return (uint64_t)total;
 }
 
+void order_keys(g2n_context* c, const uint32_t* first_of, const int64_t* src_idx, uint64_t nd, const uint64_t* h_ends,
+                uint32_t n_src, uint64_t* out) {
+  begin_call(c);
+  if (n_src == 0 || n_src > 4096) throw Failure(G2N_E_ARG, "n_src out of range");
+  if (!nd) return;
+  auto* ends = dget<uint64_t>(c, S_TEMP, n_src);
+  G2N_HIP(hipMemcpyAsync(ends, h_ends, n_src * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_order_keys, dim3(grid_for(nd)), dim3(kTPB), 0, c->stream, first_of, src_idx, nd,
+                     (const uint64_t*)ends, n_src, out);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+void rank_keys(g2n_context* c, const uint64_t* keys, uint64_t n, const uint64_t* all, const uint64_t* h_all_off,
+               uint32_t n_ranks, uint32_t self, int64_t* out) {
+  begin_call(c);
+  if (n_ranks == 0 || n_ranks > 4096 || self >= n_ranks) throw Failure(G2N_E_ARG, "ranks out of range");
+  if (!n) return;
+  auto* off = dget<uint64_t>(c, S_TEMP, n_ranks + 1);
+  G2N_HIP(hipMemcpyAsync(off, h_all_off, (n_ranks + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_rank_keys, dim3(grid_for(n)), dim3(kTPB), 0, c->stream, keys, n, all, (const uint64_t*)off,
+                     n_ranks, self, out);
+  G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
 void remap_pairs(g2n_context* c, const uint32_t* map, uint64_t n_map, int32_t* rows, int32_t* cols, uint64_t n) {
   begin_call(c);
   if (n) {
@@ -2087,6 +2111,20 @@ int g2n_gather_keys(g2n_context* ctx, const uint8_t* d_blob, const int64_t* d_of
   if (!out_len || !d_out_offsets || (n && (!d_offsets || !d_index || (out_cap && !d_out_blob)))) return G2N_E_ARG;
   G2N_CTX_CALL(ctx, *out_len = g2n::gather_keys(ctx, d_blob, d_offsets, d_index, n, d_out_blob, out_cap,
                                                 d_out_offsets));
+  return G2N_OK;
+}
+
+int g2n_order_keys(g2n_context* ctx, const uint32_t* d_first_of, const int64_t* d_src_idx, uint64_t nd,
+                   const uint64_t* src_ends, uint32_t n_src, uint64_t* d_out) {
+  if (!src_ends || (nd && (!d_first_of || !d_src_idx || !d_out))) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::order_keys(ctx, d_first_of, d_src_idx, nd, src_ends, n_src, d_out));
+  return G2N_OK;
+}
+
+int g2n_rank_keys(g2n_context* ctx, const uint64_t* d_keys, uint64_t n, const uint64_t* d_all,
+                  const uint64_t* all_offsets, uint32_t n_ranks, uint32_t self_rank, int64_t* d_out) {
+  if (!all_offsets || (n && (!d_keys || !d_out))) return G2N_E_ARG;
+  G2N_CTX_CALL(ctx, g2n::rank_keys(ctx, d_keys, n, d_all, all_offsets, n_ranks, self_rank, d_out));
   return G2N_OK;
 }
 

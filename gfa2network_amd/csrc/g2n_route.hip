@@ -168,4 +168,49 @@ __global__ void k_route_starts(const uint32_t* __restrict__ off, uint64_t n_blk,
   else if (k == n_ranks) starts[k] = (uint32_t)n;
 }
 
+// ---- the general protocol's global ids (shard.py step 4), one thread per distinct key -------------
+// Order key of an owner's distinct key j: (source rank, the key's local id there) of its first
+// arrival f = first_of[j]; the source is the one whose arrival range [ends[s - 1], ends[s]) holds f.
+// Ranges are contiguous and every source's keys arrive in its local-id order, so these keys ascend
+// with j and sort the owner's keys by global first touch (builders.py:194-198 across byte ranges).
+__global__ void __launch_bounds__(kTPB) k_order_keys(const uint32_t* __restrict__ first_of,
+                                                     const int64_t* __restrict__ src_idx, uint64_t nd,
+                                                     const uint64_t* __restrict__ ends, uint32_t n_src,
+                                                     uint64_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (j >= nd) return;
+  const uint64_t f = first_of[j];
+  uint32_t lo = 0, hi = n_src;  // first s with ends[s] > f
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ends[mid] <= f) lo = mid + 1;
+    else hi = mid;
+  }
+  out[j] = ((uint64_t)lo << 32) | (uint64_t)(uint32_t)src_idx[f];
+}
+
+// Global id of distinct key j of owner `self`: j + the number of smaller order keys every other owner
+// holds (each owner's keys ascend; all owners' keys are distinct) — the rank in the merged order.
+__global__ void __launch_bounds__(kTPB) k_rank_keys(const uint64_t* __restrict__ keys, uint64_t n,
+                                                    const uint64_t* __restrict__ all,
+                                                    const uint64_t* __restrict__ all_off, uint32_t n_ranks,
+                                                    uint32_t self, int64_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t x = keys[j];
+  uint64_t g = j;
+  for (uint32_t o = 0; o < n_ranks; o++) {
+    if (o == self) continue;
+    uint64_t lo = all_off[o], hi = all_off[o + 1];  // lower bound of x in all[lo, hi)
+    const uint64_t b = lo;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (all[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    g += lo - b;
+  }
+  out[j] = (int64_t)g;
+}
+
 }  // namespace g2n

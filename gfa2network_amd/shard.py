@@ -406,6 +406,32 @@ class HipEngine:
                     "g2n_gather_keys")
         return oblob[:got.value], ooffs
 
+    def order_keys(self, first_of, src_idx, src_counts):
+        """Each distinct key's order key (source rank << 32 | its local id there) — g2n_order_keys."""
+        torch = self.torch
+        nd = first_of.numel()
+        out = torch.empty(max(nd, 1), dtype=torch.int64, device=self.device)
+        ends = np.cumsum(np.asarray(src_counts, dtype=np.uint64)).astype(np.uint64)
+        self._sync()
+        self._check(self.lib.g2n_order_keys(self.ctx, first_of.data_ptr() if nd else None,
+                                            src_idx.data_ptr() if nd else None, nd, ends.ctypes.data, len(ends),
+                                            out.data_ptr()), "g2n_order_keys")
+        return out[:nd]
+
+    def rank_keys(self, keys, all_keys, rank: int):
+        """Global ids: each key's index plus the smaller keys of every other owner (g2n_rank_keys)."""
+        torch = self.torch
+        n = keys.numel()
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        offs = np.zeros(len(all_keys) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([x.numel() for x in all_keys])
+        flat = torch.cat([x.to(self.device) for x in all_keys]) if len(all_keys) > 1 else all_keys[0]
+        self._sync()
+        self._check(self.lib.g2n_rank_keys(self.ctx, keys.data_ptr() if n else None, n,
+                                           flat.data_ptr() if flat.numel() else None, offs.ctypes.data, len(all_keys),
+                                           rank, out.data_ptr()), "g2n_rank_keys")
+        return out[:n]
+
     def remap_pairs(self, rows, cols, gmap):
         """rows / cols (int32) through the local -> global id map, in place."""
         n = rows.numel()
@@ -815,10 +841,19 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
 
     # 3. names to owners, owner dedup in arrival (= global first-touch) order
     t1 = time.perf_counter()
-    pb, po, pidx, pst = engine.partition_keys(local.names_blob, local.names_offsets, world)
+    if world == 1:  # one owner: the keys stay where they are, in local-id order
+        n_loc = int(local.n_local_nodes)
+        pb, po = local.names_blob, local.names_offsets
+        pidx = torch.arange(n_loc, dtype=torch.int32, device=dev)
+        pst_l, po_l = [0, n_loc], [0, int(po[-1].item()) if n_loc else 0]
+    else:
+        pb, po, pidx, pst = engine.partition_keys(local.names_blob, local.names_offsets, world)
+        if local.n_local_nodes:  # the owners' key and byte counts in one host read
+            both = torch.cat([pst.to(torch.int64), po[pst.to(torch.int64)]]).tolist()
+            pst_l, po_l = both[:world + 1], both[world + 1:]
+        else:
+            pst_l, po_l = pst.tolist(), [0] * (world + 1)
     tm["partition_keys"] = (time.perf_counter() - t1) * 1e3
-    pst_l = pst.tolist()
-    po_l = po[pst.to(torch.int64)].tolist() if local.n_local_nodes else [0] * (world + 1)
     key_counts = [pst_l[k + 1] - pst_l[k] for k in range(world)]
     byte_counts = [int(po_l[k + 1] - po_l[k]) for k in range(world)]
     lens = (po[1:] - po[:-1]) if local.n_local_nodes else torch.zeros(0, dtype=torch.int64, device=dev)
@@ -833,18 +868,14 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     tm["dedup_keys"] = (time.perf_counter() - t7) * 1e3
     # order key (source rank, local id) of each distinct key: global first-touch order
     fo = first_of.to(torch.int64)
-    k_end = torch.tensor(np.cumsum(r_kc), dtype=torch.int64, device=dev)
-    dkey = (torch.searchsorted(k_end, fo, right=True) << 32) | r_idx[fo] if nd else r_idx[:0]
+    dkey = engine.order_keys(first_of, r_idx, r_kc) if nd else r_idx[:0]
     tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
 
     # 4. global ids: rank of each distinct key's order key among all owners'
     t2 = time.perf_counter()
     all_dkey = C.allgather_v(dkey)
     n_global = int(sum(x.numel() for x in all_dkey))
-    gid = torch.arange(nd, dtype=torch.int64, device=dev)
-    for o, other in enumerate(all_dkey):
-        if o != rank and other.numel() and nd:
-            gid += torch.searchsorted(other, dkey)
+    gid = engine.rank_keys(dkey, all_dkey, rank) if world > 1 else torch.arange(nd, dtype=torch.int64, device=dev)
     del all_dkey
     back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
     gmap = None

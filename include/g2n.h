@@ -316,6 +316,19 @@ int g2n_csr_from_coo_pair(g2n_context *ctx, const int32_t *a_rows, const int32_t
                           uint64_t t_nnz, int32_t maxsym, int64_t row_base, uint64_t n_rows, uint64_t n_cols,
                           int32_t dtype, int32_t uniform, int32_t force_unsorted, g2n_result *out);
 
+/* The general protocol's global node ids (shard.py step 4; builders.py:194-198 first-touch order
+ * across byte ranges), on an owner rank's distinct keys (g2n_dedup_keys):
+ * g2n_order_keys: out[j] = (source rank << 32) | the key's local id there, for the key's first arrival
+ *   f = d_first_of[j], the source being the one whose arrival range holds f (src_ends: the sources'
+ *   inclusive arrival-count prefix sums, host memory, n_src <= 4096); d_src_idx[f] = the local id the
+ *   source sent with arrival f.  The keys ascend with j.
+ * g2n_rank_keys: out[j] = j + the number of keys smaller than d_keys[j] in every other owner's sorted
+ *   run of d_all (runs at all_offsets[o] .. all_offsets[o + 1], host memory): the key's global id. */
+int g2n_order_keys(g2n_context *ctx, const uint32_t *d_first_of, const int64_t *d_src_idx, uint64_t nd,
+                   const uint64_t *src_ends, uint32_t n_src, uint64_t *d_out);
+int g2n_rank_keys(g2n_context *ctx, const uint64_t *d_keys, uint64_t n, const uint64_t *d_all,
+                  const uint64_t *all_offsets, uint32_t n_ranks, uint32_t self_rank, int64_t *d_out);
+
 /* One rank's byte range of a file split over ranks: bytes [offset, offset + len) of path, read
  * with pread into pinned staging slots and copied to d_dst (len bytes of `device`'s HBM). */
 int g2n_upload_file_range(const char *path, uint64_t offset, uint64_t len, void *d_dst, int32_t device);

@@ -144,6 +144,22 @@ class CpuEngine:
         return (torch.from_numpy(np.frombuffer(oblob, dtype=np.uint8).copy()), torch.from_numpy(ooff),
                 torch.from_numpy(order.astype(np.int32)), torch.from_numpy(starts))
 
+    def order_keys(self, first_of, src_idx, src_counts):
+        """g2n_order_keys on the host: (source rank << 32) | local id of each distinct key's first arrival."""
+        f = first_of.numpy().astype(np.int64)
+        ends = np.cumsum(np.asarray(src_counts, dtype=np.int64))
+        src = np.searchsorted(ends, f, side="right").astype(np.int64)
+        return torch.from_numpy((src << 32) | src_idx.numpy().astype(np.int64)[f])
+
+    def rank_keys(self, keys, all_keys, rank):
+        """g2n_rank_keys on the host: index + the smaller keys of every other owner."""
+        k = keys.numpy()
+        g = np.arange(len(k), dtype=np.int64)
+        for o, other in enumerate(all_keys):
+            if o != rank and other.numel():
+                g += np.searchsorted(other.numpy(), k, side="left")
+        return torch.from_numpy(g)
+
     def dedup_keys(self, blob, offsets):
         b, off = blob.numpy().tobytes(), offsets.numpy()
         seen, ids, first = {}, [], []
