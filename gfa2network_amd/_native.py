@@ -335,6 +335,7 @@ class RawResult:
     indices: np.ndarray | None = None
     data: np.ndarray | None = None
     sum_sorted: bool = True
+    sum_buckets: bool = False  # the CSR came from the bucket partition (g2n_sym.hip), not the row sums
     n_cast_overflow: int = 0
     input_bytes: int = 0
     phase_ms: dict = field(default_factory=dict)
@@ -355,6 +356,7 @@ def _from_result(ptr, rc: int) -> RawResult:
     out.n_records_before_error, out.n_edges, out.n_nodes = r.n_records_before_error, r.n_edges, r.n_nodes
     out.dtype = CODE_DTYPES.get(r.dtype, np.dtype("float64"))
     out.sum_sorted = bool(r.sum_sorted)
+    out.sum_buckets = r.sum_sorted < 0
     out.n_cast_overflow = int(r.n_cast_overflow)
     out.input_bytes = int(r.input_bytes)
     if r.format == FMT_TEXT and r.data:

@@ -81,6 +81,7 @@ struct Ctl {
   unsigned long long bad_id;          // k_remap_pairs met an id outside its map
   unsigned long long ev_dmin, ev_dmax;  // k_tile_lean_evidence: a range's S-name offsets (+ 2^62)
   unsigned long long ev_vmax;           //   and its largest edge key
+  unsigned long long w_inexact;         // the weighted bucket SUM's exactness broke (k_weight_encode / k_sumw_finish)
 };
 
 struct ParseOpts {

@@ -2741,25 +2741,51 @@ __global__ void __launch_bounds__(kTPB) k_triplets(EdgeIn E, uint64_t n_e, const
   }
 }
 
+// A value as an exact int32 (bool: 0 / 1); bad when a float value is not exactly one (fraction, |v| >= 2^31,
+// -0.0, inf, nan).  k_values (g2n_kernels.hip) encodes beside the cast; k_weight_encode otherwise.
+template <class T>
+__device__ inline uint32_t weight_enc(T v, bool& bad) {
+  if constexpr (std::is_floating_point<T>::value) {
+    const double d = (double)v;
+    bad = !(d == __builtin_trunc(d)) || !(d > -2147483648.0 && d < 2147483648.0) || (d == 0.0 && __builtin_signbit(d));
+    return bad ? 0u : (uint32_t)(int32_t)d;
+  } else if constexpr (std::is_same<T, uint8_t>::value) {
+    bad = false;
+    return v != 0 ? 1u : 0u;
+  } else {
+    bad = false;
+    return (uint32_t)(int32_t)v;
+  }
+}
+
 // Lean decimal-id builds: the parse wrote rows / cols; this writes the values (k_triplets'
 // cast, errors and float32-overflow count) when an output needs them.  uniform: no weight tag,
-// every value is dtype(1.0) (no cast can fail).
+// every value is dtype(1.0) (no cast can fail).  enc (weighted SUM CSR outputs): the values'
+// exact-int32 codes beside them for the bucket partition (csr_partition_w), ctl->w_inexact when
+// one has none.
 template <class T>
 __global__ void __launch_bounds__(kTPB) k_values(const double* __restrict__ w, uint64_t n_e, int ktrip, int uniform,
-                                                 T* __restrict__ data, Ctl* ctl) {
+                                                 T* __restrict__ data, Ctl* ctl, uint32_t* __restrict__ enc) {
   const uint64_t e = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
-  if (e >= n_e) return;
-  const double wv = uniform ? 1.0 : w[e];
-  T v;
-  const uint32_t err = Cast<T>::go(wv, &v);
-  if (std::is_same<T, float>::value && !__builtin_isinf(wv) && wv == wv && __builtin_isinf((double)v))
-    atomicAdd(&ctl->n_f32_overflow, 1ull);
-  const uint64_t o = e * (uint64_t)ktrip;
-  if (err) {
-    atomicMin(&ctl->cast_key, (unsigned long long)((o << 4) | err));
-    return;
+  bool bad = false;
+  if (e < n_e) {
+    const double wv = uniform ? 1.0 : w[e];
+    T v;
+    const uint32_t err = Cast<T>::go(wv, &v);
+    if (std::is_same<T, float>::value && !__builtin_isinf(wv) && wv == wv && __builtin_isinf((double)v))
+      atomicAdd(&ctl->n_f32_overflow, 1ull);
+    const uint64_t o = e * (uint64_t)ktrip;
+    if (err) {
+      atomicMin(&ctl->cast_key, (unsigned long long)((o << 4) | err));
+    } else {
+      for (int j = 0; j < ktrip; j++) data[o + j] = v;
+      if (enc) {
+        const uint32_t x = weight_enc<T>(v, bad);
+        for (int j = 0; j < ktrip; j++) enc[o + j] = x;
+      }
+    }
   }
-  for (int j = 0; j < ktrip; j++) data[o + j] = v;
+  if (enc && __ballot(bad) && (threadIdx.x & 63) == 0) ctl->w_inexact = 1;
 }
 
 // ======================================================= K7-K9: COO -> CSR ========
@@ -3670,7 +3696,7 @@ __global__ void __launch_bounds__(kTPB) k_edge_text(const int32_t* __restrict__ 
                                                  const uint32_t*, const RowVal<T, U>::type*, T, uint64_t,        \
                                                  uint32_t*, const uint32_t*, int32_t*, int32_t*, T*);
 #define G2N_INST(T)                                                                                              \
-  template __global__ void k_values<T>(const double*, uint64_t, int, int, T*, Ctl*);                             \
+  template __global__ void k_values<T>(const double*, uint64_t, int, int, T*, Ctl*, uint32_t*);                             \
   template __global__ void k_triplets<T>(EdgeIn, uint64_t, const uint32_t*, const DictEntry*,                      \
                                          const uint32_t*, int, int, int32_t*, int32_t*, T*, Ctl*);                \
   template __global__ void k_row_emulate<T>(const uint32_t*, uint64_t, const uint8_t*, const PV<T>*, uint32_t*,    \

@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_NSLOTS
 };
 
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
@@ -97,6 +97,7 @@ struct g2n_context {
   uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
   uint64_t err_line_off = 0;  // byte offset of the last build's error line (edge-list prefix)
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
+  const uint32_t* wenc = nullptr;  // the current build's values as exact-int32 codes (k_values), if written
   bool no_group = false;      // redo of a build whose group-slot COO the partition refused
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
@@ -186,6 +187,7 @@ static void clear_call_state(g2n_context* c) {
     c->side_pending = false;
   }
   c->gcoo = GroupedCoo{};
+  c->wenc = nullptr;
 }
 
 template <class T>
@@ -552,12 +554,119 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   return true;
 }
 
+// Weighted coo.tocsr() (utils.py:55 / builders.py:281 with a weight tag) through the same bucket
+// partition, when no duplicate sum can depend on scipy's summation order (k_weight_encode: integer
+// dtypes and bool always; float values that are integers of |v| < 2^31, not -0.0, with every
+// entry's sum of magnitudes exact in T — checked per run by k_sumw_finish).  Passes 5 / 6 carry
+// each element's value (u32) beside it; F1w sums a row's column runs in any order.  False, with
+// nothing usable written, when the partition declines (as csr_partition) or the premise fails:
+// the caller then runs the stable row-sum path.
+template <class T>
+static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
+                            uint64_t n_rows, uint64_t n_cols, g2n_result* R) {
+  if (n_rows >= (1ull << 30) || n_cols >= (1ull << 30) || n_trip > 0x7FFFFFFFull) return false;
+  const int bits = bits_for(n_rows);
+  const double per_row = (double)n_trip / (double)(n_rows ? n_rows : 1);
+  int low = 0;
+  while ((1u << (low + 1)) <= kFinTPB) low++;
+  while (low > 1 && (double)(1u << low) * per_row > (double)(kSymCap / 2)) low--;
+  if (low > bits) low = bits;
+  const int hb = bits - low;
+  if (hb > 2 * (int)kMaxDigitBits) return false;
+  const int bits1 = hb > (int)kMaxDigitBits ? std::max(hb - (int)kMaxDigitBits, std::min(8, (hb + 1) / 2)) : hb;
+  const int bits2 = hb - bits1;
+  const uint32_t n_dig1 = 1u << bits1, n_dig2 = 1u << bits2;
+  const uint64_t n_el = n_trip;
+  const uint64_t n_buckets = 1ull << hb;
+  const uint64_t n_bk = (n_rows + (1ull << low) - 1) >> low;
+  const uint32_t shift1 = (uint32_t)(low + bits2);
+  const uint32_t* enc = c->wenc;  // k_values wrote the codes beside the values (and w_inexact)
+  if (!enc) {
+    auto* e = dget<uint32_t>(c, S_WENC, n_el);
+    G2N_HIP(hipMemsetAsync(&c->ctl->w_inexact, 0, sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL((k_weight_encode<T>), dim3(grid_for(n_el)), dim3(kTPB), 0, c->stream, data, n_el, e, c->ctl);
+    enc = e;
+  }
+  G2N_HIP(hipMemsetAsync(&c->ctl->bucket_overflow, 0, sizeof(unsigned long long), c->stream));
+  PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, 1u, nullptr, nullptr, 0, 0, nullptr, nullptr,
+              nullptr, 0, nullptr, 0, (uint32_t)low + 1u, enc, nullptr};
+  // pass 5: the entries with their values, adjacent transposed twins of one value as one element
+  const uint64_t n_blk1 = (n_el + kPartTile - 1) / kPartTile;
+  auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
+  auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
+  auto* el1 = dget<uint2>(c, S_EL0, n_el);
+  auto* w1 = dget<uint32_t>(c, S_W1, n_el);
+  hipLaunchKernelGGL(k_part_hist<5>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1, cnt1,
+                     n_blk1);
+  scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+  hipLaunchKernelGGL(k_part_scatter<5>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
+                     (const uint32_t*)off1, n_blk1, el1, w1);
+  auto* bst = dget<uint32_t>(c, S_BSTART, n_buckets + 1);
+  const uint2* el = el1;
+  const uint32_t* ew = w1;
+  if (bits2 == 0) {
+    hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst);
+  } else {  // pass 6 inside each pass-5 group
+    auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
+    PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0,
+               nullptr, w1};
+    hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
+                       n_blk1, n_dig1, grp, grp + n_dig1 + 1);
+    const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
+    auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
+    auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
+    auto* el2 = dget<uint2>(c, S_EL1, n_el);
+    auto* w2 = dget<uint32_t>(c, S_W2, n_el);
+    hipLaunchKernelGGL(k_part_hist<6>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
+                       n_dig2, cnt2, n_blk2);
+    scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+    hipLaunchKernelGGL(k_part_scatter<6>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
+                       n_dig2, (const uint32_t*)off2, n_blk2, el2, w2);
+    hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                       (const uint32_t*)off2, s2, n_dig2, n_buckets, bst);
+    el = el2;
+    ew = w2;
+  }
+  phase(c, "sum");
+  auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
+  auto* btot = dget<uint32_t>(c, S_BTOT, n_bk);
+  // staged merged entries (F1w -> F2w): at most two per element (kElPair) — columns in the dead
+  // partition buffer's 8 bytes per element, values in their own array
+  auto* tcol = (uint32_t*)(el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1);
+  T* tval = dget<T>(c, S_TVAL, 2 * n_el);
+  hipLaunchKernelGGL((k_sumw_finish<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el, ew,
+                     (const uint32_t*)bst, (uint32_t)low, n_rows, btot, tcol, tval, indptr, c->ctl);
+  auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
+  scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk, boff + n_bk);
+  sync_ctl(c);
+  if (c->h_ctl->bucket_overflow || c->h_ctl->w_inexact) return false;
+  auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_el);
+  T* odata = dget<T>(c, S_ODATA, 2 * n_el);
+  hipLaunchKernelGGL((k_sumw_place<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, (const uint32_t*)bst,
+                     (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (const uint32_t*)tcol,
+                     (const T*)tval, indptr, indices, odata);
+  R->format = G2N_FMT_CSR;
+  R->indptr = indptr;
+  R->nnz = (int64_t)read_dev(c, indptr + n_rows);
+  R->indices = indices;
+  R->data = odata;
+  R->sum_sorted = -1;  // not computed: these sums cannot depend on scipy's order
+  R->sum_t_sorted = -1;
+  phase(c, "csr");
+  return true;
+}
+
 template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
                        uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
   if constexpr (kU) {
     if (n_trip && n_rows && (n_rows == n_cols || !maxsym) && !(c->test_flags & kTestNoBuckets) &&
         csr_partition<T>(c, rows, cols, n_trip, n_rows, !maxsym, R))
+      return;
+  } else {
+    if (n_trip && n_rows && !maxsym && !c->gcoo.active && !(c->test_flags & kTestNoBuckets) &&
+        csr_partition_w<T>(c, rows, cols, data, n_trip, n_rows, n_cols, R))
       return;
   }
   if (c->gcoo.active) {  // the group slots hold no stream order: redo the build without them
@@ -1384,8 +1493,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool no_values = shard_dec && uni && (o->reserved[4] & 4) != 0;
   if (coords_done) {  // values only, and only when the output or the sums read them
     if (n_e && (coo_out || !uni) && !no_values) {
+      // a weighted SUM CSR: the exact-int32 codes the bucket partition sums (csr_partition_w) beside
+      uint32_t* enc = nullptr;
+      if (!uni && !maxsym && o->output == G2N_OUT_CSR && !(c->test_flags & kTestNoBuckets) && n_trip <= 0x7FFFFFFFull)
+        c->wenc = enc = dget<uint32_t>(c, S_WENC, n_trip);
 #define G2N_VALUES(T) \
-  hipLaunchKernelGGL(k_values<T>, dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E.w, n_e, ktrip, (int)uni, (T*)data, c->ctl)
+  hipLaunchKernelGGL(k_values<T>, dim3(grid_for(n_e)), dim3(kTPB), 0, c->stream, E.w, n_e, ktrip, (int)uni, (T*)data, \
+                     c->ctl, enc)
       switch (dt) {
         case G2N_BOOL: G2N_VALUES(uint8_t); break;
         case G2N_INT8: G2N_VALUES(int8_t); break;

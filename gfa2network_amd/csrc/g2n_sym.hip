@@ -114,7 +114,17 @@ struct PartSrc {
   uint64_t gcap;          //   from entry b * gcap
   uint32_t pair_bits;     // pass 1, two per entry: 0, or low + 1 — an entry whose rows agree above bit
                           //   low (one bucket) is one kElPair element
+  const uint32_t* vals = nullptr;  // weighted SUM (passes 5 / 6): the entries' values as exact int32
+  const uint32_t* in_w = nullptr;  //   pass 6: the values beside `in`
 };
+
+// Passes 5 / 6: passes 4 / 2 of the weighted SUM CSR (coo.tocsr of a weighted COO whose duplicate
+// sums cannot depend on their order — k_weight_encode checked): each element carries its value, a
+// u32 in a parallel array, and two twins pair only when their values are equal.
+template <int kPass>
+constexpr int kBase = kPass == 5 ? 4 : kPass == 6 ? 2 : kPass;
+template <int kPass>
+constexpr bool kHasW = kPass >= 5;
 
 struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e0/2, e1/2))
   uint64_t e0, e1;
@@ -128,7 +138,7 @@ struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e
 // for every edge); 2 = pass 2 over pass-1 groups
 template <int kPass>
 __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) {
-  if (kPass != 2 && S.gcount) {
+  if (kBase<kPass> != 2 && S.gcount) {
     const uint64_t per = kPass == 1 ? 2 : 1;  // element slots per entry
     B.g = 0;
     B.j = blk;
@@ -137,7 +147,7 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
     B.e1 = B.e0 + (uint64_t)S.gcount[blk] * per;
     return true;
   }
-  if (kPass != 2) {
+  if (kBase<kPass> != 2) {
     B.g = 0;
     B.j = blk;
     B.nb = 0;
@@ -173,7 +183,7 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
 #define G2N_PART_EL4 8
 #endif
 template <int kPass>
-constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : kPass == 4 ? G2N_PART_EL4 : G2N_PART_EL2;
+constexpr uint32_t kElPer = kPass == 1 ? 2 * kSubPer : kBase<kPass> == 4 ? G2N_PART_EL4 : kPass == 6 ? 8 : G2N_PART_EL2;
 template <int kPass>
 constexpr uint32_t kSubEl = kElPer<kPass> * kPartTPB;  // element slots per sub-tile
 
@@ -181,6 +191,7 @@ template <int kPass>
 struct PartRaw {
   static constexpr uint32_t kN = kPass == 1 ? kSubPer : kElPer<kPass>;
   uint2 v[kN];
+  uint32_t w[kHasW<kPass> ? kN : 1];  // weighted passes: the values
   uint32_t valid;  // bit k: v[k] holds an entry / element
 };
 
@@ -193,16 +204,18 @@ __device__ inline void part_fetch(const PartSrc& S, uint64_t e, uint64_t e1, Par
 #pragma unroll
   for (uint32_t k = 0; k < PartRaw<kPass>::kN; k++) {
     r.v[k] = make_uint2(0, 0);
+    if constexpr (kHasW<kPass>) r.w[k] = 0;
     if (kPass == 1) {
       const uint64_t i = e / 2 + threadIdx.x + (uint64_t)k * kPartTPB;
       if (2 * i < e1) {
         r.v[k] = make_uint2(S.rows[i], S.cols[i]);
         r.valid |= 1u << k;
       }
-    } else if (kPass == 4) {  // adjacent entries per thread: item k / 2 = entries i0, i0 + 1
+    } else if (kBase<kPass> == 4) {  // adjacent entries per thread: item k / 2 = entries i0, i0 + 1
       const uint64_t i = e + 2 * (threadIdx.x + (uint64_t)(k / 2) * kPartTPB) + (k & 1);
       if (i < e1) {
         r.v[k] = make_uint2(S.rows[i] - S.row_base, S.cols[i]);
+        if constexpr (kHasW<kPass>) r.w[k] = S.vals[i];
         r.valid |= 1u << k;
       }
     } else if (kPass == 3) {
@@ -217,6 +230,7 @@ __device__ inline void part_fetch(const PartSrc& S, uint64_t e, uint64_t e1, Par
       const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
       if (i < e1) {
         r.v[k] = S.in[i];
+        if constexpr (kHasW<kPass>) r.w[k] = S.in_w[i];
         r.valid |= 1u << k;
       }
     }
@@ -243,11 +257,12 @@ __device__ inline uint32_t part_valid(const PartSrc& S, const PartRaw<kPass>& r)
     for (uint32_t k = 0; k < kSubPer; k++)
       valid |= (r.valid >> k & 1u) ? (part_pair<kPass>(S, r.v[k]) ? 1u : 3u) << (2 * k) : 0u;
     return valid;
-  } else if constexpr (kPass == 4) {
+  } else if constexpr (kBase<kPass> == 4) {
     uint32_t valid = r.valid;
 #pragma unroll
     for (uint32_t k = 0; k < kElPer<kPass>; k += 2)
-      if ((r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1])) valid &= ~(2u << k);
+      if ((r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1]) && (!kHasW<kPass> || r.w[k] == r.w[k + 1]))
+        valid &= ~(2u << k);
     return valid;
   } else {
     return r.valid;
@@ -258,8 +273,9 @@ __device__ inline uint2 part_elem(const PartSrc& S, const PartRaw<kPass>& r, uin
   if constexpr (kPass == 1) {
     const uint2 v = r.v[k / 2];
     return (k & 1) ? sym_elem(v.y, v.x, kElSide1) : sym_elem(v.x, v.y, part_pair<kPass>(S, v) ? kElPair : 0u);
-  } else if constexpr (kPass == 4) {
-    const bool tw = !(k & 1) && (r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1]);
+  } else if constexpr (kBase<kPass> == 4) {
+    const bool tw = !(k & 1) && (r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1]) &&
+                    (!kHasW<kPass> || r.w[k] == r.w[k + 1]);
     return sym_elem(r.v[k].x, r.v[k].y, tw ? kElPair : 0u);
   } else {
     return r.v[k];
@@ -276,7 +292,7 @@ __device__ inline uint32_t part_row(const PartRaw<kPass>& r, uint32_t k) {
 // gives every (block, digit) run its output position)
 template <int kPass>
 __device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint32_t d, uint32_t n_dig, uint64_t n_blk) {
-  if (kPass != 2) return (uint64_t)d * n_blk + B.j;
+  if (kBase<kPass> != 2) return (uint64_t)d * n_blk + B.j;
   return (uint64_t)S.bstart[B.g] * n_dig + (uint64_t)d * B.nb + B.j;
 }
 
@@ -322,10 +338,11 @@ __global__ void __launch_bounds__(kPartTPB)
     __attribute__((amdgpu_waves_per_eu(kPass == 1 ? G2N_PART1_WAVES : G2N_PART2_WAVES)))
     k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                        const uint32_t* __restrict__ offs, uint64_t n_blk,
-                                                       uint2* __restrict__ out) {
+                                                       uint2* __restrict__ out, uint32_t* __restrict__ wout = nullptr) {
   __shared__ uint32_t hist[1u << kDB];  // sub-tile counts, then its digit starts
   __shared__ uint32_t cur[1u << kDB];   // output position of the next element of digit d
   __shared__ uint2 stage[kSubEl<kPass>];
+  __shared__ uint32_t wstage[kHasW<kPass> ? kSubEl<kPass> : 1];  // weighted passes: the values beside
   __shared__ uint32_t red[kPartTPB / 64];
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) return;
@@ -364,12 +381,17 @@ __global__ void __launch_bounds__(kPartTPB)
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kElPer<kPass>; k++)
-      if (valid >> k & 1) stage[hist[(part_row<kPass>(raw, k) >> shift) & dmask] + rk[k]] = part_elem<kPass>(S, raw, k);
+      if (valid >> k & 1) {
+        const uint32_t at = hist[(part_row<kPass>(raw, k) >> shift) & dmask] + rk[k];
+        stage[at] = part_elem<kPass>(S, raw, k);
+        if constexpr (kHasW<kPass>) wstage[at] = raw.w[k];
+      }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kPartTPB) {
       const uint2 y = stage[i];
       const uint32_t d = (y.x >> shift) & dmask;
       out[cur[d] + (i - hist[d])] = y;
+      if constexpr (kHasW<kPass>) wout[cur[d] + (i - hist[d])] = wstage[i];
     }
     __syncthreads();
 #pragma unroll
@@ -893,6 +915,228 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
       indptr[row] += (int32_t)base;
       if (row == n_rows - 1) indptr[n_rows] += (int32_t)base;
     }
+  }
+}
+
+// ---- weighted SUM CSR (coo.tocsr of a weighted COO, utils.py:55, builders.py:281) --------------
+// When every duplicate sum is order-independent — integer dtypes (wrapping sums), bool (logical or),
+// float dtypes whose values are all integers below 2^31 in magnitude (not -0.0) and whose per-entry
+// sums of magnitudes stay below 2^24 (float32) / 2^53 (float64), so every partial sum is exact — the
+// result does not depend on scipy's std::sort order: the bucket partition (passes 5 / 6 carry the
+// values) and a finish that sums in any order replace the stable LSD sort + row sums.
+
+// the values as exact int32 (weight_enc, g2n_kernels.hip): when k_values did not write them
+template <class T>
+__global__ void __launch_bounds__(kTPB) k_weight_encode(const T* __restrict__ data, uint64_t n,
+                                                        uint32_t* __restrict__ enc, Ctl* ctl) {
+  const uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  bool bad = false;
+  if (i < n) enc[i] = weight_enc<T>(data[i], bad);
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) ctl->w_inexact = 1;
+}
+
+// A run's sum in T's arithmetic (any order): wrapping for the integer dtypes, or for bool, a plain
+// integer sum for the floats (exact under k_weight_encode's bounds; `mag` collects the magnitudes).
+template <class T>
+struct WSum {
+  int64_t s = 0;
+  uint64_t mag = 0;
+  __device__ void add(uint32_t e) {
+    if constexpr (std::is_same<T, uint8_t>::value) s |= (int64_t)e;
+    else {
+      const int32_t x = (int32_t)e;
+      s += x;
+      mag += (uint64_t)(x < 0 ? -(int64_t)x : (int64_t)x);
+    }
+  }
+  __device__ T value() const {
+    if constexpr (std::is_same<T, uint8_t>::value) return (T)(s != 0);
+    else if constexpr (std::is_same<T, int8_t>::value) return (T)(int8_t)(uint8_t)(uint64_t)s;
+    else if constexpr (std::is_same<T, int32_t>::value) return (T)(int32_t)(uint32_t)(uint64_t)s;
+    else return (T)s;
+  }
+  __device__ bool exact() const {
+    if constexpr (std::is_same<T, float>::value) return mag < (1ull << 24);
+    else if constexpr (std::is_same<T, double>::value) return mag < (1ull << 53);
+    else return true;
+  }
+};
+
+// ascending bitonic network over r[0, kN) (kN a power of two; every index compile-time)
+template <int kN, int kM>
+__device__ inline void sumw_sort_net(unsigned long long (&r)[kM]) {
+#pragma unroll
+  for (int k = 2; k <= kN; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < kN; i++) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = r[i], b = r[l];
+          const bool sw = ((i & k) == 0) ? a > b : a < b;
+          r[i] = sw ? b : a;
+          r[l] = sw ? a : b;
+        }
+      }
+}
+
+// sorts n u64 keys at seg (LDS) ascending: insertion for short rows, Shell sort beyond
+__device__ inline void sumw_sort_row(unsigned long long* seg, uint32_t n) {
+  if (n <= 1) return;
+  constexpr uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};  // Ciura
+  for (uint32_t gp : gaps) {
+    if (gp >= n) continue;
+    for (uint32_t i = gp; i < n; i++) {
+      const unsigned long long v = seg[i];
+      uint32_t jj = i;
+      while (jj >= gp && seg[jj - gp] > v) {
+        seg[jj] = seg[jj - gp];
+        jj -= gp;
+      }
+      seg[jj] = v;
+    }
+  }
+}
+
+// F1w: one block per bucket of 2^low <= kFinTPB rows (thread = row): the bucket's entries (a kElPair
+// element is the twins (a, b) and (b, a) of one value) grouped by row as (column << 32 | value) in
+// LDS, each row sorted by its lane, its column runs summed; the merged entries staged at twice the
+// bucket's input offset (columns in tcol, values in tval), local row offsets in indptr, the count
+// in btot.  ctl->bucket_overflow: a bucket past kSymCap entries; ctl->w_inexact: a float run past
+// its exact bound — the caller then takes the stable row-sum path.
+template <class T>
+__global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict__ el, const uint32_t* __restrict__ ew,
+                                                       const uint32_t* __restrict__ bstart, uint32_t low,
+                                                       uint64_t n_rows, uint32_t* __restrict__ btot,
+                                                       uint32_t* __restrict__ tcol, T* __restrict__ tval,
+                                                       int32_t* __restrict__ indptr, Ctl* ctl) {
+  __shared__ unsigned long long seg[kSymCap];
+  __shared__ uint32_t cnt[kFinTPB];
+  __shared__ uint32_t cur[kFinTPB];
+  __shared__ uint32_t red[kFinTPB / 64];
+  const uint64_t b = blockIdx.x;
+  const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
+  if (n > kSymCap) {  // block-uniform
+    if (threadIdx.x == 0) {
+      ctl->bucket_overflow = 1;
+      btot[b] = 0;
+    }
+    return;
+  }
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t rmask = (1u << low) - 1u;
+  for (uint32_t i = threadIdx.x; i < n; i += kFinTPB) {
+    const uint2 x = el[e0 + i];
+    atomicAdd(&cnt[x.x & rmask], 1u);
+    if ((x.y & 3u) == kElPair) atomicAdd(&cnt[(x.y >> 2) & rmask], 1u);
+  }
+  __syncthreads();
+  const uint32_t my = cnt[threadIdx.x];
+  uint32_t rs;
+  const uint32_t nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
+  if (nx > kSymCap) {  // block-uniform
+    if (threadIdx.x == 0) {
+      ctl->bucket_overflow = 1;
+      btot[b] = 0;
+    }
+    return;
+  }
+  cur[threadIdx.x] = rs;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kFinTPB) {
+    const uint2 x = el[e0 + i];
+    const uint32_t w = ew[e0 + i], col = x.y >> 2;
+    seg[atomicAdd(&cur[x.x & rmask], 1u)] = ((unsigned long long)col << 32) | w;
+    if ((x.y & 3u) == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = ((unsigned long long)x.x << 32) | w;
+  }
+  __syncthreads();
+  const uint64_t row = (b << low) + threadIdx.x;
+  const bool live = threadIdx.x <= rmask && row < n_rows;
+  unsigned long long* sg = seg + rs;
+  // rows of <= kR entries are sorted in registers (one LDS read each: lanes' rows sit a few
+  // entries apart, so LDS passes over them conflict on the banks), longer ones by their lane in LDS
+  constexpr int kR = 16;
+  const bool inreg = my <= (uint32_t)kR;
+  unsigned long long r[kR];
+#pragma unroll
+  for (int i = 0; i < kR; i++) r[i] = (live && i < (int)my) ? sg[i] : ~0ull;  // padding sorts last
+  uint32_t m = 0;
+  if (live) {
+    if (inreg) {
+      if (my <= 4) sumw_sort_net<4>(r);
+      else if (my <= 8) sumw_sort_net<8>(r);
+      else sumw_sort_net<16>(r);
+#pragma unroll
+      for (int i = 0; i < kR; i++)
+        m += (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) ? 1u : 0u;
+    } else {
+      sumw_sort_row(sg, my);
+      for (uint32_t i = 0; i < my; i++) m += (i + 1 == my || (sg[i + 1] >> 32) != (sg[i] >> 32)) ? 1u : 0u;
+    }
+  }
+  uint32_t off;
+  const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
+  if (threadIdx.x == 0) btot[b] = tot;
+  if (live) {
+    indptr[row] = (int32_t)off;  // local: k_sumw_place adds the bucket's offset
+    if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
+    uint32_t* oc = tcol + 2 * (uint64_t)e0 + off;
+    T* ov = tval + 2 * (uint64_t)e0 + off;
+    WSum<T> acc;
+    bool exact = true;
+    uint32_t j = 0;
+    if (inreg) {
+#pragma unroll
+      for (int i = 0; i < kR; i++) {
+        if (i < (int)my) {
+          acc.add((uint32_t)r[i]);
+          if (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32)) {
+            exact &= acc.exact();
+            oc[j] = (uint32_t)(r[i] >> 32);
+            ov[j] = acc.value();
+            j++;
+            acc = WSum<T>{};
+          }
+        }
+      }
+    } else {
+      for (uint32_t i = 0; i < my; i++) {
+        acc.add((uint32_t)sg[i]);
+        if (i + 1 == my || (sg[i + 1] >> 32) != (sg[i] >> 32)) {
+          exact &= acc.exact();
+          oc[j] = (uint32_t)(sg[i] >> 32);
+          ov[j] = acc.value();
+          j++;
+          acc = WSum<T>{};
+        }
+      }
+    }
+    if (!exact) ctl->w_inexact = 1;
+  }
+}
+
+// F2w: bucket b's staged entries (columns, values) to their CSR place, indptr rebased.
+template <class T>
+__global__ void __launch_bounds__(kFinTPB) k_sumw_place(const uint32_t* __restrict__ bstart,
+                                                      const uint32_t* __restrict__ btot,
+                                                      const uint32_t* __restrict__ boff, uint32_t low, uint64_t n_rows,
+                                                      const uint32_t* __restrict__ tcol, const T* __restrict__ tval,
+                                                      int32_t* __restrict__ indptr, int32_t* __restrict__ indices,
+                                                      T* __restrict__ data) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
+  const uint32_t* sc = tcol + 2 * (uint64_t)e0;
+  const T* sv = tval + 2 * (uint64_t)e0;
+  for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) {
+    indices[(uint64_t)base + i] = (int32_t)sc[i];
+    data[(uint64_t)base + i] = sv[i];
+  }
+  const uint64_t row = ((uint64_t)b << low) + threadIdx.x;
+  if (threadIdx.x < (1u << low) && row < n_rows) {
+    indptr[row] += (int32_t)base;
+    if (row == n_rows - 1) indptr[n_rows] += (int32_t)base;
   }
 }
 

@@ -135,7 +135,8 @@ typedef struct g2n_result {
   int32_t format;              /* G2N_FMT_COO | G2N_FMT_CSR */
   int32_t dtype;
   int32_t index_width;         /* 4 (int32) or 8 (int64) for rows/cols/indptr/indices */
-  int32_t sum_sorted;          /* scipy has_sorted_indices of the scattered COO (diagnostic) */
+  int32_t sum_sorted;          /* scipy has_sorted_indices of the scattered COO (diagnostic; -1: not
+                                  computed — the CSR came from the bucket partition) */
   int64_t nnz;                 /* COO: triplet count; CSR: stored entries */
   const void *rows;            /* COO */
   const void *cols;            /* COO */

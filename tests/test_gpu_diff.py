@@ -527,6 +527,66 @@ def test_csr_output_equals_oracle(gpu, oracle_lib, case):
     assert not bad, bad[:4]
 
 
+def _weighted_sum_cases():
+    import random
+
+    r = random.Random(17)
+    base = [f"S\t{k}\t*\n" for k in range(1, 4001)]
+    ints = [f"L\t{r.randint(1, 4000)}\t+\t{r.randint(1, 4000)}\t-\t0M\tRC:i:{r.randint(-3, 5)}\n"
+            for _ in range(24000)]
+    ints += ["L\t7\t+\t9\t+\t0M\tRC:i:1\n"] * 300 + ["L\t9\t+\t7\t+\t0M\tRC:i:2\n"] * 130  # int8 wrap
+    ints += ["L\t11\t+\t11\t+\t0M\tRC:i:-1\n", "L\t11\t+\t11\t+\t0M\tRC:i:1\n"] * 40  # sums to 0
+    ints += ["L\t12\t+\t13\t+\t0M\n"] * 3  # no tag: weight 1
+    hub = [f"L\t3000\t+\t{k}\t+\t0M\tRC:i:{k % 7}\n" for k in range(1, 4001)]  # > one bucket
+    big = ["L\t20\t+\t21\t+\t0M\tRC:i:16777216\n"] * 2  # float32: a run past 2^24
+    frac = ["L\t30\t+\t31\t+\t0M\tRC:f:0.5\n"]
+    negz = ["L\t40\t+\t41\t+\t0M\tRC:f:-0.0\n"]
+    # the dtypes whose SUM CSR must take the row sums (the cast of 0.5 / -0.0 to an integer dtype or bool
+    # is an exact integer: those stay on the buckets)
+    every, floats = {"float64", "float32", "int32", "int8", "bool"}, {"float64", "float32"}
+    return {"ints": (base + ints, set()), "hub": (base + ints + hub, every), "big": (base + ints + big, {"float32"}),
+            "frac": (base + ints + frac, floats), "negzero": (base + ints + negz, floats)}
+
+
+@pytest.mark.parametrize("case", ["ints", "hub", "big", "frac", "negzero"])
+def test_weighted_sum_buckets_match_oracle_and_classic(gpu, oracle_lib, monkeypatch, case):
+    """Weighted SUM CSRs (coo.tocsr, utils.py:55) through the value-carrying bucket partition (passes
+    5 / 6, k_sumw_finish): integer weights in every dtype family equal the oracle and the stable row-sum
+    path (TEST_NO_BUCKETS) byte for byte; a premise break — a fractional or -0.0 value, a float32 run
+    whose magnitudes pass 2^24, a bucket past its capacity — takes the row sums (sum_buckets False)."""
+    from gfa2network_amd import _native as nat
+
+    lines, rowsum = _weighted_sum_cases()[case]
+    data = "".join(lines).encode()
+    bad = []
+    for mode in ({}, {"directed": False}, {"bidirected": True}, {"asymmetric": True}):
+        for dtype in ("float64", "float32", "int32", "int8", "bool"):
+            o = oracle_lib.run(data, dtype=dtype, weight_tag="RC", **mode)
+            raw = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, dtype=dtype, weight_tag="RC",
+                                                               **mode))
+            if raw.status != o.status:
+                bad.append((mode, dtype, "status", raw.status, o.status))
+                continue
+            if o.status or raw.format != "csr":
+                continue
+            R = oracle_lib.to_raw(o, "csr")
+            same = (np.array_equal(raw.indptr, R.indptr) and np.array_equal(raw.indices, R.indices)
+                    and raw.data.tobytes() == R.data.tobytes())
+            if not same:
+                bad.append((mode, dtype, "oracle"))
+            want = dtype not in rowsum and mode != {}  # {}: MAX-SYM (weighted: the row sums)
+            if raw.sum_buckets != want:
+                bad.append((mode, dtype, "path", raw.sum_buckets))
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_BUCKETS)
+            c = nat.build_from_buffer(data, nat.make_options(output=nat.OUT_CSR, dtype=dtype, weight_tag="RC",
+                                                             **mode))
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+            if c.sum_buckets or not (np.array_equal(raw.indptr, c.indptr) and np.array_equal(raw.indices, c.indices)
+                                     and raw.data.tobytes() == c.data.tobytes()):
+                bad.append((mode, dtype, "classic"))
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("mode", [{}, {"directed": False}, {"bidirected": True}])
 def test_failed_build_leaves_no_call_state(gpu, oracle_lib, mode):
     """A build that throws after its parse and ids (TEST_THROW_AFTER_IDS: the group-slot COO active, the
