@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_NSLOTS
 };
 
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
@@ -388,18 +388,24 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
               (const uint32_t*)t_rows, (const uint32_t*)t_cols, pair ? n_t : 0, (uint32_t)row_base,
               nullptr, nullptr, nullptr, 0, grouped ? c->gcoo.gcount : nullptr, grouped ? c->gcoo.gcap : 0,
               (sum || pair) ? 0u : (uint32_t)low + 1u};
-  // pass 1: over the COO entries, both sides (grouped: one block per group slot)
+  // pass 1: over the COO entries, both sides (grouped: one block per group slot).  MAX-SYM: pair
+  // elements go out as 4-byte words (stream A, g2n_sym.hip), the rest as 8-byte elements (stream B);
+  // the count matrix holds B's digits then A's, each part scanned on its own
+  const bool words = !t_rows && (sum || !pair);  // passes 1 and 4 (not the two-stream slices' pass 3)
   const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + kPartTile - 1) / kPartTile;
-  auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
-  auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
+  const uint64_t nm1 = (uint64_t)n_dig1 * n_blk1;  // one stream's count matrix
+  auto* cnt1 = dget<uint32_t>(c, S_PCNT, (words ? 2 : 1) * nm1);
+  auto* off1 = dget<uint32_t>(c, S_POFF, (words ? 2 : 1) * nm1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
-  if (sum && !t_rows) {  // the SUM CSR: one element per entry, adjacent transposed twins as one
+  uint32_t* wa1 = words ? dget<uint32_t>(c, S_PW0, n_trip) : nullptr;
+  if (sum && !t_rows) {  // the SUM CSR: one element per entry, adjacent transposed twins as one (a word)
     src.pair_bits = (uint32_t)low + 1u;
     hipLaunchKernelGGL(k_part_hist<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, nm1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1 + nm1, off1 + nm1, nm1);
     hipLaunchKernelGGL(k_part_scatter<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
-                       (const uint32_t*)off1, n_blk1, el1);
+                       (const uint32_t*)off1, n_blk1, el1, wa1);
   } else if (sum || pair) {  // one element per entry
     hipLaunchKernelGGL(k_part_hist<3>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
@@ -409,20 +415,30 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   } else {
     hipLaunchKernelGGL(k_part_hist<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, (uint64_t)n_dig1 * n_blk1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, nm1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1 + nm1, off1 + nm1, nm1);
     hipLaunchKernelGGL(k_part_scatter<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
-                       (const uint32_t*)off1, n_blk1, el1);
+                       (const uint32_t*)off1, n_blk1, el1, wa1);
   }
   auto* bst = dget<uint32_t>(c, S_BSTART, n_buckets + 1);
+  uint32_t* bstA = words ? dget<uint32_t>(c, S_BSTARTA, n_buckets + 1) : nullptr;
   const uint2* el = el1;
+  const uint32_t* wa = wa1;
   if (bits2 == 0) {
     hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
                        (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst);
-  } else {  // pass 2 inside each pass-1 group
-    auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
+    if (words)
+      hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                         (const uint32_t*)(off1 + nm1), (const uint32_t*)(cnt1 + nm1), n_blk1, n_buckets, bstA);
+  } else {  // pass 2 inside each pass-1 group (stream A's groups: the second half of S_PGRP)
+    auto* grp = dget<uint32_t>(c, S_PGRP, 4 * ((uint64_t)n_dig1 + 1));
+    uint32_t* grpA = grp + 2 * ((uint64_t)n_dig1 + 1);
     PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0};
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
                        n_blk1, n_dig1, grp, grp + n_dig1 + 1);
+    if (words)
+      hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)(off1 + nm1),
+                         (const uint32_t*)(cnt1 + nm1), n_blk1, n_dig1, grpA, grpA + n_dig1 + 1);
     // >= the blocks the groups need (sum of ceil(group / kPartTile) <= n_el / kPartTile + n_dig1)
     const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
@@ -444,6 +460,27 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
                        (const uint32_t*)off2, s2, n_dig2, n_buckets, bst);
     el = el2;
+    if (words) {  // pass 7: stream A's words (same count / offset buffers, B's bucket starts are taken)
+      PartSrc s2a{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, nullptr, grpA, grpA + n_dig1 + 1, n_dig1,
+                  nullptr, 0, (uint32_t)low + 1u, nullptr, wa1};
+      auto* wa2 = dget<uint32_t>(c, S_PW1, n_trip);
+      if (bits2 > (int)kMaxDigitBits) {
+        hipLaunchKernelGGL((k_part_hist<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream,
+                           s2a, 2u * (uint32_t)low, n_dig2, cnt2, n_blk2);
+        scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+        hipLaunchKernelGGL((k_part_scatter<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0,
+                           c->stream, s2a, 2u * (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, (uint2*)nullptr, wa2);
+      } else {
+        hipLaunchKernelGGL(k_part_hist<7>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2a,
+                           2u * (uint32_t)low, n_dig2, cnt2, n_blk2);
+        scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+        hipLaunchKernelGGL(k_part_scatter<7>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2a,
+                           2u * (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, (uint2*)nullptr, wa2);
+      }
+      hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
+                         (const uint32_t*)off2, s2a, n_dig2, n_buckets, bstA);
+      wa = wa2;
+    }
   }
   phase(c, "sum");
   auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
@@ -470,11 +507,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata, (uint32_t)row_base);
+                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata, (uint32_t)row_base);
+                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -492,11 +529,13 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
-                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base);
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
+                       (const uint32_t*)bstA);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
-                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base);
+                       (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
+                       (const uint32_t*)bstA);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -527,7 +566,8 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     auto* indices64 = dget<int64_t>(c, S_INDICES64, n_el);
     hipLaunchKernelGGL((k_sym_place<T, int64_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
                        (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
-                       (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices64, odata, indptr64);
+                       (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices64, odata, indptr64,
+                       (const uint32_t*)bstA);
     R->format = G2N_FMT_CSR;
     R->index_width = 8;
     R->indptr = indptr64;
@@ -541,7 +581,8 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   }
   hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
                      (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
-                     (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr);
+                     (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr,
+                     (const uint32_t*)bstA);
 #endif
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
@@ -1488,9 +1529,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
-  // options.reserved[4] bit 2: a sharded decimal range whose caller routes coordinates only
-  // (uniform values, no COO result): the values array is left unwritten
-  const bool no_values = shard_dec && uni && (o->reserved[4] & 4) != 0;
+  // options.reserved[4] bit 2: a sharded range (decimal, or a general-protocol local build) whose
+  // caller routes coordinates only (uniform values, no COO result): the values array is left unwritten
+  const bool no_values = uni && (o->reserved[4] & 4) != 0;
   if (coords_done) {  // values only, and only when the output or the sums read them
     if (n_e && (coo_out || !uni) && !no_values) {
       // a weighted SUM CSR: the exact-int32 codes the bucket partition sums (csr_partition_w) beside

@@ -122,9 +122,24 @@ struct PartSrc {
 // sums cannot depend on their order — k_weight_encode checked): each element carries its value, a
 // u32 in a parallel array, and two twins pair only when their values are equal.
 template <int kPass>
-constexpr int kBase = kPass == 5 ? 4 : kPass == 6 ? 2 : kPass;
+constexpr int kBase = kPass == 5 ? 4 : (kPass == 6 || kPass == 7) ? 2 : kPass;
 template <int kPass>
-constexpr bool kHasW = kPass >= 5;
+constexpr bool kHasW = kPass == 5 || kPass == 6;
+// Pair words.  Pass 1 writes its kElPair elements — nearly every entry of a graph whose edges join
+// nearby ids — as ONE 4-byte word into a second stream (A) beside the 8-byte elements (B): both rows
+// share the bucket, so the word holds a's bits below pass 1's digit and b's bits below `low`:
+// word = (a mod 2^shift1) << low | (b mod 2^low) (shift1 + low <= 26 bits).  Pass 7 is pass 2 over
+// stream A (words in, words out; digit = word >> 2 low = bits of a >> low); F1 rebuilds (a, b) from the
+// bucket id.
+// Half the bytes of those elements through the rest of the partition and into F1.
+template <int kPass>
+constexpr bool kSplit = kPass == 1 || kPass == 4;  // MAX-SYM pass 1, and the SUM CSR's twins (pass 4)
+template <int kPass>
+constexpr bool kWords = kPass == 7;
+// (a sharded SUM slice: rows are slice rows, columns global — b's slice row is column - row_base)
+__device__ inline uint32_t pair_word(uint2 y, uint32_t shift1, uint32_t low, uint32_t row_base) {
+  return ((y.x & ((1u << shift1) - 1u)) << low) | (((y.y >> 2) - row_base) & ((1u << low) - 1u));
+}
 
 struct PartBlock {  // this block's range: elements [e0, e1) (pass 1: entries [e0/2, e1/2))
   uint64_t e0, e1;
@@ -218,6 +233,12 @@ __device__ inline void part_fetch(const PartSrc& S, uint64_t e, uint64_t e1, Par
         if constexpr (kHasW<kPass>) r.w[k] = S.vals[i];
         r.valid |= 1u << k;
       }
+    } else if (kPass == 7) {  // pair words: the word is the "row" (its digit: shift = 2 low), nothing beside
+      const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
+      if (i < e1) {
+        r.v[k] = make_uint2(S.in_w[i], 0u);
+        r.valid |= 1u << k;
+      }
     } else if (kPass == 3) {
       const uint64_t i = e + threadIdx.x + (uint64_t)k * kPartTPB;
       if (i < e1) {
@@ -290,6 +311,17 @@ __device__ inline uint32_t part_row(const PartRaw<kPass>& r, uint32_t k) {
 // index of the block's count for digit d in the count matrix: pass 1 digit-major over blocks,
 // pass 2 group by group, digit-major over the group's blocks (so one device scan of the matrix
 // gives every (block, digit) run its output position)
+// element k's digit; pass 1: the pair elements' digits follow the others' (n_dig + d: stream A)
+template <int kPass>
+__device__ inline uint32_t part_digit(const PartSrc& S, const PartRaw<kPass>& r, uint32_t k, uint32_t shift,
+                                      uint32_t dmask, uint32_t n_dig) {
+  const uint32_t d = (part_row<kPass>(r, k) >> shift) & dmask;
+  if constexpr (kPass == 1) return d + ((!(k & 1) && part_pair<kPass>(S, r.v[k / 2])) ? n_dig : 0u);
+  else if constexpr (kPass == 4)
+    return d + ((!(k & 1) && (r.valid >> k & 3u) == 3u && part_twins(S, r.v[k], r.v[k + 1])) ? n_dig : 0u);
+  else return d;
+}
+
 template <int kPass>
 __device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint32_t d, uint32_t n_dig, uint64_t n_blk) {
   if (kBase<kPass> != 2) return (uint64_t)d * n_blk + B.j;
@@ -300,8 +332,10 @@ __device__ inline uint64_t part_slot(const PartSrc& S, const PartBlock& B, uint3
 template <int kPass, uint32_t kDB = kMaxDigitBits>
 __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                     uint32_t* __restrict__ counts, uint64_t n_blk) {
-  __shared__ uint32_t hist[1u << kDB];
-  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
+  constexpr uint32_t kStreams = kSplit<kPass> ? 2 : 1;
+  __shared__ uint32_t hist[kStreams << kDB];
+  const uint32_t nd = kStreams * n_dig;  // pass 1: stream B's digits, then stream A's
+  for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB) hist[d] = 0;
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) {  // block-uniform: past the last group's blocks
     for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) counts[(uint64_t)blockIdx.x * n_dig + d] = 0;
@@ -316,10 +350,10 @@ __global__ void __launch_bounds__(kPartTPB) k_part_hist(PartSrc S, uint32_t shif
     const uint32_t valid = part_valid<kPass>(S, r);
 #pragma unroll
     for (uint32_t k = 0; k < kElPer<kPass>; k++)
-      if (valid >> k & 1) atomicAdd(&hist[(part_row<kPass>(r, k) >> shift) & dmask], 1u);
+      if (valid >> k & 1) atomicAdd(&hist[part_digit<kPass>(S, r, k, shift, dmask, n_dig)], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) counts[part_slot<kPass>(S, B, d, n_dig, n_blk)] = hist[d];
+  for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB) counts[part_slot<kPass>(S, B, d, n_dig, n_blk)] = hist[d];
 }
 
 // Scatter: per sub-tile, elements ranked in LDS (unstable), staged in digit order and written
@@ -339,35 +373,38 @@ __global__ void __launch_bounds__(kPartTPB)
     k_part_scatter(PartSrc S, uint32_t shift, uint32_t n_dig,
                                                        const uint32_t* __restrict__ offs, uint64_t n_blk,
                                                        uint2* __restrict__ out, uint32_t* __restrict__ wout = nullptr) {
-  __shared__ uint32_t hist[1u << kDB];  // sub-tile counts, then its digit starts
-  __shared__ uint32_t cur[1u << kDB];   // output position of the next element of digit d
+  constexpr uint32_t kStreams = kSplit<kPass> ? 2 : 1;
+  __shared__ uint32_t hist[kStreams << kDB];  // sub-tile counts, then its digit starts
+  __shared__ uint32_t cur[kStreams << kDB];   // output position of the next element of digit d
   __shared__ uint2 stage[kSubEl<kPass>];
   __shared__ uint32_t wstage[kHasW<kPass> ? kSubEl<kPass> : 1];  // weighted passes: the values beside
   __shared__ uint32_t red[kPartTPB / 64];
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) return;
-  for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)];
+  const uint32_t nd = kStreams * n_dig;  // pass 1: stream A's cursors (own scan, from 0) after B's
+  for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB) cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)];
   const uint32_t dmask = n_dig - 1;
+  const uint32_t low = S.pair_bits - 1;  // pass 1: the pair words' b bits
   PartRaw<kPass> raw, nraw;
   part_fetch<kPass>(S, B.e0, B.e1, raw);
   constexpr uint64_t kStep = kSubEl<kPass>;
   for (uint64_t e = B.e0; e < B.e1; e += kStep) {
-    for (uint32_t d = threadIdx.x; d < n_dig; d += kPartTPB) hist[d] = 0;
+    for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB) hist[d] = 0;
     if (G2N_PART_PREFETCH && e + kStep < B.e1) part_fetch<kPass>(S, e + kStep, B.e1, nraw);  // next sub-tile in flight
     const uint32_t valid = part_valid<kPass>(S, raw);
     __syncthreads();
     uint32_t rk[kElPer<kPass>];
 #pragma unroll
     for (uint32_t k = 0; k < kElPer<kPass>; k++)
-      rk[k] = (valid >> k & 1) ? atomicAdd(&hist[(part_row<kPass>(raw, k) >> shift) & dmask], 1u) : 0u;
+      rk[k] = (valid >> k & 1) ? atomicAdd(&hist[part_digit<kPass>(S, raw, k, shift, dmask, n_dig)], 1u) : 0u;
     __syncthreads();
-    // digit starts: kDigPer consecutive digits per thread (n_dig <= 1024)
-    constexpr uint32_t kDigPer = (1u << kDB) / kPartTPB;
+    // digit starts: kDigPer consecutive digits per thread (nd <= kStreams * 1024)
+    constexpr uint32_t kDigPer = (kStreams << kDB) / kPartTPB;
     uint32_t hv[kDigPer], hsum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kDigPer; q++) {
       const uint32_t d = threadIdx.x * kDigPer + q;
-      hv[q] = d < n_dig ? hist[d] : 0u;
+      hv[q] = d < nd ? hist[d] : 0u;
       hsum += hv[q];
     }
     uint32_t ex;
@@ -375,29 +412,40 @@ __global__ void __launch_bounds__(kPartTPB)
 #pragma unroll
     for (uint32_t q = 0; q < kDigPer; q++) {
       const uint32_t d = threadIdx.x * kDigPer + q;
-      if (d < n_dig) hist[d] = ex;
+      if (d < nd) hist[d] = ex;
       ex += hv[q];
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kElPer<kPass>; k++)
       if (valid >> k & 1) {
-        const uint32_t at = hist[(part_row<kPass>(raw, k) >> shift) & dmask] + rk[k];
+        const uint32_t at = hist[part_digit<kPass>(S, raw, k, shift, dmask, n_dig)] + rk[k];
         stage[at] = part_elem<kPass>(S, raw, k);
         if constexpr (kHasW<kPass>) wstage[at] = raw.w[k];
       }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kPartTPB) {
       const uint2 y = stage[i];
-      const uint32_t d = (y.x >> shift) & dmask;
-      out[cur[d] + (i - hist[d])] = y;
-      if constexpr (kHasW<kPass>) wout[cur[d] + (i - hist[d])] = wstage[i];
+      uint32_t d = (y.x >> shift) & dmask;
+      if constexpr (kSplit<kPass>) {
+        if ((y.y & 3u) == kElPair) {  // stream A: the pair word
+          d += n_dig;
+          wout[cur[d] + (i - hist[d])] = pair_word(y, shift, low, S.row_base);
+          continue;
+        }
+      }
+      if constexpr (kWords<kPass>) {
+        wout[cur[d] + (i - hist[d])] = y.x;
+      } else {
+        out[cur[d] + (i - hist[d])] = y;
+        if constexpr (kHasW<kPass>) wout[cur[d] + (i - hist[d])] = wstage[i];
+      }
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kDigPer; q++) {
       const uint32_t d = threadIdx.x * kDigPer + q;
-      if (d < n_dig) cur[d] += hv[q];
+      if (d < nd) cur[d] += hv[q];
     }
     if (G2N_PART_PREFETCH) raw = nraw;
     else if (e + kStep < B.e1) part_fetch<kPass>(S, e + kStep, B.e1, raw);
@@ -615,7 +663,8 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
                                                      uint32_t* __restrict__ tcol, uint16_t* __restrict__ tcn,
                                                      int32_t* __restrict__ indptr, Ctl* ctl, uint64_t* __restrict__ lbst,
                                                      int32_t* __restrict__ indices, T* __restrict__ data,
-                                                     uint32_t row_base) {
+                                                     uint32_t row_base, const uint32_t* __restrict__ wa,
+                                                     const uint32_t* __restrict__ bstA) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];    // placement cursors
@@ -629,7 +678,11 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
   const uint64_t b = blockIdx.x;
-  const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;  // stored elements (a kElPair one is two entries)
+  // stored elements (a kElPair one is two entries): stream B's (8-byte elements) and stream A's (pair
+  // words, bstA non-null); the bucket stages its entries at twice its offset in both streams together
+  const uint32_t eB = bstart[b], nB = bstart[b + 1] - eB;
+  const uint32_t eA = bstA ? bstA[b] : 0u, nA = bstA ? bstA[b + 1] - eA : 0u;
+  const uint32_t e0 = eB + eA, n = nB + nA;
   auto overflow = [&]() {  // the build's sums go through the general path
     if (threadIdx.x == 0) {
       ctl->bucket_overflow = 1;
@@ -648,11 +701,17 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     // the first kSymReg elements per thread stay in registers from the count to the placement;
     // a bucket of more stored elements (rare: a skewed bucket) reads the rest again, so F1 keeps
     // to 64 VGPRs — 4 blocks per CU
+    // the registers hold stream A's words (most of a bucket) or, without stream A, B's elements
+    const uint32_t hi = (uint32_t)b << low;  // a pair word's row bits above low
+    auto word = [&](uint32_t w) {
+      return make_uint2(hi | ((w >> low) & rmask), (((hi | (w & rmask)) + row_base) << 2) | kElPair);
+    };
+    const uint32_t nr = bstA ? nA : nB;
     uint2 xs[kSymReg];
 #pragma unroll
     for (uint32_t k = 0; k < kSymReg; k++) {  // every load in flight before the first count
       const uint32_t i = threadIdx.x + k * kFinTPB;
-      if (i < n) xs[k] = el[e0 + i];
+      if (i < nr) xs[k] = bstA ? word(wa[eA + i]) : el[eB + i];
     }
     // a kElPair element (x.x, column b) is also the entry (b, x.x): the A.T entry of MAX-SYM (side
     // 1), or the SUM CSR's twin (side 0); rows are slice rows (row - row_base), columns global
@@ -668,8 +727,10 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     };
 #pragma unroll
     for (uint32_t k = 0; k < kSymReg; k++)
-      if (threadIdx.x + k * kFinTPB < n) count(xs[k]);
-    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < n; i += kFinTPB) count(el[e0 + i]);
+      if (threadIdx.x + k * kFinTPB < nr) count(xs[k]);
+    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < nr; i += kFinTPB) count(bstA ? word(wa[eA + i]) : el[eB + i]);
+    if (bstA)
+      for (uint32_t i = threadIdx.x; i < nB; i += kFinTPB) count(el[eB + i]);
     __syncthreads();
     F1_STAMP(1);
     my = cnt[threadIdx.x];
@@ -683,8 +744,10 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kSymReg; k++)
-      if (threadIdx.x + k * kFinTPB < n) place(xs[k]);
-    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < n; i += kFinTPB) place(el[e0 + i]);
+      if (threadIdx.x + k * kFinTPB < nr) place(xs[k]);
+    for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < nr; i += kFinTPB) place(bstA ? word(wa[eA + i]) : el[eB + i]);
+    if (bstA)
+      for (uint32_t i = threadIdx.x; i < nB; i += kFinTPB) place(el[eB + i]);
     __syncthreads();
     F1_STAMP(2);
   }
@@ -884,9 +947,9 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
                                                     T one, const uint32_t* __restrict__ tcol,
                                                     const uint16_t* __restrict__ tcn, int32_t* __restrict__ indptr,
                                                     I* __restrict__ indices, T* __restrict__ data,
-                                                    int64_t* __restrict__ indptr64) {
+                                                    int64_t* __restrict__ indptr64, const uint32_t* __restrict__ bstA) {
   const uint32_t b = blockIdx.x;
-  const uint32_t e0 = bstart[b], tot = btot[b], base = boff[b];
+  const uint32_t e0 = bstart[b] + (bstA ? bstA[b] : 0u), tot = btot[b], base = boff[b];
   const uint32_t* src = tcol + 2 * (uint64_t)e0;
   const uint16_t* scn = tcn + 2 * (uint64_t)e0;
 #ifndef G2N_PLACE_U
@@ -1024,13 +1087,27 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
     }
     return;
   }
+  // the bucket's elements into registers first (kSymPer per thread, all loads in flight at once),
+  // then counted and placed from there
+  uint2 xe[kSymPer];
+  uint32_t xw[kSymPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kSymPer; k++) {
+    const uint32_t i = threadIdx.x + k * kFinTPB;
+    if (i < n) {
+      xe[k] = el[e0 + i];
+      xw[k] = ew[e0 + i];
+    }
+  }
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t rmask = (1u << low) - 1u;
-  for (uint32_t i = threadIdx.x; i < n; i += kFinTPB) {
-    const uint2 x = el[e0 + i];
-    atomicAdd(&cnt[x.x & rmask], 1u);
-    if ((x.y & 3u) == kElPair) atomicAdd(&cnt[(x.y >> 2) & rmask], 1u);
+#pragma unroll
+  for (uint32_t k = 0; k < kSymPer; k++) {
+    if (threadIdx.x + k * kFinTPB < n) {
+      atomicAdd(&cnt[xe[k].x & rmask], 1u);
+      if ((xe[k].y & 3u) == kElPair) atomicAdd(&cnt[(xe[k].y >> 2) & rmask], 1u);
+    }
   }
   __syncthreads();
   const uint32_t my = cnt[threadIdx.x];
@@ -1045,11 +1122,14 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
   }
   cur[threadIdx.x] = rs;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += kFinTPB) {
-    const uint2 x = el[e0 + i];
-    const uint32_t w = ew[e0 + i], col = x.y >> 2;
-    seg[atomicAdd(&cur[x.x & rmask], 1u)] = ((unsigned long long)col << 32) | w;
-    if ((x.y & 3u) == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = ((unsigned long long)x.x << 32) | w;
+#pragma unroll
+  for (uint32_t k = 0; k < kSymPer; k++) {
+    if (threadIdx.x + k * kFinTPB < n) {
+      const uint2 x = xe[k];
+      const uint32_t w = xw[k], col = x.y >> 2;
+      seg[atomicAdd(&cur[x.x & rmask], 1u)] = ((unsigned long long)col << 32) | w;
+      if ((x.y & 3u) == kElPair) seg[atomicAdd(&cur[col & rmask], 1u)] = ((unsigned long long)x.x << 32) | w;
+    }
   }
   __syncthreads();
   const uint64_t row = (b << low) + threadIdx.x;
@@ -1082,11 +1162,44 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
   if (live) {
     indptr[row] = (int32_t)off;  // local: k_sumw_place adds the bucket's offset
     if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
-    uint32_t* oc = tcol + 2 * (uint64_t)e0 + off;
-    T* ov = tval + 2 * (uint64_t)e0 + off;
+  }
+  uint32_t* oc = tcol + 2 * (uint64_t)e0;
+  T* ov = tval + 2 * (uint64_t)e0;
+  bool exact = true;
+  // every row in registers (block-uniform): the merged entries go through LDS (columns, then values,
+  // in seg, which no lane reads any more) and out coalesced; otherwise each lane writes its own row
+  if (!__syncthreads_or(live && !inreg)) {
+    uint32_t* sc = (uint32_t*)seg;
+    if (live) {
+      uint32_t j = off;
+#pragma unroll
+      for (int i = 0; i < kR; i++)
+        if (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) sc[j++] = (uint32_t)(r[i] >> 32);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) oc[i] = sc[i];
+    __syncthreads();
+    T* sv = (T*)seg;
+    if (live) {
+      WSum<T> acc;
+      uint32_t j = off;
+#pragma unroll
+      for (int i = 0; i < kR; i++) {
+        if (i < (int)my) {
+          acc.add((uint32_t)r[i]);
+          if (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32)) {
+            exact &= acc.exact();
+            sv[j++] = acc.value();
+            acc = WSum<T>{};
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) ov[i] = sv[i];
+  } else if (live) {
     WSum<T> acc;
-    bool exact = true;
-    uint32_t j = 0;
+    uint32_t j = off;
     if (inreg) {
 #pragma unroll
       for (int i = 0; i < kR; i++) {
@@ -1113,8 +1226,8 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
         }
       }
     }
-    if (!exact) ctl->w_inexact = 1;
   }
+  if (!exact) ctl->w_inexact = 1;
 }
 
 // F2w: bucket b's staged entries (columns, values) to their CSR place, indptr rebased.

@@ -257,12 +257,16 @@ class HipEngine:
                 raise nat.NativeUnavailable(nat.last_error())
         return self.ctx_b
 
-    def local_build(self, buf, opts: dict, unknown_warned: bool = False, view: bool = False) -> LocalShard:
+    def local_build(self, buf, opts: dict, unknown_warned: bool = False, view: bool = False,
+                    values: bool = True) -> LocalShard:
         """The range on its own (local ids, names).  view: the COO as DevArray views of the build
-        context (valid until its next build; remap_pairs rewrites them in place), the names copied."""
+        context (valid until its next build; remap_pairs rewrites them in place), the names copied.
+        values=False: a build without a weight tag leaves its values unwritten (options.reserved[4]
+        bit 2) — the caller routes coordinates only and never reads them."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=True, device=self.device_index, **opts)
         o.reserved[0] = int(unknown_warned)
+        o.reserved[4] = 0 if values else 4
         res = nat.Result()
         ctx = self._build_ctx() if view else self.ctx
         self._sync()
@@ -776,7 +780,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
 
     # 1. local build; 2. stream-order resolution of errors and the one-shot warning
     view = not keep_coo and getattr(engine, "supports_views", False)
-    local = engine.local_build(buf, opts, view=view) if view else engine.local_build(buf, opts)
+    # (uniform values are never routed: a view build, whose COO nobody else reads, skips writing them)
+    local = engine.local_build(buf, opts, view=True, values=bool(weight_tag)) if view else engine.local_build(buf, opts)
 
     def stats(sh):
         return [sh.status, sh.err_line, sh.warn_line, sh.n_lines, sh.n_records, sh.n_records_before_error,
@@ -787,10 +792,11 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     if first_unk is not None and rank > first_unk and local.warn_line >= 0:
         # an earlier range already warned: this range's unsupported records are silent
         if local.status == 8 and local.err_line == local.warn_line:
-            local = (engine.local_build(buf, opts, unknown_warned=True, view=True) if view
+            local = (engine.local_build(buf, opts, unknown_warned=True, view=True, values=bool(weight_tag)) if view
                      else engine.local_build(buf, opts, unknown_warned=True))
         local.has_warning = False
-    allst = C.allgather_list(stats(local))
+    if first_unk is not None:  # a range may have been rebuilt: its counts again
+        allst = C.allgather_list(stats(local))
     line_base = np.concatenate([[0], np.cumsum([int(s[3]) for s in allst])])
     out = ShardResult(status=0, n_lines=int(line_base[-1]), n_records=int(sum(s[4] for s in allst)),
                       n_edges=int(sum(s[6] for s in allst)))
