@@ -53,6 +53,9 @@ enum Slot {
   S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_NSLOTS
 };
 
+#ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
+#define G2N_FORK_EARLY 0
+#endif
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
 #define G2N_FIN_DIRECT 0
 #endif
@@ -356,6 +359,7 @@ template <class T>
 static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* cols, uint64_t n_trip, uint64_t n_rows,
                           bool sum, g2n_result* R, const int32_t* t_rows = nullptr, const int32_t* t_cols = nullptr,
                           uint64_t n_t = 0, int64_t row_base = 0) {
+  if (G2N_FORK_EARLY) fork_side(c);  // experiment: the side work beside the partition passes
   const bool pair = t_rows != nullptr || row_base != 0;  // one element per entry of two streams
   const int bits = bits_for(n_rows);
   const double per_row =
@@ -499,7 +503,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_f1_stamps), &f1st, sizeof(f1st), 0, hipMemcpyHostToDevice,
                                  c->stream));
 #endif
-  fork_side(c);  // F1 leaves HBM bandwidth to spare
+  fork_side(c);  // F1 leaves HBM bandwidth to spare (G2N_FORK_EARLY: forked before pass 1 instead)
 #if G2N_FIN_DIRECT
   // F1 places every bucket's entries itself, its offset from a decoupled look-back over the buckets
   auto* lbst = dget<uint64_t>(c, S_FINLB, n_bk);

@@ -708,10 +708,23 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     };
     const uint32_t nr = bstA ? nA : nB;
     uint2 xs[kSymReg];
+    uint2 xb = make_uint2(0, 0);  // with stream A: one of stream B's elements (a bucket holds a few dozen)
+    if (bstA) {  // (the stream choice hoisted out of the loads: a per-load select serializes them)
+      uint32_t ws[kSymReg];
 #pragma unroll
-    for (uint32_t k = 0; k < kSymReg; k++) {  // every load in flight before the first count
-      const uint32_t i = threadIdx.x + k * kFinTPB;
-      if (i < nr) xs[k] = bstA ? word(wa[eA + i]) : el[eB + i];
+      for (uint32_t k = 0; k < kSymReg; k++) {  // every load in flight before the first count
+        const uint32_t i = threadIdx.x + k * kFinTPB;
+        ws[k] = i < nr ? wa[eA + i] : 0u;
+      }
+      if (threadIdx.x < nB) xb = el[eB + threadIdx.x];
+#pragma unroll
+      for (uint32_t k = 0; k < kSymReg; k++) xs[k] = word(ws[k]);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kSymReg; k++) {
+        const uint32_t i = threadIdx.x + k * kFinTPB;
+        if (i < nr) xs[k] = el[eB + i];
+      }
     }
     // a kElPair element (x.x, column b) is also the entry (b, x.x): the A.T entry of MAX-SYM (side
     // 1), or the SUM CSR's twin (side 0); rows are slice rows (row - row_base), columns global
@@ -729,8 +742,10 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     for (uint32_t k = 0; k < kSymReg; k++)
       if (threadIdx.x + k * kFinTPB < nr) count(xs[k]);
     for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < nr; i += kFinTPB) count(bstA ? word(wa[eA + i]) : el[eB + i]);
-    if (bstA)
-      for (uint32_t i = threadIdx.x; i < nB; i += kFinTPB) count(el[eB + i]);
+    if (bstA) {
+      if (threadIdx.x < nB) count(xb);
+      for (uint32_t i = threadIdx.x + kFinTPB; i < nB; i += kFinTPB) count(el[eB + i]);
+    }
     __syncthreads();
     F1_STAMP(1);
     my = cnt[threadIdx.x];
@@ -746,8 +761,10 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     for (uint32_t k = 0; k < kSymReg; k++)
       if (threadIdx.x + k * kFinTPB < nr) place(xs[k]);
     for (uint32_t i = threadIdx.x + kSymReg * kFinTPB; i < nr; i += kFinTPB) place(bstA ? word(wa[eA + i]) : el[eB + i]);
-    if (bstA)
-      for (uint32_t i = threadIdx.x; i < nB; i += kFinTPB) place(el[eB + i]);
+    if (bstA) {
+      if (threadIdx.x < nB) place(xb);
+      for (uint32_t i = threadIdx.x + kFinTPB; i < nB; i += kFinTPB) place(el[eB + i]);
+    }
     __syncthreads();
     F1_STAMP(2);
   }

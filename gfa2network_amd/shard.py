@@ -73,6 +73,7 @@ class LocalShard:
     names_offsets: object = None  # torch int64, n_local_nodes + 1
     n_cast_overflow: int = 0
     parse_path: str = ""  # build_decimal: "tile_local" (the one-pass lean parse) or "k1" (tile counts first)
+    phase_ms: dict = field(default_factory=dict)  # the local build's device phases (hipEvents; diagnostics)
 
 
 @dataclass
@@ -279,6 +280,10 @@ class HipEngine:
                         warn_byte=res.warn_byte, n_lines=res.n_lines, n_records=res.n_records,
                         n_records_before_error=res.n_records_before_error, n_edges=res.n_edges,
                         n_local_nodes=res.n_nodes, n_cast_overflow=res.n_cast_overflow)
+        for j in range(res.n_phases):
+            name = res.phase_names[j].decode()
+            if not name.startswith("_"):
+                sh.phase_ms[name] = sh.phase_ms.get(name, 0.0) + res.phase_ms[j]
         if rc == 8 and res.err_detail_len:  # the bytes whose decode raises, for the message
             sh.err_detail = bytes(self._copy_out(res.err_detail, res.err_detail_len, torch.uint8).cpu().numpy())
         if rc != 0:
@@ -833,6 +838,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     out.n_records_before_error = out.n_records
     out.n_cast_overflow = int(sum(s[7] for s in allst))
     tm["local_build"] = (time.perf_counter() - t0) * 1e3
+    for k, v in local.phase_ms.items():  # its device phases beside the host stages (diagnostics)
+        tm["local_dev_" + k] = v
 
     if world == 1 and not force_protocol:  # one range: its local ids are the global ids
         out.n_nodes = local.n_local_nodes
