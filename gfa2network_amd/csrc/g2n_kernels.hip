@@ -2634,7 +2634,7 @@ __device__ __host__ inline uint64_t dec_name_off(uint64_t id, int bidir) {  // o
 // counts is what it takes from F1: byte stores straight to HBM (default) cost the C4 build 0.12-0.15 ms
 // less than the block's names staged in LDS and written as aligned 16-byte stores (G2N_NAMES_BYTES=0,
 // the same box, tools/gpu_r4r.sh), and forking it before the partition instead (G2N_FORK_EARLY) costs
-// the partition 0.4 ms.
+// the partition 0.4 ms; non-temporal stores (here, or for F2's result arrays) cost 0.2-0.5 ms.
 #ifndef G2N_NAMES_BYTES
 #define G2N_NAMES_BYTES 1
 #endif

@@ -1,9 +1,9 @@
 #!/bin/bash
-# A/B on one box: names kernel form (LDS-staged vs byte stores) x side-work fork point (before F1 vs before P1)
+# A/B on one box: non-temporal stores for the names (nnt), the F2 result arrays (pnt), both
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R && mkdir -p gpurun_out
 for rep in 1 2; do
-for v in default nbytes early early_nbytes; do
+for v in default nnt pnt both; do
   if [ $v = default ]; then unset G2N_LIB; else export G2N_LIB=$R/gfa2network_amd/_lib/exp_$v.so; fi
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-e2e --no-cpu-baseline --no-alt > gpurun_out/r4r_$v.json 2> gpurun_out/r4r_$v.err || { tail -20 gpurun_out/r4r_$v.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4r_$v.json').read().splitlines()[-1]); print('$v', d['ms_per_step'], d.get('phase_ms'))"
