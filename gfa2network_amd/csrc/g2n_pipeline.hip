@@ -396,7 +396,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   // elements go out as 4-byte words (stream A, g2n_sym.hip), the rest as 8-byte elements (stream B);
   // the count matrix holds B's digits then A's, each part scanned on its own
   const bool words = !t_rows && (sum || !pair);  // passes 1 and 4 (not the two-stream slices' pass 3)
-  const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + kPartTile - 1) / kPartTile;
+  // elements per partition block: a quarter tile below 2^24 elements, so a small input still spreads
+  // over more blocks than the 256 CUs
+  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / 4;
+  src.tile = ptile;
+  const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + ptile - 1) / ptile;
   const uint64_t nm1 = (uint64_t)n_dig1 * n_blk1;  // one stream's count matrix
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (words ? 2 : 1) * nm1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (words ? 2 : 1) * nm1);
@@ -438,13 +442,14 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     auto* grp = dget<uint32_t>(c, S_PGRP, 4 * ((uint64_t)n_dig1 + 1));
     uint32_t* grpA = grp + 2 * ((uint64_t)n_dig1 + 1);
     PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0};
+    s2.tile = ptile;
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
-                       n_blk1, n_dig1, grp, grp + n_dig1 + 1);
+                       n_blk1, n_dig1, grp, grp + n_dig1 + 1, ptile);
     if (words)
       hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)(off1 + nm1),
-                         (const uint32_t*)(cnt1 + nm1), n_blk1, n_dig1, grpA, grpA + n_dig1 + 1);
-    // >= the blocks the groups need (sum of ceil(group / kPartTile) <= n_el / kPartTile + n_dig1)
-    const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
+                         (const uint32_t*)(cnt1 + nm1), n_blk1, n_dig1, grpA, grpA + n_dig1 + 1, ptile);
+    // >= the blocks the groups need (sum of ceil(group / ptile) <= n_el / ptile + n_dig1)
+    const uint64_t n_blk2 = (n_el + ptile - 1) / ptile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
     auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
     auto* el2 = dget<uint2>(c, S_EL1, n_el);
@@ -466,7 +471,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     el = el2;
     if (words) {  // pass 7: stream A's words (same count / offset buffers, B's bucket starts are taken)
       PartSrc s2a{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, nullptr, grpA, grpA + n_dig1 + 1, n_dig1,
-                  nullptr, 0, (uint32_t)low + 1u, nullptr, wa1};
+                  nullptr, 0, (uint32_t)low + 1u, nullptr, wa1, ptile};
       auto* wa2 = dget<uint32_t>(c, S_PW1, n_trip);
       if (bits2 > (int)kMaxDigitBits) {
         hipLaunchKernelGGL((k_part_hist<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream,
@@ -636,7 +641,9 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, 1u, nullptr, nullptr, 0, 0, nullptr, nullptr,
               nullptr, 0, nullptr, 0, (uint32_t)low + 1u, enc, nullptr};
   // pass 5: the entries with their values, adjacent transposed twins of one value as one element
-  const uint64_t n_blk1 = (n_el + kPartTile - 1) / kPartTile;
+  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / 4;  // as csr_partition
+  src.tile = ptile;
+  const uint64_t n_blk1 = (n_el + ptile - 1) / ptile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
@@ -655,10 +662,10 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   } else {  // pass 6 inside each pass-5 group
     auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
     PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0,
-               nullptr, w1};
+               nullptr, w1, ptile};
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
-                       n_blk1, n_dig1, grp, grp + n_dig1 + 1);
-    const uint64_t n_blk2 = (n_el + kPartTile - 1) / kPartTile + n_dig1;
+                       n_blk1, n_dig1, grp, grp + n_dig1 + 1, ptile);
+    const uint64_t n_blk2 = (n_el + ptile - 1) / ptile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
     auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
     auto* el2 = dget<uint2>(c, S_EL1, n_el);

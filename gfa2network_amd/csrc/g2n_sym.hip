@@ -115,7 +115,8 @@ struct PartSrc {
   uint32_t pair_bits;     // pass 1, two per entry: 0, or low + 1 — an entry whose rows agree above bit
                           //   low (one bucket) is one kElPair element
   const uint32_t* vals = nullptr;  // weighted SUM (passes 5 / 6): the entries' values as exact int32
-  const uint32_t* in_w = nullptr;  //   pass 6: the values beside `in`
+  const uint32_t* in_w = nullptr;  //   pass 6: the values beside `in`; pass 7: the pair words
+  uint32_t tile = kPartTile;       // elements per block (a quarter for small inputs: more blocks than CUs)
 };
 
 // Passes 5 / 6: passes 4 / 2 of the weighted SUM CSR (coo.tocsr of a weighted COO whose duplicate
@@ -166,9 +167,9 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
     B.g = 0;
     B.j = blk;
     B.nb = 0;
-    B.e0 = (uint64_t)blk * kPartTile;
+    B.e0 = (uint64_t)blk * S.tile;
     const uint64_t n_el = kPass == 1 ? 2 * S.n_entries : S.n_entries + S.n_t;
-    B.e1 = B.e0 + kPartTile < n_el ? B.e0 + kPartTile : n_el;
+    B.e1 = B.e0 + S.tile < n_el ? B.e0 + S.tile : n_el;
     return true;
   }
   if (blk >= S.bstart[S.n_groups]) return false;
@@ -181,9 +182,9 @@ __device__ inline bool part_block(const PartSrc& S, uint32_t blk, PartBlock& B) 
   B.g = lo;
   B.j = blk - S.bstart[lo];
   B.nb = S.bstart[lo + 1] - S.bstart[lo];
-  B.e0 = (uint64_t)S.gstart[lo] + (uint64_t)B.j * kPartTile;
+  B.e0 = (uint64_t)S.gstart[lo] + (uint64_t)B.j * S.tile;
   const uint64_t ge = S.gstart[lo + 1];
-  B.e1 = B.e0 + kPartTile < ge ? B.e0 + kPartTile : ge;
+  B.e1 = B.e0 + S.tile < ge ? B.e0 + S.tile : ge;
   return true;
 }
 
@@ -462,13 +463,13 @@ __device__ inline uint32_t part_total(const uint32_t* offs, const uint32_t* coun
 __global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs1,
                                                       const uint32_t* __restrict__ cnt1, uint64_t n_blk1,
                                                       uint32_t n_groups, uint32_t* __restrict__ gstart,
-                                                      uint32_t* __restrict__ bstart) {
+                                                      uint32_t* __restrict__ bstart, uint32_t tile) {
   __shared__ uint32_t red[16];
   const uint32_t g = threadIdx.x;
   const uint32_t total = part_total(offs1, cnt1, (uint64_t)n_groups * n_blk1);
   const uint32_t s = g < n_groups ? offs1[(uint64_t)g * n_blk1] : total;
   const uint32_t e = g + 1 < n_groups ? offs1[(uint64_t)(g + 1) * n_blk1] : total;
-  const uint32_t nb = g < n_groups ? (e - s + kPartTile - 1) / kPartTile : 0u;
+  const uint32_t nb = g < n_groups ? (e - s + tile - 1) / tile : 0u;
   // block scan over 1024 threads (16 waves)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = nb;
@@ -1159,12 +1160,16 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
   unsigned long long r[kR];
 #pragma unroll
   for (int i = 0; i < kR; i++) r[i] = (live && i < (int)my) ? sg[i] : ~0ull;  // padding sorts last
+  {  // one network per wave: the longest in-register row of the wave picks it (no divergent sorts)
+    uint32_t wm = (live && inreg) ? my : 0u;
+    for (int o = 32; o > 0; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor(wm, o, 64));
+    if (wm > 8) sumw_sort_net<16>(r);
+    else if (wm > 4) sumw_sort_net<8>(r);
+    else if (wm > 1) sumw_sort_net<4>(r);
+  }
   uint32_t m = 0;
   if (live) {
     if (inreg) {
-      if (my <= 4) sumw_sort_net<4>(r);
-      else if (my <= 8) sumw_sort_net<8>(r);
-      else sumw_sort_net<16>(r);
 #pragma unroll
       for (int i = 0; i < kR; i++)
         m += (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) ? 1u : 0u;
