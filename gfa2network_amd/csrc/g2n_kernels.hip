@@ -2630,15 +2630,13 @@ __device__ __host__ inline uint64_t dec_name_off(uint64_t id, int bidir) {  // o
   return 2 * (dec_digits_upto(k) + 2 * k) + ((id & 1) ? dec_digits(k + 1) + 2 : 0);
 }
 
-// node k's key str(k + 1) (bidirected: + ":+" / ":-").  It runs on the side stream beside F1, so what
-// counts is what it takes from F1: byte stores straight to HBM (default) cost the C4 build 0.12-0.15 ms
-// less than the block's names staged in LDS and written as aligned 16-byte stores (G2N_NAMES_BYTES=0,
-// the same box, tools/gpu_r4r.sh), and forking it before the partition instead (G2N_FORK_EARLY) costs
-// the partition 0.4 ms; non-temporal stores (here, or for F2's result arrays) cost 0.2-0.5 ms.
-#ifndef G2N_NAMES_BYTES
-#define G2N_NAMES_BYTES 1
-#endif
-#if G2N_NAMES_BYTES
+// node k's key str(k + 1) (bidirected: + ":+" / ":-"), byte stores.  It runs on the side stream beside
+// F1, so what counts is what it takes from F1 (0.2-0.3 ms of F1's time on C4).  Measured dead ends
+// (same box, tools/gpu_r4r.sh / gpu_r4u.sh): the block's names staged in LDS and written in 16-byte
+// stores (+0.12-0.15 ms per build), the blob written output-centric (a thread per 16 aligned bytes,
+// the names' run found by arithmetic: +0.3 ms, VALU-heavy beside F1), the names written by the
+// tile-local parse as it meets each S line (K2 +0.34 ms, F1 -0.3: no gain), the names forked beside
+// the partition instead of F1 (+0.4 ms on it), non-temporal stores (+0.2-0.5 ms).
 __global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir, int64_t* __restrict__ offs,
                                                     uint8_t* __restrict__ blob) {
   const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
@@ -2646,7 +2644,7 @@ __global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir,
   const uint64_t o = dec_name_off(id, bidir);
   offs[id] = (int64_t)o;
   if (id == n_nodes) return;
-  uint32_t v = (uint32_t)((bidir ? id >> 1 : id) + 1);
+  uint32_t v = (uint32_t)((bidir ? id >> 1 : id) + 1);  // node ids < 2^31
   const uint32_t d = dec_digits(v);
   for (uint32_t j = d; j-- > 0;) {
     blob[o + j] = (uint8_t)('0' + v % 10u);
@@ -2657,48 +2655,6 @@ __global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir,
     blob[o + d + 1] = (id & 1) ? '-' : '+';
   }
 }
-#else
-__global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir, int64_t* __restrict__ offs,
-                                                    uint8_t* __restrict__ blob) {
-  __shared__ __attribute__((aligned(16))) uint8_t st[kTPB * 12 + 32];  // <= 10 digits + ":o" per name
-  __shared__ uint64_t s_lo, s_hi;
-  const uint64_t id0 = (uint64_t)blockIdx.x * kTPB, id = id0 + threadIdx.x;
-  const uint64_t idl = id0 + kTPB < n_nodes ? id0 + kTPB : n_nodes;  // the block's names: [id0, idl)
-  uint64_t o = 0;
-  uint32_t v = 0, d = 0;
-  if (id <= n_nodes) {
-    o = dec_name_off(id, bidir);
-    offs[id] = (int64_t)o;
-    v = (uint32_t)((bidir ? id >> 1 : id) + 1);  // node ids < 2^31
-    d = dec_digits(v);
-    if (threadIdx.x == 0) s_lo = o;
-    if (id + 1 == idl) s_hi = o + d + (bidir ? 2 : 0);  // the range's end: past the block's last name
-  }
-  __syncthreads();
-  const uint64_t lo = s_lo, hi = idl > id0 ? s_hi : lo, base = lo & ~15ull;
-  if (id < idl) {
-    uint8_t* p = st + (o - base);
-    for (uint32_t j = d; j-- > 0;) {
-      p[j] = (uint8_t)('0' + v % 10u);
-      v /= 10u;
-    }
-    if (bidir) {
-      p[d] = ':';
-      p[d + 1] = (id & 1) ? '-' : '+';
-    }
-  }
-  __syncthreads();
-  for (uint64_t k = threadIdx.x; base + 16 * k < hi; k += kTPB) {
-    const uint64_t g = base + 16 * k;
-    if (g >= lo && g + 16 <= hi) {
-      *(uint4*)(blob + g) = *(const uint4*)(st + 16 * k);
-    } else {  // the range's partial first / last 16 bytes (neighbouring blocks own the rest)
-      for (uint32_t j = 0; j < 16; j++)
-        if (g + j >= lo && g + j < hi) blob[g + j] = st[16 * k + j];
-    }
-  }
-}
-#endif
 
 // ============================================================ K6: triplets ========
 // numpy's np.array(list_of_python_floats, dtype) element conversion (builders.py:281)
