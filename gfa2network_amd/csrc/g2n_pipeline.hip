@@ -993,7 +993,9 @@ static DictOut build_dictionary(g2n_context* c, const uint8_t* in, uint64_t len,
       }
       phase(c, "ids_fast");
       tid = dget<uint32_t>(c, S_TID, n_t);
-      insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
+      // the lookup round resolves the touches that claimed nothing; on an S prefix whose every touch is
+      // an S touch (g2n_dedup_keys' distinct keys) there are none: no launch, no host round trip
+      if (!(sprefix && n_st == n_t)) insert(kModeFast, 2, cap >= full_cap ? cap : 4096, tid);
       fast = !c->h_ctl->dict_general && !c->h_ctl->table_overflow && c->h_ctl->deferred == 0;
       if (!fast) {
         tid = nullptr;
