@@ -182,6 +182,7 @@ def parse_gfa(
     split_on_alignment: bool = False,
     device: int = 0,
     shard: str = "never",
+    chunk_bytes: int | None = None,
 ):
     """GPU ``parse_gfa`` (gfa2network/builders.py:30-299), matrix outputs only.
 
@@ -193,6 +194,11 @@ def parse_gfa(
     splits the file over the ranks (``parse_gfa_sharded``) when its working set would not fit a
     GPU's free HBM on some rank, ``"always"`` splits it regardless; both are collectives — every
     rank must make the same call on the same file (checked: a different path raises ValueError).
+    On one process (no group, or ``shard="auto"`` outside one), a plain file on disk whose working set
+    would not fit the GPU's free HBM is built in line-aligned chunks of the file on this one GPU
+    (``shard.build_chunked``: decimal segment names "1".."N" in S-first order, plain unweighted builds;
+    anything else is built in one piece).  ``chunk_bytes`` (extension) forces that chunked build with
+    chunks of about that many bytes.
     """
     if backend == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
@@ -210,6 +216,15 @@ def parse_gfa(
     dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
     if shard not in ("auto", "always", "never"):
         raise ValueError("shard must be 'auto', 'always' or 'never'")
+    if build_matrix and not hasattr(path, "read") and str(path) != "-" and not str(path).endswith(".gz"):
+        cb = chunk_bytes if chunk_bytes is not None else _chunk_for(path, shard, device)
+        if cb:
+            got = _parse_gfa_chunked(str(path), cb, directed=directed, weight_tag=weight_tag, verbose=verbose,
+                                     bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                                     strip_orientation=strip_orientation, dt=dt, asymmetric=asymmetric,
+                                     raw_bytes_id=raw_bytes_id, return_node_list=return_node_list, device=device)
+            if got is not None:
+                return got
     if build_matrix and _want_shard(path, shard, device):
         return parse_gfa_sharded(path, directed=directed, weight_tag=weight_tag, strip_orientation=strip_orientation,
                                  verbose=verbose, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
@@ -356,6 +371,60 @@ def _gz_inflated_estimate(p: str, size: int) -> int:
     except OSError:
         isize = 0
     return max(isize, 4 * size)
+
+
+def _chunk_for(path, shard: str, device: int) -> int:
+    """shard="auto" on one process: the chunk size that lets a plain file on disk whose working set
+    (WORKING_SET_PER_INPUT_BYTE x its size) exceeds the GPU's free HBM be built on this GPU alone
+    (build_chunked), or 0 (the one-piece build)."""
+    if shard != "auto" or _dist_world() >= 2 or not os.path.isfile(str(path)):
+        return 0
+    import torch
+
+    size = os.path.getsize(str(path))
+    free, _ = torch.cuda.mem_get_info(device)
+    if size * WORKING_SET_PER_INPUT_BYTE <= free:
+        return 0
+    # each chunk's working set beside the triplets kept so far (8 B per edge: <= the text's bytes)
+    return max(1 << 26, int(free // (2 * WORKING_SET_PER_INPUT_BYTE)))
+
+
+def _parse_gfa_chunked(path: str, chunk_bytes: int, *, directed: bool, weight_tag, verbose: bool, bidirected: bool,
+                       keep_directed_bidir: bool, strip_orientation: bool, dt, asymmetric: bool, raw_bytes_id: bool,
+                       return_node_list: bool, device: int, engine=None):
+    """parse_gfa on one GPU in chunks of the file (shard.build_chunked), or None when that build
+    declines (the caller builds the file in one piece)."""
+    if bidirected or weight_tag or strip_orientation:
+        return None
+    from .shard import HipEngine, build_chunked, scipy_index_dtype
+
+    gd = keep_directed_bidir or directed  # builders.py:143
+    maxsym = gd and not asymmetric        # builders.py:282
+    eng = engine or HipEngine(device)
+    res = build_chunked(path, engine=eng, chunk_bytes=chunk_bytes, directed=directed,
+                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric, dtype=dt.name,
+                        gather_names=return_node_list, keep_coo=not maxsym)
+    if res is None:
+        return None
+    raw = RawResult(status=0, n_lines=res.n_lines, n_records=res.n_records,
+                    n_records_before_error=res.n_records_before_error, n_nodes=res.n_nodes, dtype=dt,
+                    n_cast_overflow=res.n_cast_overflow)
+    if not maxsym:  # parse_gfa's stream-order COO (builders.py:281)
+        raw.format = "coo"
+        idt = scipy_index_dtype(0, res.n_nodes)
+        raw.rows = res.coo[0].cpu().numpy().astype(idt, copy=False)
+        raw.cols = res.coo[1].cpu().numpy().astype(idt, copy=False)
+        raw.data = res.coo[2].cpu().numpy()
+    else:
+        raw.format = "csr"
+        idt = scipy_index_dtype(res.index_maxval, res.n_nodes)
+        raw.indptr = res.indptr.cpu().numpy().astype(idt, copy=False)
+        raw.indices = res.indices.cpu().numpy().astype(idt, copy=False)
+        raw.data = res.data.cpu().numpy()
+    if return_node_list:
+        raw.names_blob, raw.names_offsets = res.names_blob, res.names_offsets
+    return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=verbose,
+                    path=path)
 
 
 def _want_shard(path, shard: str, device: int) -> bool:

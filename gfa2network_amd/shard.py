@@ -489,8 +489,9 @@ class HipEngine:
             w = torch.empty(0, dtype=tdt).element_size()
             return (DevArray(res.indptr or 0, n_rows + 1, 4), DevArray(res.indices or 0, res.nnz, 4),
                     DevArray(res.data or 0, res.nnz, w), not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted)
-        indptr = self._copy_out(res.indptr, n_rows + 1, torch.int32)
-        indices = self._copy_out(res.indices, res.nnz, torch.int32)
+        idx = torch.int64 if res.index_width == 8 else torch.int32  # (a whole matrix past 2^31 - 1 entries)
+        indptr = self._copy_out(res.indptr, n_rows + 1, idx)
+        indices = self._copy_out(res.indices, res.nnz, idx)
         vals = self._copy_out(res.data, res.nnz, tdt)
         return indptr, indices, vals, not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted
 
@@ -747,6 +748,82 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     out.parse_path = getattr(local, "parse_path", "")
     if keep_coo:
         out.coo = (local.rows, local.cols, local.data)
+    return out
+
+
+def build_chunked(path: str, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False,
+                  asymmetric=False, dtype="float64", gather_names=False, keep_coo=False) -> ShardResult | None:
+    """One file whose working set does not fit one GPU, on that GPU alone: its line-aligned byte
+    ranges of about `chunk_bytes` are read (pread) and parsed one after another straight into GLOBAL
+    decimal ids — the sharded fast path's one pass (`build_decimal_range`), each range's premise
+    evidence kept — so only one range's text and working set are resident at a time beside the
+    growing COO; the evidence is then checked over the whole file in stream order (the rule of
+    `_build_decimal_sharded`: S lines first, each range's names continuing the S lines before it,
+    every edge key an S key) and the CSR (or, keep_coo, the stream-order COO) built once over all
+    ranges' triplets.  Returns the whole matrix as one row slice, or None when the decimal-id premise
+    fails anywhere (names not "1".."N" in S-first order, bidirected / weighted / strip builds, an
+    error or warning in a range): the caller then builds the file in one piece, which raises the
+    reference's error.  (Segment names other than 1..N need one dictionary over the whole file; no
+    chunked build for them.)"""
+    import os
+    import time
+
+    import torch
+
+    opts = dict(directed=directed, bidirected=False, keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
+                strip_orientation=False, dtype=dtype, weight_tag=None)
+    gd = keep_directed_bidir or directed  # builders.py:143 (not bidirected)
+    maxsym = gd and not asymmetric        # builders.py:282
+    size = os.path.getsize(path)
+    n_chunks = max(1, -(-size // max(1, int(chunk_bytes))))
+    tm = {}
+    t0 = time.perf_counter()
+    rows_l, cols_l, data_l, ev = [], [], [], []
+    overflow = 0
+    for lo, hi in file_line_ranges(path, n_chunks):
+        buf = engine.read_range(path, lo, hi - lo)
+        got = engine.build_decimal_range(buf, opts, view=False, values=keep_coo)
+        del buf
+        if got is None:
+            return None
+        sh, e = got
+        rows_l.append(sh.rows)
+        cols_l.append(sh.cols)
+        if keep_coo:
+            data_l.append(sh.data)
+        overflow += int(sh.n_cast_overflow)
+        ev.append([int(v) for v in e])
+    seen_edge, s_before = False, 0
+    for e in ev:  # [lines, S lines, edges, records, d, largest edge key]
+        if e[1] and (seen_edge or e[4] != s_before):
+            return None
+        seen_edge = seen_edge or e[2] > 0
+        s_before += e[1]
+    n = s_before
+    if not 0 < n < INT32_MAX or max(e[5] for e in ev) > n:
+        return None
+    tm["build"] = (time.perf_counter() - t0) * 1e3
+    rows = torch.cat(rows_l) if len(rows_l) > 1 else rows_l[0]
+    cols = torch.cat(cols_l) if len(cols_l) > 1 else cols_l[0]
+    del rows_l, cols_l
+    out = ShardResult(status=0, n_lines=sum(e[0] for e in ev), n_records=sum(e[3] for e in ev),
+                      n_edges=sum(e[2] for e in ev), n_nodes=n, n_cast_overflow=overflow)
+    out.n_records_before_error = out.n_records
+    out.row_lo, out.row_hi = 0, n
+    if maxsym or not keep_coo:  # (a SUM build that returns its stream-order COO needs no CSR)
+        t1 = time.perf_counter()
+        indptr, indices, vals, _, _ = engine.csr_pair((rows, cols, None), (cols, rows, None) if maxsym else None,
+                                                      maxsym, 0, n, n, dtype, True, -1)
+        tm["csr"] = (time.perf_counter() - t1) * 1e3
+        out.indptr, out.indices, out.data = indptr, indices, vals
+        out.index_maxval = int(indices.numel()) if maxsym else int(rows.numel())
+    if keep_coo:
+        out.coo = (rows, cols, torch.cat(data_l) if len(data_l) > 1 else data_l[0])
+    if gather_names:  # node k is str(k + 1)
+        out.names_blob, out.names_offsets = nat.decimal_names(n, False)
+    out.fast_path = True
+    out.parse_path = f"chunked x{len(ev)}"
+    out.timings_ms = tm
     return out
 
 

@@ -330,3 +330,38 @@ def test_gpu_sharded_tile_local_range_premise(gpu, oracle_lib, tmp_path, world):
     mp.spawn(_range_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}.npy").exists()
+
+
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"asymmetric": True}, {"dtype": "int8"}])
+def test_gpu_chunked_single_gpu_build(gpu, oracle_lib, tmp_path, mode):
+    """parse_gfa(..., chunk_bytes=...) on one GPU: the file pread and parsed range by range into
+    global decimal ids (shard.build_chunked), the CSR / COO built once — equal to the oracle's
+    one-piece build bit for bit, at 3 and at ~40 ranges; a premise break (hashed names) falls back
+    to the one-piece build, the same answer."""
+    from gfa2network_amd import parse_gfa, synth
+    from gfa2network_amd.api import finalize
+
+    data = synth.host_bytes(200_000, 800_000, seed=31)
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    full = oracle_lib.run(data, **mode)
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                         return_node_list=True, raw_bytes_id=False, verbose=False)
+    for chunk in (len(data) // 3 + 1, 600_000):
+        A, nodes = parse_gfa(str(path), build_graph=False, build_matrix=True, return_node_list=True,
+                             chunk_bytes=chunk, **mode)
+        assert A.format == B.format and A.shape == B.shape and nodes == bnodes, chunk
+        if A.format == "coo":
+            assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+        else:
+            assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        assert A.data.tobytes() == B.data.tobytes()
+    hashed = data.replace(b"S\t7\t", b"S\tx7\t", 1).replace(b"\t7\t+\t", b"\tx7\t+\t")
+    path.write_bytes(hashed)
+    full = oracle_lib.run(hashed, **mode)
+    B = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                 return_node_list=False, raw_bytes_id=False, verbose=False)
+    A = parse_gfa(str(path), build_graph=False, build_matrix=True, chunk_bytes=600_000, **mode)
+    assert A.format == B.format and A.data.tobytes() == B.data.tobytes()
+    if A.format == "csr":
+        assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
