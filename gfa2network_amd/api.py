@@ -196,8 +196,8 @@ def parse_gfa(
     rank must make the same call on the same file (checked: a different path raises ValueError).
     On one process (no group, or ``shard="auto"`` outside one), a plain file on disk whose working set
     would not fit the GPU's free HBM is built in line-aligned chunks of the file on this one GPU
-    (``shard.build_chunked``: decimal segment names "1".."N" in S-first order, plain unweighted builds;
-    anything else is built in one piece).  ``chunk_bytes`` (extension) forces that chunked build with
+    (``shard.build_chunked``; a chunk with a parse error or the unsupported-record warning sends the
+    file to the one-piece build, which raises the reference's error).  ``chunk_bytes`` (extension) forces that chunked build with
     chunks of about that many bytes.
     """
     if backend == "igraph":
@@ -394,15 +394,14 @@ def _parse_gfa_chunked(path: str, chunk_bytes: int, *, directed: bool, weight_ta
                        return_node_list: bool, device: int, engine=None):
     """parse_gfa on one GPU in chunks of the file (shard.build_chunked), or None when that build
     declines (the caller builds the file in one piece)."""
-    if bidirected or weight_tag or strip_orientation:
-        return None
     from .shard import HipEngine, build_chunked, scipy_index_dtype
 
-    gd = keep_directed_bidir or directed  # builders.py:143
-    maxsym = gd and not asymmetric        # builders.py:282
+    gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
+    maxsym = gd and not asymmetric                               # builders.py:282
     eng = engine or HipEngine(device)
-    res = build_chunked(path, engine=eng, chunk_bytes=chunk_bytes, directed=directed,
-                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric, dtype=dt.name,
+    res = build_chunked(path, engine=eng, chunk_bytes=chunk_bytes, directed=directed, bidirected=bidirected,
+                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
+                        strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
                         gather_names=return_node_list, keep_coo=not maxsym)
     if res is None:
         return None

@@ -751,8 +751,112 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     return out
 
 
-def build_chunked(path: str, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False,
-                  asymmetric=False, dtype="float64", gather_names=False, keep_coo=False) -> ShardResult | None:
+def build_chunked(path: str, *, engine, chunk_bytes: int, directed=True, bidirected=False, keep_directed_bidir=False,
+                  asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None, gather_names=False,
+                  keep_coo=False) -> ShardResult | None:
+    """One file whose working set does not fit one GPU, built on that GPU alone in line-aligned chunks
+    of about `chunk_bytes`: the decimal-id chunks (`_chunked_decimal`) when the file's names are
+    "1".."N" in S-first order and the build is plain, else chunks with local ids merged into one
+    dictionary as they come (`_chunked_general`).  None when neither applies (a parse error or the
+    one-shot warning in a chunk): the caller builds the file in one piece, which raises the
+    reference's error."""
+    kw = dict(engine=engine, chunk_bytes=chunk_bytes, directed=directed, keep_directed_bidir=keep_directed_bidir,
+              asymmetric=asymmetric, dtype=dtype, gather_names=gather_names, keep_coo=keep_coo)
+    if not (bidirected or weight_tag or strip_orientation):
+        got = _chunked_decimal(path, **kw)
+        if got is not None:
+            return got
+    return _chunked_general(path, bidirected=bidirected, strip_orientation=strip_orientation, weight_tag=weight_tag,
+                            **kw)
+
+
+def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirected, keep_directed_bidir, asymmetric,
+                     strip_orientation, dtype, weight_tag, gather_names, keep_coo) -> ShardResult | None:
+    """Chunks in stream order, any names: each chunk is built on its own (local first-touch ids, its
+    distinct keys in local id order), then its keys are deduplicated together with the file's keys
+    so far, those first (`dedup_keys` keeps arrival order: a known key gets its global id, a new one
+    the next id in the chunk's first-touch order — which is the file's, since every earlier chunk
+    came first), the new keys appended to the file's names (`gather_keys`) and the chunk's triplets
+    remapped to global ids (`remap_pairs`).  The CSR / COO is built once over all chunks' triplets.
+    None on a parse error or the unsupported-record warning in any chunk (the one-piece build then
+    decides)."""
+    import os
+    import time
+
+    import torch
+
+    opts = dict(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dtype, weight_tag=weight_tag)
+    gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
+    maxsym = gd and not asymmetric                               # builders.py:282
+    uniform = not weight_tag
+    size = os.path.getsize(path)
+    n_chunks = max(1, -(-size // max(1, int(chunk_bytes))))
+    t0 = time.perf_counter()
+    dev = engine.device
+    g_blob = torch.zeros(0, dtype=torch.uint8, device=dev)  # the file's distinct keys so far, in global id order
+    g_offs = torch.zeros(1, dtype=torch.int64, device=dev)
+    rows_l, cols_l, data_l = [], [], []
+    n_lines = n_records = n_edges = overflow = 0
+    for lo, hi in file_line_ranges(path, n_chunks):
+        buf = engine.read_range(path, lo, hi - lo)
+        sh = engine.local_build(buf, opts)
+        del buf
+        if sh.status != 0 or sh.has_warning:
+            return None
+        n_g, n_l = int(g_offs.numel()) - 1, int(sh.n_local_nodes)
+        blob = torch.cat([g_blob, sh.names_blob.to(dev)])
+        offs = torch.cat([g_offs, sh.names_offsets.to(dev)[1:] + g_offs[-1]])
+        ids, first_of, nd = engine.dedup_keys(blob, offs)
+        if nd > n_g:  # the chunk's new keys, in global id order, appended to the file's names
+            idx = first_of[n_g:nd]
+            idx64 = idx.to(torch.int64)
+            nbytes = int((offs[idx64 + 1] - offs[idx64]).sum().item())
+            nb, no = engine.gather_keys(blob, offs, idx, nbytes)
+            g_blob = torch.cat([g_blob, nb[:nbytes]])
+            g_offs = torch.cat([g_offs, no[1:] + g_offs[-1]])
+        del blob, offs
+        rows, cols = sh.rows, sh.cols
+        if n_l and rows.numel():
+            rows, cols = engine.remap_pairs(rows, cols, ids[n_g:n_g + n_l].contiguous())
+        rows_l.append(rows)
+        cols_l.append(cols)
+        data_l.append(sh.data)
+        n_lines += int(sh.n_lines)
+        n_records += int(sh.n_records)
+        n_edges += int(sh.n_edges)
+        overflow += int(sh.n_cast_overflow)
+    n = int(g_offs.numel()) - 1
+    if n >= INT32_MAX:
+        return None
+    tm = {"build": (time.perf_counter() - t0) * 1e3}
+    rows = torch.cat(rows_l) if len(rows_l) > 1 else rows_l[0]
+    cols = torch.cat(cols_l) if len(cols_l) > 1 else cols_l[0]
+    data = torch.cat(data_l) if len(data_l) > 1 else data_l[0]
+    del rows_l, cols_l, data_l
+    out = ShardResult(status=0, n_lines=n_lines, n_records=n_records, n_edges=n_edges, n_nodes=n,
+                      n_cast_overflow=overflow)
+    out.n_records_before_error = n_records
+    out.row_lo, out.row_hi = 0, n
+    if maxsym or not keep_coo:
+        t1 = time.perf_counter()
+        d = None if uniform else data
+        indptr, indices, vals, _, _ = engine.csr_pair((rows, cols, d), (cols, rows, d) if maxsym else None, maxsym,
+                                                      0, n, n, dtype, uniform, -1)
+        tm["csr"] = (time.perf_counter() - t1) * 1e3
+        out.indptr, out.indices, out.data = indptr, indices, vals
+        out.index_maxval = int(indices.numel()) if maxsym else int(rows.numel())
+    if keep_coo:
+        out.coo = (rows, cols, data)
+    if gather_names:
+        out.names_blob, out.names_offsets = g_blob.cpu().numpy(), g_offs.cpu().numpy()
+    out.parse_path = "chunked general"
+    out.timings_ms = tm
+    return out
+
+
+def _chunked_decimal(path: str, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False,
+                     asymmetric=False, dtype="float64", gather_names=False, keep_coo=False) -> ShardResult | None:
     """One file whose working set does not fit one GPU, on that GPU alone: its line-aligned byte
     ranges of about `chunk_bytes` are read (pread) and parsed one after another straight into GLOBAL
     decimal ids — the sharded fast path's one pass (`build_decimal_range`), each range's premise

@@ -1,8 +1,9 @@
 """One file built on one GPU in line-aligned chunks (shard.build_chunked, parse_gfa's chunked mode)
 equals the one-piece build — here on the CPU engine (the oracle per range, scipy for the CSR), on
 the HIP engine in test_gpu_shard.py.  Chunk sizes from 97 bytes (dozens of ranges, S sections and
-edge sections split anywhere) to the whole file; every premise break declines (None) so the caller
-builds in one piece."""
+edge sections split anywhere) to the whole file, decimal names (one-pass range parse) and any names
+(chunks merged into one dictionary); a parse error or warning declines (None) so the caller builds in
+one piece."""
 import random
 
 import numpy as np
@@ -69,19 +70,97 @@ def test_chunked_equals_one_piece(oracle_lib, tmp_path, mode, chunk):
 
 
 @pytest.mark.parametrize("breaks", ["late_s", "ghost", "offset", "hashed", "error"])
-def test_chunked_declines_when_the_premise_breaks(oracle_lib, tmp_path, breaks):
-    """A premise break anywhere in the file — even one only the ranges' evidence together can see
-    (an S line in a later range than an edge, names that start past 1, a key past the S count) — or
-    a parse error declines: the one-piece build then decides (and raises the reference's error)."""
+def test_chunked_decimal_premise_breaks(oracle_lib, tmp_path, breaks):
+    """A decimal-id premise break anywhere in the file — even one only the ranges' evidence together
+    can see (an S line in a later range than an edge, names that start past 1, a key past the S
+    count) — declines the decimal chunks (None); the merged-dictionary chunks then build the file
+    (the one-piece answer), and a parse error declines both (the one-piece build raises it)."""
+    from gfa2network_amd.api import finalize
+    from gfa2network_amd.shard import _chunked_decimal
+    from oracle import oracle as orc
+    from shard_cpu_engine import CpuEngine
+
     data = _decimal_gfa(22, 300, 1200, breaks)
     path = tmp_path / "in.gfa"
     path.write_bytes(data)
+    full = oracle_lib.run(data)
     for chunk in (113, 4000):
-        assert _chunked(path, chunk, {}) is None, (breaks, chunk)
+        assert _chunked_decimal(str(path), engine=CpuEngine(orc), chunk_bytes=chunk) is None, (breaks, chunk)
+        got = _chunked(path, chunk, {})
+        if breaks == "error":
+            assert got is None
+            continue
+        A, nodes = got
+        B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype("float64"), return_node_list=True,
+                             raw_bytes_id=False, verbose=False)
+        assert nodes == bnodes and np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
 
 
 @pytest.mark.parametrize("mode", [{"bidirected": True}, {"weight_tag": "RC"}])
-def test_chunked_declines_other_builds(oracle_lib, tmp_path, mode):
+def test_chunked_other_builds_take_the_general_chunks(oracle_lib, tmp_path, mode):
+    """Bidirected / weighted decimal files are not the one-pass range parse's: the merged-dictionary
+    chunks build them (same answer as one piece)."""
+    from gfa2network_amd.api import finalize
+
+    data = _decimal_gfa(23, 100, 300)
     path = tmp_path / "in.gfa"
-    path.write_bytes(_decimal_gfa(23, 100, 300))
-    assert _chunked(path, 500, mode) is None
+    path.write_bytes(data)
+    A, nodes = _chunked(path, 500, mode)
+    full = oracle_lib.run(data, **mode)
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype("float64"), return_node_list=True,
+                         raw_bytes_id=False, verbose=False)
+    assert nodes == bnodes and A.data.tobytes() == B.data.tobytes()
+
+
+def _named_gfa(seed, n_s, n_l, shuffle, extra=()):
+    """Names that are not 1..N, edges before S lines, keys no S line defines, weights."""
+    r = random.Random(seed)
+    names = [f"s{k}" if k % 4 else f"node_{k:06d}_" + "q" * r.randint(0, 20) for k in range(n_s)]
+    lines = [f"S\t{n}\t*\n" for n in names]
+    for _ in range(n_l):
+        a, b = r.choice(names), r.choice(names + ["ghost1", "ghost2"])
+        lines.append(f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t*\tRC:i:{r.randint(0, 7)}\n")
+    if shuffle:
+        r.shuffle(lines)
+    lines[len(lines) // 2:len(lines) // 2] = list(extra)
+    return "".join(lines).encode()
+
+
+GENERAL = [
+    (False, {}), (True, {}), (True, {"directed": False}), (True, {"bidirected": True}),
+    (True, {"bidirected": True, "keep_directed_bidir": True}), (True, {"asymmetric": True, "weight_tag": "RC",
+                                                                     "dtype": "int32"}),
+    (True, {"weight_tag": "RC", "dtype": "int8"}), (True, {"dtype": "bool"}),
+    (True, {"weight_tag": "RC", "directed": False}), (False, {"weight_tag": "RC", "dtype": "float32"}),
+]
+
+
+@pytest.mark.parametrize("shuffle,mode", GENERAL)
+@pytest.mark.parametrize("chunk", [211, 3000, 1 << 30])
+def test_chunked_general_names_equal_one_piece(oracle_lib, tmp_path, shuffle, mode, chunk):
+    """Any names: each chunk's keys merged into the file's dictionary in arrival order (the global
+    first-touch ids), the chunk's triplets remapped — equal to the one-piece build, node list included."""
+    from gfa2network_amd.api import finalize
+
+    data = _named_gfa(31, 250, 1200, shuffle)
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    got = _chunked(path, chunk, mode)
+    assert got is not None
+    A, nodes = got
+    full = oracle_lib.run(data, **mode)
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                         return_node_list=True, raw_bytes_id=False, verbose=False)
+    assert A.format == B.format and A.shape == B.shape and nodes == bnodes
+    if A.format == "coo":
+        assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+    else:
+        assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+    assert A.data.tobytes() == B.data.tobytes()
+
+
+@pytest.mark.parametrize("extra", [["L\tbad\t+\n"], ["W\tsample\t1\tchr1\t0\t10\t>s1\n"]])
+def test_chunked_general_declines_errors_and_warnings(oracle_lib, tmp_path, extra):
+    path = tmp_path / "in.gfa"
+    path.write_bytes(_named_gfa(32, 200, 800, True, extra))
+    assert _chunked(path, 700, {}) is None

@@ -332,16 +332,17 @@ def test_gpu_sharded_tile_local_range_premise(gpu, oracle_lib, tmp_path, world):
         assert (tmp_path / f"ok{r}.npy").exists()
 
 
-@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"asymmetric": True}, {"dtype": "int8"}])
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"asymmetric": True}, {"dtype": "int8"},
+                                  {"bidirected": True, "weight_tag": "RC"}])
 def test_gpu_chunked_single_gpu_build(gpu, oracle_lib, tmp_path, mode):
-    """parse_gfa(..., chunk_bytes=...) on one GPU: the file pread and parsed range by range into
-    global decimal ids (shard.build_chunked), the CSR / COO built once — equal to the oracle's
-    one-piece build bit for bit, at 3 and at ~40 ranges; a premise break (hashed names) falls back
-    to the one-piece build, the same answer."""
+    """parse_gfa(..., chunk_bytes=...) on one GPU: the file pread and parsed range by range
+    (shard.build_chunked: into global decimal ids, or — bidirected / weighted builds, hashed names —
+    with local ids merged into one dictionary chunk by chunk), the CSR / COO built once — equal to
+    the oracle's one-piece build bit for bit, at 3 and at ~40 ranges."""
     from gfa2network_amd import parse_gfa, synth
     from gfa2network_amd.api import finalize
 
-    data = synth.host_bytes(200_000, 800_000, seed=31)
+    data = synth.host_bytes(200_000, 800_000, seed=31, rc_tag=bool(mode.get("weight_tag")))
     path = tmp_path / "in.gfa"
     path.write_bytes(data)
     full = oracle_lib.run(data, **mode)
@@ -359,9 +360,12 @@ def test_gpu_chunked_single_gpu_build(gpu, oracle_lib, tmp_path, mode):
     hashed = data.replace(b"S\t7\t", b"S\tx7\t", 1).replace(b"\t7\t+\t", b"\tx7\t+\t")
     path.write_bytes(hashed)
     full = oracle_lib.run(hashed, **mode)
-    B = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
-                 return_node_list=False, raw_bytes_id=False, verbose=False)
-    A = parse_gfa(str(path), build_graph=False, build_matrix=True, chunk_bytes=600_000, **mode)
-    assert A.format == B.format and A.data.tobytes() == B.data.tobytes()
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                         return_node_list=True, raw_bytes_id=False, verbose=False)
+    A, nodes = parse_gfa(str(path), build_graph=False, build_matrix=True, return_node_list=True,
+                         chunk_bytes=600_000, **mode)
+    assert A.format == B.format and A.data.tobytes() == B.data.tobytes() and nodes == bnodes
     if A.format == "csr":
         assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+    else:
+        assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
