@@ -389,6 +389,9 @@ def _chunk_for(path, shard: str, device: int) -> int:
     return max(1 << 26, int(free // (2 * WORKING_SET_PER_INPUT_BYTE)))
 
 
+_CHUNK_ENGINES: dict = {}
+
+
 def _parse_gfa_chunked(path: str, chunk_bytes: int, *, directed: bool, weight_tag, verbose: bool, bidirected: bool,
                        keep_directed_bidir: bool, strip_orientation: bool, dt, asymmetric: bool, raw_bytes_id: bool,
                        return_node_list: bool, device: int, engine=None):
@@ -398,7 +401,9 @@ def _parse_gfa_chunked(path: str, chunk_bytes: int, *, directed: bool, weight_ta
 
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
-    eng = engine or HipEngine(device)
+    eng = engine or _CHUNK_ENGINES.get(device)
+    if eng is None:  # one engine (two build contexts and their grow-only arenas) per device, reused
+        eng = _CHUNK_ENGINES[device] = HipEngine(device)
     res = build_chunked(path, engine=eng, chunk_bytes=chunk_bytes, directed=directed, bidirected=bidirected,
                         keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
                         strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,

@@ -798,10 +798,19 @@ def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirecte
     g_offs = torch.zeros(1, dtype=torch.int64, device=dev)
     rows_l, cols_l, data_l = [], [], []
     n_lines = n_records = n_edges = overflow = 0
+    tm = {"read": 0.0, "local_build": 0.0, "merge_keys": 0.0, "remap": 0.0}
+
+    def lap(key, t):
+        tm[key] += (time.perf_counter() - t) * 1e3
+        return time.perf_counter()
+
     for lo, hi in file_line_ranges(path, n_chunks):
+        t = time.perf_counter()
         buf = engine.read_range(path, lo, hi - lo)
+        t = lap("read", t)
         sh = engine.local_build(buf, opts)
         del buf
+        t = lap("local_build", t)
         if sh.status != 0 or sh.has_warning:
             return None
         n_g, n_l = int(g_offs.numel()) - 1, int(sh.n_local_nodes)
@@ -816,9 +825,11 @@ def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirecte
             g_blob = torch.cat([g_blob, nb[:nbytes]])
             g_offs = torch.cat([g_offs, no[1:] + g_offs[-1]])
         del blob, offs
+        t = lap("merge_keys", t)
         rows, cols = sh.rows, sh.cols
         if n_l and rows.numel():
             rows, cols = engine.remap_pairs(rows, cols, ids[n_g:n_g + n_l].contiguous())
+        t = lap("remap", t)
         rows_l.append(rows)
         cols_l.append(cols)
         data_l.append(sh.data)
@@ -829,7 +840,7 @@ def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirecte
     n = int(g_offs.numel()) - 1
     if n >= INT32_MAX:
         return None
-    tm = {"build": (time.perf_counter() - t0) * 1e3}
+    tm["build"] = (time.perf_counter() - t0) * 1e3
     rows = torch.cat(rows_l) if len(rows_l) > 1 else rows_l[0]
     cols = torch.cat(cols_l) if len(cols_l) > 1 else cols_l[0]
     data = torch.cat(data_l) if len(data_l) > 1 else data_l[0]
