@@ -1478,11 +1478,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   if (lean_done)
     D.n_nodes = n_s * tps;
   else
-    // expected distinct keys: the S keys plus a few edge-only ones — or, when S lines are few next to
+    // expected distinct keys: the S keys plus a few edge-only ones — or, when S keys are under 1/32 of
     // the edge touches (an S-less range of a chunked build, an edge-list-like GFA), half the edge
     // touches: a table sized for the S keys alone overflows its probe bound and is redone at full size
     D = build_dictionary(c, in, len, T, n_t, n_s * tps,
-                         n_s * tps + (n_s * tps * 8 < n_e * tpe ? (n_e * tpe) / 2 : (n_e * tpe) / 16) + 1024, bidir,
+                         n_s * tps + (n_s * tps * 32 < n_e * tpe ? (n_e * tpe) / 2 : (n_e * tpe) / 16) + 1024, bidir,
                          op.tid && !c->h_ctl->int_fail ? kIntDone : kIntFailed);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
   const uint64_t n_nodes = shard_dec ? (uint64_t)o->reserved[3] : D.n_nodes;  // global ids: the file's nodes
