@@ -544,9 +544,25 @@ class Comm:
         return outs, recv
 
     def allgather_v(self, x):
-        """every rank's (variable-length) tensor, in rank order (no padding: one broadcast per
-        rank when the lengths differ)"""
-        return [t for _, t in self.parts(x, root=None)]
+        """every rank's (variable-length, 1-D) tensor, in rank order: one padded all-gather when
+        the lengths are balanced (world x the longest within twice their sum — the owners' hashed
+        key sets), else one broadcast per rank (no padding)"""
+        torch = self.torch
+        if self.world == 1:
+            return [x]
+        xc = self._c(x.contiguous())
+        n = torch.tensor([xc.numel()], dtype=torch.int64, device=xc.device)
+        ns = [torch.empty_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        sizes = [int(v.item()) for v in ns]
+        m = max(sizes)
+        if m == 0 or m * self.world > 2 * sum(sizes):
+            return [t for _, t in self.parts(x, root=None, sizes=sizes)]
+        pad = torch.zeros(m, dtype=xc.dtype, device=xc.device)
+        pad[:xc.numel()] = xc
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad, group=self.group)
+        return [o[:k].to(x.device) for o, k in zip(outs, sizes)]
 
     def parts(self, x, root=None, sizes=None):
         """Yield (rank, tensor) for every rank's (variable-length, 1-D) tensor in rank order — on
