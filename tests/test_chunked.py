@@ -164,3 +164,22 @@ def test_chunked_general_declines_errors_and_warnings(oracle_lib, tmp_path, extr
     path = tmp_path / "in.gfa"
     path.write_bytes(_named_gfa(32, 200, 800, True, extra))
     assert _chunked(path, 700, {}) is None
+
+
+def test_auto_mode_chooses_chunks_only_past_free_memory(tmp_path, monkeypatch):
+    """shard="auto" on one process: chunked only for a plain file on disk whose working set
+    (WORKING_SET_PER_INPUT_BYTE x its size) passes the GPU's free HBM; never for "never"."""
+    import torch
+
+    from gfa2network_amd import api
+
+    path = tmp_path / "in.gfa"
+    path.write_bytes(_decimal_gfa(24, 50, 100))
+    size = path.stat().st_size
+    monkeypatch.setattr(api, "_dist_world", lambda: 1)
+    for free, want in ((size * api.WORKING_SET_PER_INPUT_BYTE + 1, False), (size, True)):
+        monkeypatch.setattr(torch.cuda, "mem_get_info", lambda device=None, f=free: (f, 2 * f))
+        got = api._chunk_for(str(path), "auto", 0)
+        assert bool(got) == want and (not got or got >= 1 << 26)
+        assert api._chunk_for(str(path), "never", 0) == 0
+    assert api._chunk_for(str(tmp_path / "missing.gfa"), "auto", 0) == 0
