@@ -51,7 +51,12 @@ constexpr uint32_t kWideDigitBits = 11;            // pass 2 of a partition past
 #ifndef G2N_FIN_TPB  // experiment builds vary the finish block (one row per thread)
 #define G2N_FIN_TPB 256
 #endif
-#ifdef G2N_FIN_W8  // experiment: 8 waves per SIMD (VGPRs <= 64, some spilled)
+// F1 at 8 waves per SIMD: its 106 SGPRs held it to 7; capped, 34 of them spill to VGPR lanes (VGPRs
+// stay at 62) and the C4 build gains 0.08-0.13 ms (same box, tools/gpu_r4fw8.sh).  0: uncapped.
+#ifndef G2N_FIN_W8
+#define G2N_FIN_W8 1
+#endif
+#if G2N_FIN_W8
 #define G2N_FIN_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
 #else
 #define G2N_FIN_WAVES
