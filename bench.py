@@ -3,13 +3,22 @@
 
 One "step" = one full pass of the hot path over one HBM-resident synthetic GFA: raw bytes
 already in HBM -> CSR (indptr / indices / data) in HBM, i.e. g2n_build_device() — lines,
-classify, parse + weights, first-touch node ids, node-name blob, triplets, radix sort,
-duplicate sums and (default mode) the A.maximum(A.T) symmetrisation.  Workload = C4 of
-BASELINE.json (50M S / 200M L, default flags), the north star's 200M-edge config; the
-gzip inflate and the PCIe copy are host ingest, measured separately.
+classify, parse + weights, first-touch node ids, node-name blob, triplets and (default mode)
+the A.maximum(A.T) symmetrisation.  The gzip inflate and the PCIe copy are host ingest,
+measured separately (the end_to_end leg).
 
-`python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run: one
-rank per GPU, weak scaling — every rank builds its own independently seeded C4 input).
+* `--gpus 1` (default): C4 of BASELINE.json (50M S / 200M L, default flags), the north star's
+  200M-edge config, is `value`.  The same line carries `scaling_reference`: C5 (the multi-GPU
+  config) built by one GPU alone and through the sharded protocol at one rank, with decimal and
+  hashed segment names — the first point of the N-GPU curve on the N-GPU workload.
+* `--gpus N > 1`: C5 as ONE file byte-range-sharded over N ranks (strong scaling: the total work
+  is fixed), one process per GPU over RCCL.  Under `torch.distributed.run` the ranks come from its
+  environment; started plainly (`python bench.py --gpus N`, no WORLD_SIZE) the script launches the
+  N rank processes itself before anything touches a GPU.  Every rank checks that the process group
+  holds exactly N ranks on the nccl backend and exits non-zero otherwise.  `value` = the file's
+  edge records / max-over-ranks time (decimal names: the fast path); `alt_paths.hashed_names` times
+  the general owner protocol on the same dimensions with hashed names.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -49,10 +58,67 @@ def _args():
     ap.add_argument("--force-protocol", action="store_true",
                     help="sharded runs: the general owner protocol even where the decimal fast path (or, on one "
                          "rank, no exchange at all) applies — to time the protocol itself")
+    ap.add_argument("--no-c5-reference", action="store_true",
+                    help="--gpus 1: skip the C5 legs (one GPU alone and sharded at one rank) the N-GPU curve starts from")
     ap.add_argument("--shard", action="store_true",
                     help="byte-range-shard the workload's one file over the ranks (gfa2network_amd/shard.py; "
                          "always on for C5)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def needs_launch(n_gpus: int, env=None) -> bool:
+    """`python bench.py --gpus N > 1` started without a launcher (no WORLD_SIZE in the environment)
+    starts its own N ranks."""
+    env = os.environ if env is None else env
+    return n_gpus > 1 and "WORLD_SIZE" not in env
+
+
+def launch_ranks(n: int, argv: list, script: str | None = None, env=None, poll_s: float = 0.2) -> int:
+    """One child process per rank (RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1, a
+    free MASTER_PORT), each running `script` (this file) with `argv`; the parent never touches a GPU
+    (no HIP call happens before the children exist, and nothing is exec'ed).  Waits for all of them;
+    the first child that fails has the others terminated.  Returns the job's exit code (0, or the
+    first failure's, negative signals mapped to 128 + signal)."""
+    import subprocess
+
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, script or str(Path(__file__).resolve())] + list(argv), env=e))
+    rc, pending = 0, list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in pending:
+                    q.terminate()
+        if pending:
+            time.sleep(poll_s)
+    return rc
+
+
+def check_world(n_gpus: int, world: int, backend: str) -> None:
+    """The process group must be exactly the N ranks `--gpus N` asked for, over RCCL (nccl)."""
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but the process group holds {world} rank(s); "
+                         f"run `python bench.py --gpus {n_gpus}` (it launches its ranks) or torch.distributed.run "
+                         f"with --nproc-per-node {n_gpus}")
+    if backend != "nccl":
+        raise SystemExit(f"bench.py: process group backend is {backend!r}, not nccl (RCCL)")
 
 
 def _dist_setup(n_gpus: int, always: bool = False):
@@ -61,7 +127,8 @@ def _dist_setup(n_gpus: int, always: bool = False):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 or always:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
         import torch
@@ -69,6 +136,10 @@ def _dist_setup(n_gpus: int, always: bool = False):
 
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        check_world(n_gpus, dist.get_world_size(), dist.get_backend())
+        world = dist.get_world_size()
+    elif n_gpus != world:
+        check_world(n_gpus, world, "nccl")
     return world, rank, local
 
 
@@ -416,15 +487,16 @@ def _line_start_device(ptr: int, length: int, nominal: int) -> int:
     return length
 
 
-def main_sharded(args, wl):
-    """BASELINE config 5: ONE synthetic file byte-range-sharded over the ranks.
-    Every rank holds the whole file in its HBM (the generator is deterministic: the same bytes on
-    every rank; generation is untimed) and builds only its line-aligned range through the sharded
-    protocol (gfa2network_amd/shard.py: record counts all-gather + premise all-reduce over RCCL, the
-    range parsed into global decimal ids, triplets all-to-all to their row owners, the rank's CSR row
-    slice).  Strong scaling: the total work is the one file.  Rank 0 first times the same file built
-    by one GPU alone (g2n_build_device), the scaling reference of the same line."""
-    world, rank, local = _dist_setup(args.gpus, always=True)
+def sharded_leg(args, wl, world: int, rank: int, local: int, names: str, force_protocol: bool = False,
+                one_gpu: bool = True) -> dict:
+    """ONE synthetic file byte-range-sharded over the group's ranks.  Every rank
+    holds the whole file in its HBM (the generator is deterministic: the same bytes on every rank;
+    generation is untimed) and builds only its line-aligned range through the sharded protocol
+    (gfa2network_amd/shard.py: decimal names — one all-gather of the ranges' evidence, the range
+    parsed straight into global ids; other names — the owner protocol: keys all-to-all to their
+    owners, owner dedup, global ids by ranking; then triplets all-to-all to their row owners and
+    the rank's CSR row slice).  Strong scaling: the total work is the one file.  one_gpu: rank 0
+    first times the same file built by one GPU alone (g2n_build_device), the scaling reference."""
     import torch
     import torch.distributed as dist
 
@@ -434,79 +506,134 @@ def main_sharded(args, wl):
 
     n_s = max(1, int(wl.n_segments * args.scale))
     n_l = max(1, int(wl.n_links * args.scale))
-    dev_in = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=wl.rc_tag, device=local, names=args.names)
+    dev_in = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=wl.rc_tag, device=local, names=names)
     starts = [_line_start_device(dev_in.ptr, dev_in.len, r * dev_in.len // world) for r in range(world)] + [dev_in.len]
     lo, hi = starts[rank], starts[rank + 1]
     mode = dict(wl.mode)
     # copy_out=False: each rank's CSR slice stays in its engine's HBM arena, as the one-GPU build's
     # result stays in its context (no device-to-device copy into torch tensors)
     kw = dict(directed=mode.get("directed", True), bidirected=mode.get("bidirected", False),
-              weight_tag=mode.get("weight_tag"), dtype="float64", force_protocol=args.force_protocol,
-              copy_out=False)
+              weight_tag=mode.get("weight_tag"), dtype="float64", force_protocol=force_protocol, copy_out=False)
     one = None
     lib = nat.load()
-    if rank == 0:  # the whole file on one GPU: the scaling reference
-        ctx = lib.g2n_context_create(local)
-        o = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=local,
-                             directed=kw["directed"], bidirected=kw["bidirected"], weight_tag=kw["weight_tag"])
-        res = nat.Result()
-        for _ in range(max(1, args.warmup)):
-            assert lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res)) == 0
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            assert lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res)) == 0
-        dt = (time.perf_counter() - t0) / args.steps
-        one = {"ms_per_step": round(dt * 1e3, 3), "value": round(n_l / dt / 1e6, 2), "nnz": int(res.nnz)}
-        lib.g2n_context_destroy(ctx)
-    dist.barrier()
-    eng = HipEngine(local)
-    buf = _DevBytes(dev_in.ptr + lo, hi - lo)
-    for _ in range(args.warmup):
-        build_sharded(buf, engine=eng, **kw)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    tms = []
-    for _ in range(args.steps):
-        res = build_sharded(buf, engine=eng, **kw)
-        tms.append(res.timings_ms)
-    torch.cuda.synchronize()
-    dist.barrier()
-    elapsed = _max_over_ranks(world, time.perf_counter() - t0)
-    slice_nnz = torch.tensor([int(res.indices.numel())], dtype=torch.int64, device="cuda")
-    dist.all_reduce(slice_nnz)
-    ms = elapsed / args.steps * 1e3
+    try:
+        if one_gpu and rank == 0:  # the whole file on one GPU: the scaling reference
+            ctx = lib.g2n_context_create(local)
+            o = nat.make_options(dtype="float64", output=nat.OUT_CSR, want_node_names=True, device=local,
+                                 directed=kw["directed"], bidirected=kw["bidirected"], weight_tag=kw["weight_tag"])
+            res = nat.Result()
+            try:
+                for i in range(max(1, args.warmup) + args.steps):
+                    if i == max(1, args.warmup):
+                        t0 = time.perf_counter()
+                    rc = lib.g2n_build_device(ctx, dev_in.ptr, dev_in.len, ctypes.byref(o), ctypes.byref(res))
+                    if rc != 0:
+                        raise RuntimeError(f"one-GPU {wl.name}: {nat.status_name(rc)}: {nat.last_error()}")
+                dt = (time.perf_counter() - t0) / args.steps
+                one = {"ms_per_step": round(dt * 1e3, 3), "value": round(n_l / dt / 1e6, 2), "nnz": int(res.nnz),
+                       "n_nodes": int(res.n_nodes)}
+            finally:
+                lib.g2n_context_destroy(ctx)
+        dist.barrier()
+        eng = HipEngine(local)
+        try:
+            buf = _DevBytes(dev_in.ptr + lo, hi - lo)
+            for _ in range(args.warmup):
+                build_sharded(buf, engine=eng, **kw)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            tms = []
+            for _ in range(args.steps):
+                res = build_sharded(buf, engine=eng, **kw)
+                tms.append(res.timings_ms)
+            torch.cuda.synchronize()
+            dist.barrier()
+            elapsed = _max_over_ranks(world, time.perf_counter() - t0)
+            slice_nnz = torch.tensor([int(res.indices.numel())], dtype=torch.int64, device="cuda")
+            dist.all_reduce(slice_nnz)
+        finally:
+            eng.close()
+    finally:
+        dev_in.free()
     value = res.n_edges * args.steps / elapsed / 1e6
+    leg = {"value": round(value, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "gb_per_s_ingested": round(dev_in.len * args.steps / elapsed / 1e9, 2),
+           "n_segments": n_s, "n_links": n_l, "input_bytes": dev_in.len, "n_nodes": res.n_nodes,
+           "nnz": int(slice_nnz.item()), "segment_names": names,
+           "id_path": ("decimal-id fast path" if res.fast_path else
+                       "general owner protocol" + (" (forced at one rank)" if force_protocol else "")),
+           "host_ms_per_stage_rank0": {k: round(sum(t.get(k, 0.0) for t in tms) / len(tms), 2) for k in tms[0]}}
+    if one is not None:
+        leg["one_gpu"] = one
+        leg["speedup_vs_one_gpu"] = round(value / one["value"], 3)
+        leg["same_shape_as_one_gpu"] = one["nnz"] == leg["nnz"] and one["n_nodes"] == leg["n_nodes"]
+    return leg
+
+
+def main_sharded(args, wl):
+    """`--gpus N > 1` (or `--shard`): the N-rank line (module docstring)."""
+    import torch.distributed as dist
+
+    world, rank, local = _dist_setup(args.gpus, always=True)
+    leg = sharded_leg(args, wl, world, rank, local, args.names, args.force_protocol)
+    alt = None
+    if not args.no_alt and args.names == "decimal":
+        alt = sharded_leg(args, wl, world, rank, local, "hashed")
+    mode = dict(wl.mode)
     line = {
         "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",
-        "value": round(value, 2), "unit": "M edge records/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong",
+        "value": leg["value"], "unit": "M edge records/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": leg["ms_per_step"], "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u8/int64 (float64 weights)",
         "data": "synthetic (deterministic generator, gfa2network_amd/csrc/synth.h), generated in HBM on every rank",
+        "world_size": world, "backend": dist.get_backend(),
         "config": {"workload": f"{wl.name}: {wl.note}, one file byte-range-sharded over {world} rank(s)"
                                + (f" x{args.scale}" if args.scale != 1 else ""),
-                   "n_segments": n_s, "n_links": n_l, "input_bytes": dev_in.len, "n_nodes": res.n_nodes,
-                   "nnz": int(slice_nnz.item()), "mode": mode or "default", "output": "csr row slice per rank",
-                   "parallelism": f"shard x{world} (RCCL: all-gather of range counts, all-reduce of the "
-                                  f"id premise, all-to-all of triplets to row owners)",
-                   "segment_names": args.names,
-                   "id_path": ("decimal-id fast path" if res.fast_path else
-                               "general owner protocol" + (" (forced)" if args.force_protocol else ""))},
-        "gb_per_s_ingested": round(dev_in.len * args.steps / elapsed / 1e9, 2),
-        "host_ms_per_stage_rank0": {k: round(sum(t.get(k, 0.0) for t in tms) / len(tms), 2) for k in tms[0]},
+                   "n_segments": leg["n_segments"], "n_links": leg["n_links"], "input_bytes": leg["input_bytes"],
+                   "n_nodes": leg["n_nodes"], "nnz": leg["nnz"], "mode": mode or "default",
+                   "output": "csr row slice per rank",
+                   "parallelism": f"shard x{world} (RCCL: all-gather of the ranges' evidence, all-to-all of "
+                                  f"triplets to row owners; hashed names: keys to owners, all-gather of order keys)",
+                   "segment_names": args.names, "id_path": leg["id_path"]},
+        "gb_per_s_ingested": leg["gb_per_s_ingested"],
+        "host_ms_per_stage_rank0": leg["host_ms_per_stage_rank0"],
     }
-    if one is not None:
-        line["one_gpu"] = one
-        line["speedup_vs_one_gpu"] = round(value / one["value"], 3)
+    if "one_gpu" in leg:
+        line["one_gpu"] = leg["one_gpu"]
+        line["speedup_vs_one_gpu"] = leg["speedup_vs_one_gpu"]
+    if alt is not None:
+        line["alt_paths"] = {"hashed_names": dict(alt, note="the same dimensions with hashed segment names "
+                                                  "(not 1..N): the general owner protocol over RCCL")}
     if rank == 0:
         print(json.dumps(line))
-    eng.close()
-    dev_in.free()
     dist.destroy_process_group()
+
+
+def scaling_reference(args) -> dict:
+    """The first point of the N-GPU curve on the N-GPU workload (C5), for the `--gpus 1` line: C5
+    built by one GPU alone and through the sharded protocol at one rank (a world-1 RCCL group),
+    decimal names (the fast path) and hashed names (the owner protocol forced at one rank, so the
+    exchange steps run as they do at N > 1)."""
+    import torch.distributed as dist
+
+    from gfa2network_amd import synth
+
+    wl = synth.WORKLOADS["C5"]
+    world, rank, local = _dist_setup(1, always=True)
+    try:
+        out = {"workload": f"{wl.name}: {wl.note}", "world_size": world, "backend": dist.get_backend(),
+               "decimal": sharded_leg(args, wl, world, rank, local, "decimal"),
+               "hashed": sharded_leg(args, wl, world, rank, local, "hashed", force_protocol=True)}
+    finally:
+        dist.destroy_process_group()
+    return out
 
 
 def main():
     args = _args()
+    if needs_launch(args.gpus):  # before anything touches a GPU: this process only waits for its ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload is None:
         args.workload = "C5" if max(world_env, args.gpus) > 1 else "C4"
@@ -684,6 +811,9 @@ def main():
     if world == 1 and not args.no_alt and args.workload == "C4" and args.scale == 1:
         line["other_configs"] = {w: config_leg(lib, nat, synth, synth.WORKLOADS[w], local, max(args.steps, 10),
                                                max(args.warmup, 2)) for w in ("C2", "C3")}
+    if world == 1 and not args.no_c5_reference and args.workload == "C4" and args.scale == 1:
+        line["scaling_reference"] = scaling_reference(args)
+    line["world_size"], line["backend"] = world, ("nccl" if world > 1 else None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
     if rank == 0 and world == 1 and not args.no_e2e:

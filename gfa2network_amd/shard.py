@@ -487,7 +487,8 @@ class HipEngine:
         tdt = getattr(torch, TORCH_DTYPES[dtype])
         if not copy:
             w = torch.empty(0, dtype=tdt).element_size()
-            return (DevArray(res.indptr or 0, n_rows + 1, 4), DevArray(res.indices or 0, res.nnz, 4),
+            iw = 8 if res.index_width == 8 else 4  # (a whole matrix past 2^31 - 1 entries: int64 views)
+            return (DevArray(res.indptr or 0, n_rows + 1, iw), DevArray(res.indices or 0, res.nnz, iw),
                     DevArray(res.data or 0, res.nnz, w), not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted)
         idx = torch.int64 if res.index_width == 8 else torch.int32  # (a whole matrix past 2^31 - 1 entries)
         indptr = self._copy_out(res.indptr, n_rows + 1, idx)

@@ -1,0 +1,46 @@
+#!/bin/bash
+# One gpurun job made of steps, run in order, each under its own time limit; the job stops at the
+# first failing step and prints the tail of its log.  Replaces the one-off launch scripts.
+#
+# usage (on the box):  bash tools/gpu_job.sh <tag> <step> [<step> ...]
+#   tests:<pytest args>     python -m pytest -m gpu <args>            -> gpurun_out/<tag>_s<i>.log
+#   bench:<bench.py args>   python bench.py <args>                    -> gpurun_out/<tag>_s<i>.json (+ .err)
+#   prof:<bench.py args>    rocprofv3 --kernel-trace --stats of bench.py <args>; top kernels printed,
+#                           database under gpurun_out/<tag>_s<i>/
+#   pmc:<bench.py args>     tools/gpu_counters.sh passes on bench.py <args> -> gpurun_out/<tag>_pmc.json
+#   py:<script + args>      python -u <script + args>                 -> gpurun_out/<tag>_s<i>.log
+# limits (seconds): T_TESTS (900), T_BENCH (600), T_PROF (300), T_PY (600); COMMIT tags the pmc summary.
+# example:
+#   gpurun --timeout 1200 -- 'bash tools/gpu_job.sh r5a "tests:tests/test_gpu_diff.py -k int64" "bench:--steps 5"'
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R" && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+TAG=${1:?tag}; shift
+i=0
+for step in "$@"; do
+  i=$((i + 1))
+  kind=${step%%:*}; args=${step#*:}
+  base=gpurun_out/${TAG}_s$i
+  echo "== step $i: $kind $args"
+  case $kind in
+    tests)
+      timeout -k 10 ${T_TESTS:-900} python -u -X faulthandler -m pytest -m gpu -x -q --timeout 300 \
+        --timeout-method thread $args > $base.log 2>&1 || { tail -60 $base.log; exit 1; }
+      tail -2 $base.log ;;
+    bench)
+      timeout -k 10 ${T_BENCH:-600} python -u bench.py $args > $base.json 2> $base.err || { tail -40 $base.err; exit 1; }
+      tail -1 $base.json | cut -c1-3000 ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${T_PROF:-300} rocprofv3 --kernel-trace --stats \
+        -d "$R/$base" -o run -- python3 "$R/bench.py" $args > "$R/$base.log" 2>&1) || { tail -30 $base.log; exit 1; }
+      python3 tools/rocpd_stats.py $base/run_results.db 16 | tee $base.txt ;;
+    pmc)
+      OUT_JSON=$R/gpurun_out/${TAG}_pmc.json COMMIT=${COMMIT:-unknown} BENCH_ARGS="$args" \
+        bash tools/gpu_counters.sh ${TAG}_ctr "g2n::" || exit 1 ;;
+    py)
+      timeout -k 10 ${T_PY:-600} python -u $args > $base.log 2>&1 || { tail -40 $base.log; exit 1; }
+      tail -5 $base.log ;;
+    *) echo "unknown step kind: $kind"; exit 2 ;;
+  esac
+done
