@@ -765,7 +765,7 @@ def main():
         line["alt_paths"] = {"hash_dictionary": {
             "ms_per_step": round(t_h * 1e3, 3), "m_edges_per_s": round(n_edges / t_h / 1e6, 2),
             "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
-            "note": "options.reserved[1] = TEST_DICT_HASH: segment names resolved through the GPU hash table (inputs whose S lines "
+            "note": "options.test_flags = G2N_TEST_DICT_HASH: segment names resolved through the GPU hash table (inputs whose S lines "
                     "are not named 1..N in order)"}}
     if t_x is not None:
         xt = x_ph.get("edge_text", 0.0)

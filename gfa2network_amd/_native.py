@@ -16,7 +16,7 @@ import numpy as np
 
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libg2n.so"
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_PHASES = 40
 
 # status codes (include/g2n.h)
@@ -33,7 +33,7 @@ FMT_COO, FMT_CSR, FMT_TEXT = 0, 1, 2
 
 # every symbol include/g2n.h declares (tests check the library exports all of them)
 EXPORTED = [
-    "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_last_error",
+    "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_device_memory", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
@@ -41,7 +41,7 @@ EXPORTED = [
 ]
 
 
-# options.reserved[1] test flags (include/g2n.h): the builds of this process take normally-rare
+# options.test_flags (include/g2n.h G2N_TEST_*): the builds of this process take normally-rare
 # paths when a test sets them; 0 in every real use
 TEST_NO_BUCKETS = 2      # MAX-SYM through the general row-sum path
 TEST_NO_LEAN = 4         # decimal ids without the lean parse (ids per touch, then k_triplets)
@@ -54,6 +54,10 @@ TEST_NO_HASH_LEAN = 256  # names that are not decimal ids: the classic hash tier
 TEST_THROW_AFTER_IDS = 512  # the build throws (G2N_E_DEVICE) once its ids and names are set up: call-state tests
 TEST_INDEX64 = 1024      # unweighted CSR results in int64 indptr / indices (the > 2^31 - 1 entries path)
 TEST_FLAGS = 0
+# options.range_flags (include/g2n.h G2N_RANGE_*): set by the sharded / chunked protocol (shard.py)
+RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)
+RANGE_EVIDENCE = 2       # report the range's evidence instead of checking (g2n_build_decimal_range sets it)
+RANGE_NO_VALUES = 4      # coordinates only: values left unwritten
 
 
 class Options(ctypes.Structure):
@@ -69,7 +73,12 @@ class Options(ctypes.Structure):
         ("weight_tag", ctypes.c_char_p),
         ("want_node_names", ctypes.c_int32),
         ("device", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("unknown_warned", ctypes.c_int32),
+        ("range_flags", ctypes.c_int32),
+        ("range_s_base", ctypes.c_int64),
+        ("range_n_segments", ctypes.c_int64),
+        ("test_flags", ctypes.c_uint32),
+        ("reserved_", ctypes.c_int32 * 3),
     ]
 
 
@@ -186,6 +195,8 @@ def load() -> ctypes.CDLL:
     lib.g2n_options_init.argtypes = [ctypes.POINTER(Options)]
     lib.g2n_options_init.restype = None
     lib.g2n_device_count.restype = ctypes.c_int
+    lib.g2n_device_memory.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.g2n_device_memory.restype = ctypes.c_int
     lib.g2n_build_from_path.argtypes = [ctypes.c_char_p, ctypes.POINTER(Options),
                                         ctypes.POINTER(ctypes.POINTER(Result))]
     lib.g2n_build_from_path.restype = ctypes.c_int
@@ -196,7 +207,7 @@ def load() -> ctypes.CDLL:
     lib.g2n_result_free.restype = None
     lib.g2n_coo_to_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                    ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                   ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Result))]
+                                   ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(Result))]
     lib.g2n_coo_to_csr.restype = ctypes.c_int
     lib.g2n_context_create.argtypes = [ctypes.c_int]
     lib.g2n_context_create.restype = ctypes.c_void_p
@@ -280,8 +291,8 @@ def make_options(*, directed=True, bidirected=False, keep_directed_bidir=False, 
     o.weight_tag = weight_tag.encode("utf-8") if weight_tag else None
     o.want_node_names = int(bool(want_node_names))
     o.device = int(device)
-    # tests only: force a normally rare path (same results); see include/g2n.h reserved[1]
-    o.reserved[1] = int(TEST_FLAGS if test_flags is None else test_flags)
+    # tests only: force a normally rare path (same results); include/g2n.h G2N_TEST_*
+    o.test_flags = int(TEST_FLAGS if test_flags is None else test_flags)
     return o
 
 
@@ -402,19 +413,24 @@ def build_from_buffer(data: bytes | bytearray | memoryview | np.ndarray, opts: O
 
 
 def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int, n_cols: int,
-               device: int = 0) -> RawResult:
+               device: int = 0, test_flags: int | None = None) -> RawResult:
+    """scipy coo.tocsr() on the GPU (g2n_coo_to_csr): indptr / indices in scipy's index dtype
+    (int64 past 2^31 - 1 entries)."""
     lib = load()
     dt = np.dtype(data.dtype)
     if dt.name not in DTYPE_CODES:
         raise NotImplementedError(f"GPU COO->CSR supports {sorted(DTYPE_CODES)}, not {dt}")
-    if max(n_rows, n_cols, len(data)) >= 2**31 - 1:
-        raise NotImplementedError("GPU COO->CSR currently needs int32 indices")
+    if max(n_rows, n_cols) >= 2**31 - 1:
+        raise NotImplementedError("GPU COO->CSR needs node ids below 2^31 - 1")
     r = np.ascontiguousarray(rows, dtype=np.int32)
     c = np.ascontiguousarray(cols, dtype=np.int32)
     d = np.ascontiguousarray(data)
     res = ctypes.POINTER(Result)()
+    flags = TEST_FLAGS if test_flags is None else test_flags
     rc = lib.g2n_coo_to_csr(r.ctypes.data, c.ctypes.data, d.ctypes.data, len(d), n_rows, n_cols, 4,
-                            DTYPE_CODES[dt.name], device, ctypes.byref(res))
+                            DTYPE_CODES[dt.name], device, flags, ctypes.byref(res))
+    if rc == E_UNSUPPORTED:  # a documented size limit (include/g2n.h)
+        raise NotImplementedError(f"GPU COO->CSR: {last_error()}")
     out = _from_result(res, rc)
     if out.status != OK:
         raise RuntimeError(f"{status_name(out.status)}: {out.message}")
@@ -625,6 +641,15 @@ def first_bad_utf8(blob: np.ndarray, offsets: np.ndarray) -> int:
 
 def device_count() -> int:
     return int(load().g2n_device_count())
+
+
+def device_memory(device: int = 0) -> tuple[int, int]:
+    """(free, total) HBM bytes of `device` (hipMemGetInfo, g2n_device_memory)."""
+    f, t = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = load().g2n_device_memory(int(device), ctypes.byref(f), ctypes.byref(t))
+    if rc != OK:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    return int(f.value), int(t.value)
 
 
 def version() -> str:

@@ -189,16 +189,17 @@ def parse_gfa(
     Returns ``A`` or ``(A, node_list)`` exactly as the reference does for
     ``build_graph=False, build_matrix=True``.
 
-    ``shard`` (extension; the reference has no such argument): ``"never"`` (default) builds on
-    this process's GPU.  With torch.distributed initialized over more than one rank, ``"auto"``
-    splits the file over the ranks (``parse_gfa_sharded``) when its working set would not fit a
-    GPU's free HBM on some rank, ``"always"`` splits it regardless; both are collectives — every
-    rank must make the same call on the same file (checked: a different path raises ValueError).
-    On one process (no group, or ``shard="auto"`` outside one), a plain file on disk whose working set
-    would not fit the GPU's free HBM is built in line-aligned chunks of the file on this one GPU
-    (``shard.build_chunked``; a chunk with a parse error or the unsupported-record warning sends the
-    file to the one-piece build, which raises the reference's error).  ``chunk_bytes`` (extension) forces that chunked build with
-    chunks of about that many bytes.
+    ``shard`` (extension; the reference has no such argument) decides only whether the ranks of a
+    torch.distributed group split the file: ``"never"`` (default) builds on this process's GPU;
+    with more than one rank, ``"auto"`` splits the file over the ranks (``parse_gfa_sharded``) when
+    its working set would not fit a GPU's free HBM on some rank, ``"always"`` splits it regardless;
+    both are collectives — every rank must make the same call on the same file (checked: a different
+    path raises ValueError).  On this process's GPU, an input whose working set would not fit its
+    free HBM — a plain file, a ``.gz`` (inflated on the host), stdin or a file object — is built in
+    line-aligned chunks on that one GPU (``shard.build_chunked``: errors, cast errors and the
+    one-shot warning come out as one piece would raise / emit them; the whole-matrix CSR is
+    assembled in row bands when it does not fit either).  ``chunk_bytes`` (extension) forces that
+    chunked build with chunks of about that many bytes.
     """
     if backend == "igraph":
         raise NotImplementedError("backend='igraph' is outside the GPU GFA->CSR path")
@@ -216,26 +217,25 @@ def parse_gfa(
     dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
     if shard not in ("auto", "always", "never"):
         raise ValueError("shard must be 'auto', 'always' or 'never'")
-    if build_matrix and not hasattr(path, "read") and str(path) != "-" and not str(path).endswith(".gz"):
-        cb = chunk_bytes if chunk_bytes is not None else _chunk_for(path, shard, device)
-        if cb:
-            got = _parse_gfa_chunked(str(path), cb, directed=directed, weight_tag=weight_tag, verbose=verbose,
-                                     bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
-                                     strip_orientation=strip_orientation, dt=dt, asymmetric=asymmetric,
-                                     raw_bytes_id=raw_bytes_id, return_node_list=return_node_list, device=device)
-            if got is not None:
-                return got
     if build_matrix and _want_shard(path, shard, device):
         return parse_gfa_sharded(path, directed=directed, weight_tag=weight_tag, strip_orientation=strip_orientation,
                                  verbose=verbose, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
                                  dtype=dt.name, asymmetric=asymmetric, raw_bytes_id=raw_bytes_id,
                                  return_node_list=return_node_list, device=device)
+    src = path
+    if build_matrix:  # one GPU, an input past its working set: chunks of it (any input kind)
+        done, src = _one_gpu_chunked(path, chunk_bytes, device, directed=directed, weight_tag=weight_tag,
+                                     verbose=verbose, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
+                                     strip_orientation=strip_orientation, dt=dt, asymmetric=asymmetric,
+                                     raw_bytes_id=raw_bytes_id, return_node_list=return_node_list)
+        if done is not None:
+            return done
     opts = nat.make_options(
         directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
         asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
         weight_tag=weight_tag or None, output=nat.OUT_PARSE,
         want_node_names=bool(return_node_list), device=device)
-    raw = _run(path, opts)
+    raw = _run(src, opts)
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
                     verbose=verbose, build_matrix=build_matrix, path=path)
 
@@ -373,62 +373,123 @@ def _gz_inflated_estimate(p: str, size: int) -> int:
     return max(isize, 4 * size)
 
 
-def _chunk_for(path, shard: str, device: int) -> int:
-    """shard="auto" on one process: the chunk size that lets a plain file on disk whose working set
-    (WORKING_SET_PER_INPUT_BYTE x its size) exceeds the GPU's free HBM be built on this GPU alone
-    (build_chunked), or 0 (the one-piece build)."""
-    if shard != "auto" or _dist_world() >= 2 or not os.path.isfile(str(path)):
-        return 0
-    import torch
+def _free_hbm(device: int) -> int | None:
+    """Free HBM of `device` (hipMemGetInfo through the C-ABI: no torch on the one-GPU path); None
+    without such a device (the build itself then raises G2N_E_DEVICE)."""
+    try:
+        return nat.device_memory(device)[0]
+    except RuntimeError:
+        return None
 
-    size = os.path.getsize(str(path))
-    free, _ = torch.cuda.mem_get_info(device)
-    if size * WORKING_SET_PER_INPUT_BYTE <= free:
+
+def _chunk_plan(size: int, device: int) -> int:
+    """The chunk size that lets an input of `size` bytes whose working set (WORKING_SET_PER_INPUT_BYTE
+    x its size) exceeds the GPU's free HBM be built on this GPU alone (shard.build_chunked), or 0 (the
+    one-piece build): each chunk's working set is then about half the free HBM."""
+    free = _free_hbm(device)
+    if free is None or size * WORKING_SET_PER_INPUT_BYTE <= free:
         return 0
-    # each chunk's working set beside the triplets kept so far (8 B per edge: <= the text's bytes)
     return max(1 << 26, int(free // (2 * WORKING_SET_PER_INPUT_BYTE)))
 
 
-_CHUNK_ENGINES: dict = {}
+class _Bytes:
+    """Input already read into host memory, handed to the one-piece build as a file object."""
+
+    def __init__(self, arr):
+        self.arr = arr
+
+    def read(self):
+        return self.arr
 
 
-def _parse_gfa_chunked(path: str, chunk_bytes: int, *, directed: bool, weight_tag, verbose: bool, bidirected: bool,
+def _one_gpu_chunked(path, chunk_bytes, device: int, **kw):
+    """parse_gfa's one-GPU route for an input past the GPU's working set (any input kind the
+    reference reads, parser.py:95-112): (the result, None) when it was built in chunks, else (None,
+    the input for the one-piece build).  A plain file is measured on disk and its chunks pread;
+    stdin and file objects are read into host memory first (the one-piece build would read them
+    whole too); a ``.gz`` whose inflated size (last ISIZE, or 4x the compressed bytes) may not fit is
+    inflated on the host (member-parallel / chunk-parallel, g2n_gunzip) and chunked from there — one
+    that does not inflate cleanly goes to the one-piece build, whose exact reader raises gzip.py's
+    error after the lines before it.  `chunk_bytes` (extension) forces chunks of about that size."""
+    from .shard import FileSource, HostSource
+
+    if hasattr(path, "read") or str(path) == "-":
+        data = path.read() if hasattr(path, "read") else sys.stdin.buffer.read()
+        arr = data if isinstance(data, np.ndarray) else np.frombuffer(data, dtype=np.uint8)
+        cb = chunk_bytes or _chunk_plan(len(arr), device)
+        if cb:
+            return _parse_gfa_chunked(HostSource(arr), cb, device=device, path=path, **kw), None
+        return None, _Bytes(arr)
+    p = str(path)
+    if not os.path.isfile(p):
+        return None, path  # the one-piece build raises the reference's OSError
+    size = os.path.getsize(p)
+    if p.endswith(".gz"):
+        free = None if chunk_bytes else _free_hbm(device)
+        if not chunk_bytes and (free is None or _gz_inflated_estimate(p, size) * WORKING_SET_PER_INPUT_BYTE <= free):
+            return None, path
+        with open(p, "rb") as fh:
+            blob = fh.read()
+        try:
+            data, _ = nat.gunzip(blob)
+        except nat.GzipFailure:
+            return None, path
+        del blob
+        arr = np.frombuffer(data, dtype=np.uint8)
+        cb = chunk_bytes or _chunk_plan(len(arr), device)
+        if cb:
+            return _parse_gfa_chunked(HostSource(arr), cb, device=device, path=path, **kw), None
+        return None, _Bytes(arr)
+    cb = chunk_bytes or _chunk_plan(size, device)
+    if cb:
+        return _parse_gfa_chunked(FileSource(p), cb, device=device, path=path, **kw), None
+    return None, path
+
+
+def _parse_gfa_chunked(source, chunk_bytes: int, *, directed: bool, weight_tag, verbose: bool, bidirected: bool,
                        keep_directed_bidir: bool, strip_orientation: bool, dt, asymmetric: bool, raw_bytes_id: bool,
-                       return_node_list: bool, device: int, engine=None):
-    """parse_gfa on one GPU in chunks of the file (shard.build_chunked), or None when that build
-    declines (the caller builds the file in one piece)."""
-    from .shard import HipEngine, build_chunked, scipy_index_dtype
+                       return_node_list: bool, device: int, engine=None, path=None, free_hbm=None, bands=None):
+    """parse_gfa on one GPU in chunks of the input (shard.build_chunked; source: a path, FileSource or
+    HostSource), or None past 2^31 - 1 nodes (the one-piece build reports that limit).  Errors and the
+    warning come out as the one-piece build's (finalize).  The engine — two build contexts and their
+    grow-only arenas — lives for this call only unless the caller passes one."""
+    from .shard import HipEngine, _np, build_chunked, scipy_index_dtype
 
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
-    eng = engine or _CHUNK_ENGINES.get(device)
-    if eng is None:  # one engine (two build contexts and their grow-only arenas) per device, reused
-        eng = _CHUNK_ENGINES[device] = HipEngine(device)
-    res = build_chunked(path, engine=eng, chunk_bytes=chunk_bytes, directed=directed, bidirected=bidirected,
-                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
-                        strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
-                        gather_names=return_node_list, keep_coo=not maxsym)
-    if res is None:
-        return None
-    raw = RawResult(status=0, n_lines=res.n_lines, n_records=res.n_records,
-                    n_records_before_error=res.n_records_before_error, n_nodes=res.n_nodes, dtype=dt,
-                    n_cast_overflow=res.n_cast_overflow)
-    if not maxsym:  # parse_gfa's stream-order COO (builders.py:281)
-        raw.format = "coo"
-        idt = scipy_index_dtype(0, res.n_nodes)
-        raw.rows = res.coo[0].cpu().numpy().astype(idt, copy=False)
-        raw.cols = res.coo[1].cpu().numpy().astype(idt, copy=False)
-        raw.data = res.coo[2].cpu().numpy()
-    else:
-        raw.format = "csr"
-        idt = scipy_index_dtype(res.index_maxval, res.n_nodes)
-        raw.indptr = res.indptr.cpu().numpy().astype(idt, copy=False)
-        raw.indices = res.indices.cpu().numpy().astype(idt, copy=False)
-        raw.data = res.data.cpu().numpy()
-    if return_node_list:
-        raw.names_blob, raw.names_offsets = res.names_blob, res.names_offsets
+    eng = engine or HipEngine(device)
+    try:
+        res = build_chunked(source, engine=eng, chunk_bytes=chunk_bytes, directed=directed, bidirected=bidirected,
+                            keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
+                            strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
+                            gather_names=return_node_list, keep_coo=not maxsym, free_hbm=free_hbm, bands=bands)
+        if res is None:
+            return None
+        raw = RawResult(status=res.status, err_line=res.err_line, err_index=res.err_index, err_value=res.err_value,
+                        err_detail=res.err_detail, has_warning=res.has_warning, warn_byte=res.warn_byte,
+                        warn_line=res.warn_line, n_lines=res.n_lines, n_records=res.n_records,
+                        n_records_before_error=res.n_records_before_error, n_nodes=res.n_nodes, dtype=dt,
+                        n_cast_overflow=res.n_cast_overflow)
+        if res.status == 0:
+            if not maxsym:  # parse_gfa's stream-order COO (builders.py:281)
+                raw.format = "coo"
+                idt = scipy_index_dtype(0, res.n_nodes)
+                raw.rows = _np(res.coo[0]).astype(idt, copy=False)
+                raw.cols = _np(res.coo[1]).astype(idt, copy=False)
+                raw.data = _np(res.coo[2])
+            else:
+                raw.format = "csr"
+                idt = scipy_index_dtype(res.index_maxval, res.n_nodes)
+                raw.indptr = _np(res.indptr).astype(idt, copy=False)
+                raw.indices = _np(res.indices).astype(idt, copy=False)
+                raw.data = _np(res.data)
+            if return_node_list:
+                raw.names_blob, raw.names_offsets = res.names_blob, res.names_offsets
+    finally:
+        if engine is None:
+            eng.close()
     return finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id, verbose=verbose,
-                    path=path)
+                    path=path if path is not None else getattr(source, "path", None))
 
 
 def _want_shard(path, shard: str, device: int) -> bool:
@@ -450,8 +511,8 @@ def _want_shard(path, shard: str, device: int) -> bool:
         p = str(path)
         size = os.path.getsize(p)
         work = (_gz_inflated_estimate(p, size) if p.endswith(".gz") else size) * WORKING_SET_PER_INPUT_BYTE
-        free, _ = torch.cuda.mem_get_info(device)
-        need = int(work > free)
+        free = _free_hbm(device)
+        need = int(free is not None and work > free)
     ident = zlib.crc32(os.fsencode(os.path.abspath(str(path)))) if here else 0
     size = os.path.getsize(str(path)) if here else -1
     nccl = dist.get_backend() == "nccl"
@@ -656,18 +717,27 @@ def export_edge_list(gfa, output="-", *, bidirected: bool = False, device: int =
             fh.close()
 
 
+def _keep_index_dtype(M, raw):
+    """scipy's coo.tocsr() / tocsc() past 2^31 - 1 COO entries keeps int64 indptr / indices even when
+    summing duplicates leaves fewer entries (_coo_to_compressed sizes by coo.nnz); the compressed
+    constructor's content check alone would narrow them."""
+    if raw.indptr.dtype == np.int64 and M.indptr.dtype != np.int64:
+        M.indices, M.indptr = raw.indices, raw.indptr
+    return M
+
+
 def _native_tocsr(A, device: int = 0):
     """scipy coo.tocsr() on the GPU: duplicates summed in dtype in scipy's order."""
     n_rows, n_cols = A.shape
     raw = nat.coo_to_csr(A.row, A.col, A.data, n_rows, n_cols, device)
-    return sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype)
+    return _keep_index_dtype(sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
 
 
 def _native_tocsc(A, device: int = 0):
     """scipy coo.tocsc(): the CSR of the transposed coordinates, read as CSC."""
     n_rows, n_cols = A.shape
     raw = nat.coo_to_csr(A.col, A.row, A.data, n_cols, n_rows, device)
-    return sp.csc_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype)
+    return _keep_index_dtype(sp.csc_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
 
 
 def convert_format(A, fmt: str, *, verbose: bool = False):

@@ -242,7 +242,7 @@ int g2n_build_from_path(const char* path, const g2n_options* opts, g2n_result** 
     }
     std::vector<g2n::ZMember> zm;
     size_t zout = 0;
-    if (!(opts->reserved[1] & g2n::kTestHostInflate) && g2n::bgzf_members(raw.p, rlen, zm, &zout)) {
+    if (!(opts->test_flags & g2n::kTestHostInflate) && g2n::bgzf_members(raw.p, rlen, zm, &zout)) {
       // BGZF: the members inflate on the GPU (the host readers only when one does not cleanly)
       const int rcz = g2n::build_host_bgzf(raw.p, rlen, zm, zout, opts, out, g2n::now_ms() - t0);
       if (rcz != g2n::kBgzfFallback) return rcz;

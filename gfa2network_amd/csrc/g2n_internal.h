@@ -109,7 +109,7 @@ bool bgzf_members(const uint8_t* in, size_t n, std::vector<ZMember>& out, size_t
 // inflated there (g2n_inflate.hip), then the build.  kBgzfFallback: a member did not inflate
 // cleanly — the caller reads the file with the host readers instead.
 constexpr int kBgzfFallback = -1;
-constexpr int32_t kTestHostInflate = 64;  // options.reserved[1]: BGZF read by the host readers
+constexpr uint32_t kTestHostInflate = G2N_TEST_HOST_INFLATE;  // BGZF read by the host readers
 int build_host_bgzf(const uint8_t* z, size_t zlen, const std::vector<ZMember>& members, size_t total_out,
                     const g2n_options* opts, g2n_result** out, double read_ms);
 // gzip.open's reader restated (serial, exact errors): false with *sub = 1 BadGzipFile,

@@ -60,19 +60,19 @@ enum Slot {
 #define G2N_FIN_DIRECT 0
 #endif
 
-// options.reserved[1] bits (tests only): take a path that is normally rare, same results
 #ifndef G2N_K2_PERSIST  // experiment builds: 1 = the persistent parse, next tile in registers (k_tile_lean_p)
 #define G2N_K2_PERSIST 0
 #endif
-constexpr uint32_t kTestNoBuckets = 2;      // MAX-SYM through the general row-sum path
-constexpr uint32_t kTestNoLean = 4;         // decimal ids without the lean parse (ids per touch, k_triplets)
-constexpr uint32_t kTestDictHash = 8;       // no decimal ids: the hash dictionary tiers
-constexpr uint32_t kTestDictGeneral = 16;   // no decimal ids, no S-first fast path: the general rounds
-constexpr uint32_t kTestNoTileLocal = 32;   // the lean parse after K1 (tile bases) instead of tile-local
-constexpr uint32_t kTestNoGroup = 128;      // tile-local parse into per-tile slots + compaction, never group slots
-constexpr uint32_t kTestNoHashLean = 256;   // names that are not decimal ids: the classic hash tiers, never the lean one
-constexpr uint32_t kTestThrowAfterIds = 512;  // a build that throws once its ids and names are set up (call-state tests)
-constexpr uint32_t kTestIndex64 = 1024;     // CSR results with int64 indptr / indices (the > 2^31 - 1 entries path)
+// options.test_flags (tests only; include/g2n.h G2N_TEST_*): take a path that is normally rare, same results
+constexpr uint32_t kTestNoBuckets = G2N_TEST_NO_BUCKETS;
+constexpr uint32_t kTestNoLean = G2N_TEST_NO_LEAN;
+constexpr uint32_t kTestDictHash = G2N_TEST_DICT_HASH;
+constexpr uint32_t kTestDictGeneral = G2N_TEST_DICT_GENERAL;
+constexpr uint32_t kTestNoTileLocal = G2N_TEST_NO_TILE_LOCAL;
+constexpr uint32_t kTestNoGroup = G2N_TEST_NO_GROUP;
+constexpr uint32_t kTestNoHashLean = G2N_TEST_NO_HASH_LEAN;
+constexpr uint32_t kTestThrowAfterIds = G2N_TEST_THROW_AFTER_IDS;
+constexpr uint32_t kTestIndex64 = G2N_TEST_INDEX64;
 
 
 struct DevBuf {
@@ -97,7 +97,7 @@ struct GroupedCoo {
 struct g2n_context {
   int device = 0;
   int n_cu = 256;  // compute units: persistent launches size their grid from it
-  uint32_t test_flags = 0;  // options.reserved[1] of the current build: forces rare paths (tests)
+  uint32_t test_flags = 0;  // options.test_flags of the current build: forces rare paths (tests)
   uint64_t err_line_off = 0;  // byte offset of the last build's error line (edge-list prefix)
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
   const uint32_t* wenc = nullptr;  // the current build's values as exact-int32 codes (k_values), if written
@@ -1071,7 +1071,7 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 
 // grouped: the COO goes to group slots instead (k_tile_lean<true>, GroupedCoo) and is not compacted
 // — for builds whose only consumer is the unweighted bucket partition.
-// s_base / n_seg_all: a byte range of a sharded file with global decimal ids (options.reserved[2..3]):
+// s_base / n_seg_all: a byte range of a sharded file with global decimal ids (options.range_s_base / range_n_segments):
 // the S lines before the range and in the whole file; 0 / 0 for a whole file.
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
@@ -1259,7 +1259,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   clear_call_state(c);
-  c->test_flags = (uint32_t)o->reserved[1];
+  c->test_flags = o->test_flags;
   R->input_bytes = len;
   c->n_ev = 0;
   G2N_HIP(hipEventRecord(c->ev[0], c->stream));
@@ -1277,10 +1277,10 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto* tcnt = dget<TileCnt>(c, S_TILE_CNT, n_tiles + 1);
   auto* tbase = dget<TileCnt>(c, S_TILE_BASE, n_tiles + 1);
   TileCnt tot{};
-  const bool shard_dec = (o->reserved[4] & 1) != 0;
+  const bool shard_dec = (o->range_flags & G2N_RANGE_DECIMAL) != 0;
   // g2n_build_decimal_range: the S lines before the range are not known yet — the one-pass parse
   // reports the range's offset evidence instead of checking it (the caller checks across ranges)
-  const bool shard_deferred = shard_dec && (o->reserved[4] & 2) != 0;
+  const bool shard_deferred = shard_dec && (o->range_flags & G2N_RANGE_EVIDENCE) != 0;
   c->range_has_s = false;
   c->range_d = -1;
   c->range_vmax = 0;
@@ -1294,11 +1294,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
                        !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
   // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
   const bool local_done =
-      n_tiles && (first_one || (shard_dec && (shard_deferred || (o->reserved[2] >= 0 && o->reserved[3] > 0)))) &&
+      n_tiles && (first_one || (shard_dec && (shard_deferred || (o->range_s_base >= 0 && o->range_n_segments > 0)))) &&
       !bidir && !(o->weight_tag && *o->weight_tag) && !o->strip_orientation &&
       !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
       tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped,
-                       shard_dec ? (uint64_t)o->reserved[2] : 0, shard_dec ? (uint64_t)o->reserved[3] : 0,
+                       shard_dec ? (uint64_t)o->range_s_base : 0, shard_dec ? (uint64_t)o->range_n_segments : 0,
                        shard_deferred);
   if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
     throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
@@ -1359,17 +1359,17 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   auto* cols = dget<int32_t>(c, S_COLS, in_groups ? 1 : n_trip);
   // decimal-id dictionary, computed by the parse itself (lean: straight into rows / cols) when
   // the first S line names "1" (a cheap guess: a wrong one costs one extra parse)
-  // options.reserved[4] bit 0: one byte range of a sharded build whose node ids are decimal and
-  // GLOBAL: reserved[2] S lines precede the range, reserved[3] S lines in the whole file (the
+  // options.range_flags G2N_RANGE_DECIMAL: one byte range of a sharded build whose node ids are decimal and
+  // GLOBAL: range_s_base S lines precede the range, range_n_segments S lines in the whole file (the
   // caller checked across ranges that no edge line precedes an S line).  Lean parse or nothing.
-  if (shard_dec && (o->output != G2N_OUT_COO || o->want_node_names || o->reserved[2] < 0 || o->reserved[3] < 0))
+  if (shard_dec && (o->output != G2N_OUT_COO || o->want_node_names || o->range_s_base < 0 || o->range_n_segments < 0))
     throw Failure(G2N_E_ARG, "sharded decimal-id build: output COO without names, s_base / n_seg >= 0");
   const bool int_ids = n_t && (shard_dec || first_one);
   const bool lean = int_ids && (shard_dec || !(c->test_flags & kTestNoLean));
   if (int_ids) {
     op.tid = dget<uint32_t>(c, S_TID, z(n_t));
-    op.n_seg = shard_dec ? (uint64_t)o->reserved[3] : n_s;
-    op.s_base = shard_dec ? (uint64_t)o->reserved[2] : 0;
+    op.n_seg = shard_dec ? (uint64_t)o->range_n_segments : n_s;
+    op.s_base = shard_dec ? (uint64_t)o->range_s_base : 0;
   }
   auto* wl = dget<uint64_t>(c, S_WL, z(2 * n_e));
   auto* deferred = dget<DeferredLine>(c, S_DEFER, n_tiles + 1);
@@ -1434,9 +1434,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   uint64_t err_key = c->h_ctl->err_key;
   uint64_t err_line = err_key == ~0ull ? ~0ull : (err_key >> 5);
   int err_code = err_key == ~0ull ? 0 : (int)(err_key & 31);
-  // options.reserved[0] != 0: an earlier shard of a sharded build already met an unsupported
+  // options.unknown_warned: an earlier shard of a sharded build already met an unsupported
   // record, so later ones are skipped silently (parser.py:125-131 warns once per parser)
-  const uint64_t warn_line = o->reserved[0] ? ~0ull : c->h_ctl->warn_line;
+  const uint64_t warn_line = o->unknown_warned ? ~0ull : c->h_ctl->warn_line;
   if (warn_line != ~0ull) R->warn_line = (int64_t)warn_line;  // first unsupported line, warned or not
   if (warn_line != ~0ull && warn_line < err_line) {
     uint64_t off = read_dev(c, ls + warn_line);
@@ -1485,7 +1485,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
                          n_s * tps + (n_s * tps * 32 < n_e * tpe ? (n_e * tpe) / 2 : (n_e * tpe) / 16) + 1024, bidir,
                          op.tid && !c->h_ctl->int_fail ? kIntDone : kIntFailed);
   TouchIn TI{T.noff, T.nlen, T.ooff, T.olen};
-  const uint64_t n_nodes = shard_dec ? (uint64_t)o->reserved[3] : D.n_nodes;  // global ids: the file's nodes
+  const uint64_t n_nodes = shard_dec ? (uint64_t)o->range_n_segments : D.n_nodes;  // global ids: the file's nodes
   if (n_nodes >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 nodes");
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");
@@ -1546,9 +1546,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
   phase(c, "_prep");
-  // options.reserved[4] bit 2: a sharded range (decimal, or a general-protocol local build) whose
+  // options.range_flags G2N_RANGE_NO_VALUES: a sharded range (decimal, or a general-protocol local build) whose
   // caller routes coordinates only (uniform values, no COO result): the values array is left unwritten
-  const bool no_values = uni && (o->reserved[4] & 4) != 0;
+  const bool no_values = uni && (o->range_flags & G2N_RANGE_NO_VALUES) != 0;
   if (coords_done) {  // values only, and only when the output or the sums read them
     if (n_e && (coo_out || !uni) && !no_values) {
       // a weighted SUM CSR: the exact-int32 codes the bucket partition sums (csr_partition_w) beside
@@ -1903,32 +1903,64 @@ int build_host(const void* buf, size_t len, const g2n_options* opts, g2n_result*
 }
 
 // --------------------------------------------------------- convert_format ------
+// *not_one = 1 when some value differs from T(1) (bool: false; floats: anything but exactly 1.0,
+// NaN included).  Racing plain stores of the same word: no atomics needed.
+template <class T>
+__global__ void k_values_not_one(const T* __restrict__ d, uint64_t n, unsigned int* not_one) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) bad |= !(d[i] == (T)1);
+  if (bad) *not_one = 1u;
+}
+
 template <class T>
 static void coo_to_csr_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t nnz,
-                         uint64_t n_rows, uint64_t n_cols, g2n_result* R) {
-  assemble<T>(c, rows, cols, data, nnz, n_rows, n_cols, false, false, R);
+                         uint64_t n_rows, uint64_t n_cols, bool uniform, g2n_result* R) {
+  // uniform (every value T(1): what parse_gfa returns without a weight tag): the copy count per
+  // entry is the sum, through the unweighted bucket partition — the path with int64 results past
+  // 2^31 - 1 entries (scipy's _coo_to_compressed sizes its index dtype by coo.nnz)
+  assemble<T>(c, rows, cols, data, nnz, n_rows, n_cols, false, uniform, R);
 }
 
 int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows, int64_t n_cols,
-               int32_t index_width, int32_t dtype, int32_t device, g2n_result** out) {
+               int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags, g2n_result** out) {
   if (index_width != 4) throw Failure(G2N_E_UNSUPPORTED, "only int32 COO indices are supported");
   if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) throw Failure(G2N_E_ARG, "unsupported dtype");
   if (nnz < 0 || n_rows < 0 || n_cols < 0) throw Failure(G2N_E_ARG, "negative size");
-  if (nnz >= 0x7FFFFFFF) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 entries");
+  if (n_rows >= 0x7FFFFFFF || n_cols >= 0x7FFFFFFF) throw Failure(G2N_E_UNSUPPORTED, "2^31-1 or more rows / columns");
+  if ((uint64_t)nnz >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "2^32-1 or more entries");
   g2n_context* c = shared_context(device);
   std::lock_guard<std::mutex> lk(c->mu);
   G2N_HIP(hipSetDevice(c->device));
   clear_call_state(c);
-  c->test_flags = 0;  // a build's test flags are not this conversion's
+  c->test_flags = test_flags & (kTestNoBuckets | kTestIndex64);  // the conversion's own rare paths
   const size_t w = dtype_size(dtype);
   auto* dr = dget<int32_t>(c, S_ROWS, (uint64_t)nnz);
   auto* dc = dget<int32_t>(c, S_COLS, (uint64_t)nnz);
   void* dd = dbuf(c, S_DATA, (size_t)nnz * w);
+  auto* not_one = dget<unsigned int>(c, S_ZBAD, 1);
+  G2N_HIP(hipMemsetAsync(not_one, 0, sizeof(unsigned int), c->stream));
   if (nnz) {
     G2N_HIP(hipMemcpyAsync(dr, rows, (size_t)nnz * 4, hipMemcpyHostToDevice, c->stream));
     G2N_HIP(hipMemcpyAsync(dc, cols, (size_t)nnz * 4, hipMemcpyHostToDevice, c->stream));
     G2N_HIP(hipMemcpyAsync(dd, data, (size_t)nnz * w, hipMemcpyHostToDevice, c->stream));
+    const unsigned g = (unsigned)std::min<uint64_t>(grid_for((uint64_t)nnz), 8192);
+    switch (dtype) {
+      case G2N_BOOL:
+      case G2N_INT8: hipLaunchKernelGGL(k_values_not_one<uint8_t>, dim3(g), dim3(kTPB), 0, c->stream,
+                                        (const uint8_t*)dd, (uint64_t)nnz, not_one); break;
+      case G2N_INT32: hipLaunchKernelGGL(k_values_not_one<int32_t>, dim3(g), dim3(kTPB), 0, c->stream,
+                                         (const int32_t*)dd, (uint64_t)nnz, not_one); break;
+      case G2N_FLOAT32: hipLaunchKernelGGL(k_values_not_one<float>, dim3(g), dim3(kTPB), 0, c->stream,
+                                           (const float*)dd, (uint64_t)nnz, not_one); break;
+      default: hipLaunchKernelGGL(k_values_not_one<double>, dim3(g), dim3(kTPB), 0, c->stream, (const double*)dd,
+                                  (uint64_t)nnz, not_one); break;
+    }
   }
+  // the unweighted partition packs (col << 2 | side) in 32 bits: columns below 2^30
+  const bool uniform = nnz > 0 && n_cols < (1ll << 30) && read_dev(c, not_one) == 0u;
+  if ((uint64_t)nnz > 0x7FFFFFFEull && !uniform)
+    throw Failure(G2N_E_UNSUPPORTED, "2^31-1 or more entries with values other than 1 (a weighted matrix)");
   g2n_result D;
   fill_defaults(&D);
   c->n_ev = 0;
@@ -1938,11 +1970,11 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   D.index_width = 4;
   D.n_nodes = n_rows;
   switch (dtype) {
-    case G2N_BOOL: coo_to_csr_t<uint8_t>(c, dr, dc, (const uint8_t*)dd, nnz, n_rows, n_cols, &D); break;
-    case G2N_INT8: coo_to_csr_t<int8_t>(c, dr, dc, (const int8_t*)dd, nnz, n_rows, n_cols, &D); break;
-    case G2N_INT32: coo_to_csr_t<int32_t>(c, dr, dc, (const int32_t*)dd, nnz, n_rows, n_cols, &D); break;
-    case G2N_FLOAT32: coo_to_csr_t<float>(c, dr, dc, (const float*)dd, nnz, n_rows, n_cols, &D); break;
-    default: coo_to_csr_t<double>(c, dr, dc, (const double*)dd, nnz, n_rows, n_cols, &D); break;
+    case G2N_BOOL: coo_to_csr_t<uint8_t>(c, dr, dc, (const uint8_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
+    case G2N_INT8: coo_to_csr_t<int8_t>(c, dr, dc, (const int8_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
+    case G2N_INT32: coo_to_csr_t<int32_t>(c, dr, dc, (const int32_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
+    case G2N_FLOAT32: coo_to_csr_t<float>(c, dr, dc, (const float*)dd, nnz, n_rows, n_cols, uniform, &D); break;
+    default: coo_to_csr_t<double>(c, dr, dc, (const double*)dd, nnz, n_rows, n_cols, uniform, &D); break;
   }
   finish_timings(c, &D);
   HostResult* H = new_host_result();
@@ -2212,9 +2244,10 @@ int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, c
     return G2N_E_ARG;
   }
   g2n_options o = *opts;
-  o.reserved[2] = 0;
-  o.reserved[3] = 0;
-  o.reserved[4] = 3 | (opts->reserved[4] & 4);  // sharded decimal ids, offset evidence instead of the check
+  o.range_s_base = 0;
+  o.range_n_segments = 0;
+  // sharded decimal ids, offset evidence instead of the check
+  o.range_flags = G2N_RANGE_DECIMAL | G2N_RANGE_EVIDENCE | (opts->range_flags & G2N_RANGE_NO_VALUES);
   const int rc = g2n_build_device(ctx, d_input, len, &o, out);
   if (rc == G2N_OK) {
     ev6[0] = out->n_lines;
@@ -2228,11 +2261,12 @@ int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, c
 }
 
 int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows,
-                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, g2n_result** out) {
+                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags,
+                   g2n_result** out) {
   if (!out) return G2N_E_ARG;
   *out = nullptr;
   try {
-    return g2n::coo_to_csr(rows, cols, data, nnz, n_rows, n_cols, index_width, dtype, device, out);
+    return g2n::coo_to_csr(rows, cols, data, nnz, n_rows, n_cols, index_width, dtype, device, test_flags, out);
   } catch (const g2n::Failure& f) {
     g2n::set_last_error(f.what());
     return f.status;
@@ -2352,6 +2386,28 @@ int g2n_count_device(g2n_context* ctx, const void* d_input, size_t len, int64_t*
     out4[2] = (int64_t)tot.edges;
     out4[3] = (int64_t)tot.recs;
   });
+  return G2N_OK;
+}
+
+int g2n_device_memory(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return G2N_E_ARG;
+  *free_bytes = *total_bytes = 0;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    g2n::set_last_error("g2n_device_memory: no such HIP device");
+    return G2N_E_DEVICE;
+  }
+  size_t f = 0, t = 0;
+  const hipError_t e = hipMemGetInfo(&f, &t);
+  (void)hipSetDevice(cur);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    g2n::set_last_error(std::string("hipMemGetInfo failed: ") + hipGetErrorString(e));
+    return G2N_E_DEVICE;
+  }
+  *free_bytes = f;
+  *total_bytes = t;
   return G2N_OK;
 }
 

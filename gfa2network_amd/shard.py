@@ -24,7 +24,7 @@ synthetic configs): when the file's S lines come first and name their segments "
 order, a node's global id is arithmetic on its name, so steps 2-4 collapse to an all-gather of
 the ranges' record counts (each rank learns how many S lines precede it and N) and one
 all-reduce of the ranges' verdicts ("every range's ids are global decimals"): each rank parses
-its range straight into global ids (`g2n_build_device` with options.reserved[2..4]), routes the
+its range straight into global ids (`g2n_build_device` with options.range_flags = G2N_RANGE_DECIMAL), routes the
 triplets with an identity map and builds its slice.  Any range that breaks the premise (or
 holds an error / warning / slow weight) makes every rank take the general protocol above.
 
@@ -147,15 +147,22 @@ def concat_indptr(parts, dtype) -> np.ndarray:
 def line_ranges(data: bytes | np.ndarray, n_ranks: int) -> list[tuple[int, int]]:
     """Contiguous line-aligned byte ranges: range r starts at the first line start at or after
     r * len / G (the line holding that offset belongs to the range holding its first byte)."""
-    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     n = len(buf)
     starts = [0]
     for r in range(1, n_ranks):
         nominal = r * n // n_ranks
         s = nominal
         if 0 < s < n and buf[s - 1] != 0x0A:
-            nl = np.flatnonzero(buf[s:] == 0x0A)
-            s = n if len(nl) == 0 else s + int(nl[0]) + 1
+            pos, win = s, 1 << 16  # growing windows: no scan past the next newline
+            s = n
+            while pos < n:
+                nl = np.flatnonzero(buf[pos:pos + win] == 0x0A)
+                if len(nl):
+                    s = pos + int(nl[0]) + 1
+                    break
+                pos += win
+                win = min(win * 2, 1 << 26)
         starts.append(max(s, starts[-1]))
     return [(starts[r], starts[r + 1] if r + 1 < n_ranks else n) for r in range(n_ranks)]
 
@@ -262,12 +269,12 @@ class HipEngine:
                     values: bool = True) -> LocalShard:
         """The range on its own (local ids, names).  view: the COO as DevArray views of the build
         context (valid until its next build; remap_pairs rewrites them in place), the names copied.
-        values=False: a build without a weight tag leaves its values unwritten (options.reserved[4]
-        bit 2) — the caller routes coordinates only and never reads them."""
+        values=False: a build without a weight tag leaves its values unwritten (options.range_flags
+        G2N_RANGE_NO_VALUES) — the caller routes coordinates only and never reads them."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=True, device=self.device_index, **opts)
-        o.reserved[0] = int(unknown_warned)
-        o.reserved[4] = 0 if values else 4
+        o.unknown_warned = int(unknown_warned)
+        o.range_flags = 0 if values else nat.RANGE_NO_VALUES
         res = nat.Result()
         ctx = self._build_ctx() if view else self.ctx
         self._sync()
@@ -311,6 +318,31 @@ class HipEngine:
                                                        self.device_index), "g2n_upload_file_range")
         return t
 
+    def upload(self, arr):
+        """Host bytes (a numpy uint8 array: a chunk of text inflated / read into host memory) to this
+        GPU's HBM."""
+        t = self.torch.empty(len(arr), dtype=self.torch.uint8, device=self.device)
+        if len(arr):
+            a = np.ascontiguousarray(arr)
+            self._sync()
+            if self._hip.hipMemcpy(t.data_ptr(), a.ctypes.data, len(a), 1) != 0:  # host to device
+                raise RuntimeError("hipMemcpy failed")
+        return t
+
+    def free_memory(self) -> int:
+        """Free HBM on this GPU (hipMemGetInfo through the C-ABI)."""
+        return nat.device_memory(self.device_index)[0]
+
+    def reset(self):
+        """Release both build contexts' grow-only arenas and torch's cached blocks, keeping a fresh
+        context: before a chunked build's whole-matrix assembly, whose buffers then
+        have the GPU to themselves.  Views of earlier results become invalid."""
+        self.close()
+        self.torch.cuda.empty_cache()
+        self.ctx = self.lib.g2n_context_create(self.device_index)
+        if not self.ctx:
+            raise nat.NativeUnavailable(nat.last_error())
+
     def count(self, buf):
         """{lines, S lines, edge records, records} of the range (g2n_count_device: K1 only)."""
         out = (ctypes.c_int64 * 4)()
@@ -325,7 +357,8 @@ class HipEngine:
         view: the COO as DevArray views of the build context (valid until the next build_decimal)."""
         torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
-        o.reserved[2], o.reserved[3], o.reserved[4] = int(s_base), int(n_seg), 1 | (0 if values else 4)
+        o.range_s_base, o.range_n_segments = int(s_base), int(n_seg)
+        o.range_flags = nat.RANGE_DECIMAL | (0 if values else nat.RANGE_NO_VALUES)
         res = nat.Result()
         self._build_ctx()
         self._sync()
@@ -343,7 +376,7 @@ class HipEngine:
         largest edge key]) — the caller checks d against the S lines before the range and the key
         against the file's S count — or None when the one pass declines (count + build_decimal then)."""
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
-        o.reserved[4] = 0 if values else 4  # values: the caller reads them (a COO result, weights)
+        o.range_flags = 0 if values else nat.RANGE_NO_VALUES  # values: the caller reads them (a COO result, weights)
         res = nat.Result()
         ev = (ctypes.c_int64 * 6)()
         self._build_ctx()
@@ -768,68 +801,266 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     return out
 
 
-def build_chunked(path: str, *, engine, chunk_bytes: int, directed=True, bidirected=False, keep_directed_bidir=False,
+class FileSource:
+    """A plain file on disk: each chunk is pread straight into HBM (g2n_upload_file_range)."""
+
+    def __init__(self, path):
+        self.path = str(path)
+        self.size = os.path.getsize(self.path)
+
+    def ranges(self, n: int):
+        return file_line_ranges(self.path, n)
+
+    def upload(self, engine, lo: int, hi: int):
+        return engine.read_range(self.path, lo, hi - lo)
+
+
+class HostSource:
+    """Bytes already in host memory — a ``.gz`` inflated on the host, stdin, a file object's read():
+    each chunk is copied to HBM on its own."""
+
+    def __init__(self, data):
+        self.arr = data if isinstance(data, np.ndarray) else np.frombuffer(data, dtype=np.uint8)
+        self.size = len(self.arr)
+
+    def ranges(self, n: int):
+        return line_ranges(self.arr, n)
+
+    def upload(self, engine, lo: int, hi: int):
+        return engine.upload(self.arr[lo:hi])
+
+
+def _as_source(src):
+    return src if hasattr(src, "ranges") else FileSource(src)
+
+
+_ITEMSIZE = {"bool": 1, "int8": 1, "int32": 4, "float32": 4, "float64": 8}
+
+
+def csr_bytes_estimate(n_a: int, n_t: int, n_rows: int, w: int) -> int:
+    """HBM one g2n_csr_from_coo_pair call over n_a A entries and n_t A.T entries takes beyond its
+    inputs — the bucket partition's two element buffers and pair words, the staged merged entries,
+    the result (int32 or int64 indices, w-byte values) and the count matrices — an upper bound
+    (g2n_pipeline.hip csr_partition / csr_partition_w)."""
+    n_el = n_a + n_t
+    return int(n_el * (40 + w) + 24 * n_rows + (256 << 20))
+
+
+class ChunkedAssemblyTooLarge(MemoryError):
+    pass
+
+
+def _np(x):
+    return x if isinstance(x, np.ndarray) else x.cpu().numpy()
+
+
+def _assemble_csr(engine, parts, n: int, maxsym: bool, uniform: bool, dtype: str, tm: dict, free_hbm, bands=None):
+    """The whole matrix's CSR over every chunk's triplets (parts: per chunk (rows, cols, data) device
+    tensors, stream order): one g2n_csr_from_coo_pair when it fits the GPU's free HBM, else in row
+    bands — each chunk's triplets routed by band (g2n_route_triplets: stable, so every row keeps its
+    stream order and scipy's duplicate-summation order), each band's CSR built (row_base) and copied
+    to host memory, the bands' indptrs rebased (the sharded gather's rule, concat_indptr).  Returns
+    (indptr, indices, data, index_maxval) — device tensors (one piece) or numpy (bands)."""
+    import time
+
+    torch = engine.torch if hasattr(engine, "torch") else __import__("torch")
+    t1 = time.perf_counter()
+    n_trip = sum(int(p[0].numel()) for p in parts)
+    w = _ITEMSIZE[dtype]
+    wv = 0 if uniform else w
+    engine.reset()  # the chunk builds' arenas go before the assembly's buffers come
+    free = int(free_hbm())
+    n_t = n_trip if maxsym else 0
+    whole = csr_bytes_estimate(n_trip, n_t, n, w) + n_trip * (8 + wv) * (2 if maxsym else 1)
+    if bands is None:
+        bands = 1 if whole <= free else None
+    if bands is None:
+        routed = n_trip * (8 + wv) * (2 if maxsym else 1)  # the band-ordered copies (A, and A.T for MAX-SYM)
+        room = free - routed - n_trip * (8 + wv)  # the chunks' own triplets while they are routed
+        per = csr_bytes_estimate(n_trip, n_t, n, w)
+        if room <= per // 64:
+            raise ChunkedAssemblyTooLarge(
+                f"parse_gfa: the CSR of {n_trip} triplets over {n} nodes needs about {(whole + routed) / 1e9:.1f} GB "
+                f"of HBM even in row bands; {free / 1e9:.1f} GB free")
+        bands = max(2, -(-per // int(room * 0.8)))
+    d = lambda x: None if uniform else x  # noqa: E731  (uniform values are never read)
+    if bands == 1:
+        cat = (lambda xs: torch.cat(xs) if len(xs) > 1 else xs[0])
+        rows, cols = cat([p[0] for p in parts]), cat([p[1] for p in parts])
+        data = None if uniform else cat([p[2] for p in parts])
+        parts.clear()
+        indptr, indices, vals, _, _ = engine.csr_pair((rows, cols, data), (cols, rows, data) if maxsym else None, maxsym,
+                                                      0, n, n, dtype, uniform, -1)
+        tm["csr"] = (time.perf_counter() - t1) * 1e3
+        return indptr, indices, vals, int(indices.numel()) if maxsym else n_trip
+    # row bands: rank k of a `bands`-rank sharded build owns rows [ceil(k n / B), ceil((k+1) n / B))
+    ra, rt = [], []
+    while parts:
+        r, c, x = parts.pop(0)
+        ra.append(engine.route_triplets(r, c, d(x), dtype, None, n, bands, False))
+        if maxsym:
+            rt.append(engine.route_triplets(r, c, d(x), dtype, None, n, bands, True))
+        del r, c, x
+    starts_a = [[int(v) for v in s[3].tolist()] for s in ra]
+    starts_t = [[int(v) for v in s[3].tolist()] for s in rt]
+
+    def band(routed, starts, k):
+        pieces = [(g[0][s[k]:s[k + 1]], g[1][s[k]:s[k + 1]], None if g[2] is None else g[2][s[k]:s[k + 1]])
+                  for g, s in zip(routed, starts)]
+        cat = (lambda xs: torch.cat(xs) if len(xs) > 1 else xs[0])
+        return (cat([p[0] for p in pieces]), cat([p[1] for p in pieces]),
+                None if uniform else cat([p[2] for p in pieces]))
+
+    force = -1
+    if not uniform and dtype in ("float32", "float64"):
+        # scipy's has_sorted_indices is a property of the whole matrix: OR over the bands first
+        fa = ft = 0
+        for k in range(bands):
+            lo, hi = (k * n + bands - 1) // bands, ((k + 1) * n + bands - 1) // bands
+            _, _, _, ua, ut = engine.csr_pair(band(ra, starts_a, k), band(rt, starts_t, k) if maxsym else None,
+                                              maxsym, lo, hi - lo, n, dtype, uniform, -1)
+            fa, ft = fa | int(ua), ft | int(ut)
+        force = fa | (ft << 1)
+    ptrs, idx, vals = [], [], []
+    for k in range(bands):
+        lo, hi = (k * n + bands - 1) // bands, ((k + 1) * n + bands - 1) // bands
+        ip, ix, vv, _, _ = engine.csr_pair(band(ra, starts_a, k), band(rt, starts_t, k) if maxsym else None, maxsym,
+                                           lo, hi - lo, n, dtype, uniform, force)
+        ptrs.append(_np(ip).astype(np.int64))
+        idx.append(_np(ix))
+        vals.append(_np(vv))
+        del ip, ix, vv
+    ra.clear()
+    rt.clear()
+    nnz = sum(len(x) for x in idx)
+    idt = scipy_index_dtype(nnz if maxsym else n_trip, n)
+    indptr = concat_indptr(ptrs, idt)
+    indices = np.concatenate(idx).astype(idt, copy=False) if idx else np.zeros(0, dtype=idt)
+    data = np.concatenate(vals) if vals else np.zeros(0)
+    tm["csr"] = (time.perf_counter() - t1) * 1e3
+    tm["csr_bands"] = bands
+    return indptr, indices, data, nnz if maxsym else n_trip
+
+
+def build_chunked(source, *, engine, chunk_bytes: int, directed=True, bidirected=False, keep_directed_bidir=False,
                   asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None, gather_names=False,
-                  keep_coo=False) -> ShardResult | None:
+                  keep_coo=False, free_hbm=None, bands=None) -> ShardResult | None:
     """One file whose working set does not fit one GPU, built on that GPU alone in line-aligned chunks
     of about `chunk_bytes`: the decimal-id chunks (`_chunked_decimal`) when the file's names are
     "1".."N" in S-first order and the build is plain, else chunks with local ids merged into one
-    dictionary as they come (`_chunked_general`).  None when neither applies (a parse error or the
-    one-shot warning in a chunk): the caller builds the file in one piece, which raises the
-    reference's error."""
+    dictionary as they come (`_chunked_general`).  `source`: a path (FileSource) or a HostSource.
+    Parse errors, cast errors and the one-shot unsupported-record warning are resolved across the
+    chunks in stream order, as one piece would raise / emit them (build_sharded's rule).  The
+    whole-matrix CSR is assembled after the chunk builds' arenas are released, in row bands when it
+    does not fit (`_assemble_csr`); a COO result (keep_coo without MAX-SYM) is kept in host memory
+    chunk by chunk.  None only past 2^31 - 1 nodes (the one-piece build reports that limit)."""
+    src = _as_source(source)
+    free_hbm = free_hbm or engine.free_memory
     kw = dict(engine=engine, chunk_bytes=chunk_bytes, directed=directed, keep_directed_bidir=keep_directed_bidir,
-              asymmetric=asymmetric, dtype=dtype, gather_names=gather_names, keep_coo=keep_coo)
+              asymmetric=asymmetric, dtype=dtype, gather_names=gather_names, keep_coo=keep_coo, free_hbm=free_hbm,
+              bands=bands)
     if not (bidirected or weight_tag or strip_orientation):
-        got = _chunked_decimal(path, **kw)
+        got = _chunked_decimal(src, **kw)
         if got is not None:
             return got
-    return _chunked_general(path, bidirected=bidirected, strip_orientation=strip_orientation, weight_tag=weight_tag,
+    return _chunked_general(src, bidirected=bidirected, strip_orientation=strip_orientation, weight_tag=weight_tag,
                             **kw)
 
 
-def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirected, keep_directed_bidir, asymmetric,
-                     strip_orientation, dtype, weight_tag, gather_names, keep_coo) -> ShardResult | None:
+def _keep_part(keep_host: bool, rows, cols, data):
+    """A chunk's stream-order triplets, kept on the device (the CSR is built over them) or moved to
+    host memory (a COO result never needs them on the GPU again)."""
+    if keep_host:
+        return _np(rows).copy(), _np(cols).copy(), _np(data).copy()
+    return rows, cols, data
+
+
+def _finish_chunked(engine, out, parts, n, maxsym, uniform, dtype, keep_coo, tm, free_hbm, bands):
+    out.row_lo, out.row_hi = 0, n
+    if keep_coo and not maxsym:  # parse_gfa's stream-order COO, already in host memory
+        out.coo = tuple(np.concatenate([p[j] for p in parts]) if parts else np.zeros(0, np.int32) for j in range(3))
+        out.index_maxval = int(len(out.coo[0]))
+        return out
+    if keep_coo:
+        out.coo = tuple(np.concatenate([_np(p[j]) for p in parts]) for j in range(3))
+    out.indptr, out.indices, out.data, out.index_maxval = _assemble_csr(engine, parts, n, maxsym, uniform, dtype, tm,
+                                                                        free_hbm, bands)
+    return out
+
+
+def _chunked_general(src, *, engine, chunk_bytes: int, directed, bidirected, keep_directed_bidir, asymmetric,
+                     strip_orientation, dtype, weight_tag, gather_names, keep_coo, free_hbm=None,
+                     bands=None) -> ShardResult | None:
     """Chunks in stream order, any names: each chunk is built on its own (local first-touch ids, its
     distinct keys in local id order), then its keys are deduplicated together with the file's keys
     so far, those first (`dedup_keys` keeps arrival order: a known key gets its global id, a new one
     the next id in the chunk's first-touch order — which is the file's, since every earlier chunk
     came first), the new keys appended to the file's names (`gather_keys`) and the chunk's triplets
     remapped to global ids (`remap_pairs`).  The CSR / COO is built once over all chunks' triplets.
-    None on a parse error or the unsupported-record warning in any chunk (the one-piece build then
-    decides)."""
-    import os
+    Stream-order resolution (parser.py:114-132, builders.py:281): the first parse error ends the
+    build with its global line; a cast error is kept while later chunks are parsed (a later parse
+    error still wins, as the reference casts after its loop); the first unsupported record warns once
+    and every later chunk is built with it already warned (options.unknown_warned)."""
     import time
 
     import torch
 
+    src = _as_source(src)
+    free_hbm = free_hbm or engine.free_memory
     opts = dict(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
                 asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dtype, weight_tag=weight_tag)
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
     uniform = not weight_tag
-    size = os.path.getsize(path)
-    n_chunks = max(1, -(-size // max(1, int(chunk_bytes))))
+    keep_host = keep_coo and not maxsym
+    n_chunks = max(1, -(-src.size // max(1, int(chunk_bytes))))
     t0 = time.perf_counter()
     dev = engine.device
     g_blob = torch.zeros(0, dtype=torch.uint8, device=dev)  # the file's distinct keys so far, in global id order
     g_offs = torch.zeros(1, dtype=torch.int64, device=dev)
-    rows_l, cols_l, data_l = [], [], []
-    n_lines = n_records = n_edges = overflow = 0
+    parts = []
+    n_lines = n_records = n_edges = overflow = n_trip = 0
+    warned = None      # (global warn line, warn byte) of the first unsupported record
+    cast_err = None    # (status, global triplet index, value) of the first cast error
     tm = {"read": 0.0, "local_build": 0.0, "merge_keys": 0.0, "remap": 0.0}
 
     def lap(key, t):
         tm[key] += (time.perf_counter() - t) * 1e3
         return time.perf_counter()
 
-    for lo, hi in file_line_ranges(path, n_chunks):
+    def result(**kw):
+        r = ShardResult(n_lines=n_lines, n_records=n_records, n_edges=n_edges, n_nodes=int(g_offs.numel()) - 1,
+                        n_cast_overflow=overflow, **kw)
+        if warned is not None:
+            r.has_warning, r.warn_line, r.warn_byte = True, warned[0], warned[1]
+        return r
+
+    for lo, hi in src.ranges(n_chunks):
         t = time.perf_counter()
-        buf = engine.read_range(path, lo, hi - lo)
+        buf = src.upload(engine, lo, hi)
         t = lap("read", t)
-        sh = engine.local_build(buf, opts)
+        sh = engine.local_build(buf, opts, unknown_warned=warned is not None)
+        if warned is None and sh.has_warning and not (sh.status == 8 and sh.err_line == sh.warn_line):
+            warned = (n_lines + sh.warn_line, sh.warn_byte)
         del buf
         t = lap("local_build", t)
-        if sh.status != 0 or sh.has_warning:
-            return None
+        if sh.status != 0 and sh.status not in CAST_ERRORS:  # a parse error: the build ends here
+            if warned is not None and warned[0] >= n_lines + sh.err_line:
+                warned = None  # (the warning would have come after the error)
+            out = result(status=int(sh.status), err_line=n_lines + int(sh.err_line), err_detail=sh.err_detail)
+            out.n_lines, out.n_records = n_lines + int(sh.n_lines), n_records + int(sh.n_records)
+            out.n_records_before_error = n_records + int(sh.n_records_before_error)
+            return out
+        n_lines += int(sh.n_lines)
+        n_records += int(sh.n_records)
+        if sh.status in CAST_ERRORS:
+            if cast_err is None:
+                cast_err = (int(sh.status), n_trip + int(sh.err_index), float(sh.err_value))
+            continue
+        n_edges += int(sh.n_edges)
+        overflow += int(sh.n_cast_overflow)
+        if cast_err is not None:
+            continue  # (the build raises the cast error; only later parse errors still matter)
         n_g, n_l = int(g_offs.numel()) - 1, int(sh.n_local_nodes)
         blob = torch.cat([g_blob, sh.names_blob.to(dev)])
         offs = torch.cat([g_offs, sh.names_offsets.to(dev)[1:] + g_offs[-1]])
@@ -847,112 +1078,81 @@ def _chunked_general(path: str, *, engine, chunk_bytes: int, directed, bidirecte
         if n_l and rows.numel():
             rows, cols = engine.remap_pairs(rows, cols, ids[n_g:n_g + n_l].contiguous())
         t = lap("remap", t)
-        rows_l.append(rows)
-        cols_l.append(cols)
-        data_l.append(sh.data)
-        n_lines += int(sh.n_lines)
-        n_records += int(sh.n_records)
-        n_edges += int(sh.n_edges)
-        overflow += int(sh.n_cast_overflow)
+        n_trip += int(rows.numel())
+        parts.append(_keep_part(keep_host, rows, cols, sh.data))
+        del rows, cols, sh
+    if cast_err is not None:
+        return result(status=cast_err[0], err_index=cast_err[1], err_value=cast_err[2])
     n = int(g_offs.numel()) - 1
     if n >= INT32_MAX:
         return None
     tm["build"] = (time.perf_counter() - t0) * 1e3
-    rows = torch.cat(rows_l) if len(rows_l) > 1 else rows_l[0]
-    cols = torch.cat(cols_l) if len(cols_l) > 1 else cols_l[0]
-    data = torch.cat(data_l) if len(data_l) > 1 else data_l[0]
-    del rows_l, cols_l, data_l
-    out = ShardResult(status=0, n_lines=n_lines, n_records=n_records, n_edges=n_edges, n_nodes=n,
-                      n_cast_overflow=overflow)
+    out = result(status=0)
     out.n_records_before_error = n_records
-    out.row_lo, out.row_hi = 0, n
-    if maxsym or not keep_coo:
-        t1 = time.perf_counter()
-        d = None if uniform else data
-        indptr, indices, vals, _, _ = engine.csr_pair((rows, cols, d), (cols, rows, d) if maxsym else None, maxsym,
-                                                      0, n, n, dtype, uniform, -1)
-        tm["csr"] = (time.perf_counter() - t1) * 1e3
-        out.indptr, out.indices, out.data = indptr, indices, vals
-        out.index_maxval = int(indices.numel()) if maxsym else int(rows.numel())
-    if keep_coo:
-        out.coo = (rows, cols, data)
     if gather_names:
         out.names_blob, out.names_offsets = g_blob.cpu().numpy(), g_offs.cpu().numpy()
+    del g_blob, g_offs
+    _finish_chunked(engine, out, parts, n, maxsym, uniform, dtype, keep_coo, tm, free_hbm, bands)
     out.parse_path = "chunked general"
     out.timings_ms = tm
     return out
 
 
-def _chunked_decimal(path: str, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False,
-                     asymmetric=False, dtype="float64", gather_names=False, keep_coo=False) -> ShardResult | None:
+def _chunked_decimal(src, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False, asymmetric=False,
+                     dtype="float64", gather_names=False, keep_coo=False, free_hbm=None,
+                     bands=None) -> ShardResult | None:
     """One file whose working set does not fit one GPU, on that GPU alone: its line-aligned byte
-    ranges of about `chunk_bytes` are read (pread) and parsed one after another straight into GLOBAL
-    decimal ids — the sharded fast path's one pass (`build_decimal_range`), each range's premise
-    evidence kept — so only one range's text and working set are resident at a time beside the
-    growing COO; the evidence is then checked over the whole file in stream order (the rule of
-    `_build_decimal_sharded`: S lines first, each range's names continuing the S lines before it,
-    every edge key an S key) and the CSR (or, keep_coo, the stream-order COO) built once over all
-    ranges' triplets.  Returns the whole matrix as one row slice, or None when the decimal-id premise
-    fails anywhere (names not "1".."N" in S-first order, bidirected / weighted / strip builds, an
-    error or warning in a range): the caller then builds the file in one piece, which raises the
-    reference's error.  (Segment names other than 1..N need one dictionary over the whole file; no
-    chunked build for them.)"""
-    import os
+    ranges of about `chunk_bytes` are uploaded and parsed one after another straight into GLOBAL
+    decimal ids — the sharded fast path's one pass (`build_decimal_range`) — so only one range's text
+    and working set are resident at a time beside the growing COO.  Each range's premise evidence
+    is checked as it comes (the rule of `_build_decimal_sharded`: S lines first, each range's names
+    continuing the S lines before it), every edge key against the S count at the end; the CSR (or,
+    keep_coo, the stream-order COO) is then built once over all ranges' triplets.  Returns the whole
+    matrix as one row slice, or None when the decimal-id premise fails anywhere (names not "1".."N"
+    in S-first order, an error or warning in a range): the caller then runs the merged-dictionary
+    chunks, which resolve errors and warnings in stream order."""
     import time
 
-    import torch
-
+    src = _as_source(src)
+    free_hbm = free_hbm or engine.free_memory
     opts = dict(directed=directed, bidirected=False, keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
                 strip_orientation=False, dtype=dtype, weight_tag=None)
     gd = keep_directed_bidir or directed  # builders.py:143 (not bidirected)
     maxsym = gd and not asymmetric        # builders.py:282
-    size = os.path.getsize(path)
-    n_chunks = max(1, -(-size // max(1, int(chunk_bytes))))
+    keep_host = keep_coo and not maxsym
+    n_chunks = max(1, -(-src.size // max(1, int(chunk_bytes))))
     tm = {}
     t0 = time.perf_counter()
-    rows_l, cols_l, data_l, ev = [], [], [], []
+    parts, ev = [], []
     overflow = 0
-    for lo, hi in file_line_ranges(path, n_chunks):
-        buf = engine.read_range(path, lo, hi - lo)
+    seen_edge, s_before, vmax = False, 0, 0
+    for lo, hi in src.ranges(n_chunks):
+        buf = src.upload(engine, lo, hi)
         got = engine.build_decimal_range(buf, opts, view=False, values=keep_coo)
         del buf
         if got is None:
             return None
         sh, e = got
-        rows_l.append(sh.rows)
-        cols_l.append(sh.cols)
-        if keep_coo:
-            data_l.append(sh.data)
-        overflow += int(sh.n_cast_overflow)
-        ev.append([int(v) for v in e])
-    seen_edge, s_before = False, 0
-    for e in ev:  # [lines, S lines, edges, records, d, largest edge key]
+        e = [int(v) for v in e]  # [lines, S lines, edges, records, d, largest edge key]
         if e[1] and (seen_edge or e[4] != s_before):
-            return None
+            return None  # an S line after an edge line, or names not continuing the S lines before
         seen_edge = seen_edge or e[2] > 0
         s_before += e[1]
+        vmax = max(vmax, e[5])
+        parts.append(_keep_part(keep_host, sh.rows, sh.cols, sh.data))
+        overflow += int(sh.n_cast_overflow)
+        ev.append(e)
+        del sh
     n = s_before
-    if not 0 < n < INT32_MAX or max(e[5] for e in ev) > n:
+    if not 0 < n < INT32_MAX or vmax > n:
         return None
     tm["build"] = (time.perf_counter() - t0) * 1e3
-    rows = torch.cat(rows_l) if len(rows_l) > 1 else rows_l[0]
-    cols = torch.cat(cols_l) if len(cols_l) > 1 else cols_l[0]
-    del rows_l, cols_l
     out = ShardResult(status=0, n_lines=sum(e[0] for e in ev), n_records=sum(e[3] for e in ev),
                       n_edges=sum(e[2] for e in ev), n_nodes=n, n_cast_overflow=overflow)
     out.n_records_before_error = out.n_records
-    out.row_lo, out.row_hi = 0, n
-    if maxsym or not keep_coo:  # (a SUM build that returns its stream-order COO needs no CSR)
-        t1 = time.perf_counter()
-        indptr, indices, vals, _, _ = engine.csr_pair((rows, cols, None), (cols, rows, None) if maxsym else None,
-                                                      maxsym, 0, n, n, dtype, True, -1)
-        tm["csr"] = (time.perf_counter() - t1) * 1e3
-        out.indptr, out.indices, out.data = indptr, indices, vals
-        out.index_maxval = int(indices.numel()) if maxsym else int(rows.numel())
-    if keep_coo:
-        out.coo = (rows, cols, torch.cat(data_l) if len(data_l) > 1 else data_l[0])
     if gather_names:  # node k is str(k + 1)
         out.names_blob, out.names_offsets = nat.decimal_names(n, False)
+    _finish_chunked(engine, out, parts, n, maxsym, True, dtype, keep_coo, tm, free_hbm, bands)
     out.fast_path = True
     out.parse_path = f"chunked x{len(ev)}"
     out.timings_ms = tm

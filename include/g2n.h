@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define G2N_ABI_VERSION 1u
+#define G2N_ABI_VERSION 2u /* 2: named range / test fields replace options.reserved[] */
 
 /* ---- status codes ------------------------------------------------------------------ */
 enum {
@@ -92,22 +92,44 @@ typedef struct g2n_options {
   const char *weight_tag;      /* UTF-8, NUL-terminated; NULL or "" = no weights */
   int32_t want_node_names;     /* 1 (default): produce the names blob in id order */
   int32_t device;              /* HIP device ordinal, default 0 */
-  int32_t reserved[6];         /* [0]: unsupported records skipped silently (an earlier shard of a
-                                  sharded build warned already);
-                                  [1]: test flags (normally rare paths, same results): 2 = MAX-SYM / SUM CSR through
-                                  the general row sums, 4 = decimal ids without the lean parse,
-                                  8 = hash dictionary, 16 = general dictionary rounds,
-                                  32 = decimal ids parsed after K1 (not the tile-local pass),
-                                  64 = a BGZF .gz read by the host readers (not inflated on the GPU);
-                                  [2], [3], [4] bit 0: sharded decimal-id build — this byte range's
-                                  node ids are global decimals: [2] = S lines before the range,
-                                  [3] = S lines in the file (output G2N_OUT_COO, no names; returns
-                                  G2N_E_UNSUPPORTED when the range needs the general protocol:
-                                  ids that are not decimal, errors, warnings, slow weights);
-                                  [4] bit 2: no weight tag and the caller reads coordinates only —
-                                  the result's values are left unwritten;
-                                  [5] = 0 */
+  /* ---- set by the sharded / chunked protocol (gfa2network_amd/shard.py); 0 in a plain build ---- */
+  int32_t unknown_warned;      /* 1: unsupported records are skipped silently (an earlier byte range
+                                  of the same file already raised the one-shot warning) */
+  int32_t range_flags;         /* G2N_RANGE_* bits, below */
+  int64_t range_s_base;        /* G2N_RANGE_DECIMAL: S lines in the file before this byte range */
+  int64_t range_n_segments;    /* G2N_RANGE_DECIMAL: S lines in the whole file */
+  /* ---- tests only ---- */
+  uint32_t test_flags;         /* G2N_TEST_* bits: take a normally rare path (same results) */
+  int32_t reserved_[3];        /* must be 0 (g2n_options_init) */
 } g2n_options;
+
+/* g2n_options.range_flags */
+enum {
+  G2N_RANGE_DECIMAL = 1,        /* one byte range of a sharded decimal-id build: this range's node ids
+                                   are global decimals (range_s_base / range_n_segments); output
+                                   G2N_OUT_COO, no names; G2N_E_UNSUPPORTED when the range needs the
+                                   general protocol (ids that are not decimal, errors, warnings, slow
+                                   weights) */
+  G2N_RANGE_EVIDENCE = 2,       /* with DECIMAL: report the range's evidence instead of checking the
+                                   premise (set by g2n_build_decimal_range) */
+  G2N_RANGE_NO_VALUES = 4       /* no weight tag and the caller reads coordinates only: the result's
+                                   values are left unwritten */
+};
+
+/* g2n_options.test_flags (tests only; every real build leaves 0): the same results through a path
+ * that is normally rare on the given input. */
+enum {
+  G2N_TEST_NO_BUCKETS = 2,      /* MAX-SYM / SUM CSR through the general row sums */
+  G2N_TEST_NO_LEAN = 4,         /* decimal ids without the lean parse */
+  G2N_TEST_DICT_HASH = 8,       /* hash dictionary (no decimal ids) */
+  G2N_TEST_DICT_GENERAL = 16,   /* general dictionary rounds */
+  G2N_TEST_NO_TILE_LOCAL = 32,  /* decimal ids parsed after K1 (not the tile-local pass) */
+  G2N_TEST_HOST_INFLATE = 64,   /* a BGZF .gz read by the host readers (not inflated on the GPU) */
+  G2N_TEST_NO_GROUP = 128,      /* tile-local parse into per-tile slots + compaction */
+  G2N_TEST_NO_HASH_LEAN = 256,  /* the classic hash tiers, never the lean S-first one */
+  G2N_TEST_THROW_AFTER_IDS = 512, /* the build fails (G2N_E_DEVICE) once its ids are set up */
+  G2N_TEST_INDEX64 = 1024       /* CSR results in int64 indptr / indices (the > 2^31 - 1 entries path) */
+};
 
 #define G2N_MAX_PHASES 40
 
@@ -162,6 +184,9 @@ const char *g2n_version(void);
 uint32_t g2n_abi_version(void);
 void g2n_options_init(g2n_options *opts);      /* reference defaults (builders.py:30-50) */
 int g2n_device_count(void);                    /* HIP devices visible (0 without a GPU) */
+/* hipMemGetInfo of `device`: free / total HBM bytes (G2N_E_DEVICE without such a device).  What
+ * parse_gfa sizes its one-GPU chunked build by (gfa2network_amd/api.py), without torch. */
+int g2n_device_memory(int32_t device, uint64_t *free_bytes, uint64_t *total_bytes);
 const char *g2n_last_error(void);              /* thread-local message of the last failure */
 const char *g2n_status_name(int status);
 
@@ -244,9 +269,15 @@ int64_t g2n_first_bad_utf8(const uint8_t *blob, const int64_t *offsets, uint64_t
 
 /* convert_format(A, "csr") for a COO matrix (utils.py:40-63 -> scipy coo.tocsr):
  * sums duplicates in dtype with scipy's summation order, keeps explicit zeros.
- * rows/cols have index_width bytes per element, data has dtype elements; n_rows x n_cols. */
+ * rows/cols have index_width (4) bytes per element, data has dtype elements; n_rows x n_cols
+ * (each < 2^31 - 1).  indptr / indices come back in scipy's index dtype: int64 (index_width 8)
+ * once nnz passes 2^31 - 1 (_coo_to_compressed: maxval = coo.nnz, duplicates included).  Up to
+ * 2^32 - 2 entries when every value is dtype(1) (a parse without a weight tag); other values
+ * past 2^31 - 2 entries return G2N_E_UNSUPPORTED.  test_flags: G2N_TEST_INDEX64 /
+ * G2N_TEST_NO_BUCKETS (tests only; 0 otherwise). */
 int g2n_coo_to_csr(const void *rows, const void *cols, const void *data, int64_t nnz, int64_t n_rows,
-                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, g2n_result **out);
+                   int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags,
+                   g2n_result **out);
 
 /* ---- device-resident entry points (the measured hot path) ------------------------------ */
 typedef struct g2n_context g2n_context;
@@ -347,10 +378,10 @@ int g2n_count_device(g2n_context *ctx, const void *d_input, size_t len, int64_t 
  *             the premise needs d == the S lines of the ranges before),
  *          the largest edge key value (the premise needs it <= the file's S lines)}.
  * Options: output G2N_OUT_COO, no names, not bidirected, no weight tag, no strip (else G2N_E_ARG);
- * reserved[2..4] are set by the call (reserved[4] bit 2 is kept: values left unwritten).  G2N_E_UNSUPPORTED when the one pass declines (a line past
+ * range_* are set by the call (G2N_RANGE_NO_VALUES is kept).  G2N_E_UNSUPPORTED when the one pass declines (a line past
  * its tile window, a record outside the lean shapes, S names that are not one decimal run, an S
  * line after an edge line in the range): the caller then counts the ranges (g2n_count_device) and
- * builds with reserved[2..4] (g2n_build_device), whose check decides.  Replaces the count pass of
+ * builds with G2N_RANGE_DECIMAL (g2n_build_device), whose check decides.  Replaces the count pass of
  * the sharded build for the common layout; results as g2n_build_device's (device pointers). */
 int g2n_build_decimal_range(g2n_context *ctx, const void *d_input, size_t len, const g2n_options *opts,
                             int64_t *ev6, g2n_result *out);

@@ -215,3 +215,18 @@ class CpuEngine:
         tdt = getattr(torch, TORCH_DTYPES[dtype])
         return (torch.from_numpy(M.indptr.astype(np.int32)), torch.from_numpy(M.indices.astype(np.int32)),
                 torch.from_numpy(data).to(tdt), False, False)
+
+    # the chunked build's source / memory hooks (shard.build_chunked)
+    free_bytes = 1 << 60
+
+    def upload(self, arr):
+        return torch.from_numpy(np.array(arr, dtype=np.uint8))
+
+    def free_memory(self):
+        return self.free_bytes
+
+    def reset(self):
+        pass
+
+    def close(self):
+        pass

@@ -38,14 +38,32 @@ def test_abi_version_and_defaults():
     assert o.dtype == _native.DTYPE_CODES["float64"] and o.want_node_names == 1
 
 
-def test_struct_sizes_match_header():
-    """ctypes layouts agree with the C structs (offsets of the last fields)."""
+def test_struct_sizes_match_header(tmp_path):
+    """ctypes layouts agree with the C structs: every field's offset and both sizes, as gcc lays
+    out include/g2n.h."""
+    import subprocess
+
     from gfa2network_amd import _native
 
-    assert ctypes.sizeof(_native.Options) == 4 * 8 + 8 + 4 * 8
-    r = _native.Result
-    assert r.priv_.offset + 8 == ctypes.sizeof(r)
-    assert r.phase_ms.offset % 8 == 0
+    structs = {"g2n_options": _native.Options, "g2n_result": _native.Result}
+    lines = []
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"g2n.h\"\nint main(void) {\n"
+                   + "\n".join(lines) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), "-o", str(exe), str(src)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        s, f, v = ln.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
 
 
 @pytest.mark.skipif(__import__("gfa2network_amd._native", fromlist=["x"]).device_count() > 0,

@@ -86,11 +86,11 @@ def test_chunked_decimal_premise_breaks(oracle_lib, tmp_path, breaks):
     full = oracle_lib.run(data)
     for chunk in (113, 4000):
         assert _chunked_decimal(str(path), engine=CpuEngine(orc), chunk_bytes=chunk) is None, (breaks, chunk)
-        got = _chunked(path, chunk, {})
-        if breaks == "error":
-            assert got is None
+        if breaks == "error":  # the merged-dictionary chunks raise the one-piece build's error
+            with pytest.raises(ValueError, match="Malformed L record"):
+                _chunked(path, chunk, {})
             continue
-        A, nodes = got
+        A, nodes = _chunked(path, chunk, {})
         B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype("float64"), return_node_list=True,
                              raw_bytes_id=False, verbose=False)
         assert nodes == bnodes and np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
@@ -159,27 +159,216 @@ def test_chunked_general_names_equal_one_piece(oracle_lib, tmp_path, shuffle, mo
     assert A.data.tobytes() == B.data.tobytes()
 
 
-@pytest.mark.parametrize("extra", [["L\tbad\t+\n"], ["W\tsample\t1\tchr1\t0\t10\t>s1\n"]])
-def test_chunked_general_declines_errors_and_warnings(oracle_lib, tmp_path, extra):
+def _outcome(fn):
+    """(kind, value, warnings): kind "ok" with (A, nodes), or "exc" with (type name, message)."""
+    import warnings
+
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        try:
+            got = ("ok", fn())
+        except Exception as e:  # noqa: BLE001 - compared against the one-piece build
+            got = ("exc", (type(e).__name__, str(e)))
+    return got[0], got[1], [str(x.message) for x in w]
+
+
+def _one_piece(oracle_lib, data, mode):
+    from gfa2network_amd.api import finalize
+
+    def run():
+        o = oracle_lib.run(data, **mode)
+        return finalize(oracle_lib.to_raw(o, "parse"), dtype=np.dtype(mode.get("dtype", "float64")),
+                        return_node_list=True, raw_bytes_id=False, verbose=False)
+    return _outcome(run)
+
+
+def _same(a, b):
+    assert a[0] == b[0] and a[2] == b[2], (a[0], b[0], a[1] if a[0] == "exc" else "", b[1] if b[0] == "exc" else "",
+                                           a[2], b[2])
+    if a[0] == "exc":
+        assert a[1] == b[1]
+        return
+    (A, na), (B, nb) = a[1], b[1]
+    assert A.format == B.format and A.shape == B.shape and A.dtype == B.dtype and na == nb
+    if A.format == "coo":
+        assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col) and A.row.dtype == B.row.dtype
+    else:
+        assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        assert A.indptr.dtype == B.indptr.dtype
+    assert A.data.tobytes() == B.data.tobytes()
+
+
+ERRORS = {  # (text inserted near the middle of the file, mode): errors, cast errors and the warning
+    "malformed_l": (["L\tbad\t+\n"], {}),
+    "warning": (["W\tsample\t1\tchr1\t0\t10\t>s1\n"], {}),
+    "two_warnings": (["W\tsample\t1\tchr1\t0\t10\t>s1\n", "J\tx\n"] * 3, {}),
+    "warning_then_error": (["W\tsample\n"] + ["L\ts1\t+\ts2\t+\t*\n"] * 200 + ["L\tbad\n"], {}),
+    "short_s": (["S\n"], {}),
+    "cast_int8": (["L\ts1\t+\ts2\t+\t*\tRC:i:300\n"], {"weight_tag": "RC", "dtype": "int8"}),
+    "cast_then_parse_error": (["L\ts1\t+\ts2\t+\t*\tRC:i:300\n"] + ["L\ts3\t+\ts1\t+\t*\n"] * 300
+                              + ["L\tq\n"], {"weight_tag": "RC", "dtype": "int8"}),
+    "float32_overflow": (["L\ts1\t+\ts2\t+\t*\tRC:i:" + "9" * 60 + "\n"], {"weight_tag": "RC", "dtype": "float32"}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(ERRORS))
+@pytest.mark.parametrize("chunk", [300, 2500, 1 << 30])
+def test_chunked_errors_and_warnings_as_one_piece(oracle_lib, tmp_path, case, chunk):
+    """Errors, cast errors and the one-shot unsupported-record warning anywhere in the file come out of
+    the chunked build exactly as from one piece (parser.py:114-132, builders.py:281): the first parse
+    error with its line (a cast error loses to a later parse error: the reference casts after its
+    loop), one warning, float32 overflow warnings per element (GFA 1.1 W / J lines no longer
+    send a large file to the one-piece build)."""
+    extra, mode = ERRORS[case]
+    data = _named_gfa(33, 150, 700, True, extra)
     path = tmp_path / "in.gfa"
-    path.write_bytes(_named_gfa(32, 200, 800, True, extra))
-    assert _chunked(path, 700, {}) is None
+    path.write_bytes(data)
+    _same(_outcome(lambda: _chunked(path, chunk, mode)), _one_piece(oracle_lib, data, mode))
 
 
-def test_auto_mode_chooses_chunks_only_past_free_memory(tmp_path, monkeypatch):
-    """shard="auto" on one process: chunked only for a plain file on disk whose working set
-    (WORKING_SET_PER_INPUT_BYTE x its size) passes the GPU's free HBM; never for "never"."""
-    import torch
+def _cpu_engine_factory(monkeypatch, oracle_mod, free=None):
+    from gfa2network_amd import shard
+    from shard_cpu_engine import CpuEngine
 
+    def make(device=0):
+        e = CpuEngine(oracle_mod)
+        if free is not None:
+            e.free_bytes = free
+        return e
+    monkeypatch.setattr(shard, "HipEngine", make)
+
+
+@pytest.mark.parametrize("kind", ["gz", "stdin", "fileobj", "plain"])
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"bidirected": True, "weight_tag": "RC"}])
+def test_parse_gfa_chunks_every_input_kind(oracle_lib, tmp_path, monkeypatch, kind, mode):
+    """parse_gfa itself (default shard="never") takes the one-GPU chunked build for an input past the
+    GPU's working set, whatever its kind: a plain file (pread chunks), a .gz (inflated on the host, then
+    chunked from host memory), stdin and a file object (read, then chunked) — equal to one piece.  Here
+    the GPU's free HBM is reported small and the CPU engine stands in for the HIP one."""
+    import gzip
+    import io
+    import sys
+
+    from gfa2network_amd import api, parse_gfa
+
+    data = _named_gfa(34, 200, 900, True)
+    _cpu_engine_factory(monkeypatch, __import__("oracle.oracle", fromlist=["x"]))
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0: 1000)  # every input is past the working set
+    monkeypatch.setattr(api, "_chunk_plan", lambda size, device: 1500 if size * 8 > 1000 else 0)
+    calls = []
+    real = api._parse_gfa_chunked
+    monkeypatch.setattr(api, "_parse_gfa_chunked", lambda *a, **k: calls.append(1) or real(*a, **k))
+    if kind == "gz":
+        src = tmp_path / "in.gfa.gz"
+        src.write_bytes(gzip.compress(data[:len(data) // 2]) + gzip.compress(data[len(data) // 2:]))
+    elif kind == "plain":
+        src = tmp_path / "in.gfa"
+        src.write_bytes(data)
+    elif kind == "fileobj":
+        src = io.BytesIO(data)
+    else:
+        src = "-"
+        monkeypatch.setattr(sys, "stdin", type("S", (), {"buffer": io.BytesIO(data)})())
+    got = _outcome(lambda: parse_gfa(src, build_graph=False, build_matrix=True, return_node_list=True, **mode))
+    assert calls, "the chunked build did not run"
+    _same(got, _one_piece(oracle_lib, data, mode))
+
+
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"dtype": "int8"},
+                                  {"weight_tag": "RC", "dtype": "float32"}, {"weight_tag": "RC", "asymmetric": True},
+                                  {"bidirected": True}])
+@pytest.mark.parametrize("bands", [2, 5])
+def test_chunked_csr_in_row_bands_equals_one_piece(oracle_lib, tmp_path, mode, bands):
+    """The whole-matrix CSR of a chunked build assembled in row bands (each chunk's triplets routed by
+    band, stable; each band's CSR with its row base; indptrs rebased) equals one piece — the path a
+    file takes when its CSR does not fit the GPU beside its triplets (floats: scipy's whole-matrix
+    has_sorted_indices verdict OR-ed over the bands first)."""
+    from gfa2network_amd.api import _dtype_of, _parse_gfa_chunked
+    from oracle import oracle as orc
+    from shard_cpu_engine import CpuEngine
+
+    data = _named_gfa(35, 120, 900, True)
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    kw = dict(directed=mode.get("directed", True), weight_tag=mode.get("weight_tag"), verbose=False,
+              bidirected=mode.get("bidirected", False), keep_directed_bidir=False, strip_orientation=False,
+              dt=_dtype_of(mode.get("dtype", "float64")), asymmetric=mode.get("asymmetric", False),
+              raw_bytes_id=False, return_node_list=True, device=0)
+    got = _outcome(lambda: _parse_gfa_chunked(str(path), 900, engine=CpuEngine(orc), bands=bands, **kw))
+    _same(got, _one_piece(oracle_lib, data, mode))
+
+
+def test_chunked_assembly_sizes_bands_from_free_memory(oracle_lib, tmp_path):
+    """With the GPU's free HBM below the whole CSR's estimate the assembly picks row bands by itself
+    (equal to one piece); below even the band-ordered triplets it raises MemoryError (ADVICE r04:
+    a clear error instead of running out of device memory part way)."""
+    from gfa2network_amd import shard
+    from gfa2network_amd.api import _dtype_of, _parse_gfa_chunked
+    from oracle import oracle as orc
+    from shard_cpu_engine import CpuEngine
+
+    data = _decimal_gfa(36, 300, 3000)
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    kw = dict(directed=True, weight_tag=None, verbose=False, bidirected=False, keep_directed_bidir=False,
+              strip_orientation=False, dt=_dtype_of("float64"), asymmetric=False, raw_bytes_id=False,
+              return_node_list=True, device=0)
+    n_trip = 3000
+    whole = shard.csr_bytes_estimate(n_trip, n_trip, 300, 8) + 16 * n_trip
+    seen = {}
+    real = shard._assemble_csr
+
+    def spy(*a, **k):
+        out = real(*a, **k)
+        seen["bands"] = a[6].get("csr_bands", 1)
+        return out
+    shard._assemble_csr = spy
+    try:
+        eng = CpuEngine(orc)
+        eng.free_bytes = whole // 2
+        got = _outcome(lambda: _parse_gfa_chunked(str(path), 5000, engine=eng, **kw))
+        _same(got, _one_piece(oracle_lib, data, {}))
+        assert seen["bands"] >= 2
+        eng.free_bytes = 1000
+        with pytest.raises(MemoryError, match="needs about"):
+            _parse_gfa_chunked(str(path), 5000, engine=eng, **kw)
+    finally:
+        shard._assemble_csr = real
+
+
+def test_chunk_plan_only_past_free_memory(tmp_path, monkeypatch):
+    """The one-GPU chunked build starts only for an input whose working set (WORKING_SET_PER_INPUT_BYTE
+    x its size) passes the GPU's free HBM, read through the C-ABI (no torch); without a device no chunks
+    (the build raises the device error)."""
     from gfa2network_amd import api
 
-    path = tmp_path / "in.gfa"
-    path.write_bytes(_decimal_gfa(24, 50, 100))
-    size = path.stat().st_size
-    monkeypatch.setattr(api, "_dist_world", lambda: 1)
+    size = 10 << 20
     for free, want in ((size * api.WORKING_SET_PER_INPUT_BYTE + 1, False), (size, True)):
-        monkeypatch.setattr(torch.cuda, "mem_get_info", lambda device=None, f=free: (f, 2 * f))
-        got = api._chunk_for(str(path), "auto", 0)
+        monkeypatch.setattr(api, "_free_hbm", lambda device=0, f=free: f)
+        got = api._chunk_plan(size, 0)
         assert bool(got) == want and (not got or got >= 1 << 26)
-        assert api._chunk_for(str(path), "never", 0) == 0
-    assert api._chunk_for(str(tmp_path / "missing.gfa"), "auto", 0) == 0
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0: None)
+    assert api._chunk_plan(size, 0) == 0
+
+
+def test_line_ranges_windowed_search():
+    """line_ranges over a host buffer finds each boundary without scanning past the next newline
+    (a chunked .gz / stdin input may be hundreds of GB); long lines and missing newlines kept."""
+    from gfa2network_amd.shard import line_ranges
+
+    r = __import__("random").Random(5)
+    for _ in range(50):
+        parts = [b"x" * r.choice([0, 1, 5, 70000, 200000]) + b"\n" for _ in range(r.randint(0, 12))]
+        data = b"".join(parts) + (b"tail" if r.random() < 0.5 else b"")
+        arr = np.frombuffer(data, dtype=np.uint8)
+        n = r.randint(1, 9)
+        got = line_ranges(arr, n)
+        want, starts = [], [0]
+        for k in range(1, n):
+            s = k * len(data) // n
+            if 0 < s < len(data) and data[s - 1] != 0x0A:
+                j = data.find(b"\n", s)
+                s = len(data) if j < 0 else j + 1
+            starts.append(max(s, starts[-1]))
+        want = [(starts[k], starts[k + 1] if k + 1 < n else len(data)) for k in range(n)]
+        assert got == want

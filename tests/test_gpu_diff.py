@@ -5,6 +5,8 @@
 * bench-size properties (C4: 200M edges) that hold whatever the size: symmetry of the
   MAX-SYM CSR, canonical CSR, node names = "1".."N" in S order.
 """
+import io
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -648,4 +650,39 @@ def test_int64_index_path_equals_oracle(gpu, oracle_lib, case):
                 if not (np.array_equal(raw.indptr, R.indptr) and np.array_equal(raw.indices, R.indices)
                         and raw.data.tobytes() == R.data.tobytes()):
                     bad.append((mode, dtype, out))
+    assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("case", ["synth_dense", "synth"])
+def test_convert_format_int64_path_equals_oracle(gpu, oracle_lib, monkeypatch, case):
+    """convert_format(A, "csr" | "csc") of a COO parse_gfa returns (utils.py:55; cli.py:239 for
+    `convert --undirected`) through the int64 index path g2n_coo_to_csr takes past 2^31 - 1 entries
+    (TEST_INDEX64 forces it on a small input): int64 indptr / indices holding exactly scipy's values, in
+    every COO mode and every CLI dtype; a weighted COO keeps its own path (int32, equal values)."""
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import convert_format, parse_gfa
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(3000, 60000, seed=9) if case == "synth_dense" else _csr_cases()[case]
+    bad = []
+    for mode in ({"directed": False}, {"asymmetric": True}, {"bidirected": True},
+                 {"keep_directed_bidir": True, "asymmetric": True}, {"directed": False, "weight_tag": "RC"}):
+        for dtype in ("float64", "float32", "int32", "int8", "bool"):
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+            A = parse_gfa(io.BytesIO(data), build_graph=False, build_matrix=True, dtype=dtype, **mode)
+            assert A.format == "coo"
+            o = oracle_lib.run(data, dtype=dtype, **mode)
+            R = oracle_lib.to_raw(o, "csr")  # what convert_format(parse_gfa(...), "csr") returns
+            Rc = sp.coo_matrix((o.data, (o.rows.astype(np.int32), o.cols.astype(np.int32))),
+                               shape=A.shape).tocsc()
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_INDEX64)
+            for fmt, ref in (("csr", R), ("csc", Rc)):
+                C = convert_format(A, fmt)
+                want = np.int32 if mode.get("weight_tag") else np.int64
+                if C.indptr.dtype != want or C.indices.dtype != want:
+                    bad.append((mode, dtype, fmt, "dtype", C.indptr.dtype))
+                    continue
+                if not (np.array_equal(C.indptr, ref.indptr) and np.array_equal(C.indices, ref.indices)
+                        and C.data.tobytes() == ref.data.tobytes()):
+                    bad.append((mode, dtype, fmt))
     assert not bad, bad[:4]

@@ -241,3 +241,60 @@ def test_int64_indices_past_2_31_entries(gpu):
     finally:
         lib.g2n_context_destroy(ctx)
         dev.free()
+
+
+class _Reader:
+    """A file object over bytes already in host memory (parse_gfa reads file objects whole,
+    parser.py:90-92): no second copy of a 36 GB input."""
+
+    def __init__(self, arr):
+        self.arr = arr
+
+    def read(self):
+        return self.arr
+
+
+def test_convert_format_int64_past_2_31_entries(gpu):
+    """`convert --undirected` at more than 2^31 - 1 COO entries (utils.py:55, cli.py:239): 275M S /
+    1.1G L through the product's parse_gfa(directed=False) — the stream-order COO of 2.2G triplets in
+    host memory — then convert_format(A, "csr") (g2n_coo_to_csr), whose result scipy gives int64
+    indptr / indices (_coo_to_compressed sizes by coo.nnz).  Checked: the COO's size and twin pairing,
+    int64 indptr from 0 to nnz, non-decreasing; every row's columns strictly increasing and < n; the
+    values sum to 2 x edges (exact in float64).  Parity beyond these properties: the forced int64 path
+    (test_gpu_diff.py::test_convert_format_int64_path_equals_oracle) and the int32 conversions."""
+    from gfa2network_amd import convert_format, parse_gfa
+    from gfa2network_amd import synth
+
+    n_s, n_l = 275_000_000, 1_100_000_000
+    dev = synth.DeviceInput(n_s, n_l, seed=0)
+    try:
+        text = np.empty(dev.len, dtype=np.uint8)
+        assert synth._lib().g2n_synth_download(text.ctypes.data, dev.ptr, dev.len) == 0
+    finally:
+        dev.free()
+    A = parse_gfa(_Reader(text), build_graph=False, build_matrix=True, directed=False)
+    del text
+    assert A.format == "coo" and A.shape == (n_s, n_s) and A.nnz == 2 * n_l > 2**31 - 1
+    step = 1 << 28
+    for k in range(0, A.nnz, step):  # every L line adds (u, v) then (v, u)
+        r, c = A.row[k:k + step], A.col[k:k + step]
+        assert np.array_equal(r[0::2], c[1::2]) and np.array_equal(c[0::2], r[1::2])
+    C = convert_format(A, "csr")
+    del A
+    assert C.format == "csr" and C.indptr.dtype == np.int64 and C.indices.dtype == np.int64
+    ip, ix = C.indptr, C.indices
+    nnz = int(ip[-1])
+    assert int(ip[0]) == 0 and nnz == len(ix) == len(C.data) and bool(np.all(ip[1:] >= ip[:-1]))
+    total = 0.0
+    starts = np.zeros(step + 1, dtype=bool)
+    for k in range(0, nnz, step):
+        seg = ix[k:k + step + 1]
+        assert int(seg.min()) >= 0 and int(seg.max()) < n_s
+        starts[:] = False  # row starts inside [k, k + len(seg)) may break the increase
+        lo, hi = np.searchsorted(ip, [k, k + len(seg)])
+        rs = ip[lo:hi] - k
+        starts[rs[(rs > 0) & (rs < len(seg))]] = True
+        inc = seg[1:] > seg[:-1]
+        assert bool(np.all(inc | starts[1:len(seg)]))
+        total += float(C.data[k:k + step].sum())
+    assert total == 2.0 * n_l

@@ -369,3 +369,129 @@ def test_gpu_chunked_single_gpu_build(gpu, oracle_lib, tmp_path, mode):
         assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
     else:
         assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+
+
+def _gz_variants(data: bytes, tmp_path):
+    """The same text as multi-member gzip, BGZF (bench.write_bgzf's layout) and one gzip member."""
+    import gzip
+    import struct
+    import zlib
+
+    out = {}
+    p = tmp_path / "multi.gfa.gz"
+    step = max(1, len(data) // 5)
+    p.write_bytes(b"".join(gzip.compress(data[k:k + step]) for k in range(0, len(data), step)))
+    out["multi_member"] = p
+    body = bytearray()
+    for k in range(0, len(data), 65280):
+        chunk = data[k:k + 65280]
+        co = zlib.compressobj(6, zlib.DEFLATED, -zlib.MAX_WBITS)
+        z = co.compress(chunk) + co.flush()
+        body += (b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", 12 + 6 + len(z) + 8 - 1)
+                 + z + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    body += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    p = tmp_path / "bgzf.gfa.gz"
+    p.write_bytes(bytes(body))
+    out["bgzf"] = p
+    p = tmp_path / "single.gfa.gz"
+    p.write_bytes(gzip.compress(data))
+    out["single_member"] = p
+    return out
+
+
+@pytest.mark.parametrize("mode", [{}, {"directed": False}, {"bidirected": True, "weight_tag": "RC"}])
+def test_gpu_chunked_gzip_and_default_route(gpu, oracle_lib, tmp_path, monkeypatch, mode):
+    """The one-GPU chunked build for every input kind on the HIP engine: .gz files
+    (multi-member, BGZF, one member) inflated on the host and chunked from host memory with
+    chunk_bytes; then the DEFAULT parse_gfa (no chunk_bytes, shard="never") on a plain file and a .gz
+    with the GPU's free HBM reported below the input's working set — it chunks by itself (sized from
+    the reported free memory) — and a file object; all bit-exact against the oracle's one-piece build."""
+    from gfa2network_amd import api, parse_gfa, synth
+    from gfa2network_amd.api import finalize
+
+    data = synth.host_bytes(100_000, 400_000, seed=41, rc_tag=bool(mode.get("weight_tag")))
+    full = oracle_lib.run(data, **mode)
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype("float64"), return_node_list=True,
+                         raw_bytes_id=False, verbose=False)
+
+    def check(A, nodes, what):
+        assert A.format == B.format and A.shape == B.shape and nodes == bnodes, what
+        if A.format == "coo":
+            assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col), what
+        else:
+            assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices), what
+        assert A.data.tobytes() == B.data.tobytes(), what
+
+    gz = _gz_variants(data, tmp_path)
+    for kind, p in gz.items():
+        A, nodes = parse_gfa(str(p), build_graph=False, build_matrix=True, return_node_list=True,
+                             chunk_bytes=len(data) // 4 + 1, **mode)
+        check(A, nodes, kind)
+    plain = tmp_path / "in.gfa"
+    plain.write_bytes(data)
+    calls = []
+    real = api._parse_gfa_chunked
+    monkeypatch.setattr(api, "_parse_gfa_chunked", lambda *a, **k: calls.append(a[1]) or real(*a, **k))
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0: len(data) * 2)  # the working set does not fit
+    monkeypatch.setattr(api, "_chunk_plan", lambda size, device: (len(data) // 3 + 1) if size * 8 > len(data) * 2 else 0)
+    import io
+
+    for what, src in (("plain", str(plain)), ("gz", str(gz["multi_member"])), ("fileobj", io.BytesIO(data))):
+        n = len(calls)
+        A, nodes = parse_gfa(src, build_graph=False, build_matrix=True, return_node_list=True, **mode)
+        assert len(calls) == n + 1, f"{what}: the default route did not chunk"
+        check(A, nodes, what)
+
+
+@pytest.mark.parametrize("mode", [{}, {"directed": False, "weight_tag": "RC", "dtype": "float32"}])
+def test_gpu_chunked_row_bands_and_errors(gpu, oracle_lib, tmp_path, mode):
+    """The chunked build's whole-matrix CSR in row bands on the HIP engine (g2n_route_triplets by band +
+    g2n_csr_from_coo_pair per band) equals one piece; and an error / warning in a later chunk comes out
+    as one piece raises / emits it."""
+    import warnings
+
+    from gfa2network_amd import synth
+    from gfa2network_amd.api import _dtype_of, _parse_gfa_chunked, finalize
+
+    data = synth.host_bytes(50_000, 200_000, seed=43, rc_tag=True)
+    path = tmp_path / "in.gfa"
+    path.write_bytes(data)
+    dt = mode.get("dtype", "float64")
+    kw = dict(directed=mode.get("directed", True), weight_tag=mode.get("weight_tag"), verbose=False, bidirected=False,
+              keep_directed_bidir=False, strip_orientation=False, dt=_dtype_of(dt), asymmetric=False,
+              raw_bytes_id=False, return_node_list=True, device=0)
+    full = oracle_lib.run(data, **mode)
+    B, bnodes = finalize(oracle_lib.to_raw(full, "parse"), dtype=np.dtype(dt), return_node_list=True,
+                         raw_bytes_id=False, verbose=False)
+    for bands in (3, 7):
+        A, nodes = _parse_gfa_chunked(str(path), len(data) // 4 + 1, bands=bands, **kw)
+        assert nodes == bnodes and A.format == B.format
+        if A.format == "csr":
+            assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        else:
+            assert np.array_equal(A.row, B.row) and np.array_equal(A.col, B.col)
+        assert A.data.tobytes() == B.data.tobytes()
+    cut = data.index(b"\nL\t", len(data) * 3 // 4) + 1
+    for extra, exc in ((b"W\tsample\t1\tchr1\t0\t10\t>s1\n", None), (b"L\tbroken\n", ValueError)):
+        bad = data[:cut] + extra + data[cut:]
+        path.write_bytes(bad)
+        o = oracle_lib.run(bad, **mode)
+        with warnings.catch_warnings(record=True) as w1:
+            warnings.simplefilter("always")
+            if exc:
+                with pytest.raises(exc) as e1:
+                    _parse_gfa_chunked(str(path), len(bad) // 5 + 1, **kw)
+            else:
+                A, nodes = _parse_gfa_chunked(str(path), len(bad) // 5 + 1, **kw)
+        with warnings.catch_warnings(record=True) as w2:
+            warnings.simplefilter("always")
+            if exc:
+                with pytest.raises(exc) as e2:
+                    finalize(oracle_lib.to_raw(o, "parse"), dtype=np.dtype(dt), return_node_list=True,
+                             raw_bytes_id=False, verbose=False)
+                assert str(e1.value) == str(e2.value)
+            else:
+                B2, n2 = finalize(oracle_lib.to_raw(o, "parse"), dtype=np.dtype(dt), return_node_list=True,
+                                  raw_bytes_id=False, verbose=False)
+                assert nodes == n2 and A.data.tobytes() == B2.data.tobytes()
+        assert [str(x.message) for x in w1] == [str(x.message) for x in w2]

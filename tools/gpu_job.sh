@@ -9,6 +9,7 @@
 #                           database under gpurun_out/<tag>_s<i>/
 #   pmc:<bench.py args>     tools/gpu_counters.sh passes on bench.py <args> -> gpurun_out/<tag>_pmc.json
 #   py:<script + args>      python -u <script + args>                 -> gpurun_out/<tag>_s<i>.log
+# step arguments are word-split by the shell (eval): quote inside them, e.g. "tests:f.py -k 'a or b'".
 # limits (seconds): T_TESTS (900), T_BENCH (600), T_PROF (300), T_PY (600); COMMIT tags the pmc summary.
 # example:
 #   gpurun --timeout 1200 -- 'bash tools/gpu_job.sh r5a "tests:tests/test_gpu_diff.py -k int64" "bench:--steps 5"'
@@ -25,8 +26,8 @@ for step in "$@"; do
   echo "== step $i: $kind $args"
   case $kind in
     tests)
-      timeout -k 10 ${T_TESTS:-900} python -u -X faulthandler -m pytest -m gpu -x -q --timeout 300 \
-        --timeout-method thread $args > $base.log 2>&1 || { tail -60 $base.log; exit 1; }
+      eval "timeout -k 10 ${T_TESTS:-900} python -u -X faulthandler -m pytest -m gpu -x -q --timeout 300 \
+        --timeout-method thread $args" > $base.log 2>&1 || { tail -60 $base.log; exit 1; }
       tail -2 $base.log ;;
     bench)
       timeout -k 10 ${T_BENCH:-600} python -u bench.py $args > $base.json 2> $base.err || { tail -40 $base.err; exit 1; }
