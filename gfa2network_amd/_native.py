@@ -45,7 +45,7 @@ EXPORTED = [
 # paths when a test sets them; 0 in every real use
 TEST_NO_BUCKETS = 2      # MAX-SYM through the general row-sum path
 TEST_NO_LEAN = 4         # decimal ids without the lean parse (ids per touch, then k_triplets)
-TEST_DICT_HASH = 8       # no decimal ids: the hash dictionary tiers
+TEST_DICT_HASH = 8       # no decimal ids, no direct-address tier: the hash dictionary tiers
 TEST_DICT_GENERAL = 16   # no decimal ids, no S-first fast path: the general insert rounds
 TEST_NO_TILE_LOCAL = 32  # decimal ids: the lean parse after K1's tile bases, not the tile-local pass
 TEST_HOST_INFLATE = 64   # a BGZF ".gz" read by the host gzip readers instead of the GPU inflate
@@ -53,6 +53,8 @@ TEST_NO_GROUP = 128      # tile-local parse into per-tile slots + compaction (ne
 TEST_NO_HASH_LEAN = 256  # names that are not decimal ids: the classic hash tiers, never the lean S-first one
 TEST_THROW_AFTER_IDS = 512  # the build throws (G2N_E_DEVICE) once its ids and names are set up: call-state tests
 TEST_INDEX64 = 1024      # unweighted CSR results in int64 indptr / indices (the > 2^31 - 1 entries path)
+TEST_DICT_DIRECT = 2048  # decimal ids in S order through the direct-address tier (not the decimal-id parse)
+TEST_NO_DIRECT = 4096    # never the direct-address tier: the lean hash tier instead
 TEST_FLAGS = 0
 # options.range_flags (include/g2n.h G2N_RANGE_*): set by the sharded / chunked protocol (shard.py)
 RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)

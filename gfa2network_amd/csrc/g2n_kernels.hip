@@ -1679,7 +1679,12 @@ __device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) { 
 // repeated name (or a 32-bit tag shared by two S names), an edge key that is no S name, an S line
 // after an edge line, a line outside the lean shapes — fails the pass and the classic hash tiers
 // (full parse + dictionary rounds) run instead.
-enum : int { kLeanDecimal = 0, kLeanClaim = 1, kLeanEdges = 2 };
+// Direct-address tier (modes kLeanDirClaim / kLeanDirEdges): when every S name is one common prefix
+// (possibly empty) followed by a canonical decimal v < direct_cap — decimal ids out of S order,
+// minigraph's "s<n>" — the table is a plain array: S line k claims direct[v] = k (a second claim of
+// v is a repeated name: the pass fails), and an edge name costs one random 4-byte read instead of a
+// 32-byte probe plus a key compare.  Same premise and fallbacks as the hash modes.
+enum : int { kLeanDecimal = 0, kLeanClaim = 1, kLeanEdges = 2, kLeanDirClaim = 3, kLeanDirEdges = 4 };
 #ifndef G2N_HL_LINES  // edge lines per thread per step in kLeanEdges (2, four probes in flight: 105 VGPRs, slower)
 #define G2N_HL_LINES 1
 #endif
@@ -1695,7 +1700,12 @@ struct HashLeanArgs {
   int32_t* rows;         // kLeanEdges: stream-order COO, ktrip entries per edge line
   int32_t* cols;
   uint32_t ktrip;
+  uint32_t* direct;      // kLeanDir*: name value -> node id (~0u: no S line names it)
+  uint64_t direct_cap;   //            values below this
+  uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
+  uint32_t pre_len;
 };
+
 
 // The first min(l, 16) bytes at tile offset x of the staged tile, little-endian, zero padded
 // (aligned 8-byte LDS reads; never past x + l rounded up to 8)
@@ -1716,6 +1726,16 @@ __device__ inline bool tail_eq_in(const uint8_t* __restrict__ in, uint64_t a, ui
   for (uint32_t j = 16; j < len; j++)
     if (in[a + j] != in[b + j]) return false;
   return true;
+}
+
+// the value of the name at tile offset x (length l) when it is H.pre followed by a canonical
+// decimal (no sign, no leading zero, <= 10 digits) below H.direct_cap
+__device__ inline bool lean_direct_value(const uint8_t* buf, const HashLeanArgs& H, uint32_t x, uint32_t l,
+                                         uint64_t& v) {
+  const uint32_t p = H.pre_len;
+  if (l <= p) return false;
+  if (p && (uint64_t)lds_span16(buf, x, p) != H.pre) return false;
+  return dec_lds(buf, x + p, l - p, &v) && v < H.direct_cap;
 }
 
 // S line at tile offset so (its '\n' at next - 1): the name's tile offset and length (fields[1],
@@ -1958,6 +1978,35 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       if (mm) return 16 * c + (uint32_t)__builtin_ctz(mm) + 1;
       return lim == len - t0 ? lim + 1 : 0u;
     };
+    if constexpr (kMode == kLeanDirEdges) {
+#pragma unroll 1
+      for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
+        const uint32_t x = rec[j];
+        if (((x >> 15) & 3u) != 2u) continue;
+        const uint32_t o = x & 0x7FFFu;
+        const uint32_t next = line_next(j, o);
+        uint32_t xa, la, xb, lb;
+        uint64_t va, vb;
+        if (!next || !lean_edge_names(buf, tabm, o, next, xa, la, xb, lb) || !lean_direct_value(buf, H, xa, la, va) ||
+            !lean_direct_value(buf, H, xb, lb, vb)) {
+          is.fail = 1;
+          continue;
+        }
+        const uint32_t ida = H.direct[va], idb = H.direct[vb];  // both random reads in flight
+        if (ida == ~0u || idb == ~0u) {  // a key no S line defined: a new node (not S-first)
+          is.fail = 1;
+          continue;
+        }
+        const uint64_t eb = (ebase + (x >> 17)) * H.ktrip;
+        H.rows[eb] = (int32_t)ida;
+        H.cols[eb] = (int32_t)idb;
+        if (H.ktrip >= 2) {
+          H.rows[eb + 1] = (int32_t)idb;
+          H.cols[eb + 1] = (int32_t)ida;
+        }
+      }
+      continue;  // next window
+    }
     if constexpr (kMode == kLeanEdges) {
       // kHL lines per thread per step: their names' first probes are all in flight at once
       constexpr int kHL = G2N_HL_LINES;
@@ -2130,7 +2179,24 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
         if (__popcll((w >> sh) & ((1ull << (n > 48 ? 48 : n)) - 1)) < 2) is.fail = 1;  // the full parse decides
         continue;
       }
-      if constexpr (kMode == kLeanClaim) {  // S line: claim its name for node id (S lines before) + pref
+      if constexpr (kMode == kLeanDirClaim) {  // S line: direct[its value] = node id (S lines before) + pref
+        if (code != 1) continue;
+        uint32_t x, l;
+        uint64_t v;
+        if (!lean_s_name(buf, tabm, o, next, x, l) || !lean_direct_value(buf, H, x, l, v)) {
+          is.fail = 1;
+          continue;
+        }
+        const uint32_t id = (uint32_t)(sbase + pref);
+        if (atomicCAS(H.direct + v, ~0u, id) != ~0u) {  // a repeated S name: the classic tiers decide
+          is.fail = 1;
+          continue;
+        }
+        H.noff[id] = t0 + x;
+        H.nlen[id] = l;
+        claimed_bytes += l;
+        continue;
+      } else if constexpr (kMode == kLeanClaim) {  // S line: claim its name for node id (S lines before) + pref
         if (code != 1) continue;
         uint32_t x, l;
         if (!lean_s_name(buf, tabm, o, next, x, l)) {
@@ -2179,7 +2245,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   K2_LEAN_STAMP(5);
   if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
     if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
-    if constexpr (kMode == kLeanClaim) {
+    if constexpr (kMode == kLeanClaim || kMode == kLeanDirClaim) {
       unsigned long long nb = claimed_bytes;
       for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
       if ((threadIdx.x & 63) == 0 && nb) atomicAdd(&ctl->names_len, nb);
@@ -2258,14 +2324,17 @@ __global__ void G2N_LEAN_ATTR
     k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl, TileCnt* __restrict__ tcnt_out,
                 TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount, uint64_t gcap, HashLeanArgs H) {
   const uint64_t tile = blockIdx.x;
-  if constexpr (kMode == kLeanClaim) {  // tiles with S or P / O lines (block-uniform)
+  if constexpr (kMode != kLeanDecimal) {  // a pass that already failed elsewhere: the rest is wasted work
+    if (*(volatile const unsigned long long*)&ctl->int_fail) return;
+  }
+  if constexpr (kMode == kLeanClaim || kMode == kLeanDirClaim) {  // tiles with S or P / O lines (block-uniform)
     const TileCnt c = H.tcnt[tile];
     if (c.segs == 0 && c.recs == c.segs + c.edges) return;
     if (c.segs && H.tbase[tile].edges) {  // an edge line before this tile's S lines
       if (threadIdx.x == 0) ctl->int_fail = 1;
       return;
     }
-  } else if constexpr (kMode == kLeanEdges) {  // tiles with edge lines
+  } else if constexpr (kMode == kLeanEdges || kMode == kLeanDirEdges) {  // tiles with edge lines
     if (H.tcnt[tile].edges == 0) return;
   }
   LeanRegs R;

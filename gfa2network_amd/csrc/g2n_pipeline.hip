@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_NSLOTS
 };
 
 #ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
@@ -73,6 +73,8 @@ constexpr uint32_t kTestNoGroup = G2N_TEST_NO_GROUP;
 constexpr uint32_t kTestNoHashLean = G2N_TEST_NO_HASH_LEAN;
 constexpr uint32_t kTestThrowAfterIds = G2N_TEST_THROW_AFTER_IDS;
 constexpr uint32_t kTestIndex64 = G2N_TEST_INDEX64;
+constexpr uint32_t kTestDictDirect = G2N_TEST_DICT_DIRECT;
+constexpr uint32_t kTestNoDirect = G2N_TEST_NO_DIRECT;
 
 
 struct DevBuf {
@@ -1059,6 +1061,39 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
   return true;  // no S line seen yet (long header lines): try
 }
 
+// The first S line's name (in the first 64 KiB) as the direct-address tier's premise: a common prefix
+// of at most 8 non-digit bytes, then a canonical decimal of at most 10 digits.  False otherwise (the
+// hash tiers decide); every other name is checked by the passes themselves.
+static bool first_segment_prefix(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t* pre, uint32_t* pre_len) {
+  const size_t n = (size_t)std::min<uint64_t>(len, 1 << 16);
+  if (n == 0) return false;
+  std::vector<uint8_t> h(n);
+  G2N_HIP(hipMemcpyAsync(h.data(), in, n, hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  for (size_t p = 0; p + 2 < n;) {
+    if (h[p] == 'S' && h[p + 1] == '\t') {
+      size_t e = p + 2;
+      while (e < n && h[e] != '\t' && h[e] != '\n') e++;
+      if (e == n) return false;
+      size_t d = p + 2;
+      while (d < e && (h[d] < '0' || h[d] > '9')) d++;
+      const size_t pl = d - (p + 2), nd = e - d;
+      if (pl > 8 || nd == 0 || nd > 10 || h[d] == '0') return false;
+      for (size_t k = d; k < e; k++)
+        if (h[k] < '0' || h[k] > '9') return false;
+      uint64_t w = 0;
+      for (size_t k = 0; k < pl; k++) w |= (uint64_t)h[p + 2 + k] << (8 * k);
+      *pre = w;
+      *pre_len = (uint32_t)pl;
+      return true;
+    }
+    const void* q = std::memchr(h.data() + p, '\n', n - p);
+    if (!q) break;
+    p = (size_t)((const uint8_t*)q - h.data()) + 1;
+  }
+  return false;
+}
+
 // The lean decimal-id parse in one pass over the input, without K1: every tile parses with
 // tile-local positions, writes its COO to a slot of kTileEdgeCap edges and its own counts
 // (k_tile_parse with ParseOpts.tile_pad); one scan of those counts gives the tile bases, a check
@@ -1256,6 +1291,55 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
   return true;
 }
 
+// The direct-address tier on the lean front end (k_tile_lean kLeanDirClaim / kLeanDirEdges, after K1):
+// S names that are one prefix + a canonical decimal v < cap claim direct[v] = S index, then every edge
+// line's names are found with one 4-byte read each and the stream-order COO written.  cap = 4 x the S
+// lines (at least 64 Ki, at most 2^28 values: 1 GiB): ids "1".."N" out of order, or with gaps, fit.
+// False (and a clean slate) when any name breaks the shape, a value repeats or passes cap, or the
+// input is not S-first: the lean hash tier runs next.
+static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
+                              const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
+                              uint64_t pre, uint32_t pre_len, uint64_t** noff_out, uint32_t** nlen_out,
+                              uint64_t* names_len) {
+  if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
+  const uint64_t cap = std::min<uint64_t>(1ull << 28, std::max<uint64_t>(4 * n_s, 1ull << 16));
+  auto* direct = dget<uint32_t>(c, S_DIRECT, cap);
+  G2N_HIP(hipMemsetAsync(direct, 0xFF, cap * sizeof(uint32_t), c->stream));
+  auto* noff = dget<uint64_t>(c, S_NOFF, n_s);
+  auto* nlen = dget<uint32_t>(c, S_NLEN, n_s);
+  HashLeanArgs H{tbase, tcnt, nullptr, 0, 0, noff, nlen, rows, cols, ktrip};
+  H.direct = direct;
+  H.direct_cap = cap;
+  H.pre = pre;
+  H.pre_len = pre_len;
+  phase(c, "table_init");
+#ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
+  unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
+  G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_k2_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
+                                 c->stream));
+#endif
+  hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                     len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  phase(c, "direct_claim");
+  sync_ctl(c);
+  if (c->h_ctl->int_fail) {
+    reset_ctl(c);
+    return false;
+  }
+  *names_len = c->h_ctl->names_len;
+  hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                     len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  phase(c, "direct_lookup");
+  sync_ctl(c);
+  if (c->h_ctl->int_fail) {
+    reset_ctl(c);
+    return false;
+  }
+  *noff_out = noff;
+  *nlen_out = nlen;
+  return true;
+}
+
 static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
   fill_defaults(R);
   clear_call_state(c);
@@ -1286,7 +1370,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   c->range_vmax = 0;
   c->range_nseg = 0;
   const bool first_one =
-      !shard_dec && !(c->test_flags & (kTestDictHash | kTestDictGeneral)) && first_segment_is_one(c, in, len);
+      !shard_dec && !(c->test_flags & (kTestDictHash | kTestDictGeneral | kTestDictDirect)) &&
+      first_segment_is_one(c, in, len);
   // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
   // group slots when the COO's only reader is the unweighted bucket partition (a CSR output)
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
@@ -1392,10 +1477,18 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   uint64_t* hl_noff = nullptr;
   uint32_t* hl_nlen = nullptr;
   uint64_t hl_names_len = 0;
-  const bool hash_done = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
-                         !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s &&
-                         hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, &hl_noff,
-                                         &hl_nlen, &hl_names_len);
+  const bool lean_hash_ok = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
+                            !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s;
+  // decimal names out of S order (or behind one prefix): the direct-address tier first
+  uint64_t pre = 0;
+  uint32_t pre_len = 0;
+  const bool direct_done = lean_hash_ok && !(c->test_flags & (kTestDictHash | kTestNoDirect)) &&
+                           first_segment_prefix(c, in, len, &pre, &pre_len) &&
+                           direct_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, pre,
+                                             pre_len, &hl_noff, &hl_nlen, &hl_names_len);
+  const bool hash_done = direct_done || (lean_hash_ok && hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s,
+                                                                          (uint32_t)ktrip, rows, cols, &hl_noff,
+                                                                          &hl_nlen, &hl_names_len));
   bool lean_done = local_done || hash_done;  // rows / cols hold the stream-order COO already
   if (lean && !local_done) {
     ParseOpts lo = op;

@@ -33,6 +33,7 @@ static SynthSpec to_spec(const g2n_synth_spec* p) {
   s.rc = p->rc_tag;
   s.names = p->names;
   s.far = p->far_links;
+  s.pmul = s.names == 2 ? synth_perm_mul(s.n_s) : 1;
   return s;
 }
 

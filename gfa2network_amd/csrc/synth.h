@@ -5,7 +5,8 @@
 // produce identical bytes for the same spec:
 //   line 0:            H\tVN:Z:1.0
 //   S lines i=1..N_S:  S\t{name(i)}\t{seq}  |seq| ~ Geometric(1/8) over ACGT;
-//                      name(i) = "i", or (names = 1) "s" + 8 hex digits of a u32 bijection of i
+//                      name(i) = "i", or (names = 1) "s" + 8 hex digits of a u32 bijection of i,
+//                      or (names = 2) the decimal of a permutation of 1..N_S (affine mod N_S)
 //   L lines j:         L\t{name(src)}\t{o1}\t{name(dst)}\t{o2}\t0M[\tRC:i:{k}]
 //                      src ~ U[1,N_S], dst = min(src + Geometric(5/16), N_S) (far = 1: dst ~ U[1,N_S]),
 //                      o = '+' with probability 922/1024, k ~ U[1,99]
@@ -24,9 +25,33 @@ namespace g2n {
 struct SynthSpec {
   uint64_t n_s, n_l, seed;
   int32_t rc;
-  int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32)
+  int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32); 2: permuted decimal
   int32_t far;    // 1: dst ~ U[1, N_S] instead of src + Geometric(5/16)
+  uint64_t pmul;  // names = 2: multiplier coprime to n_s (synth_perm_mul)
 };
+
+G2N_HD inline uint64_t synth_gcd(uint64_t a, uint64_t b) {
+  while (b) {
+    const uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// names = 2: segment i is named perm(i) = ((i - 1) * pmul + n_s / 2) mod n_s + 1, a bijection of 1..n_s
+// (pmul coprime to n_s): decimal names "1".."N" in a shuffled order, perm(1) != 1 for n_s > 1
+inline uint64_t synth_perm_mul(uint64_t n) {
+  if (n < 2) return 1;
+  uint64_t a = 2654435761ull % n;
+  if (a < 2) a = 2;
+  while (synth_gcd(a, n) != 1) a++;
+  return a;
+}
+
+G2N_HD inline uint64_t synth_perm(const struct SynthSpec& s, uint64_t i) {
+  return (uint64_t)(((unsigned __int128)(i - 1) * s.pmul + (s.n_s >> 1)) % s.n_s) + 1;
+}
 
 G2N_HD inline uint64_t smix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -117,10 +142,13 @@ G2N_HD inline uint32_t synth_name_mix(uint32_t x) {
   return x;
 }
 
-G2N_HD inline uint32_t synth_name_len(const SynthSpec& s, uint64_t i) { return s.names ? 9u : synth_digits(i); }
+G2N_HD inline uint32_t synth_name_len(const SynthSpec& s, uint64_t i) {
+  return s.names == 1 ? 9u : synth_digits(s.names == 2 ? synth_perm(s, i) : i);
+}
 
 G2N_HD inline char* synth_put_name(const SynthSpec& s, char* o, uint64_t i) {
   if (!s.names) return synth_put_u64(o, i);
+  if (s.names == 2) return synth_put_u64(o, synth_perm(s, i));
   const uint32_t h = synth_name_mix((uint32_t)i);
   *o++ = 's';
   for (int k = 7; k >= 0; k--) {

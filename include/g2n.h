@@ -121,14 +121,16 @@ enum {
 enum {
   G2N_TEST_NO_BUCKETS = 2,      /* MAX-SYM / SUM CSR through the general row sums */
   G2N_TEST_NO_LEAN = 4,         /* decimal ids without the lean parse */
-  G2N_TEST_DICT_HASH = 8,       /* hash dictionary (no decimal ids) */
+  G2N_TEST_DICT_HASH = 8,       /* hash dictionary (no decimal ids, no direct-address tier) */
   G2N_TEST_DICT_GENERAL = 16,   /* general dictionary rounds */
   G2N_TEST_NO_TILE_LOCAL = 32,  /* decimal ids parsed after K1 (not the tile-local pass) */
   G2N_TEST_HOST_INFLATE = 64,   /* a BGZF .gz read by the host readers (not inflated on the GPU) */
   G2N_TEST_NO_GROUP = 128,      /* tile-local parse into per-tile slots + compaction */
   G2N_TEST_NO_HASH_LEAN = 256,  /* the classic hash tiers, never the lean S-first one */
   G2N_TEST_THROW_AFTER_IDS = 512, /* the build fails (G2N_E_DEVICE) once its ids are set up */
-  G2N_TEST_INDEX64 = 1024       /* CSR results in int64 indptr / indices (the > 2^31 - 1 entries path) */
+  G2N_TEST_INDEX64 = 1024,      /* CSR results in int64 indptr / indices (the > 2^31 - 1 entries path) */
+  G2N_TEST_DICT_DIRECT = 2048,  /* decimal ids in S order through the direct-address tier */
+  G2N_TEST_NO_DIRECT = 4096     /* never the direct-address tier (the lean hash tier instead) */
 };
 
 #define G2N_MAX_PHASES 40

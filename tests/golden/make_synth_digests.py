@@ -25,10 +25,12 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 OUT = ROOT / "tests" / "golden" / "expected" / "synth_digests.json"
 
-CASES = {  # name -> (n_segments, n_links, rc_tag, seed, mode)
+CASES = {  # name -> (n_segments, n_links, rc_tag, seed, mode[, segment names])
     "C2": (1_000_000, 4_000_000, False, 0, {"directed": False}),
     "C3": (1_000_000, 4_000_000, True, 0, {"bidirected": True, "weight_tag": "RC"}),
     "C4": (50_000_000, 200_000_000, False, 0, {}),
+    # C4's dimensions with the decimal names permuted (synth names="permuted"): the direct-address tier
+    "C4P": (50_000_000, 200_000_000, False, 0, {}, "permuted"),
 }
 
 
@@ -45,12 +47,14 @@ def main(names):
 
     doc = json.loads(OUT.read_text()) if OUT.exists() else {}
     for name in names:
-        n_s, n_l, rc, seed, mode = CASES[name]
+        n_s, n_l, rc, seed, mode = CASES[name][:5]
+        names_mode = CASES[name][5] if len(CASES[name]) > 5 else "decimal"
         t0 = time.time()
-        data = synth.host_bytes(n_s, n_l, seed=seed, rc_tag=rc)
+        data = synth.host_bytes(n_s, n_l, seed=seed, rc_tag=rc, names=names_mode)
         o = oracle.run(data, **mode)
         assert o.status == 0, o.status
         ent = {"n_segments": n_s, "n_links": n_l, "rc_tag": rc, "seed": seed, "mode": mode, "dtype": "float64",
+               "segment_names": names_mode,
                "input_bytes": len(data), "n_nodes": int(o.n_nodes),
                "names": digest(o.names_blob), "names_bytes": int(o.names_offsets[-1])}
         if o.maxsym:

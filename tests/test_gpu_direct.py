@@ -1,0 +1,133 @@
+"""The direct-address dictionary tier on the lean front end (k_tile_lean kLeanDirClaim /
+kLeanDirEdges): inputs whose S lines come first and whose segment names are one common prefix
+(possibly empty) followed by a canonical decimal — decimal ids out of S order, minigraph's "s<n>" —
+take a plain array as the dictionary (S line k claims direct[v] = k; an edge name is one random
+4-byte read).  builders.py:190-198: with every S line first and no repeated name, a key's first
+touch is its S line, so node id = S index.  Every case is compared with the oracle, with the lean
+hash tier (TEST_NO_DIRECT) and with the classic tiers (TEST_NO_HASH_LEAN); cases that break the
+premise (a repeated value, a value past the table, another prefix, leading zeros, "0", 11 digits,
+an edge key no S line names, an S line after an edge line, unsupported or malformed records) must
+fall back and still match.
+"""
+import random
+
+import pytest
+
+from test_gpu_diff import gpu_run, oracle_run, outcome
+
+pytestmark = pytest.mark.gpu
+
+MODES = [{}, {"directed": False}, {"asymmetric": True}]
+
+
+def _gfa(seed, n_s, n_l, prefix="", spread=1, ov="0M"):
+    r = random.Random(seed)
+    vals = r.sample(range(1, spread * n_s + 1), n_s)  # distinct values, out of S order
+    names = [f"{prefix}{v}" for v in vals]
+    lines = [f"S\t{k}\t{'ACGT' * r.randint(0, 3)}\n" for k in names]
+    for _ in range(n_l):
+        a = r.randrange(n_s)
+        b = min(n_s - 1, a + r.randint(0, 5))
+        lines.append(f"L\t{names[a]}\t{r.choice('+-')}\t{names[b]}\t{r.choice('+-')}\t{ov}\n")
+    return names, lines
+
+
+def _case(name):
+    names, L = _gfa(21, 6000, 30000)
+    n = 6000
+    if name == "permuted":
+        return L, True
+    if name == "prefix_s":
+        return _gfa(22, 6000, 30000, prefix="s")[1], True
+    if name == "prefix_8_bytes_gaps":  # values up to 3 x the S lines: inside the 4 x table
+        return _gfa(23, 6000, 30000, prefix="node_id_", spread=3)[1], True
+    if name == "ten_digit_values":
+        _, L2 = _gfa(24, 3000, 12000)
+        return [ln.replace("S\t", "S\t10000", 1) if ln.startswith("S") else
+                ln.replace("L\t", "L\t10000", 1).replace("\t+\t", "\t+\t10000", 1).replace("\t-\t", "\t-\t10000", 1)
+                for ln in L2], False  # (values past the table: the hash tiers)
+    if name == "p_and_header_lines":
+        return ["H\tVN:Z:1.0\n"] + L[:n] + ["P\tp1\t" + names[0] + "+," + names[1] + "-\t*\n"] + L[n:], True
+    if name == "repeated_value":
+        return L[:n] + ["S\t" + names[77] + "\tAC\n"] + L[n:], False
+    if name == "other_prefix":
+        return L[:50] + ["S\tx5000000\t*\n"] + L[50:], False
+    if name == "leading_zero":
+        return L[:50] + ["S\t0777777\t*\n"] + L[50:], False
+    if name == "zero":
+        return L[:50] + ["S\t0\t*\n"] + L[50:], False
+    if name == "eleven_digits":
+        return L[:50] + ["S\t12345678901\t*\n"] + L[50:], False
+    if name == "value_past_table":
+        return L[:50] + ["S\t99999999\t*\n"] + L[50:], False
+    if name == "s_after_edges":
+        return L[:100] + L[n:n + 100] + L[100:n] + L[n + 100:], False
+    if name == "edge_to_undefined_value":
+        return L[:7000] + ["L\t999999\t+\t" + names[3] + "\t-\t0M\n"] + L[7000:], False
+    if name == "edge_to_non_decimal":
+        return L[:7000] + ["L\tnobody\t+\t" + names[3] + "\t-\t0M\n"] + L[7000:], False
+    if name == "unsupported_record":
+        return L[:7000] + ["W\tsample\t1\tchr1\t0\t10\t>x\n"] + L[7000:], False
+    if name == "malformed_link":
+        return L[:7000] + ["L\t" + names[1] + "\t+\n"] + L[7000:], False
+    raise KeyError(name)
+
+
+CASES = ["permuted", "prefix_s", "prefix_8_bytes_gaps", "ten_digit_values", "p_and_header_lines", "repeated_value",
+         "other_prefix", "leading_zero", "zero", "eleven_digits", "value_past_table", "s_after_edges",
+         "edge_to_undefined_value", "edge_to_non_decimal", "unsupported_record", "malformed_link"]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_direct_tier_equals_oracle_and_other_tiers(gpu, oracle_lib, monkeypatch, case):
+    from gfa2network_amd import _native as nat
+
+    lines, eligible = _case(case)
+    data = "".join(lines).encode()
+    for mode in MODES:
+        raw = nat.build_from_buffer(data, nat.make_options(**mode))
+        ph = raw.phase_ms
+        took = "direct_lookup" in ph and "insert_lookup" not in ph and "parse" not in ph
+        if raw.status == 0:
+            assert took == eligible, (case, mode, sorted(ph))
+        for dtype in ("float64", "int8", "bool"):
+            a = outcome(gpu_run(data, mode, dtype, None))
+            assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, None)), (case, mode, dtype)
+            for flags, what in ((nat.TEST_NO_DIRECT, "lean hash"), (nat.TEST_NO_HASH_LEAN, "classic")):
+                monkeypatch.setattr(nat, "TEST_FLAGS", flags)
+                assert a == outcome(gpu_run(data, mode, dtype, None)), (case, mode, dtype, what)
+                monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+
+
+def test_direct_tier_on_ids_in_order(gpu, oracle_lib, monkeypatch):
+    """TEST_DICT_DIRECT: decimal ids "1".."N" in S order through the direct tier instead of the
+    decimal-id parse — same answer, every mode family."""
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(30_000, 120_000, seed=8)
+    for mode in MODES:
+        want = outcome(gpu_run(data, mode, "float64", None))
+        monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_DICT_DIRECT)
+        raw = nat.build_from_buffer(data, nat.make_options(**mode))
+        assert "direct_lookup" in raw.phase_ms, sorted(raw.phase_ms)
+        assert outcome(gpu_run(data, mode, "float64", None)) == want, mode
+        monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+        assert want == outcome(oracle_run(oracle_lib, data, mode, "float64", None)), mode
+
+
+def test_direct_tier_synthetic_large_equals_lean_hash(gpu, monkeypatch):
+    """10^7 edges of the generator with permuted decimal names (names="permuted"): the direct tier
+    against the lean hash tier, bit for bit, CSR and COO outputs, names included."""
+    from gfa2network_amd import _native as nat
+    from gfa2network_amd import synth
+
+    data = synth.host_bytes(2_000_000, 8_000_000, seed=5, names="permuted")
+    for mode in ({}, {"directed": False}):
+        raw = nat.build_from_buffer(data, nat.make_options(**mode))
+        assert raw.status == 0 and "direct_lookup" in raw.phase_ms and "parse" not in raw.phase_ms, sorted(raw.phase_ms)
+        a = outcome(gpu_run(data, mode, "float64", None))
+        monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_DIRECT)
+        b = outcome(gpu_run(data, mode, "float64", None))
+        monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+        assert a == b, mode
