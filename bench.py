@@ -52,9 +52,10 @@ def _args():
                     help="skip the end-to-end leg (file on the page cache -> scipy CSR + node list in host memory)")
     ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
     ap.add_argument("--no-alt", action="store_true", help="skip the hash-dictionary comparison build")
-    ap.add_argument("--names", default="decimal", choices=["decimal", "hashed"],
-                    help="segment names of the synthetic file: decimal ids 1..N (the configs' layout) or hashed "
-                         "(unique non-decimal names: the hash dictionary / the general sharded protocol)")
+    ap.add_argument("--names", default="decimal", choices=["decimal", "hashed", "permuted"],
+                    help="segment names of the synthetic file: decimal ids 1..N (the configs' layout), hashed "
+                         "(unique non-decimal names: the hash dictionary / the general sharded protocol) or permuted "
+                         "(decimal names out of S order: the direct-address dictionary)")
     ap.add_argument("--force-protocol", action="store_true",
                     help="sharded runs: the general owner protocol even where the decimal fast path (or, on one "
                          "rank, no exchange at all) applies — to time the protocol itself")
@@ -701,6 +702,32 @@ def main():
         t_h = time.perf_counter()
         hash_ph = step(hopts)
         t_h = time.perf_counter() - t_h
+    # decimal names out of S order (a permutation of 1..N): the direct-address dictionary tier
+    if not args.no_alt and args.names == "decimal":
+        perm = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local, names="permuted")
+        try:
+            pph = []
+            for i in range(1 + max(2, min(args.steps, 5))):
+                t_p = time.perf_counter()
+                rc = lib.g2n_build_device(ctx, perm.ptr, perm.len, ctypes.byref(opts), ctypes.byref(res))
+                t_p = time.perf_counter() - t_p
+                if rc != 0:
+                    raise RuntimeError(f"{nat.status_name(rc)}: {nat.last_error()}")
+                if i:
+                    pph.append(({res.phase_names[k].decode(): res.phase_ms[k] for k in range(res.n_phases)
+                                 if not res.phase_names[k].decode().startswith("_")}, t_p))
+            p_avg = {k: sum(p[0].get(k, 0.0) for p in pph) / len(pph) for k in pph[0][0]}
+            p_ms = sum(p[1] for p in pph) / len(pph) * 1e3
+            line_alt_perm = {
+                "ms_per_step": round(p_ms, 3), "m_edges_per_s": round(int(res.n_edges) / (p_ms / 1e3) / 1e6, 2),
+                "device_ms_per_step": round(sum(p_avg.values()), 3), "input_bytes": perm.len, "nnz": int(res.nnz),
+                "phase_ms": {k: round(v, 3) for k, v in p_avg.items()},
+                "note": "same dimensions and flags, segment names a permutation of 1..N (synth names='permuted'): the "
+                        "direct-address dictionary (S lines claim direct[v], each edge name one 4-byte read)"}
+        finally:
+            perm.free()
+    else:
+        line_alt_perm = None
     # export --format edge-list on the same input (the text rendered in HBM)
     t_x, x_ph, x_bytes = None, None, 0
     if not args.no_alt:
@@ -767,6 +794,8 @@ def main():
             "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
             "note": "options.test_flags = G2N_TEST_DICT_HASH: segment names resolved through the GPU hash table (inputs whose S lines "
                     "are not named 1..N in order)"}}
+    if line_alt_perm is not None:
+        line.setdefault("alt_paths", {})["permuted_names"] = line_alt_perm
     if t_x is not None:
         xt = x_ph.get("edge_text", 0.0)
         line.setdefault("alt_paths", {})["export_edge_list"] = {
@@ -844,8 +873,10 @@ class _DevBytes:
 KERNEL_OF_PHASE = {  # phases that time exactly one kernel launch per build
     "tiles": "g2n::k_tile_count",
     "parse": "g2n::k_tile_lean<0, true>",  # the tile-local lean parse (decimal ids, no K1, group slots)
-    "insert_claim": "g2n::k_insert_round<0>",
-    "insert_lookup": "g2n::k_lookup_fast<2>",
+    "insert_claim": "g2n::k_tile_lean<1, false>",  # the lean S-first hash tier (claim / edge passes)
+    "insert_lookup": "g2n::k_tile_lean<2, false>",
+    "direct_claim": "g2n::k_tile_lean<3, false>",  # the direct-address tier
+    "direct_lookup": "g2n::k_tile_lean<4, false>",
     "triplets": "g2n::k_triplets<double>",
 }
 
@@ -874,6 +905,11 @@ def kernel_bytes(phase, *, n_lines, n_edges, n_nodes, in_bytes, names_bytes, bid
         k = n_s * tps if phase == "insert_claim" else n_edges * tpe
         per = 1 + 12 + d_o + avg_key + 32 + 4  # state, descriptor, key bytes, 32-B entry, slot / node id
         return (int(n_t * 1 + k * (per - 1)), f"1 B/touch + {per - 1:.1f} B per processed touch ({k} touches)")
+    if phase == "direct_lookup":  # the edge lines' bytes, two 4-byte id reads and the COO per edge
+        per = 8 + 4 * k_trip * 2
+        return in_bytes + per * n_edges, f"B_in + {per} B/edge (direct-address edge pass)"
+    if phase == "direct_claim":  # the S lines' bytes, one 4-byte claim + the name's offset / length per S line
+        return in_bytes + 16 * n_s, "B_in + 16 B/S line (direct-address claim pass)"
     if phase == "triplets":
         per = 4 + 8 + tpe * 4 + k_trip * (4 + 4 + w_dtype)  # tb, w, node id per touch, COO out
         return n_edges * per, f"{per} B/edge"

@@ -50,11 +50,14 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_NSLOTS
 };
 
 #ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
 #define G2N_FORK_EARLY 0
+#endif
+#ifndef G2N_F2_OVERLAP  // bucket finish: F1 / F2 in this many bucket ranges, F2 of one beside F1 of the next (1: off)
+#define G2N_F2_OVERLAP 1
 #endif
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
 #define G2N_FIN_DIRECT 0
@@ -107,6 +110,8 @@ struct g2n_context {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
   hipEvent_t side_ev[2] = {nullptr, nullptr};  // main -> side fork, side -> main join
+  hipStream_t place = nullptr;  // F2 (k_sym_place) of earlier bucket ranges beside F1 of later ones
+  hipEvent_t ov_ev[17] = {};    // F1 range k done (main -> place); [16]: place -> main join
   bool side_pending = false;    // the main stream has not joined the side stream's last work yet
   uint64_t lean_blocks = 0;     // k_tile_lean_p blocks resident on the device at once (its grid)
   bool range_has_s = false;     // g2n_build_decimal_range: the range's evidence (k_tile_lean_evidence)
@@ -205,12 +210,14 @@ static T read_dev(g2n_context* c, const T* p) {
 
 // exclusive scan of n items (k_scan_excl, decoupled look-back); *total (device, optional) = sum
 template <class TIn, class TOut>
-static void scan_excl(g2n_context* c, const TIn* in, TOut* out, uint64_t n, TOut* total = nullptr) {
+static void scan_excl(g2n_context* c, const TIn* in, TOut* out, uint64_t n, TOut* total = nullptr,
+                      hipStream_t s = nullptr, int slot = S_SCANST) {
   if (n == 0 && !total) return;
+  if (!s) s = c->stream;
   const uint64_t tiles = scan_tiles(n);
-  auto* st = dget<unsigned long long>(c, S_SCANST, tiles + 1);  // status words + the ticket
-  G2N_HIP(hipMemsetAsync(st, 0, (tiles + 1) * sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL((k_scan_excl<TIn, TOut>), dim3((unsigned)tiles), dim3(256), 0, c->stream, in, out, n, st,
+  auto* st = dget<unsigned long long>(c, slot, tiles + 1);  // status words + the ticket
+  G2N_HIP(hipMemsetAsync(st, 0, (tiles + 1) * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL((k_scan_excl<TIn, TOut>), dim3((unsigned)tiles), dim3(256), 0, s, in, out, n, st,
                      (uint32_t*)(st + tiles), total);
 }
 template <class T>
@@ -518,11 +525,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA);
+                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA, 0u);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, true>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl, lbst,
-                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA);
+                       indices, odata, (uint32_t)row_base, wa, (const uint32_t*)bstA, 0u);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -537,16 +544,70 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
 #else
+  // F1 / F2 overlapped by bucket ranges: F1 of range k + 1 on the main stream runs beside the scan and
+  // F2 of range k on the place stream (F1 is latency-bound, F2 a copy that F1 leaves bandwidth for);
+  // F2 adds the entries of the ranges before its own to the range-relative offsets
+  const uint32_t n_ov = (G2N_F2_OVERLAP > 1 && n_el <= 0x7FFFFFFFull && !(c->test_flags & kTestIndex64) &&
+                         n_bk >= 64ull * G2N_F2_OVERLAP)
+                            ? (uint32_t)std::min(G2N_F2_OVERLAP, 16)
+                            : 1u;
+  if (n_ov > 1) {
+    auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
+    auto* rtot = dget<uint32_t>(c, S_RTOT, n_ov);
+    uint64_t st_words = 0;  // every range's scan status words + ticket, allocated once (no realloc mid-way)
+    for (uint32_t k = 0; k < n_ov; k++) st_words += scan_tiles(n_bk * (k + 1) / n_ov - n_bk * k / n_ov) + 1;
+    auto* st = dget<unsigned long long>(c, S_SCANST2, st_words);
+    for (uint32_t k = 0; k < n_ov; k++) {
+      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov;
+      if (sum)
+        hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->stream, el,
+                           (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
+                           (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
+                           (const uint32_t*)bstA, (uint32_t)b0);
+      else
+        hipLaunchKernelGGL((k_sym_finish<T, false, false>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->stream,
+                           el, (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
+                           (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
+                           (const uint32_t*)bstA, (uint32_t)b0);
+      G2N_HIP(hipEventRecord(c->ov_ev[k], c->stream));
+    }
+    unsigned long long* stk = st;
+    for (uint32_t k = 0; k < n_ov; k++) {
+      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov, tiles = scan_tiles(b1 - b0);
+      G2N_HIP(hipStreamWaitEvent(c->place, c->ov_ev[k], 0));
+      G2N_HIP(hipMemsetAsync(stk, 0, (tiles + 1) * sizeof(unsigned long long), c->place));
+      hipLaunchKernelGGL((k_scan_excl<uint32_t, uint32_t>), dim3((unsigned)tiles), dim3(256), 0, c->place,
+                         (const uint32_t*)(btot + b0), boff + b0, b1 - b0, stk, (uint32_t*)(stk + tiles), rtot + k);
+      hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->place,
+                         (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows,
+                         (T)1, (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr,
+                         (const uint32_t*)bstA, (uint32_t)b0, (const uint32_t*)rtot, k);
+      stk += tiles + 1;
+    }
+    G2N_HIP(hipEventRecord(c->ov_ev[16], c->place));
+    G2N_HIP(hipStreamWaitEvent(c->stream, c->ov_ev[16], 0));
+    sync_ctl(c);
+    if (c->h_ctl->bucket_overflow) return false;
+    R->format = G2N_FMT_CSR;
+    R->indptr = indptr;
+    R->nnz = (int64_t)read_dev(c, indptr + n_rows);
+    R->indices = indices;
+    R->data = odata;
+    R->sum_sorted = -1;
+    R->sum_t_sorted = -1;
+    phase(c, sum ? "csr" : "maxsym");
+    return true;
+  }
   if (sum)
     hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
                        (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
-                       (const uint32_t*)bstA);
+                       (const uint32_t*)bstA, 0u);
   else
     hipLaunchKernelGGL((k_sym_finish<T, false, false>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el,
                        (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
                        (uint64_t*)nullptr, (int32_t*)nullptr, (T*)nullptr, (uint32_t)row_base, wa,
-                       (const uint32_t*)bstA);
+                       (const uint32_t*)bstA, 0u);
 #ifdef G2N_F1_STAMPS
   if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
     std::vector<unsigned long long> h(n_bk * kF1Stamps);
@@ -578,7 +639,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     hipLaunchKernelGGL((k_sym_place<T, int64_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
                        (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
                        (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices64, odata, indptr64,
-                       (const uint32_t*)bstA);
+                       (const uint32_t*)bstA, 0u, (const uint32_t*)nullptr, 0u);
     R->format = G2N_FMT_CSR;
     R->index_width = 8;
     R->indptr = indptr64;
@@ -593,7 +654,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream,
                      (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
                      (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr,
-                     (const uint32_t*)bstA);
+                     (const uint32_t*)bstA, 0u, (const uint32_t*)nullptr, 0u);
 #endif
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
@@ -1820,7 +1881,9 @@ static g2n_context* context_create(int device) {
   G2N_HIP(hipSetDevice(device));
   G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   G2N_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  G2N_HIP(hipStreamCreateWithFlags(&c->place, hipStreamNonBlocking));
   for (auto& e : c->side_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : c->ov_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   G2N_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
   if (c->n_cu <= 0) c->n_cu = 1;
   {  // the persistent decimal parse's grid: every block resident at once (LDS-limited: 3 per CU)
@@ -1844,6 +1907,7 @@ static void context_destroy(g2n_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->place) (void)hipStreamSynchronize(c->place);
   for (auto& b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   if (c->ctl) (void)hipFree(c->ctl);
@@ -1852,7 +1916,10 @@ static void context_destroy(g2n_context* c) {
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
   for (auto& e : c->side_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ov_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->place) (void)hipStreamDestroy(c->place);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

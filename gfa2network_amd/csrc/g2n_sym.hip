@@ -670,7 +670,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
                                                      int32_t* __restrict__ indptr, Ctl* ctl, uint64_t* __restrict__ lbst,
                                                      int32_t* __restrict__ indices, T* __restrict__ data,
                                                      uint32_t row_base, const uint32_t* __restrict__ wa,
-                                                     const uint32_t* __restrict__ bstA) {
+                                                     const uint32_t* __restrict__ bstA, uint32_t b0) {
   __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];    // placement cursors
@@ -683,7 +683,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   F1_STAMP(0);
   cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) mcount = 0;
-  const uint64_t b = blockIdx.x;
+  const uint64_t b = b0 + blockIdx.x;  // b0: the first bucket of this launch (F1 / F2 overlapped by ranges)
   // stored elements (a kElPair one is two entries): stream B's (8-byte elements) and stream A's (pair
   // words, bstA non-null); the bucket stages its entries at twice its offset in both streams together
   const uint32_t eB = bstart[b], nB = bstart[b + 1] - eB;
@@ -970,9 +970,14 @@ __global__ void __launch_bounds__(kFinTPB) k_sym_place(const uint32_t* __restric
                                                     T one, const uint32_t* __restrict__ tcol,
                                                     const uint16_t* __restrict__ tcn, int32_t* __restrict__ indptr,
                                                     I* __restrict__ indices, T* __restrict__ data,
-                                                    int64_t* __restrict__ indptr64, const uint32_t* __restrict__ bstA) {
-  const uint32_t b = blockIdx.x;
-  const uint32_t e0 = bstart[b] + (bstA ? bstA[b] : 0u), tot = btot[b], base = boff[b];
+                                                    int64_t* __restrict__ indptr64, const uint32_t* __restrict__ bstA,
+                                                    uint32_t b0, const uint32_t* __restrict__ rtot, uint32_t rk) {
+  // b0: the first bucket of this launch; rtot[0 .. rk): the entries of the bucket ranges before it
+  // (boff then holds offsets relative to the range: F1 / F2 overlapped by ranges), or rtot null
+  const uint32_t b = b0 + blockIdx.x;
+  uint32_t rbase = 0;
+  for (uint32_t j = 0; rtot && j < rk; j++) rbase += rtot[j];
+  const uint32_t e0 = bstart[b] + (bstA ? bstA[b] : 0u), tot = btot[b], base = boff[b] + rbase;
   const uint32_t* src = tcol + 2 * (uint64_t)e0;
   const uint16_t* scn = tcn + 2 * (uint64_t)e0;
 #ifndef G2N_PLACE_U
