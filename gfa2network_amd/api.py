@@ -541,9 +541,12 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     or on rank ``root`` only (the other ranks return None; a failed build raises on every rank).
     ``device``: this rank's GPU (default: torch's current device) — the one ``shard="auto"`` measured.  Index dtypes follow scipy (int64 once
     the entries pass 2^31 - 1).  Exceptions, the one-shot warning and the verbose strings are the
-    reference's (builders.py:95-299).  A ``.gz`` file is inflated by every rank (its byte ranges
-    are not seekable); one that does not inflate cleanly is built by every rank on its own GPU
-    through the single-GPU path, whose gzip errors and prefix semantics are the reference's."""
+    reference's (builders.py:95-299).  A multi-member / BGZF ``.gz`` is inflated member-wise: each
+    rank inflates the members that start in its share of the compressed bytes and one all-to-all
+    moves the text to the line-aligned ranges (``shard.gz_rank_text``); a file that does not split
+    into clean member chains (one member, damage) is inflated by every rank, and one that does not
+    inflate cleanly is built by every rank on its own GPU through the single-GPU path, whose gzip
+    errors and prefix semantics are the reference's."""
     import torch
 
     from .shard import HipEngine, build_sharded, file_line_ranges, gather_coo, gather_csr, scipy_index_dtype
@@ -565,27 +568,33 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
     if p.endswith(".gz"):
-        with open(p, "rb") as fh:
-            blob = fh.read()
-        try:
-            data, _ = nat.gunzip(blob)
-        except nat.GzipFailure:
-            del blob
-            opts = nat.make_options(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
-                                    asymmetric=asymmetric, strip_orientation=strip_orientation, dtype=dt.name,
-                                    weight_tag=weight_tag or None, output=nat.OUT_CSR if output == "csr" else nat.OUT_PARSE,
-                                    want_node_names=bool(return_node_list), device=dev())
-            raw = _run(p, opts)  # the exact reader raises gzip.py's error after the prefix's lines
-            out = finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
-                           verbose=verbose, path=path)
-            return out if root is None or rank == root else None
-        del blob
-        from .shard import line_ranges
+        from .shard import gz_rank_text, line_ranges
 
         eng = engine or HipEngine(dev())
-        lo, hi = line_ranges(data, world)[rank]
-        buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
-        del data
+        got = gz_rank_text(p, eng, group)  # each rank inflates the members in its share of the bytes
+        if got is not None:
+            buf = got[0]
+        else:  # not a clean member chain in slices (one member, damage): the whole file on every rank
+            with open(p, "rb") as fh:
+                blob = fh.read()
+            try:
+                data, _ = nat.gunzip(blob)
+            except nat.GzipFailure:
+                del blob
+                opts = nat.make_options(directed=directed, bidirected=bidirected,
+                                        keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
+                                        strip_orientation=strip_orientation, dtype=dt.name,
+                                        weight_tag=weight_tag or None,
+                                        output=nat.OUT_CSR if output == "csr" else nat.OUT_PARSE,
+                                        want_node_names=bool(return_node_list), device=dev())
+                raw = _run(p, opts)  # the exact reader raises gzip.py's error after the prefix's lines
+                out = finalize(raw, dtype=dt, return_node_list=return_node_list, raw_bytes_id=raw_bytes_id,
+                               verbose=verbose, path=path)
+                return out if root is None or rank == root else None
+            del blob
+            lo, hi = line_ranges(data, world)[rank]
+            buf = torch.from_numpy(np.frombuffer(data, dtype=np.uint8)[lo:hi].copy()).to(eng.device)
+            del data
     else:
         eng = engine or HipEngine(dev())
         lo, hi = file_line_ranges(p, world)[rank]

@@ -57,7 +57,7 @@ enum Slot {
 #define G2N_FORK_EARLY 0
 #endif
 #ifndef G2N_F2_OVERLAP  // bucket finish: F1 / F2 in this many bucket ranges, F2 of one beside F1 of the next (1: off)
-#define G2N_F2_OVERLAP 1
+#define G2N_F2_OVERLAP 4
 #endif
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
 #define G2N_FIN_DIRECT 0

@@ -1421,3 +1421,114 @@ def gather_csr(res: ShardResult, group=None, root=None):
         data.view(np.uint8)[pos:pos + k] = x.cpu().numpy()
         pos += k
     return indptr, indices, data
+
+
+# ------------------------------------------------------- sharded .gz: per-rank inflate --
+def gz_member_at_or_after(path: str, off: int, size: int, window: int = 1 << 20) -> int:
+    """The first gzip member start at or after byte `off` of a .gz file (RFC 1952: 1f 8b 08, reserved
+    flag bits clear, and a header + first deflate bytes that zlib accepts), or `size` when there is
+    none.  A false candidate inside compressed data is caught later: the slice before it does not
+    inflate to a clean member chain (gz_rank_text)."""
+    import zlib
+
+    if off <= 0:
+        return 0
+    with open(path, "rb") as fh:
+        fd = fh.fileno()
+        pos = off
+        while pos < size:
+            blk = os.pread(fd, window + 2, pos)
+            k = 0
+            while True:
+                k = blk.find(b"\x1f\x8b\x08", k)
+                if k < 0 or k >= window:
+                    break
+                cand = pos + k
+                head = os.pread(fd, 1 << 16, cand)
+                if len(head) >= 10 and head[3] & 0xE0 == 0:
+                    try:
+                        zlib.decompressobj(31).decompress(head, 1 << 16)
+                        return cand
+                    except zlib.error:
+                        pass
+                k += 1
+            pos += window
+    return size
+
+
+def gz_rank_text(path: str, engine, group=None):
+    """This rank's line-aligned range of a multi-member / BGZF .gz, inflating only the members that
+    start in its share of the compressed bytes (every rank inflated the whole file).
+
+    1. rank r takes the members starting in [r * size / G, (r + 1) * size / G) of the compressed file
+       (gz_member_at_or_after at both ends: every rank finds the same cut points) and inflates that
+       slice on its host (g2n_gunzip: member-parallel) — each slice a clean member chain, so together
+       they are the whole file's chain (gzip.py's reader sees the same bytes);
+    2. the ranks' text lengths are all-gathered: the inflated stream's line-aligned split points
+       (shard.line_ranges' rule — the first line start at or after r * N / G) are found from what each
+       rank reports about its own text (the byte before a split, the first newline at or after it);
+    3. one all-to-all-v moves the bytes to their owners (on the GPU with RCCL): rank r ends with
+       exactly the range line_ranges would give it over the whole inflated file.
+    Returns (device uint8 tensor, inflated bytes) — or None on every rank when any slice does not
+    inflate cleanly (a false member candidate, corruption, a single huge member cut by a candidate):
+    the caller then takes the whole-file path, whose exact reader raises gzip.py's errors."""
+    import torch
+
+    C = Comm(group)
+    world, rank = C.world, C.rank
+    size = os.path.getsize(path)
+    c0 = gz_member_at_or_after(path, rank * size // world, size)
+    c1 = gz_member_at_or_after(path, (rank + 1) * size // world, size) if rank + 1 < world else size
+    text, ok = b"", 1
+    if c1 > c0:
+        with open(path, "rb") as fh:
+            blob = os.pread(fh.fileno(), c1 - c0, c0)
+        try:
+            text, _ = nat.gunzip(blob)
+        except (nat.GzipFailure, RuntimeError):
+            ok = 0
+        del blob
+    lens = C.allgather_list([len(text), ok])
+    if not all(x[1] for x in lens):
+        return None
+    n_r = [int(x[0]) for x in lens]
+    P = np.concatenate([[0], np.cumsum(n_r)]).astype(np.int64)
+    N = int(P[-1])
+    arr = np.frombuffer(text, dtype=np.uint8)
+    # 2. what this rank knows about each nominal split m_k = k N / G: the byte before it, and the
+    #    first newline at or after it inside this rank's text (-1: none here)
+    rep = []
+    for k in range(1, world):
+        m = k * N // world
+        before = int(arr[m - 1 - P[rank]]) if P[rank] <= m - 1 < P[rank + 1] else -1
+        nl = -1
+        lo = max(m, int(P[rank])) - int(P[rank])
+        if lo < len(arr):
+            pos, win = lo, 1 << 16
+            while pos < len(arr):
+                hit = np.flatnonzero(arr[pos:pos + win] == 0x0A)
+                if len(hit):
+                    nl = int(P[rank]) + pos + int(hit[0])
+                    break
+                pos += win
+                win = min(win * 2, 1 << 26)
+        rep += [before, nl]
+    allrep = C.allgather_list(rep) if world > 1 else [rep]
+    starts = [0]
+    for k in range(1, world):
+        m = k * N // world
+        before = max(r[2 * (k - 1)] for r in allrep)
+        nls = [r[2 * (k - 1) + 1] for r in allrep if r[2 * (k - 1) + 1] >= 0]
+        if m <= 0 or m >= N or before == 0x0A:
+            s = min(max(m, 0), N)
+        else:
+            s = min(nls) + 1 if nls else N
+        starts.append(max(s, starts[-1]))
+    starts.append(N)
+    # 3. the bytes of [P_r, P_r + n_r) to the ranks whose [starts_k, starts_k+1) they overlap
+    send = [max(0, min(int(P[rank + 1]), starts[k + 1]) - max(int(P[rank]), starts[k])) for k in range(world)]
+    t = torch.from_numpy(arr.copy()) if len(arr) else torch.zeros(0, dtype=torch.uint8)
+    t = t.to(engine.device)
+    del text, arr
+    got, _ = C.a2av(t, send)
+    return got.to(engine.device), N

@@ -398,3 +398,100 @@ def test_sharded_range_premise_one_pass(oracle_lib, tmp_path, world):
     mp.spawn(_range_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def _gz_files(data: bytes, tmp_path):
+    """The same text as several gzip layouts: many members (more than ranks), BGZF, fewer members than
+    ranks (some ranks inflate nothing), one member (rank 0 inflates it all; the all-to-all spreads it),
+    zero padding after the last member."""
+    import gzip
+    import struct
+    import zlib
+
+    out = {}
+
+    def members(k):
+        step = max(1, -(-len(data) // k))
+        return b"".join(gzip.compress(data[i:i + step]) for i in range(0, len(data), step))
+    out["many"] = members(11)
+    out["two"] = members(2)
+    out["one"] = gzip.compress(data)
+    body = bytearray()
+    for k in range(0, len(data), 4000):
+        chunk = data[k:k + 4000]
+        co = zlib.compressobj(6, zlib.DEFLATED, -zlib.MAX_WBITS)
+        z = co.compress(chunk) + co.flush()
+        body += (b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", 25 + len(z))
+                 + z + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    out["bgzf"] = bytes(body) + bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    out["padded"] = members(5) + b"\x00" * 64
+    paths = {}
+    for name, blob in out.items():
+        p = tmp_path / f"{name}.gfa.gz"
+        p.write_bytes(blob)
+        paths[name] = str(p)
+    return paths
+
+
+def _gz_rank_worker(rank, world, port, paths, data_path, outdir):
+    """gz_rank_text: each rank inflates only the members starting in its share of the compressed bytes
+    and ends with exactly line_ranges' range of the whole inflated text; parse_gfa_sharded over it
+    equals the oracle's one-piece build."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gfa2network_amd import shard
+        from gfa2network_amd.api import finalize, parse_gfa_sharded
+        from oracle import oracle as orc
+        from shard_cpu_engine import CpuEngine
+
+        data = open(data_path, "rb").read()
+        want = shard.line_ranges(data, world)[rank]
+        full = orc.run(data)
+        B, bnodes = finalize(orc.to_raw(full, "parse"), dtype=np.dtype("float64"), return_node_list=True,
+                             raw_bytes_id=False, verbose=False)
+        for name, path in paths.items():
+            got = shard.gz_rank_text(path, CpuEngine(orc))  # ("one": rank 0 inflates it, the others nothing)
+            assert got is not None, name
+            buf, n = got
+            assert n == len(data) and bytes(buf.numpy()) == data[want[0]:want[1]], (name, rank)
+            A, nodes = parse_gfa_sharded(path, engine=CpuEngine(orc), return_node_list=True)
+            assert nodes == bnodes and np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_gzip_inflates_per_rank(oracle_lib, tmp_path, world):
+    import torch.multiprocessing as mp
+
+    data = _gfa(41, 300, 2500, True)
+    data_path = tmp_path / "in.gfa"
+    data_path.write_bytes(data)
+    paths = _gz_files(data, tmp_path)
+    mp.spawn(_gz_rank_worker, args=(world, _free_port(), paths, str(data_path), str(tmp_path)), nprocs=world,
+             join=True)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}.npy").exists()
+
+
+def test_gz_member_candidates(tmp_path):
+    """gz_member_at_or_after finds the next real member start (not a 1f 8b 08 inside a name or in
+    deflate data that zlib refuses), or the file size."""
+    import gzip
+
+    from gfa2network_amd.shard import gz_member_at_or_after
+
+    a = gzip.compress(b"S\t\x1f\x8b\x08fake\t*\n" * 50)
+    b = gzip.compress(b"L\tx\t+\ty\t+\t*\n" * 50)
+    p = tmp_path / "x.gz"
+    p.write_bytes(a + b)
+    size = len(a) + len(b)
+    assert gz_member_at_or_after(str(p), 0, size) == 0
+    assert gz_member_at_or_after(str(p), 1, size) == len(a)
+    assert gz_member_at_or_after(str(p), len(a), size) == len(a)
+    assert gz_member_at_or_after(str(p), len(a) + 1, size) == size
