@@ -143,6 +143,19 @@ def test_c4_full_size_equals_oracle(gpu, flags):
     assert hashlib.sha256(out["blob"].tobytes()).hexdigest() == d["names"]
 
 
+def test_c4_permuted_names_full_size_equals_oracle(gpu):
+    """C4's dimensions with the segment names a permutation of 1..N (synth names="permuted"): the
+    direct-address dictionary tier (S lines claim direct[v], one 4-byte read per edge name) bit for
+    bit against the oracle's digest of the same bytes (tests/golden/make_synth_digests.py C4P)."""
+    from gfa2network_amd import _native as nat
+
+    d = DIGESTS["C4P"]
+    out = _device_build(d["n_segments"], d["n_links"], names="permuted", output=nat.OUT_PARSE)
+    assert out["format"] == nat.FMT_CSR and out["n"] == d["n_nodes"] and out["nnz"] == d["parse"]["nnz"]
+    assert _digest(out["indptr"], out["indices"], out["data"]) == d["parse"]["digest"]
+    assert hashlib.sha256(out["blob"].tobytes()).hexdigest() == d["names"]
+
+
 def test_c5_single_gpu_properties(gpu):
     """C5 at full size on one GPU (16 GB in HBM): the undirected SUM CSR's size-independent
     properties, and the stream-order COO (parse_gfa's return value for directed=False)."""
