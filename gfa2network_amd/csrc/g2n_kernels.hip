@@ -1704,7 +1704,30 @@ struct HashLeanArgs {
   uint64_t direct_cap;   //            values below this
   uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
   uint32_t pre_len;
+  uint32_t* dvals;       // kLeanDirClaim: node id -> its name's value (k_direct_verify)
 };
+
+#ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)
+#define G2N_DIRECT_LINES 4
+#endif
+
+// After kLeanDirClaim's plain stores: every S line's value must map back to its own id (a repeated
+// value maps to one of them only: the other fails the premise).  n ids; 4 per thread, reads in flight.
+// (A claim pass that failed part way leaves ids unwritten: values are bounds-checked against cap.)
+__global__ void __launch_bounds__(256) k_direct_verify(const uint32_t* __restrict__ direct,
+                                                       const uint32_t* __restrict__ dvals, uint64_t n, uint64_t cap,
+                                                       Ctl* ctl) {
+  const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  uint32_t v[4], d[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) v[q] = i0 + q < n ? dvals[i0 + q] : 0u;
+#pragma unroll
+  for (int q = 0; q < 4; q++) d[q] = i0 + q < n && v[q] < cap ? direct[v[q]] : ~0u;
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < 4; q++) bad |= i0 + q < n && d[q] != (uint32_t)(i0 + q);
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
+}
 
 
 // The first min(l, 16) bytes at tile offset x of the staged tile, little-endian, zero padded
@@ -1979,30 +2002,55 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       return lim == len - t0 ? lim + 1 : 0u;
     };
     if constexpr (kMode == kLeanDirEdges) {
+      // kDL lines per thread per step: their 2 kDL random reads all in flight at once (the pass is
+      // bound by the random-read rate of the direct array, not by the parse)
+      constexpr uint32_t kDL = G2N_DIRECT_LINES;
 #pragma unroll 1
-      for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
-        const uint32_t x = rec[j];
-        if (((x >> 15) & 3u) != 2u) continue;
-        const uint32_t o = x & 0x7FFFu;
-        const uint32_t next = line_next(j, o);
-        uint32_t xa, la, xb, lb;
-        uint64_t va, vb;
-        if (!next || !lean_edge_names(buf, tabm, o, next, xa, la, xb, lb) || !lean_direct_value(buf, H, xa, la, va) ||
-            !lean_direct_value(buf, H, xb, lb, vb)) {
-          is.fail = 1;
-          continue;
+      for (uint32_t j0 = threadIdx.x; j0 < n_win; j0 += kDL * kLeanTPB) {
+        uint32_t va[kDL], vb[kDL], eo[kDL];  // values (< 2^28), edge index in the window's tile
+        bool act[kDL];
+#pragma unroll
+        for (uint32_t q = 0; q < kDL; q++) {
+          const uint32_t j = j0 + q * kLeanTPB;
+          act[q] = false;
+          va[q] = vb[q] = eo[q] = 0;
+          if (j >= n_win) continue;
+          const uint32_t x = rec[j];
+          if (((x >> 15) & 3u) != 2u) continue;
+          const uint32_t o = x & 0x7FFFu;
+          const uint32_t next = line_next(j, o);
+          uint32_t xa, la, xb, lb;
+          uint64_t a, b;
+          if (!next || !lean_edge_names(buf, tabm, o, next, xa, la, xb, lb) || !lean_direct_value(buf, H, xa, la, a) ||
+              !lean_direct_value(buf, H, xb, lb, b)) {
+            is.fail = 1;
+            continue;
+          }
+          act[q] = true;
+          va[q] = (uint32_t)a;
+          vb[q] = (uint32_t)b;
+          eo[q] = x >> 17;
         }
-        const uint32_t ida = H.direct[va], idb = H.direct[vb];  // both random reads in flight
-        if (ida == ~0u || idb == ~0u) {  // a key no S line defined: a new node (not S-first)
-          is.fail = 1;
-          continue;
+        uint32_t ida[kDL], idb[kDL];
+#pragma unroll
+        for (uint32_t q = 0; q < kDL; q++) {
+          ida[q] = act[q] ? H.direct[va[q]] : 0u;
+          idb[q] = act[q] ? H.direct[vb[q]] : 0u;
         }
-        const uint64_t eb = (ebase + (x >> 17)) * H.ktrip;
-        H.rows[eb] = (int32_t)ida;
-        H.cols[eb] = (int32_t)idb;
-        if (H.ktrip >= 2) {
-          H.rows[eb + 1] = (int32_t)idb;
-          H.cols[eb + 1] = (int32_t)ida;
+#pragma unroll
+        for (uint32_t q = 0; q < kDL; q++) {
+          if (!act[q]) continue;
+          if (ida[q] == ~0u || idb[q] == ~0u) {  // a key no S line defined: a new node (not S-first)
+            is.fail = 1;
+            continue;
+          }
+          const uint64_t eb = (ebase + eo[q]) * H.ktrip;
+          H.rows[eb] = (int32_t)ida[q];
+          H.cols[eb] = (int32_t)idb[q];
+          if (H.ktrip >= 2) {
+            H.rows[eb + 1] = (int32_t)idb[q];
+            H.cols[eb + 1] = (int32_t)ida[q];
+          }
         }
       }
       continue;  // next window
@@ -2188,10 +2236,10 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
           continue;
         }
         const uint32_t id = (uint32_t)(sbase + pref);
-        if (atomicCAS(H.direct + v, ~0u, id) != ~0u) {  // a repeated S name: the classic tiers decide
-          is.fail = 1;
-          continue;
-        }
+        // plain stores: of two S lines naming v one store wins, and k_direct_verify (direct[vals[id]]
+        // == id for every id) sees the other — a repeated S name, for the classic tiers to decide
+        H.direct[v] = id;
+        H.dvals[id] = (uint32_t)v;
         H.noff[id] = t0 + x;
         H.nlen[id] = l;
         claimed_bytes += l;
