@@ -1704,30 +1704,13 @@ struct HashLeanArgs {
   uint64_t direct_cap;   //            values below this
   uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
   uint32_t pre_len;
-  uint32_t* dvals;       // kLeanDirClaim: node id -> its name's value (k_direct_verify)
 };
 
 #ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)
 #define G2N_DIRECT_LINES 4
 #endif
 
-// After kLeanDirClaim's plain stores: every S line's value must map back to its own id (a repeated
-// value maps to one of them only: the other fails the premise).  n ids; 4 per thread, reads in flight.
-// (A claim pass that failed part way leaves ids unwritten: values are bounds-checked against cap.)
-__global__ void __launch_bounds__(256) k_direct_verify(const uint32_t* __restrict__ direct,
-                                                       const uint32_t* __restrict__ dvals, uint64_t n, uint64_t cap,
-                                                       Ctl* ctl) {
-  const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  uint32_t v[4], d[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) v[q] = i0 + q < n ? dvals[i0 + q] : 0u;
-#pragma unroll
-  for (int q = 0; q < 4; q++) d[q] = i0 + q < n && v[q] < cap ? direct[v[q]] : ~0u;
-  bool bad = false;
-#pragma unroll
-  for (int q = 0; q < 4; q++) bad |= i0 + q < n && d[q] != (uint32_t)(i0 + q);
-  if (__ballot(bad) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
-}
+
 
 
 // The first min(l, 16) bytes at tile offset x of the staged tile, little-endian, zero padded
@@ -2236,10 +2219,11 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
           continue;
         }
         const uint32_t id = (uint32_t)(sbase + pref);
-        // plain stores: of two S lines naming v one store wins, and k_direct_verify (direct[vals[id]]
-        // == id for every id) sees the other — a repeated S name, for the classic tiers to decide
-        H.direct[v] = id;
-        H.dvals[id] = (uint32_t)v;
+        // (plain stores plus a verify pass measured slower: 4.13 against 3.70 ms on C4's 50M S lines)
+        if (atomicCAS(H.direct + v, ~0u, id) != ~0u) {  // a repeated S name: the classic tiers decide
+          is.fail = 1;
+          continue;
+        }
         H.noff[id] = t0 + x;
         H.nlen[id] = l;
         claimed_bytes += l;

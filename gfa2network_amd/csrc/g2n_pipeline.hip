@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_DVALS, S_RTOT, S_SCANST2, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_NSLOTS
 };
 
 #ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
@@ -1373,7 +1373,6 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
   H.direct_cap = cap;
   H.pre = pre;
   H.pre_len = pre_len;
-  H.dvals = dget<uint32_t>(c, S_DVALS, n_s);
   phase(c, "table_init");
 #ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
@@ -1382,9 +1381,6 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
 #endif
   hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
                      len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
-  if (n_s)
-    hipLaunchKernelGGL(k_direct_verify, dim3(grid_for((n_s + 3) / 4, 256)), dim3(256), 0, c->stream,
-                       (const uint32_t*)direct, (const uint32_t*)H.dvals, n_s, cap, c->ctl);
   phase(c, "direct_claim");
   sync_ctl(c);
   if (c->h_ctl->int_fail) {
