@@ -135,8 +135,11 @@ def _dist_setup(n_gpus: int, always: bool = False):
         import torch
         import torch.distributed as dist
 
+        from datetime import timedelta
+
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        # a collective that never completes ends the run (exit non-zero) instead of holding the node
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local), timeout=timedelta(minutes=5))
         check_world(n_gpus, dist.get_world_size(), dist.get_backend())
         world = dist.get_world_size()
     elif n_gpus != world:
@@ -580,7 +583,10 @@ def main_sharded(args, wl):
     leg = sharded_leg(args, wl, world, rank, local, args.names, args.force_protocol)
     alt = None
     if not args.no_alt and args.names == "decimal":
-        alt = sharded_leg(args, wl, world, rank, local, "hashed")
+        try:
+            alt = sharded_leg(args, wl, world, rank, local, "hashed")
+        except Exception as exc:  # noqa: BLE001 - the headline (decimal) leg is already measured
+            alt = {"error": f"{type(exc).__name__}: {exc}"}
     mode = dict(wl.mode)
     line = {
         "metric": "M edges/sec GFA->CSR (device-resident), + GB/s ingested",

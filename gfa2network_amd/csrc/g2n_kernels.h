@@ -111,6 +111,11 @@ struct ParseOpts {
   // experiment (G2N_K2_PREFETCH): the one-tile-per-block lean parse warms the cache with tile
   // blockIdx + pf_dist (0: off)
   uint32_t pf_dist;
+  // the extended tile-local lean parse (k_tile_lean kExt: bidirected keys, one integer weight tag):
+  // edge e's weight at ew[e] (the tile slots' layout, one double per edge line); the weight tag's
+  // bytes little-endian (wt_len <= 8) for the comparison against the staged line
+  double* ew;
+  uint64_t wt_pack;
 };
 constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
 

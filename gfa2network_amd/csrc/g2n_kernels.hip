@@ -944,6 +944,33 @@ __device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, 
   return w;
 }
 
+// "<tag>:i:<int>" at tile offset x, length l: the weight float(int(value)) the reference takes
+// (parser.py:179-204, builders.py:205-209) for the canonical spellings only — an optional '-' and 1-9
+// digits without a leading zero; any other spelling (CPython's int() accepts more) or tag is false
+// (the full parse decides)
+__device__ inline bool lean_int_tag(const uint8_t* buf, uint32_t x, uint32_t l, const ParseOpts& op, double* w) {
+  const uint32_t tl = op.wt_len;
+  if (tl == 0 || tl > 8 || l < tl + 4) return false;
+  for (uint32_t k = 0; k < tl; k++)
+    if (buf[x + k] != (uint8_t)(op.wt_pack >> (8 * k))) return false;
+  if (buf[x + tl] != ':' || buf[x + tl + 1] != 'i' || buf[x + tl + 2] != ':') return false;
+  uint32_t j = x + tl + 3, e = x + l;
+  const bool neg = buf[j] == '-';
+  j += neg ? 1u : 0u;
+  const uint32_t nd = e - j;
+  if (nd == 0 || nd > 9 || (buf[j] == '0' && nd > 1)) return false;
+  int64_t v = 0;
+  for (; j < e; j++) {
+    const uint32_t c = buf[j];
+    if (c - '0' > 9u) return false;
+    v = v * 10 + (c - '0');
+  }
+  *w = (double)(neg ? -v : v);
+  return true;
+}
+
+// kExt: the extended instance (bidirected keys, one integer weight tag), tile-local builds only
+template <bool kExt = false>
 __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next, uint8_t k,
                                  uint64_t t0, uint64_t tb, uint64_t eb, const ParseOpts& op, const TouchOut& T,
                                  IntState& is) {
@@ -987,7 +1014,34 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
   }
   const uint32_t vm = (uint32_t)(a > b ? a : b);
   is.vmax = vm > is.vmax ? vm : is.vmax;
-  const uint64_t o = ((op.tile_pad && !op.grouped ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
+  const uint64_t e = (op.tile_pad && !op.grouped ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb;
+  const uint64_t o = e * op.ktrip;
+  if constexpr (kExt) {
+    if (op.has_wt) {  // builders.py:205-209: the tag's value, or 1.0 without it
+      double wv = 1.0;
+      if (p[5] < n) {  // a field after the overlap: exactly one, the weight tag
+        if (m || !lean_int_tag(buf, so + p[5] + 1, n - p[5] - 1, op, &wv)) {
+          is.fail = 1;
+          return true;
+        }
+      }
+      op.ew[e] = wv;
+    }
+    if (op.bidir) {  // builders.py:211-234: "name:o" keys, S line k minting 2k (+) and 2k + 1 (-)
+      const uint32_t ia = 2u * (uint32_t)(a - 1) + (c2 == '-'), ib = 2u * (uint32_t)(b - 1) + (c4 == '-');
+      op.rows[o] = (int32_t)ia;
+      op.cols[o] = (int32_t)ib;
+      if (op.ktrip == 4) {  // undirected (b, a), then the reverse twin (v:rev, u:rev) both ways
+        op.rows[o + 1] = (int32_t)ib;
+        op.cols[o + 1] = (int32_t)ia;
+        op.rows[o + 2] = (int32_t)(ib ^ 1u);
+        op.cols[o + 2] = (int32_t)(ia ^ 1u);
+        op.rows[o + 3] = (int32_t)(ia ^ 1u);
+        op.cols[o + 3] = (int32_t)(ib ^ 1u);
+      }
+      return true;
+    }
+  }
   op.rows[o] = (int32_t)(a - 1);
   op.cols[o] = (int32_t)(b - 1);
   if (op.ktrip >= 2) {
@@ -1400,17 +1454,21 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean_evidence(const TileCnt* __re
 }
 
 // Tile-local lean parse, last: each tile's COO slot to its stream-order place.
+// (w_p / w: the extended lean parse's per-edge weights, compacted beside; null without a weight tag)
 __global__ void __launch_bounds__(kTPB) k_tile_compact(const int32_t* __restrict__ rows_p,
                                                        const int32_t* __restrict__ cols_p, uint32_t pad,
                                                        uint32_t ktrip, const TileCnt* __restrict__ cnt,
                                                        const TileCnt* __restrict__ tbase, int32_t* __restrict__ rows,
-                                                       int32_t* __restrict__ cols) {
+                                                       int32_t* __restrict__ cols, const double* __restrict__ w_p,
+                                                       double* __restrict__ w) {
   const uint64_t t = blockIdx.x;
   const uint64_t n = cnt[t].edges * ktrip, src = t * (uint64_t)pad * ktrip, dst = tbase[t].edges * ktrip;
   for (uint64_t i = threadIdx.x; i < n; i += kTPB) {
     rows[dst + i] = rows_p[src + i];
     cols[dst + i] = cols_p[src + i];
   }
+  if (w_p)
+    for (uint64_t i = threadIdx.x; i < cnt[t].edges; i += kTPB) w[tbase[t].edges + i] = w_p[t * (uint64_t)pad + i];
 }
 
 // Lines whose fields run past their tile's staged window: parsed from global memory.
@@ -1827,7 +1885,7 @@ using LeanRegs = TileRegs<kTileHalo, kLeanTPB>;
 // One tile of the lean front end.  R holds the tile's staged bytes on entry (loaded by the caller);
 // after they are in LDS, R is refilled with tile next_tile's bytes (next_tile < n_tiles), which stay
 // in flight through this tile's parse — the persistent decimal kernel's prefetch.
-template <int kMode, bool kGrouped>
+template <int kMode, bool kGrouped, bool kExt = false>
 __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl,
                                           TileCnt* __restrict__ tcnt_out, TileLean* __restrict__ tlean,
                                           uint32_t* __restrict__ gcount, uint64_t gcap, const HashLeanArgs& H,
@@ -2268,7 +2326,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
         continue;
       } else {
         // S line: tb = its S index (no edge precedes it); edge line: eb = its edge index
-        if (!lean_line(buf, tabm, o, next, code == 1 ? kS : kEdge, t0, code == 1 ? pref : 0ull,
+        if (!lean_line<kExt>(buf, tabm, o, next, code == 1 ? kS : kEdge, t0, code == 1 ? pref : 0ull,
                        code == 1 ? 0ull : pref, op, TouchOut{}, is))
           is.fail = 1;
       }
@@ -2351,7 +2409,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
 #else
 #define G2N_LEAN_ATTR __launch_bounds__(kLeanTPB, kLeanTPB == 1024 ? 2 : 1)
 #endif
-template <int kMode, bool kGrouped>
+template <int kMode, bool kGrouped, bool kExt = false>
 __global__ void G2N_LEAN_ATTR
     k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl, TileCnt* __restrict__ tcnt_out,
                 TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount, uint64_t gcap, HashLeanArgs H) {
@@ -2380,7 +2438,7 @@ __global__ void G2N_LEAN_ATTR
   const bool do_pf = op.pf_dist && threadIdx.x < (kTile + kTileHalo) / 128 && pf < len;
   if (do_pf) asm volatile("global_load_dword %0, %1, off" : "=v"(sink) : "v"(in + pf) : "memory");
 #endif
-  lean_tile<kMode, kGrouped>(in, len, op, ctl, tcnt_out, tlean, gcount, gcap, H, tile, R, ~0ull, 0);
+  lean_tile<kMode, kGrouped, kExt>(in, len, op, ctl, tcnt_out, tlean, gcount, gcap, H, tile, R, ~0ull, 0);
 #if G2N_K2_PREFETCH
   asm volatile("s_waitcnt vmcnt(0)" : : "v"(sink) : "memory");
 #endif

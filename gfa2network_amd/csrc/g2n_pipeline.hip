@@ -50,7 +50,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_NSLOTS
 };
 
 #ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
@@ -78,6 +78,7 @@ constexpr uint32_t kTestThrowAfterIds = G2N_TEST_THROW_AFTER_IDS;
 constexpr uint32_t kTestIndex64 = G2N_TEST_INDEX64;
 constexpr uint32_t kTestDictDirect = G2N_TEST_DICT_DIRECT;
 constexpr uint32_t kTestNoDirect = G2N_TEST_NO_DIRECT;
+constexpr uint32_t kTestNoExtLean = G2N_TEST_NO_EXT_LEAN;
 
 
 struct DevBuf {
@@ -1169,9 +1170,13 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 // — for builds whose only consumer is the unweighted bucket partition.
 // s_base / n_seg_all: a byte range of a sharded file with global decimal ids (options.range_s_base / range_n_segments):
 // the S lines before the range and in the whole file; 0 / 0 for a whole file.
+// xo (the extended instance, k_tile_lean kExt): bidirected keys and / or one integer weight tag —
+// bidir / keep / has_wt / wt_len / wt_pack read from it; the per-edge weights go to S_EW in stream
+// order beside the compacted COO (never group slots).
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
-                             uint64_t n_seg_all = 0, bool deferred = false) {
+                             uint64_t n_seg_all = 0, bool deferred = false, const ParseOpts* xo = nullptr) {
+  if (xo) grouped = false;
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
 #endif
@@ -1194,6 +1199,15 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
   lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
+  double* ew_p = nullptr;
+  if (xo) {
+    lo.bidir = xo->bidir;
+    lo.keep = xo->keep;
+    lo.has_wt = xo->has_wt;
+    lo.wt_len = xo->wt_len;
+    lo.wt_pack = xo->wt_pack;
+    if (xo->has_wt) lo.ew = ew_p = dget<double>(c, S_EWP, n_tiles * kTileEdgeCap);
+  }
 #ifdef G2N_K2_STAMPS
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
   G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));
@@ -1215,7 +1229,10 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL((k_tile_lean_p<false>), dim3(grid), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
                        tlean, (uint32_t*)nullptr, (uint64_t)0, n_tiles);
 #else
-  if (grouped)
+  if (xo)
+    hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0,
+                       c->stream, in, len, lo, c->ctl, tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0, HashLeanArgs{});
+  else if (grouped)
     hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
                        len, lo, c->ctl, tcnt, tlean, gcount, gcap, HashLeanArgs{});
   else
@@ -1277,9 +1294,10 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
       const uint64_t n_trip = tot.edges * ktrip;
       auto* rows = dget<int32_t>(c, S_ROWS, n_trip);
       auto* cols = dget<int32_t>(c, S_COLS, n_trip);
+      double* ew = ew_p ? dget<double>(c, S_EW, tot.edges) : nullptr;  // E.w: k_values reads the weights there
       hipLaunchKernelGGL(k_tile_compact, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, (const int32_t*)rows_p,
                          (const int32_t*)cols_p, kTileEdgeCap, ktrip, (const TileCnt*)tcnt, (const TileCnt*)tbase,
-                         rows, cols);
+                         rows, cols, (const double*)ew_p, ew);
       phase(c, "place");
       *tot_out = tot;
       return true;
@@ -1438,14 +1456,23 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   const bool grouped = !G2N_NO_GROUP_DEFAULT && !coo_wanted && !c->no_group &&
                        !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
+  // bidirected keys / one integer weight tag: the extended tile-local instance (whole files only)
+  const size_t wt_bytes = o->weight_tag ? std::strlen(o->weight_tag) : 0;
+  ParseOpts xo{};
+  xo.bidir = bidir;
+  xo.keep = keep;
+  xo.has_wt = wt_bytes > 0;
+  xo.wt_len = (uint32_t)wt_bytes;
+  for (size_t k = 0; k < wt_bytes && k < 8; k++) xo.wt_pack |= (uint64_t)(uint8_t)o->weight_tag[k] << (8 * k);
+  const bool ext = bidir || wt_bytes > 0;
+  const bool ext_ok = !shard_dec && wt_bytes <= 8 && !(c->test_flags & kTestNoExtLean);
   // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
   const bool local_done =
       n_tiles && (first_one || (shard_dec && (shard_deferred || (o->range_s_base >= 0 && o->range_n_segments > 0)))) &&
-      !bidir && !(o->weight_tag && *o->weight_tag) && !o->strip_orientation &&
-      !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
-      tile_local_parse(c, in, len, n_tiles, gd ? 1u : 2u, tcnt, tbase, &tot, grouped,
+      (!ext || ext_ok) && !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
+      tile_local_parse(c, in, len, n_tiles, tpe == 4 ? 4u : (gd ? 1u : 2u), tcnt, tbase, &tot, grouped,
                        shard_dec ? (uint64_t)o->range_s_base : 0, shard_dec ? (uint64_t)o->range_n_segments : 0,
-                       shard_deferred);
+                       shard_deferred, ext ? &xo : nullptr);
   if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
     throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
   // ---- K1: per-tile counts -> tile bases
@@ -1492,8 +1519,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   TouchOut T{dget<uint64_t>(c, S_NOFF, z(n_t)), dget<uint32_t>(c, S_NLEN, z(n_t)),
              bidir ? dget<uint64_t>(c, S_OOFF, z(n_t)) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, z(n_t)) : nullptr,
              dget<uint8_t>(c, S_TKIND, z(n_t))};
-  // (E.w is read by k_values only for weights: a tile-local build has none)
-  EdgeOut E{dget<double>(c, S_EW, z(n_e)), dget<uint32_t>(c, S_ETB, z(n_e))};
+  // (E.w is read by k_values only for weights: a tile-local build holds them there when it has a tag)
+  EdgeOut E{dget<double>(c, S_EW, local_done && !wt_bytes ? 1 : n_e), dget<uint32_t>(c, S_ETB, z(n_e))};
   const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
   const uint64_t n_trip = n_e * (uint64_t)ktrip;
   // the stream-order COO holds int32 node ids (< 2^31 - 1, checked below) at 64-bit positions; the

@@ -130,7 +130,9 @@ enum {
   G2N_TEST_THROW_AFTER_IDS = 512, /* the build fails (G2N_E_DEVICE) once its ids are set up */
   G2N_TEST_INDEX64 = 1024,      /* CSR results in int64 indptr / indices (the > 2^31 - 1 entries path) */
   G2N_TEST_DICT_DIRECT = 2048,  /* decimal ids in S order through the direct-address tier */
-  G2N_TEST_NO_DIRECT = 4096     /* never the direct-address tier (the lean hash tier instead) */
+  G2N_TEST_NO_DIRECT = 4096,    /* never the direct-address tier (the lean hash tier instead) */
+  G2N_TEST_NO_EXT_LEAN = 8192   /* bidirected / weighted decimal builds: K1 + the lean parse, not the
+                                   extended tile-local parse */
 };
 
 #define G2N_MAX_PHASES 40

@@ -131,3 +131,70 @@ def test_direct_tier_synthetic_large_equals_lean_hash(gpu, monkeypatch):
         b = outcome(gpu_run(data, mode, "float64", None))
         monkeypatch.setattr(nat, "TEST_FLAGS", 0)
         assert a == b, mode
+
+
+# ---- the extended tile-local lean parse: bidirected keys and one integer weight tag (round 5) ----
+def _ext_case(name):
+    r = random.Random(31)
+    n_s, n_l = 3000, 12000
+    S = [f"S\t{k}\t{'ACGT' * r.randint(0, 2)}\n" for k in range(1, n_s + 1)]
+
+    def link(tag=True):
+        a = r.randint(1, n_s)
+        b = min(n_s, a + r.randint(0, 4))
+        t = f"\tRC:i:{r.randint(-50, 99)}" if tag and r.random() < 0.9 else ""
+        return f"L\t{a}\t{r.choice('+-')}\t{b}\t{r.choice('+-')}\t0M{t}\n"
+    L = [link() for _ in range(n_l)]
+    if name == "canonical":
+        return S + L, True
+    if name == "no_tags":
+        return S + [link(False) for _ in range(n_l)], True
+    if name == "zero_and_negative":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:i:0\n", "L\t2\t-\t3\t-\t0M\tRC:i:-7\n"] + L[100:], True
+    if name == "leading_zero_value":  # int("007") == 7: the full parse decides, same answer
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:i:007\n"] + L[100:], False
+    if name == "plus_sign":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:i:+5\n"] + L[100:], False
+    if name == "float_type":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:f:1.5\n"] + L[100:], False
+    if name == "other_tag":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tID:Z:x\n"] + L[100:], False
+    if name == "two_tags":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:i:3\tRC:i:4\n"] + L[100:], False
+    if name == "ten_digits":
+        return S + L[:100] + ["L\t1\t+\t2\t-\t0M\tRC:i:1234567890\n"] + L[100:], False
+    if name == "bad_orientation":
+        return S + L[:100] + ["L\t1\t*\t2\t-\t0M\n"] + L[100:], False
+    raise KeyError(name)
+
+
+TAG_ONLY = {"leading_zero_value", "plus_sign", "float_type", "other_tag", "two_tags", "ten_digits"}
+EXT_CASES = ["canonical", "no_tags", "zero_and_negative", "leading_zero_value", "plus_sign", "float_type",
+             "other_tag", "two_tags", "ten_digits", "bad_orientation"]
+EXT_MODES = [({"bidirected": True}, None), ({"bidirected": True}, "RC"), ({"bidirected": True, "keep_directed_bidir": True}, "RC"),
+             ({}, "RC"), ({"directed": False}, "RC"), ({"asymmetric": True}, "RC")]
+
+
+@pytest.mark.parametrize("case", EXT_CASES)
+def test_extended_lean_parse_equals_oracle(gpu, oracle_lib, monkeypatch, case):
+    """Decimal-id files built bidirected and / or with a weight tag take the extended tile-local lean
+    parse (no K1, no full parse): "name:o" keys 2k / 2k + 1, the reverse twins (builders.py:211-234) and
+    the tag's canonical integer value (parser.py:179-204); other spellings fall back to the full parse.
+    Every mode x dtype equals the oracle and the K1 + lean-parse path (TEST_NO_EXT_LEAN)."""
+    from gfa2network_amd import _native as nat
+
+    lines, eligible = _ext_case(case)
+    data = "".join(lines).encode()
+    for mode, wt in EXT_MODES:
+        raw = nat.build_from_buffer(data, nat.make_options(weight_tag=wt, **mode))
+        if raw.status == 0 and (wt or mode.get("bidirected")):
+            took = "tiles" not in raw.phase_ms and "parse" in raw.phase_ms
+            # (a tag the lean parse refuses matters only when the build reads that tag)
+            want = eligible or (wt is None and case in TAG_ONLY)
+            assert took == want, (case, mode, wt, sorted(raw.phase_ms))
+        for dtype in ("float64", "float32", "int8", "bool"):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, wt)), (case, mode, wt, dtype)
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_EXT_LEAN)
+            assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, wt, dtype, "K1 path")
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
