@@ -1902,6 +1902,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     const uint64_t b = tile * (uint64_t)op.tile_pad * op.ktrip;
     op.rows += b;
     op.cols += b;
+    if (kExt && op.ew) op.ew += tile * (uint64_t)op.tile_pad;  // one weight per edge line
   }
   op.grouped = op.tile_pad ? 1u : 0u;  // lean_line: positions relative to the tile's base in its slot
   uint64_t sbase = 0, ebase = 0;     // hash modes: S lines / edge lines before this tile (K1's bases)
