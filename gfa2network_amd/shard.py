@@ -763,6 +763,11 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
                 return None
             local = got[0]
             tm["build"] = (time.perf_counter() - t0) * 1e3
+        elif all(e[0] < 0 for e in alle):
+            # every range declined: names that are not the decimal ids (a shape the one pass refuses in
+            # every range would be unusual) — the general protocol, without a count + build that would
+            # decline again (C5 with hashed names: 5 ms per build)
+            return None
         # else some range declined the one pass: count and build with the range offsets known
     if local is None:
         t0 = time.perf_counter()
