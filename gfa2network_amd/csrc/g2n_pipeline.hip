@@ -548,8 +548,10 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   // F1 / F2 overlapped by bucket ranges: F1 of range k + 1 on the main stream runs beside the scan and
   // F2 of range k on the place stream (F1 is latency-bound, F2 a copy that F1 leaves bandwidth for);
   // F2 adds the entries of the ranges before its own to the range-relative offsets
+  // (large builds only: on C2's 3.9K buckets the extra launches cost more than the overlap gives,
+  // 0.455 -> 0.549 ms per build)
   const uint32_t n_ov = (G2N_F2_OVERLAP > 1 && n_el <= 0x7FFFFFFFull && !(c->test_flags & kTestIndex64) &&
-                         n_bk >= 64ull * G2N_F2_OVERLAP)
+                         n_bk >= 32768ull)
                             ? (uint32_t)std::min(G2N_F2_OVERLAP, 16)
                             : 1u;
   if (n_ov > 1) {
