@@ -56,6 +56,7 @@ TEST_INDEX64 = 1024      # unweighted CSR results in int64 indptr / indices (the
 TEST_DICT_DIRECT = 2048  # decimal ids in S order through the direct-address tier (not the decimal-id parse)
 TEST_NO_DIRECT = 4096    # never the direct-address tier: the lean hash tier instead
 TEST_NO_EXT_LEAN = 8192  # bidirected / weighted decimal builds through K1 + the lean parse (not tile-local)
+TEST_NO_DEC_TEXT = 16384  # edge-list export of decimal ids through the names blob (not the arithmetic render)
 TEST_FLAGS = 0
 # options.range_flags (include/g2n.h G2N_RANGE_*): set by the sharded / chunked protocol (shard.py)
 RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)

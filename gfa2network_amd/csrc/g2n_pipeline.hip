@@ -79,6 +79,7 @@ constexpr uint32_t kTestIndex64 = G2N_TEST_INDEX64;
 constexpr uint32_t kTestDictDirect = G2N_TEST_DICT_DIRECT;
 constexpr uint32_t kTestNoDirect = G2N_TEST_NO_DIRECT;
 constexpr uint32_t kTestNoExtLean = G2N_TEST_NO_EXT_LEAN;
+constexpr uint32_t kTestNoDecText = G2N_TEST_NO_DEC_TEXT;
 
 
 struct DevBuf {
@@ -108,6 +109,8 @@ struct g2n_context {
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
   const uint32_t* wenc = nullptr;  // the current build's values as exact-int32 codes (k_values), if written
   bool no_group = false;      // redo of a build whose group-slot COO the partition refused
+  bool edge_text = false;     // run_edge_list's build: decimal names are left to the text render
+  bool names_dec = false;     // ... and that build's names were the decimal ids (no blob written)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;   // work that overlaps the main stream (the decimal names blob)
   hipEvent_t side_ev[2] = {nullptr, nullptr};  // main -> side fork, side -> main join
@@ -1692,6 +1695,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     R->names_blob = blob;
     R->names_offsets = offs;
     phase(c, "names");
+  } else if (o->want_node_names && lean_done && c->edge_text) {
+    c->names_dec = true;  // k_edge_dec_text renders them from the ids
   } else if (o->want_node_names && lean_done) {
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     const uint64_t names_len = dec_name_off(n_nodes, (int)bidir);
@@ -1821,7 +1826,42 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
   b.dtype = G2N_BOOL;
   b.output = G2N_OUT_COO;
   b.want_node_names = 1;
+  b.range_flags = G2N_RANGE_NO_VALUES;  // the text reads ids only: a decimal-id build writes no values
+  struct TextFlag {  // run_build leaves decimal names to the render (names_dec), exceptions included
+    g2n_context* c;
+    ~TextFlag() { c->edge_text = false; }
+  } guard{c};
+  c->edge_text = !(c->test_flags & kTestNoDecText);
+  c->names_dec = false;
   const int rc = run_build(c, in, len, &b, R);
+  c->edge_text = false;
+  if (rc == G2N_OK && c->names_dec) {
+    const uint64_t n = (uint64_t)R->nnz;
+    const auto* rows = (const int32_t*)R->rows;
+    const auto* cols = (const int32_t*)R->cols;
+    const int bd = o->bidirected ? 1 : 0;
+    const uint64_t nb = (n + kTextEdges - 1) / kTextEdges;
+    auto* bsum = dget<uint64_t>(c, S_ELEN, nb + 1);
+    auto* bpos = dget<uint64_t>(c, S_EPOS, nb + 1);
+    if (nb)
+      hipLaunchKernelGGL(k_edge_dec_sum, dim3((unsigned)nb), dim3(kTPB), 0, c->stream, rows, cols, n, bd, bsum);
+    G2N_HIP(hipMemsetAsync(bsum + nb, 0, sizeof(uint64_t), c->stream));
+    excl_scan<uint64_t>(c, bsum, bpos, nb + 1);
+    const uint64_t total = read_dev(c, bpos + nb);
+    auto* text = dget<uint8_t>(c, S_ETEXT, total + 16);
+    if (nb)
+      hipLaunchKernelGGL(k_edge_dec_text, dim3((unsigned)nb), dim3(kTPB), 0, c->stream, rows, cols, n, bd, bpos, text);
+    phase(c, "edge_text");
+    R->format = G2N_FMT_TEXT;
+    R->rows = R->cols = nullptr;
+    R->data = text;
+    R->nnz = (int64_t)total;
+    R->names_blob = nullptr;
+    R->names_offsets = nullptr;
+    R->names_bytes = 0;
+    finish_timings(c, R);
+    return G2N_OK;
+  }
   if (rc >= G2N_E_MALFORMED_L && rc <= G2N_E_INT_TOO_LARGE && R->err_line >= 0) {
     // the reference's loop wrote the lines of the records before the failing one
     // (cli.py:270-281): render the prefix [0, start of the failing line) from the same input

@@ -131,8 +131,10 @@ enum {
   G2N_TEST_INDEX64 = 1024,      /* CSR results in int64 indptr / indices (the > 2^31 - 1 entries path) */
   G2N_TEST_DICT_DIRECT = 2048,  /* decimal ids in S order through the direct-address tier */
   G2N_TEST_NO_DIRECT = 4096,    /* never the direct-address tier (the lean hash tier instead) */
-  G2N_TEST_NO_EXT_LEAN = 8192   /* bidirected / weighted decimal builds: K1 + the lean parse, not the
+  G2N_TEST_NO_EXT_LEAN = 8192,  /* bidirected / weighted decimal builds: K1 + the lean parse, not the
                                    extended tile-local parse */
+  G2N_TEST_NO_DEC_TEXT = 16384  /* edge-list export of a decimal-id build through the names blob, not
+                                   the arithmetic render */
 };
 
 #define G2N_MAX_PHASES 40

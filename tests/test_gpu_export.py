@@ -111,3 +111,45 @@ def test_gpu_export_gzip_and_stdin(gpu, tmp_path, name):
     assert (r.returncode != 0) == (want_exc is not None)
     if want_exc:
         assert r.stderr.decode().rstrip().splitlines()[-1] == f"{want_exc[0]}: {want_exc[1]}"
+
+
+def _dec_cases():
+    """Decimal-id inputs (S line k names "k+1", S lines first): the arithmetic render; and inputs
+    that break the premise (blob render)."""
+    from gfa2network_amd import synth
+
+    base = synth.host_bytes(3000, 12_345, seed=11)  # ragged: 12345 edges, not a multiple of 4 / 1024
+    lines = base.split(b"\n")
+    n_s = sum(1 for ln in lines if ln.startswith(b"S"))
+    yield "synthetic", base, True
+    yield "one_edge", b"S\t1\t*\nS\t2\t*\nL\t1\t+\t2\t-\t0M\n", True
+    yield "no_edges", b"S\t1\t*\nS\t2\t*\n", True
+    yield "multi_digit", b"".join(b"S\t%d\t*\n" % k for k in range(1, 12)) + b"L\t11\t+\t9\t-\t0M\n" * 5, True
+    yield "edge_before_s", b"L\t5\t+\t2\t-\t0M\n" + base, False  # first touch "5": id 0
+    yield "named", base.replace(b"S\t1\t", b"S\tx\t", 1), False
+    # a malformed line: the lines before it are written (the prefix takes the arithmetic render)
+    yield "malformed_prefix", b"\n".join(lines[: n_s + 700] + [b"L\t1\t+"] + lines[n_s + 700:]), True
+
+
+@pytest.mark.parametrize("case", ["synthetic", "one_edge", "no_edges", "multi_digit", "edge_before_s", "named",
+                                  "malformed_prefix"])
+def test_gpu_export_decimal_render(gpu, oracle_lib, monkeypatch, case):
+    """A decimal-id build's lines are rendered from the ids (k_edge_dec_sum / k_edge_dec_text: no
+    names blob); same bytes and failure as the blob render (TEST_NO_DEC_TEXT) and the oracle."""
+    from gfa2network_amd import _native as nat
+
+    data, dec = next((d, e) for n, d, e in _dec_cases() if n == case)
+    for bidir in (False, True):
+        opts = nat.make_options(bidirected=bidir, output=nat.OUT_EDGE_LIST)
+        raw = nat.build_from_buffer(data, opts)
+        text = bytes(raw.data) if raw.format == "text" else b""
+        if raw.status == 0:
+            assert ("names" not in raw.phase_ms) == dec, (case, sorted(raw.phase_ms))
+        monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_DEC_TEXT)
+        ref = nat.build_from_buffer(data, opts)
+        monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+        assert (raw.status, raw.err_line) == (ref.status, ref.err_line), case
+        assert text == (bytes(ref.data) if ref.format == "text" else b""), (case, bidir)
+        want, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
+        assert text == want, (case, bidir)
+        assert (err is None) == (raw.status == 0), (case, err)
