@@ -9,6 +9,7 @@
 #                           database under gpurun_out/<tag>_s<i>/
 #   pmc:<bench.py args>     tools/gpu_counters.sh passes on bench.py <args> -> gpurun_out/<tag>_pmc.json
 #   py:<script + args>      python -u <script + args>                 -> gpurun_out/<tag>_s<i>.log
+#   ab:<libs> <bench args>  bench.py per library (main, or exp_<x>.so from tools/exp_build.sh), twice
 # step arguments are word-split by the shell (eval): quote inside them, e.g. "tests:f.py -k 'a or b'".
 # limits (seconds): T_TESTS (900), T_BENCH (600), T_PROF (300), T_PY (600); COMMIT tags the pmc summary.
 # example:
@@ -39,6 +40,14 @@ for step in "$@"; do
     pmc)
       OUT_JSON=$R/gpurun_out/${TAG}_pmc.json COMMIT=${COMMIT:-unknown} BENCH_ARGS="$args" \
         bash tools/gpu_counters.sh ${TAG}_ctr "g2n::" || exit 1 ;;
+    ab)  # ab:<lib,lib,...> <bench.py args>: each library in turn (main = libg2n.so, x = exp_x.so), twice
+      libs=${args%% *}; bargs=${args#* }
+      for rep in 1 2; do for l in ${libs//,/ }; do
+        lp=$R/gfa2network_amd/_lib/$([ "$l" = main ] && echo libg2n.so || echo exp_$l.so)
+        G2N_LIB=$lp timeout -k 10 ${T_BENCH:-600} python -u bench.py $bargs > ${base}_${l}_$rep.json 2>> $base.err ||
+          { tail -20 $base.err; exit 1; }
+        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d.get('device_ms_per_step'), d.get('phase_ms'))" ${base}_${l}_$rep.json $l
+      done; done ;;
     py)
       timeout -k 10 ${T_PY:-600} python -u $args > $base.log 2>&1 || { tail -40 $base.log; exit 1; }
       tail -5 $base.log ;;
