@@ -82,6 +82,8 @@ struct Ctl {
   unsigned long long ev_dmin, ev_dmax;  // k_tile_lean_evidence: a range's S-name offsets (+ 2^62)
   unsigned long long ev_vmax;           //   and its largest edge key
   unsigned long long w_inexact;         // the weighted bucket SUM's exactness broke (k_weight_encode / k_sumw_finish)
+  unsigned long long warn_tile;         // tile-local lean parse: the first tile holding an unsupported record
+  unsigned long long warn_off;          //   and that record's byte offset (k_lean_warn; warn_line its line)
 };
 
 struct ParseOpts {
@@ -116,6 +118,10 @@ struct ParseOpts {
   // bytes little-endian (wt_len <= 8) for the comparison against the staged line
   double* ew;
   uint64_t wt_pack;
+  // the tile-local decimal parse: tile t's first unsupported record (first byte not in SLPECOHF,
+  // ASCII) as its line rank in the tile << 15 | its tile offset, the tile index atomicMin'd into
+  // ctl->warn_tile (the one-shot warning without the full parse); null: such a record fails the pass
+  uint32_t* tunk;
 };
 constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
 

@@ -1422,6 +1422,17 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restr
 // once the ranges' counts are exchanged); no edge may precede an S line inside the range; the
 // range's largest edge key goes to the caller too (checked against the file's S count).  d is
 // biased by 2^62 for the unsigned atomics.
+// The one-shot unsupported-record warning of a tile-local lean parse (parser.py:125-131): the first
+// tile holding such a record, its rank among the tile's lines and its offset -> the record's line and
+// byte offset (ctl->warn_line / warn_off), after the tile bases are known.
+__global__ void k_lean_warn(const uint32_t* __restrict__ tunk, const TileCnt* __restrict__ tbase, Ctl* ctl) {
+  const unsigned long long w = ctl->warn_tile;
+  if (w == ~0ull) return;
+  const uint32_t u = tunk[w];
+  ctl->warn_line = tbase[w].lines + (u >> 15);
+  ctl->warn_off = w * kTile + (u & 0x7FFFu);
+}
+
 __global__ void __launch_bounds__(kTPB) k_tile_lean_evidence(const TileCnt* __restrict__ cnt,
                                                              const TileCnt* __restrict__ tbase,
                                                              const TileLean* __restrict__ tlean, uint64_t n_tiles,
@@ -1897,6 +1908,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   __shared__ uint32_t rec[kLeanLines + 1];
   __shared__ unsigned long long red64[kW];
   __shared__ uint32_t s_gbase;
+  __shared__ uint32_t s_unk;  // the tile's first unsupported record (op.tunk): rank << 15 | offset
   const uint64_t t0 = tile * kTile;
   if (!kGrouped && op.tile_pad) {  // this tile's slot (positions relative to it, as in a group slot)
     const uint64_t b = tile * (uint64_t)op.tile_pad * op.ktrip;
@@ -1905,6 +1917,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     if (kExt && op.ew) op.ew += tile * (uint64_t)op.tile_pad;  // one weight per edge line
   }
   op.grouped = op.tile_pad ? 1u : 0u;  // lean_line: positions relative to the tile's base in its slot
+  if (threadIdx.x == 0) s_unk = ~0u;  // (published by the staging barrier)
   uint64_t sbase = 0, ebase = 0;     // hash modes: S lines / edge lines before this tile (K1's bases)
   if constexpr (kMode != kLeanDecimal) {
     sbase = H.tbase[tile].segs;
@@ -1952,8 +1965,19 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   const uint32_t n_st = (uint32_t)__popcll(st);
   uint32_t n_s = 0, n_e = 0, n_po = 0;
   // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
-  // then the kinds (2-bit codes kept for the record pass); any further start one by one
-  uint32_t codes = 0;
+  // then the kinds (2-bit codes kept for the record pass); any further start one by one.  An
+  // unsupported record (parser.py:125-131) fails the pass unless op.tunk takes it: its index among
+  // the thread's starts and its offset, ranked after the scan (the warning's line, k_lean_warn) —
+  // a first byte >= 0x80 still fails (its warning is a UnicodeDecodeError: the full parse decides)
+  uint32_t codes = 0, q_unk = ~0u, o_unk = 0;
+  auto unsupported = [&](uint32_t q, uint32_t o, uint32_t b0) {
+    if (!op.tunk || b0 >= 0x80u) {
+      is.fail = 1;
+    } else if (q_unk == ~0u) {
+      q_unk = q;
+      o_unk = o;
+    }
+  };
   {
     unsigned long long m = st;
     uint32_t off[kLeanBatch];
@@ -1974,7 +1998,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       if (off[q] == 0xFFFFu) continue;
       const bool exact = t0 + off[q] + 1 >= len || x0[q] == '\n' || x1[q] == '\t' || x1[q] == '\n';
       const uint8_t kd = line_kind((uint8_t)x0[q], exact);
-      if (kd == kUnknown) is.fail = 1;  // the one-shot warning needs the full parse
+      if (kd == kUnknown) unsupported(q, off[q], x0[q]);
       const uint32_t code = lean_code(kd);
       codes |= code << (2 * q);
       n_s += code == 1;
@@ -1982,11 +2006,11 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       n_po += code == 3;
     }
 #pragma unroll 1
-    while (m) {  // more than kLeanBatch lines start in these 64 bytes
+    for (uint32_t q = kLeanBatch; m; q++) {  // more than kLeanBatch lines start in these 64 bytes
       const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
       m &= m - 1;
       const uint8_t kd = kind_at(buf, o, t0 + o, len);
-      if (kd == kUnknown) is.fail = 1;
+      if (kd == kUnknown) unsupported(q, o, buf[o]);
       const uint32_t code = lean_code(kd);
       n_s += code == 1;
       n_e += code == 2;
@@ -1999,6 +2023,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       (unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40), &tot, red64);
   const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
                  e_tot = (uint32_t)(tot >> 40);
+  if (q_unk != ~0u) atomicMin(&s_unk, (((uint32_t)(ex & 0xFFFFFu) + q_unk) << 15) | o_unk);  // (read at the finish)
   K2_LEAN_STAMP(3);
   const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
   if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
@@ -2258,10 +2283,13 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       const uint32_t code = (x >> 15) & 3u;
       if (code == 0) continue;
       const uint32_t o = x & 0x7FFFu, pref = x >> 17;
-      const uint32_t next = line_next(j, o);
-      if (!next) {  // the line runs past the staged window
-        is.fail = 1;
-        continue;
+      uint32_t next = line_next(j, o);
+      if (!next) {  // the line runs past the staged window (a long sequence or path): an S, P or O
+        if (code == 2) {  // line needs only its first fields, which must then sit in the 48-byte tab
+          is.fail = 1;    // view (lean_line / lean_s_name with a line longer than it); an edge line fails
+          continue;
+        }
+        next = o + 50;
       }
       if (code == 3) {  // parser.py:229-247, 343-361: >= 3 fields, nothing else for the matrix
         const uint32_t n = next - 1 - o, sh = o & 15;
@@ -2391,6 +2419,10 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     c.recs = (uint64_t)s_tot + e_tot + npo;
     tcnt_out[tile] = c;
     tlean[tile] = TileLean{dmn, dmx, vm};  // no S line: dmn > dmx (the check skips the tile)
+    if (s_unk != ~0u) {
+      op.tunk[tile] = s_unk;
+      atomicMin(&ctl->warn_tile, (unsigned long long)tile);
+    }
   }
   if (failed && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
   K2_LEAN_STAMP(6);

@@ -48,7 +48,7 @@ enum Slot {
   S_SLOT, S_FIRST, S_NID, S_FLEN, S_BLOB, S_OFFS, S_ROWS, S_COLS, S_DATA, S_KEYS0, S_KEYS1, S_VALS0, S_VALS1,
   S_KV, S_ODATA, S_INDPTR, S_INDICES, S_TEMP, S_WT, S_TKIND, S_TSTATE, S_RSTART0, S_RSTART1, S_ROUT0,
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
-  S_INV, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
+  S_INV, S_TUNK, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
   S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_NSLOTS
 };
@@ -937,6 +937,7 @@ static void reset_ctl(g2n_context* c) {
   c->h_ctl->warn_line = ~0ull;
   c->h_ctl->cast_key = ~0ull;
   c->h_ctl->ev_dmin = ~0ull;
+  c->h_ctl->warn_tile = ~0ull;
   G2N_HIP(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
 }
 
@@ -1180,7 +1181,8 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 // order beside the compacted COO (never group slots).
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
-                             uint64_t n_seg_all = 0, bool deferred = false, const ParseOpts* xo = nullptr) {
+                             uint64_t n_seg_all = 0, bool deferred = false, const ParseOpts* xo = nullptr,
+                             bool warn_ok = false) {
   if (xo) grouped = false;
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
@@ -1204,6 +1206,10 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
   lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
+  // a whole-file build takes the unsupported-record warning itself (k_lean_warn); a sharded range
+  // leaves it to the general protocol
+  uint32_t* tunk = warn_ok ? dget<uint32_t>(c, S_TUNK, n_tiles) : nullptr;
+  lo.tunk = tunk;
   double* ew_p = nullptr;
   if (xo) {
     lo.bidir = xo->bidir;
@@ -1267,6 +1273,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL(k_struct_scan_parts<TileCnt>, dim3(1), dim3(256), 0, c->stream, part, n_parts, part + n_parts);
     hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
+    if (tunk) hipLaunchKernelGGL(k_lean_warn, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)tunk, (const TileCnt*)tbase, c->ctl);
     const TileCnt tot = read_dev(c, part + n_parts);
     if (deferred)  // the range's offset evidence, checked by the caller across ranges
       hipLaunchKernelGGL(k_tile_lean_evidence, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream,
@@ -1477,7 +1484,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
       (!ext || ext_ok) && !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
       tile_local_parse(c, in, len, n_tiles, tpe == 4 ? 4u : (gd ? 1u : 2u), tcnt, tbase, &tot, grouped,
                        shard_dec ? (uint64_t)o->range_s_base : 0, shard_dec ? (uint64_t)o->range_n_segments : 0,
-                       shard_deferred, ext ? &xo : nullptr);
+                       shard_deferred, ext ? &xo : nullptr, !shard_dec);
   if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
     throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
   // ---- K1: per-tile counts -> tile bases
@@ -1625,7 +1632,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const uint64_t warn_line = o->unknown_warned ? ~0ull : c->h_ctl->warn_line;
   if (warn_line != ~0ull) R->warn_line = (int64_t)warn_line;  // first unsupported line, warned or not
   if (warn_line != ~0ull && warn_line < err_line) {
-    uint64_t off = read_dev(c, ls + warn_line);
+    // (a tile-local lean build has no line starts: k_lean_warn found the record's offset)
+    uint64_t off = local_done ? c->h_ctl->warn_off : read_dev(c, ls + warn_line);
     uint8_t b = read_dev(c, in + off);
     if (b >= 0x80) {  // parser.py:127 line[:1].decode() raises
       err_line = warn_line;
