@@ -1406,9 +1406,11 @@ __global__ void __launch_bounds__(kTPB) k_tile_parse(const uint8_t* __restrict__
 __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restrict__ cnt,
                                                           const TileCnt* __restrict__ tbase,
                                                           const TileLean* __restrict__ tlean, uint64_t n_tiles,
-                                                          uint64_t n_seg, uint64_t s_base, Ctl* ctl) {
+                                                          uint64_t n_seg, const TileCnt* __restrict__ tot,
+                                                          uint64_t s_base, Ctl* ctl) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (t >= n_tiles) return;
+  if (!n_seg) n_seg = tot->segs;  // a whole file: its S lines (the tile scan's total)
   const TileLean e = tlean[t];
   bool bad = e.vmax > n_seg;  // (s_base: S lines before this byte range of a sharded file)
   if (cnt[t].segs)
@@ -1773,6 +1775,9 @@ struct HashLeanArgs {
   uint64_t direct_cap;   //            values below this
   uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
   uint32_t pre_len;
+  uint32_t suf_len;      //            ... and common suffix (no digit in it, <= 8 bytes)
+  uint64_t suf;
+  uint32_t width;        //            0: canonical decimals; w: exactly w digits, leading zeros allowed
 };
 
 #ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)
@@ -1803,14 +1808,32 @@ __device__ inline bool tail_eq_in(const uint8_t* __restrict__ in, uint64_t a, ui
   return true;
 }
 
-// the value of the name at tile offset x (length l) when it is H.pre followed by a canonical
-// decimal (no sign, no leading zero, <= 10 digits) below H.direct_cap
+// fixed-width digits, leading zeros allowed (zero-padded names: one width, so value <-> name)
+__device__ inline bool dec_lds_pad(const uint8_t* buf, uint32_t x, uint32_t l, uint64_t* v) {
+  if (l == 0 || l > 10) return false;
+  uint64_t y = 0;
+  for (uint32_t j = 0; j < l; j++) {
+    const uint32_t c = buf[x + j];
+    if (c - '0' > 9u) return false;
+    y = y * 10 + (c - '0');
+  }
+  *v = y;
+  return true;
+}
+
+// the value of the name at tile offset x (length l) when it is H.pre, a decimal and H.suf — the
+// decimal canonical (no sign, no leading zero, <= 10 digits) or, with H.width, exactly that many
+// digits (hifiasm's "utg000123l") — and below H.direct_cap.  Prefix, suffix and the digit rule make
+// the value one name's.
 __device__ inline bool lean_direct_value(const uint8_t* buf, const HashLeanArgs& H, uint32_t x, uint32_t l,
                                          uint64_t& v) {
-  const uint32_t p = H.pre_len;
-  if (l <= p) return false;
+  const uint32_t p = H.pre_len, q = H.suf_len;
+  if (l <= p + q) return false;
   if (p && (uint64_t)lds_span16(buf, x, p) != H.pre) return false;
-  return dec_lds(buf, x + p, l - p, &v) && v < H.direct_cap;
+  if (q && (uint64_t)lds_span16(buf, x + l - q, q) != H.suf) return false;
+  const uint32_t nd = l - p - q;
+  if (H.width) return nd == H.width && dec_lds_pad(buf, x + p, nd, &v) && v < H.direct_cap;
+  return dec_lds(buf, x + p, nd, &v) && v < H.direct_cap;
 }
 
 // S line at tile offset so (its '\n' at next - 1): the name's tile offset and length (fields[1],

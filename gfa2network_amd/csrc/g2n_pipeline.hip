@@ -86,6 +86,12 @@ struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
 };
+struct ScanSlot {  // a scan status slot (scan_excl): the buffer it last cleared, the epoch / ticket in use
+  void* p = nullptr;
+  size_t cap = 0;
+  uint32_t epoch = 0;
+  uint64_t ticket = 0;
+};
 
 // The tile-local lean parse's COO in GROUP slots (k_tile_lean<true>): group g's entries are
 // [g * gcap, g * gcap + gcount[g]) of rows / cols, its tiles in arbitrary order — for the
@@ -109,6 +115,7 @@ struct g2n_context {
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
   const uint32_t* wenc = nullptr;  // the current build's values as exact-int32 codes (k_values), if written
   bool no_group = false;      // redo of a build whose group-slot COO the partition refused
+  g2n::ScanSlot scan_slot[g2n::S_NSLOTS];  // scan_excl's per-slot epoch / ticket state
   bool edge_text = false;     // run_edge_list's build: decimal names are left to the text render
   bool names_dec = false;     // ... and that build's names were the decimal ids (no blob written)
   hipStream_t stream = nullptr;
@@ -212,17 +219,30 @@ static T read_dev(g2n_context* c, const T* p) {
   return v;
 }
 
-// exclusive scan of n items (k_scan_excl, decoupled look-back); *total (device, optional) = sum
+// exclusive scan of n items (k_scan_excl, decoupled look-back); *total (device, optional) = sum.
+// The slot's buffer (ticket, then status words) is cleared only when it is (re)allocated or its
+// epochs run out: each launch takes the next epoch and the ticket base (one launch per slot at a
+// time, in the order of stream s — a slot belongs to one stream)
 template <class TIn, class TOut>
 static void scan_excl(g2n_context* c, const TIn* in, TOut* out, uint64_t n, TOut* total = nullptr,
                       hipStream_t s = nullptr, int slot = S_SCANST) {
   if (n == 0 && !total) return;
   if (!s) s = c->stream;
   const uint64_t tiles = scan_tiles(n);
-  auto* st = dget<unsigned long long>(c, slot, tiles + 1);  // status words + the ticket
-  G2N_HIP(hipMemsetAsync(st, 0, (tiles + 1) * sizeof(unsigned long long), s));
-  hipLaunchKernelGGL((k_scan_excl<TIn, TOut>), dim3((unsigned)tiles), dim3(256), 0, s, in, out, n, st,
-                     (uint32_t*)(st + tiles), total);
+  auto* st = dget<unsigned long long>(c, slot, tiles + 1);  // the ticket, then the status words
+  ScanSlot& ss = c->scan_slot[slot];
+  const size_t cap = c->bufs[slot].cap;
+  if (ss.p != (void*)st || ss.cap != cap || ss.epoch >= kStEpochs) {
+    G2N_HIP(hipMemsetAsync(st, 0, cap, s));
+    ss.p = st;
+    ss.cap = cap;
+    ss.epoch = 0;
+    ss.ticket = 0;
+  }
+  ss.epoch++;
+  hipLaunchKernelGGL((k_scan_excl<TIn, TOut>), dim3((unsigned)tiles), dim3(256), 0, s, in, out, n, st + 1, st, total,
+                     ss.epoch, (unsigned long long)ss.ticket);
+  ss.ticket += tiles;
 }
 template <class T>
 static void excl_scan(g2n_context* c, const T* in, T* out, uint64_t n) {
@@ -547,6 +567,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
 #endif
   sync_ctl(c);
   if (c->h_ctl->bucket_overflow) return false;
+  const int32_t nnz = read_dev(c, indptr + n_rows);
 #else
   // F1 / F2 overlapped by bucket ranges: F1 of range k + 1 on the main stream runs beside the scan and
   // F2 of range k on the place stream (F1 is latency-bound, F2 a copy that F1 leaves bandwidth for);
@@ -560,9 +581,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   if (n_ov > 1) {
     auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
     auto* rtot = dget<uint32_t>(c, S_RTOT, n_ov);
-    uint64_t st_words = 0;  // every range's scan status words + ticket, allocated once (no realloc mid-way)
-    for (uint32_t k = 0; k < n_ov; k++) st_words += scan_tiles(n_bk * (k + 1) / n_ov - n_bk * k / n_ov) + 1;
-    auto* st = dget<unsigned long long>(c, S_SCANST2, st_words);
+    (void)dget<unsigned long long>(c, S_SCANST2, scan_tiles(n_bk) + 1);  // sized once, before the ranges' scans
     for (uint32_t k = 0; k < n_ov; k++) {
       const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov;
       if (sum)
@@ -577,26 +596,24 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                            (const uint32_t*)bstA, (uint32_t)b0);
       G2N_HIP(hipEventRecord(c->ov_ev[k], c->stream));
     }
-    unsigned long long* stk = st;
     for (uint32_t k = 0; k < n_ov; k++) {
-      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov, tiles = scan_tiles(b1 - b0);
+      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov;
       G2N_HIP(hipStreamWaitEvent(c->place, c->ov_ev[k], 0));
-      G2N_HIP(hipMemsetAsync(stk, 0, (tiles + 1) * sizeof(unsigned long long), c->place));
-      hipLaunchKernelGGL((k_scan_excl<uint32_t, uint32_t>), dim3((unsigned)tiles), dim3(256), 0, c->place,
-                         (const uint32_t*)(btot + b0), boff + b0, b1 - b0, stk, (uint32_t*)(stk + tiles), rtot + k);
+      scan_excl<uint32_t, uint32_t>(c, (const uint32_t*)(btot + b0), boff + b0, b1 - b0, rtot + k, c->place, S_SCANST2);
       hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->place,
                          (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows,
                          (T)1, (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr,
                          (const uint32_t*)bstA, (uint32_t)b0, (const uint32_t*)rtot, k);
-      stk += tiles + 1;
     }
     G2N_HIP(hipEventRecord(c->ov_ev[16], c->place));
     G2N_HIP(hipStreamWaitEvent(c->stream, c->ov_ev[16], 0));
+    int32_t nnz = 0;  // one wait for the overflow flag and the entry count
+    G2N_HIP(hipMemcpyAsync(&nnz, indptr + n_rows, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     sync_ctl(c);
     if (c->h_ctl->bucket_overflow) return false;
     R->format = G2N_FMT_CSR;
     R->indptr = indptr;
-    R->nnz = (int64_t)read_dev(c, indptr + n_rows);
+    R->nnz = (int64_t)nnz;
     R->indices = indices;
     R->data = odata;
     R->sum_sorted = -1;
@@ -627,8 +644,11 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
 #endif
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk, boff + n_bk);
-  sync_ctl(c);
-  if (c->h_ctl->bucket_overflow) return false;
+  // (an overflowed bucket is found after F2: its placement is then dropped with the rest)
+  if (n_el > 0x7FFFFFFFull || (c->test_flags & kTestIndex64)) {
+    sync_ctl(c);
+    if (c->h_ctl->bucket_overflow) return false;
+  }
   // scipy's index dtype (get_index_dtype(maxval=nnz)): int64 indptr / indices once the result holds
   // more than 2^31 - 1 entries (utils.py:55 coo.tocsr, builders.py:283 maximum) — only possible when
   // the partition's upper bound passes it, so the total is read only then
@@ -661,10 +681,14 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                      (const uint32_t*)bst, (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (T)1,
                      (const uint32_t*)tcol, (const uint16_t*)tcn, indptr, indices, odata, (int64_t*)nullptr,
                      (const uint32_t*)bstA, 0u, (const uint32_t*)nullptr, 0u);
+  int32_t nnz = 0;  // one wait for the overflow flag and the entry count
+  G2N_HIP(hipMemcpyAsync(&nnz, indptr + n_rows, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  sync_ctl(c);
+  if (c->h_ctl->bucket_overflow) return false;
 #endif
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
-  R->nnz = (int64_t)read_dev(c, indptr + n_rows);
+  R->nnz = (int64_t)nnz;
   R->indices = indices;
   R->data = odata;
   R->sum_sorted = -1;  // not computed: unweighted sums cannot depend on scipy's order
@@ -760,16 +784,19 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
                      (const uint32_t*)bst, (uint32_t)low, n_rows, btot, tcol, tval, indptr, c->ctl);
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk, boff + n_bk);
-  sync_ctl(c);
-  if (c->h_ctl->bucket_overflow || c->h_ctl->w_inexact) return false;
+  // (an overflowed bucket or an inexact sum is found after F2w: its placement is then dropped)
   auto* indices = dget<int32_t>(c, S_INDICES, 2 * n_el);
   T* odata = dget<T>(c, S_ODATA, 2 * n_el);
   hipLaunchKernelGGL((k_sumw_place<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, (const uint32_t*)bst,
                      (const uint32_t*)btot, (const uint32_t*)boff, (uint32_t)low, n_rows, (const uint32_t*)tcol,
                      (const T*)tval, indptr, indices, odata);
+  int32_t nnz = 0;  // one wait for the flags and the entry count
+  G2N_HIP(hipMemcpyAsync(&nnz, indptr + n_rows, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  sync_ctl(c);
+  if (c->h_ctl->bucket_overflow || c->h_ctl->w_inexact) return false;
   R->format = G2N_FMT_CSR;
   R->indptr = indptr;
-  R->nnz = (int64_t)read_dev(c, indptr + n_rows);
+  R->nnz = (int64_t)nnz;
   R->indices = indices;
   R->data = odata;
   R->sum_sorted = -1;  // not computed: these sums cannot depend on scipy's order
@@ -1129,30 +1156,42 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
   return true;  // no S line seen yet (long header lines): try
 }
 
-// The first S line's name (in the first 64 KiB) as the direct-address tier's premise: a common prefix
-// of at most 8 non-digit bytes, then a canonical decimal of at most 10 digits.  False otherwise (the
-// hash tiers decide); every other name is checked by the passes themselves.
-static bool first_segment_prefix(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t* pre, uint32_t* pre_len) {
+// The first S line's name (in the first 64 KiB) as the direct-address tier's premise: a prefix of
+// at most 8 non-digit bytes, a run of at most 10 digits, a suffix of at most 8 bytes without a digit
+// ("s123", "utg000123l", "node_42").  A run that starts with '0' fixes the width (zero-padded
+// names: every name then has exactly that many digits); otherwise the run must be a canonical
+// decimal.  False otherwise (the hash tiers decide); every other name is checked by the passes.
+struct NamePattern {
+  uint64_t pre = 0, suf = 0;
+  uint32_t pre_len = 0, suf_len = 0, width = 0;
+};
+static bool first_segment_pattern(g2n_context* c, const uint8_t* in, uint64_t len, NamePattern* np) {
   const size_t n = (size_t)std::min<uint64_t>(len, 1 << 16);
   if (n == 0) return false;
   std::vector<uint8_t> h(n);
   G2N_HIP(hipMemcpyAsync(h.data(), in, n, hipMemcpyDeviceToHost, c->stream));
   G2N_HIP(hipStreamSynchronize(c->stream));
+  auto digit = [&](size_t k) { return h[k] >= '0' && h[k] <= '9'; };
   for (size_t p = 0; p + 2 < n;) {
     if (h[p] == 'S' && h[p + 1] == '\t') {
       size_t e = p + 2;
       while (e < n && h[e] != '\t' && h[e] != '\n') e++;
       if (e == n) return false;
       size_t d = p + 2;
-      while (d < e && (h[d] < '0' || h[d] > '9')) d++;
-      const size_t pl = d - (p + 2), nd = e - d;
-      if (pl > 8 || nd == 0 || nd > 10 || h[d] == '0') return false;
-      for (size_t k = d; k < e; k++)
-        if (h[k] < '0' || h[k] > '9') return false;
-      uint64_t w = 0;
-      for (size_t k = 0; k < pl; k++) w |= (uint64_t)h[p + 2 + k] << (8 * k);
-      *pre = w;
-      *pre_len = (uint32_t)pl;
+      while (d < e && !digit(d)) d++;
+      size_t f = d;
+      while (f < e && digit(f)) f++;
+      const size_t pl = d - (p + 2), nd = f - d, sl = e - f;
+      if (pl > 8 || sl > 8 || nd == 0 || nd > 10) return false;
+      for (size_t k = f; k < e; k++)
+        if (digit(k)) return false;
+      NamePattern r;
+      for (size_t k = 0; k < pl; k++) r.pre |= (uint64_t)h[p + 2 + k] << (8 * k);
+      for (size_t k = 0; k < sl; k++) r.suf |= (uint64_t)h[f + k] << (8 * k);
+      r.pre_len = (uint32_t)pl;
+      r.suf_len = (uint32_t)sl;
+      r.width = h[d] == '0' ? (uint32_t)nd : 0u;
+      *np = r;
       return true;
     }
     const void* q = std::memchr(h.data() + p, '\n', n - p);
@@ -1263,9 +1302,9 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     }
   }
 #endif
-  sync_ctl(c);
-  bool ok = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && c->h_ctl->warn_line == ~0ull;
-  if (ok) {
+  // the tile scan, the warning's line and the premise check run unconditionally behind the parse
+  // (on a failed parse their results are dropped), so the host waits once for all of them
+  {
     const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
     auto* part = dget<TileCnt>(c, S_TEMP, n_parts + 1);
     hipLaunchKernelGGL(k_struct_reduce<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
@@ -1274,16 +1313,18 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
     if (tunk) hipLaunchKernelGGL(k_lean_warn, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)tunk, (const TileCnt*)tbase, c->ctl);
-    const TileCnt tot = read_dev(c, part + n_parts);
     if (deferred)  // the range's offset evidence, checked by the caller across ranges
       hipLaunchKernelGGL(k_tile_lean_evidence, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream,
                          (const TileCnt*)tcnt, (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, c->ctl);
-    else
+    else  // (the file's S count: n_seg_all, or the total the scan just wrote)
       hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
-                         (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles,
-                         n_seg_all ? n_seg_all : (uint64_t)tot.segs, s_base, c->ctl);
+                         (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, n_seg_all,
+                         (const TileCnt*)(part + n_parts), s_base, c->ctl);
+    TileCnt tot;
+    G2N_HIP(hipMemcpyAsync(&tot, part + n_parts, sizeof(TileCnt), hipMemcpyDeviceToHost, c->stream));
     sync_ctl(c);
-    ok = !c->h_ctl->int_fail && tot.touches < 0xFFFFFFFFull && tot.edges * ktrip < 0xFFFFFFFFull;
+    bool ok = !c->h_ctl->int_fail && c->h_ctl->err_key == ~0ull && tot.touches < 0xFFFFFFFFull &&
+              tot.edges * ktrip < 0xFFFFFFFFull;
     if (deferred) {
       const Ctl& h = *c->h_ctl;
       ok = ok && (h.ev_dmin == ~0ull || h.ev_dmin == h.ev_dmax);
@@ -1390,7 +1431,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 // input is not S-first: the lean hash tier runs next.
 static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
                               const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
-                              uint64_t pre, uint32_t pre_len, uint64_t** noff_out, uint32_t** nlen_out,
+                              const NamePattern& np, uint64_t** noff_out, uint32_t** nlen_out,
                               uint64_t* names_len) {
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   const uint64_t cap = std::min<uint64_t>(1ull << 28, std::max<uint64_t>(4 * n_s, 1ull << 16));
@@ -1401,8 +1442,11 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
   HashLeanArgs H{tbase, tcnt, nullptr, 0, 0, noff, nlen, rows, cols, ktrip};
   H.direct = direct;
   H.direct_cap = cap;
-  H.pre = pre;
-  H.pre_len = pre_len;
+  H.pre = np.pre;
+  H.pre_len = np.pre_len;
+  H.suf = np.suf;
+  H.suf_len = np.suf_len;
+  H.width = np.width;
   phase(c, "table_init");
 #ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
@@ -1580,12 +1624,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool lean_hash_ok = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
                             !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s;
   // decimal names out of S order (or behind one prefix): the direct-address tier first
-  uint64_t pre = 0;
-  uint32_t pre_len = 0;
+  NamePattern np;
   const bool direct_done = lean_hash_ok && !(c->test_flags & (kTestDictHash | kTestNoDirect)) &&
-                           first_segment_prefix(c, in, len, &pre, &pre_len) &&
-                           direct_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, pre,
-                                             pre_len, &hl_noff, &hl_nlen, &hl_names_len);
+                           first_segment_pattern(c, in, len, &np) &&
+                           direct_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, np,
+                                             &hl_noff, &hl_nlen, &hl_names_len);
   const bool hash_done = direct_done || (lean_hash_ok && hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s,
                                                                           (uint32_t)ktrip, rows, cols, &hl_noff,
                                                                           &hl_nlen, &hl_names_len));

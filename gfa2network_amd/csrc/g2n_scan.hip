@@ -9,8 +9,11 @@
 // from an atomic ticket, so every tile before a block's own is resident or done when it looks
 // back (forward progress without relying on launch order).  Each tile publishes a 64-bit status
 // word per tile: bits 63..62 = 1 (aggregate of the tile) or 2 (inclusive prefix through the
-// tile), bits 61..0 the value — one atomic store, so value and flag are never seen torn.  The
-// look-back is done by the first wave, 64 predecessors per step.
+// tile), bits 61..50 the launch's epoch, bits 49..0 the value — one atomic store, so value and
+// flag are never seen torn.  The look-back is done by the first wave, 64 predecessors per step.
+// The epoch and a ticket that only grows (tile = ticket - the launch's base) let launches reuse
+// one status buffer without clearing it: a word of another epoch reads as unpublished (the host
+// clears the buffer once per 4095 launches, and whenever it is reallocated).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,7 +22,8 @@ namespace g2n {
 
 constexpr uint32_t kScanPer = 16;                 // items per thread
 constexpr uint32_t kScanTile = kScanPer * 256;    // items per block
-constexpr unsigned long long kStAgg = 1ull << 62, kStInc = 2ull << 62, kStVal = (1ull << 62) - 1;
+constexpr unsigned long long kStAgg = 1ull << 62, kStInc = 2ull << 62, kStVal = (1ull << 50) - 1;
+constexpr uint32_t kStEpochs = 4095;  // epochs 1 .. 4095 (0 = cleared memory)
 
 __device__ inline unsigned long long status_load(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -32,21 +36,27 @@ __device__ inline void status_store(unsigned long long* p, unsigned long long v)
 // publishes the aggregate, walks back over the predecessors' status words and returns the
 // exclusive prefix of the tile (the inclusive prefix is published before returning).
 __device__ inline unsigned long long lookback(unsigned long long* __restrict__ status, uint64_t tile,
-                                              unsigned long long agg) {
+                                              unsigned long long agg, uint32_t epoch) {
   const int lane = threadIdx.x & 63;
+  const unsigned long long tag = (unsigned long long)epoch << 50;
   if (tile == 0) {
-    if (lane == 0) status_store(&status[0], kStInc | agg);
+    if (lane == 0) status_store(&status[0], kStInc | tag | agg);
     return 0;
   }
-  if (lane == 0) status_store(&status[tile], kStAgg | agg);
+  if (lane == 0) status_store(&status[tile], kStAgg | tag | agg);
+  // a word of another launch (epoch) is not published yet
+  auto load = [&](int64_t q) {
+    const unsigned long long v = status_load(&status[q]);
+    return ((v >> 50) & 0xFFFu) == epoch ? v : 0ull;
+  };
   unsigned long long excl = 0;
   int64_t w = (int64_t)tile - 1;  // highest predecessor of the current window
   while (true) {
     const int64_t q = w - lane;
-    unsigned long long s = q >= 0 ? status_load(&status[q]) : kStInc;  // before tile 0: prefix 0
+    unsigned long long s = q >= 0 ? load(q) : kStInc;  // before tile 0: prefix 0
     // wait until every lane of the window sees a published word
     while (__ballot((s >> 62) == 0)) {
-      if ((s >> 62) == 0) s = status_load(&status[q]);
+      if ((s >> 62) == 0) s = load(q);
       __builtin_amdgcn_s_sleep(1);
     }
     const unsigned long long inc = __ballot((s >> 62) == 2);
@@ -57,19 +67,21 @@ __device__ inline unsigned long long lookback(unsigned long long* __restrict__ s
     if (inc) break;
     w -= 64;
   }
-  if (lane == 0) status_store(&status[tile], kStInc | (excl + agg));
+  if (lane == 0) status_store(&status[tile], kStInc | tag | (excl + agg));
   return excl;
 }
 
 // Exclusive scan of n items of TIn into TOut; *total (optional) = the sum of all items.
-// status: one u64 per tile, zeroed; ticket: one u32, zeroed.
+// status: one u64 per tile, no word of this epoch in it (1 <= epoch <= kStEpochs); ticket: the
+// launch's first ticket is t_base.
 template <class TIn, class TOut>
 __global__ void __launch_bounds__(256) k_scan_excl(const TIn* __restrict__ in, TOut* __restrict__ out, uint64_t n,
                                                    unsigned long long* __restrict__ status,
-                                                   uint32_t* __restrict__ ticket, TOut* __restrict__ total) {
+                                                   unsigned long long* __restrict__ ticket, TOut* __restrict__ total,
+                                                   uint32_t epoch, unsigned long long t_base) {
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_wave[4], s_base;
-  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - t_base);
   __syncthreads();
   const uint64_t tile = s_tile;
   const uint64_t i0 = tile * kScanTile + (uint64_t)threadIdx.x * kScanPer;
@@ -110,7 +122,7 @@ __global__ void __launch_bounds__(256) k_scan_excl(const TIn* __restrict__ in, T
     agg += s_wave[q];
   }
   if (wid == 0) {
-    const unsigned long long b = lookback(status, tile, agg);
+    const unsigned long long b = lookback(status, tile, agg, epoch);
     if (lane == 0) s_base = b;
   }
   __syncthreads();

@@ -112,7 +112,7 @@ int g2n_synth_device(int device, const g2n_synth_spec* spec, void** d_out, size_
     if (hipMemset(tmp, 0, tb) != hipSuccess) { rc = G2N_E_DEVICE; goto done; }
     auto* st = (unsigned long long*)tmp;
     hipLaunchKernelGGL((k_scan_excl<uint64_t, uint64_t>), dim3((unsigned)tiles), dim3(256), 0, 0, (const uint64_t*)dlen,
-                       doff, n, st, (uint32_t*)(st + tiles), (uint64_t*)nullptr);
+                       doff, n, st + 1, st, (uint64_t*)nullptr, 1u, 0ull);  // (zeroed: epoch 1, ticket 0)
   }
   if (hipMemcpy(&last_len, dlen + n - 1, 8, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(&last_off, doff + n - 1, 8, hipMemcpyDeviceToHost) != hipSuccess) { rc = G2N_E_DEVICE; goto done; }

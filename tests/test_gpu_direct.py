@@ -1,6 +1,8 @@
 """The direct-address dictionary tier on the lean front end (k_tile_lean kLeanDirClaim /
 kLeanDirEdges): inputs whose S lines come first and whose segment names are one common prefix
-(possibly empty) followed by a canonical decimal — decimal ids out of S order, minigraph's "s<n>" —
+(possibly empty), a decimal and one common suffix without digits (possibly empty) — the decimal
+canonical, or zero-padded to one width — decimal ids out of S order, minigraph's "s<n>", hifiasm's
+"utg000123l" —
 take a plain array as the dictionary (S line k claims direct[v] = k; an edge name is one random
 4-byte read).  builders.py:190-198: with every S line first and no repeated name, a key's first
 touch is its S line, so node id = S index.  Every case is compared with the oracle, with the lean
@@ -20,10 +22,10 @@ pytestmark = pytest.mark.gpu
 MODES = [{}, {"directed": False}, {"asymmetric": True}]
 
 
-def _gfa(seed, n_s, n_l, prefix="", spread=1, ov="0M"):
+def _gfa(seed, n_s, n_l, prefix="", spread=1, ov="0M", fmt=None, in_order=False):
     r = random.Random(seed)
-    vals = r.sample(range(1, spread * n_s + 1), n_s)  # distinct values, out of S order
-    names = [f"{prefix}{v}" for v in vals]
+    vals = list(range(1, n_s + 1)) if in_order else r.sample(range(1, spread * n_s + 1), n_s)  # distinct values
+    names = [fmt % v if fmt else f"{prefix}{v}" for v in vals]
     lines = [f"S\t{k}\t{'ACGT' * r.randint(0, 3)}\n" for k in names]
     for _ in range(n_l):
         a = r.randrange(n_s)
@@ -41,6 +43,23 @@ def _case(name):
         return _gfa(22, 6000, 30000, prefix="s")[1], True
     if name == "prefix_8_bytes_gaps":  # values up to 3 x the S lines: inside the 4 x table
         return _gfa(23, 6000, 30000, prefix="node_id_", spread=3)[1], True
+    if name == "hifiasm_utg_in_order":  # zero-padded, common suffix: "utg000001l", ...
+        return _gfa(25, 6000, 30000, fmt="utg%06dl", in_order=True)[1], True
+    if name == "zero_padded_shuffled":
+        return _gfa(26, 6000, 30000, fmt="node%07d", spread=3)[1], True
+    if name == "canonical_with_suffix":
+        return _gfa(27, 6000, 30000, fmt="ctg%dc")[1], True
+    if name == "width_break":  # one name one digit wider: value 77 twice (the width keeps names apart)
+        _, L2 = _gfa(28, 6000, 30000, fmt="utg%06dl", in_order=True)
+        return L2[:50] + ["S\tutg0000077l\t*\n"] + L2[50:], False
+    if name == "suffix_break":
+        _, L2 = _gfa(29, 6000, 30000, fmt="utg%06dl", in_order=True)
+        return L2[:50] + ["S\tutg999999c\t*\n"] + L2[50:], False
+    if name == "suffix_with_digit":  # the first name's suffix holds a digit: no pattern
+        return _gfa(30, 6000, 30000, fmt="tig%da1")[1], False
+    if name == "padded_edge_unpadded":  # an edge names "utg77l" (unpadded): not a defined name
+        _, L2 = _gfa(31, 6000, 30000, fmt="utg%06dl", in_order=True)
+        return L2[:7000] + ["L\tutg77l\t+\tutg000003l\t-\t0M\n"] + L2[7000:], False
     if name == "ten_digit_values":
         _, L2 = _gfa(24, 3000, 12000)
         return [ln.replace("S\t", "S\t10000", 1) if ln.startswith("S") else
@@ -73,7 +92,9 @@ def _case(name):
     raise KeyError(name)
 
 
-CASES = ["permuted", "prefix_s", "prefix_8_bytes_gaps", "ten_digit_values", "p_and_header_lines", "repeated_value",
+CASES = ["permuted", "prefix_s", "prefix_8_bytes_gaps", "hifiasm_utg_in_order", "zero_padded_shuffled",
+         "canonical_with_suffix", "width_break", "suffix_break", "suffix_with_digit", "padded_edge_unpadded",
+         "ten_digit_values", "p_and_header_lines", "repeated_value",
          "other_prefix", "leading_zero", "zero", "eleven_digits", "value_past_table", "s_after_edges",
          "edge_to_undefined_value", "edge_to_non_decimal", "unsupported_record", "malformed_link"]
 
