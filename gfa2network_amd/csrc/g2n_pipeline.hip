@@ -53,6 +53,9 @@ enum Slot {
   S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_NSLOTS
 };
 
+#ifndef G2N_PTILE_SMALL_DIV  // partition blocks below 2^24 elements: kPartTile / this many (C2: 8 and 4 alike, 2 slower)
+#define G2N_PTILE_SMALL_DIV 4
+#endif
 #ifndef G2N_FORK_EARLY  // experiment builds: 1 = the deferred side work forked before the partition
 #define G2N_FORK_EARLY 0
 #endif
@@ -431,7 +434,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   const bool words = !t_rows && (sum || !pair);  // passes 1 and 4 (not the two-stream slices' pass 3)
   // elements per partition block: a quarter tile below 2^24 elements, so a small input still spreads
   // over more blocks than the 256 CUs
-  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / 4;
+  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / G2N_PTILE_SMALL_DIV;
   src.tile = ptile;
   const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + ptile - 1) / ptile;
   const uint64_t nm1 = (uint64_t)n_dig1 * n_blk1;  // one stream's count matrix
@@ -734,7 +737,7 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   PartSrc src{(const uint32_t*)rows, (const uint32_t*)cols, n_trip, 1u, nullptr, nullptr, 0, 0, nullptr, nullptr,
               nullptr, 0, nullptr, 0, (uint32_t)low + 1u, enc, nullptr};
   // pass 5: the entries with their values, adjacent transposed twins of one value as one element
-  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / 4;  // as csr_partition
+  const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / G2N_PTILE_SMALL_DIV;  // as csr_partition
   src.tile = ptile;
   const uint64_t n_blk1 = (n_el + ptile - 1) / ptile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
