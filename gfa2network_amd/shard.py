@@ -1291,19 +1291,27 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         r_off[1:] = torch.cumsum(r_lens, 0)
     tm["key_exchange"] = (time.perf_counter() - t1) * 1e3 - tm["partition_keys"]
     t7 = time.perf_counter()
-    ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
+    if world == 1:  # one range: its local dictionary's keys are distinct already, in first-touch order
+        nd = int(r_off.numel()) - 1
+        ids = first_of = torch.arange(nd, dtype=torch.int32, device=dev)
+    else:
+        ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
     tm["dedup_keys"] = (time.perf_counter() - t7) * 1e3
     # order key (source rank, local id) of each distinct key: global first-touch order
     fo = first_of.to(torch.int64)
-    dkey = engine.order_keys(first_of, r_idx, r_kc) if nd else r_idx[:0]
+    dkey = engine.order_keys(first_of, r_idx, r_kc) if nd and world > 1 else r_idx[:0]
     tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
 
-    # 4. global ids: rank of each distinct key's order key among all owners'
+    # 4. global ids: rank of each distinct key's order key among all owners' (one owner: its order)
     t2 = time.perf_counter()
-    all_dkey = C.allgather_v(dkey)
-    n_global = int(sum(x.numel() for x in all_dkey))
-    gid = engine.rank_keys(dkey, all_dkey, rank) if world > 1 else torch.arange(nd, dtype=torch.int64, device=dev)
-    del all_dkey
+    if world > 1:
+        all_dkey = C.allgather_v(dkey)
+        n_global = int(sum(x.numel() for x in all_dkey))
+        gid = engine.rank_keys(dkey, all_dkey, rank)
+        del all_dkey
+    else:
+        n_global = nd
+        gid = torch.arange(nd, dtype=torch.int64, device=dev)
     back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
     gmap = None
     if rank > 0:  # rank 0's map is the identity (step 5)
