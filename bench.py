@@ -853,6 +853,8 @@ def main():
     if world == 1 and not args.no_c5_reference and args.workload == "C4" and args.scale == 1:
         line["scaling_reference"] = scaling_reference(args)
     line["world_size"], line["backend"] = world, ("nccl" if world > 1 else None)
+    if nat.TEST_FLAGS:  # (G2N_TEST_FLAGS forced a non-default path: the line says so)
+        line["test_flags"] = int(nat.TEST_FLAGS)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample_links, n_l))
     if rank == 0 and world == 1 and not args.no_e2e:

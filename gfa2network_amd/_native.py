@@ -57,7 +57,7 @@ TEST_DICT_DIRECT = 2048  # decimal ids in S order through the direct-address tie
 TEST_NO_DIRECT = 4096    # never the direct-address tier: the lean hash tier instead
 TEST_NO_EXT_LEAN = 8192  # bidirected / weighted decimal builds through K1 + the lean parse (not tile-local)
 TEST_NO_DEC_TEXT = 16384  # edge-list export of decimal ids through the names blob (not the arithmetic render)
-TEST_FLAGS = 0
+TEST_FLAGS = int(os.environ.get("G2N_TEST_FLAGS", "0"), 0)  # (diagnostics: force the paths below for a whole run)
 # options.range_flags (include/g2n.h G2N_RANGE_*): set by the sharded / chunked protocol (shard.py)
 RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)
 RANGE_EVIDENCE = 2       # report the range's evidence instead of checking (g2n_build_decimal_range sets it)

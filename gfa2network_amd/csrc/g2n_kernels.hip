@@ -948,11 +948,11 @@ __device__ inline uint64_t tab_window(const uint8_t* buf, const uint16_t* tabm, 
 // (parser.py:179-204, builders.py:205-209) for the canonical spellings only — an optional '-' and 1-9
 // digits without a leading zero; any other spelling (CPython's int() accepts more) or tag is false
 // (the full parse decides)
-__device__ inline bool lean_int_tag(const uint8_t* buf, uint32_t x, uint32_t l, const ParseOpts& op, double* w) {
-  const uint32_t tl = op.wt_len;
+__device__ inline bool lean_int_tag(const uint8_t* buf, uint32_t x, uint32_t l, uint32_t tl, uint64_t wt_pack,
+                                    double* w) {
   if (tl == 0 || tl > 8 || l < tl + 4) return false;
   for (uint32_t k = 0; k < tl; k++)
-    if (buf[x + k] != (uint8_t)(op.wt_pack >> (8 * k))) return false;
+    if (buf[x + k] != (uint8_t)(wt_pack >> (8 * k))) return false;
   if (buf[x + tl] != ':' || buf[x + tl + 1] != 'i' || buf[x + tl + 2] != ':') return false;
   uint32_t j = x + tl + 3, e = x + l;
   const bool neg = buf[j] == '-';
@@ -1020,7 +1020,7 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
     if (op.has_wt) {  // builders.py:205-209: the tag's value, or 1.0 without it
       double wv = 1.0;
       if (p[5] < n) {  // a field after the overlap: exactly one, the weight tag
-        if (m || !lean_int_tag(buf, so + p[5] + 1, n - p[5] - 1, op, &wv)) {
+        if (m || !lean_int_tag(buf, so + p[5] + 1, n - p[5] - 1, op.wt_len, op.wt_pack, &wv)) {
           is.fail = 1;
           return true;
         }
@@ -1778,6 +1778,12 @@ struct HashLeanArgs {
   uint32_t suf_len;      //            ... and common suffix (no digit in it, <= 8 bytes)
   uint64_t suf;
   uint32_t width;        //            0: canonical decimals; w: exactly w digits, leading zeros allowed
+  // the edge passes' extended instance (kExt: bidirected keys / one integer weight tag, lean_line's
+  // rules): node ids 2 id + [ori == '-'] with the reverse twins, the weight of edge e at ew[e]
+  int bidir, has_wt;
+  uint32_t wt_len;
+  uint64_t wt_pack;
+  double* ew;
 };
 
 #ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)
@@ -1853,9 +1859,14 @@ __device__ inline bool lean_s_name(const uint8_t* buf, const uint16_t* tabm, uin
   return true;
 }
 
-// L / E / C line in the link_fast shape (lean_line's): the two names' tile offsets and lengths
+// L / E / C line in the link_fast shape (lean_line's): the two names' tile offsets and lengths.
+// kExt (bidirected / weighted lean tiers): also the orientations (bit 0: the first is '-', bit 1: the
+// second) and, with H.has_wt, the weight — one trailing canonical "<tag>:i:<int>" field or 1.0 without
+// it (builders.py:205-209; another spelling or an extra field is false: the full parse decides)
+template <bool kExt = false>
 __device__ inline bool lean_edge_names(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next,
-                                       uint32_t& xa, uint32_t& la, uint32_t& xb, uint32_t& lb) {
+                                       uint32_t& xa, uint32_t& la, uint32_t& xb, uint32_t& lb,
+                                       const HashLeanArgs* H = nullptr, uint32_t* ori = nullptr, double* wv = nullptr) {
   const uint32_t n = next - 1 - so;
   if (n > 48) return false;
   const uint64_t w = tab_window(buf, tabm, so >> 4);
@@ -1874,7 +1885,46 @@ __device__ inline bool lean_edge_names(const uint8_t* buf, const uint16_t* tabm,
   la = p[1] - p[0] - 1;
   xb = so + p[2] + 1;
   lb = p[3] - p[2] - 1;
+  if constexpr (kExt) {
+    *ori = (c2 == '-' ? 1u : 0u) | (c4 == '-' ? 2u : 0u);
+    *wv = 1.0;
+    if (H->has_wt && p[5] < n &&
+        (m || !lean_int_tag(buf, so + p[5] + 1, n - p[5] - 1, H->wt_len, H->wt_pack, wv)))
+      return false;
+  }
   return true;
+}
+
+// an edge's entries from its two S indices (lean hash / direct tiers): plain, or (kExt, H.bidir)
+// the "name:o" ids 2 i + o and the reverse twins of an undirected bidirected build
+// (builders.py:211-234, lean_line's order); edge index e, its weight when H.has_wt
+template <bool kExt>
+__device__ inline void lean_edge_out(const HashLeanArgs& H, uint64_t e, uint32_t ida, uint32_t idb, uint32_t ori,
+                                     double wv) {
+  const uint64_t o = e * H.ktrip;
+  if constexpr (kExt) {
+    if (H.has_wt) H.ew[e] = wv;
+    if (H.bidir) {
+      const uint32_t ia = 2u * ida + (ori & 1u), ib = 2u * idb + (ori >> 1);
+      H.rows[o] = (int32_t)ia;
+      H.cols[o] = (int32_t)ib;
+      if (H.ktrip == 4) {
+        H.rows[o + 1] = (int32_t)ib;
+        H.cols[o + 1] = (int32_t)ia;
+        H.rows[o + 2] = (int32_t)(ib ^ 1u);
+        H.cols[o + 2] = (int32_t)(ia ^ 1u);
+        H.rows[o + 3] = (int32_t)(ia ^ 1u);
+        H.cols[o + 3] = (int32_t)(ib ^ 1u);
+      }
+      return;
+    }
+  }
+  H.rows[o] = (int32_t)ida;
+  H.cols[o] = (int32_t)idb;
+  if (H.ktrip >= 2) {
+    H.rows[o + 1] = (int32_t)idb;
+    H.cols[o + 1] = (int32_t)ida;
+  }
 }
 
 // key head + hash of the name at tile offset x (input offset t0 + x), the classic tiers' key_hash
@@ -2097,13 +2147,15 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       constexpr uint32_t kDL = G2N_DIRECT_LINES;
 #pragma unroll 1
       for (uint32_t j0 = threadIdx.x; j0 < n_win; j0 += kDL * kLeanTPB) {
-        uint32_t va[kDL], vb[kDL], eo[kDL];  // values (< 2^28), edge index in the window's tile
+        uint32_t va[kDL], vb[kDL], eo[kDL], ori[kDL];  // values (< 2^28), edge index in the window's tile
+        double wv[kDL];
         bool act[kDL];
 #pragma unroll
         for (uint32_t q = 0; q < kDL; q++) {
           const uint32_t j = j0 + q * kLeanTPB;
           act[q] = false;
-          va[q] = vb[q] = eo[q] = 0;
+          va[q] = vb[q] = eo[q] = ori[q] = 0;
+          wv[q] = 1.0;
           if (j >= n_win) continue;
           const uint32_t x = rec[j];
           if (((x >> 15) & 3u) != 2u) continue;
@@ -2111,8 +2163,8 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
           const uint32_t next = line_next(j, o);
           uint32_t xa, la, xb, lb;
           uint64_t a, b;
-          if (!next || !lean_edge_names(buf, tabm, o, next, xa, la, xb, lb) || !lean_direct_value(buf, H, xa, la, a) ||
-              !lean_direct_value(buf, H, xb, lb, b)) {
+          if (!next || !lean_edge_names<kExt>(buf, tabm, o, next, xa, la, xb, lb, &H, &ori[q], &wv[q]) ||
+              !lean_direct_value(buf, H, xa, la, a) || !lean_direct_value(buf, H, xb, lb, b)) {
             is.fail = 1;
             continue;
           }
@@ -2134,13 +2186,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
             is.fail = 1;
             continue;
           }
-          const uint64_t eb = (ebase + eo[q]) * H.ktrip;
-          H.rows[eb] = (int32_t)ida[q];
-          H.cols[eb] = (int32_t)idb[q];
-          if (H.ktrip >= 2) {
-            H.rows[eb + 1] = (int32_t)idb[q];
-            H.cols[eb + 1] = (int32_t)ida[q];
-          }
+          lean_edge_out<kExt>(H, ebase + eo[q], ida[q], idb[q], ori[q], wv[q]);
         }
       }
       continue;  // next window
@@ -2151,13 +2197,16 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
 #pragma unroll 1
       for (uint32_t j0 = threadIdx.x; j0 < n_win; j0 += kHL * kLeanTPB) {
         bool act[kHL];
-        uint32_t xs[2 * kHL], ls[2 * kHL];
+        uint32_t xs[2 * kHL], ls[2 * kHL], ori[kHL];
+        double wv[kHL];
         uint64_t ebs[kHL];
 #pragma unroll
         for (int q = 0; q < kHL; q++) {
           const uint32_t j = j0 + q * kLeanTPB;
           act[q] = false;
           ebs[q] = 0;
+          ori[q] = 0;
+          wv[q] = 1.0;
           xs[2 * q] = xs[2 * q + 1] = 0;
           ls[2 * q] = ls[2 * q + 1] = 0;
           if (j >= n_win) continue;
@@ -2165,12 +2214,13 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
           if (((x >> 15) & 3u) != 2u) continue;
           const uint32_t o = x & 0x7FFFu;
           const uint32_t next = line_next(j, o);
-          if (!next || !lean_edge_names(buf, tabm, o, next, xs[2 * q], ls[2 * q], xs[2 * q + 1], ls[2 * q + 1])) {
+          if (!next || !lean_edge_names<kExt>(buf, tabm, o, next, xs[2 * q], ls[2 * q], xs[2 * q + 1], ls[2 * q + 1],
+                                              &H, &ori[q], &wv[q])) {
             is.fail = 1;
             continue;
           }
           act[q] = true;
-          ebs[q] = (ebase + (x >> 17)) * H.ktrip;
+          ebs[q] = ebase + (x >> 17);  // the edge index
         }
         KeyHead kh[2 * kHL];
         uint64_t h[2 * kHL];
@@ -2194,12 +2244,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
             is.fail = 1;
             continue;
           }
-          H.rows[ebs[q]] = (int32_t)ida;
-          H.cols[ebs[q]] = (int32_t)idb;
-          if (H.ktrip >= 2) {
-            H.rows[ebs[q] + 1] = (int32_t)idb;
-            H.cols[ebs[q] + 1] = (int32_t)ida;
-          }
+          lean_edge_out<kExt>(H, ebs[q], ida, idb, ori[q], wv[q]);
         }
       }
       continue;  // next window
@@ -2821,6 +2866,32 @@ __global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, 
     blob[o + nl] = ':';
     for (uint32_t j = 0; j < ol; j++) blob[o + nl + 1 + j] = (oo & kConstFlag) ? (uint8_t)(oo & 0xFF) : in[oo + j];
   }
+}
+
+// Names of a bidirected lean hash / direct build: S line k's name (noff / nlen, soff = the exclusive
+// scan of nlen) as node 2k "name:+" and node 2k + 1 "name:-" (builders.py:190-198: S minting both)
+__global__ void __launch_bounds__(kTPB) k_names_lean_bidir(const uint8_t* __restrict__ in,
+                                                           const uint64_t* __restrict__ noff,
+                                                           const uint32_t* __restrict__ nlen,
+                                                           const int64_t* __restrict__ soff, uint64_t n_s,
+                                                           int64_t* __restrict__ offs, uint8_t* __restrict__ blob) {
+  const uint64_t k = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (k > n_s) return;
+  const uint64_t o = 2 * (uint64_t)soff[k] + 4 * k;
+  offs[2 * k] = (int64_t)o;
+  if (k == n_s) return;
+  const uint32_t nl = nlen[k];
+  offs[2 * k + 1] = (int64_t)(o + nl + 2);
+  const uint8_t* src = in + noff[k];
+  for (uint32_t j = 0; j < nl; j++) {
+    const uint8_t b = src[j];
+    blob[o + j] = b;
+    blob[o + nl + 2 + j] = b;
+  }
+  blob[o + nl] = ':';
+  blob[o + nl + 1] = '+';
+  blob[o + 2 * nl + 2] = ':';
+  blob[o + 2 * nl + 3] = '-';
 }
 
 // Names of a decimal-id build (the premise held: S line k names "k+1", S lines first): node id's

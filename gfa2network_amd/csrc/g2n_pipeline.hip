@@ -1363,13 +1363,22 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   return false;
 }
 
+// the edge passes' extended fields (bidirected keys / one integer weight tag) from X
+static void lean_ext_args(HashLeanArgs& H, const HashLeanArgs& X) {
+  H.bidir = X.bidir;
+  H.has_wt = X.has_wt;
+  H.wt_len = X.wt_len;
+  H.wt_pack = X.wt_pack;
+  H.ew = X.ew;
+}
+
 // The S-first hash dictionary on the lean front end (k_tile_lean kLeanClaim / kLeanEdges, after K1):
 // S names claimed with node id = S index, then every edge line's names found straight from its
 // staged tile and the stream-order COO written.  False (and a clean slate) when the input is not
 // S-first with unique names in the lean shapes: the classic parse + dictionary tiers run instead.
 static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
                             const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
-                            uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
+                            const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
 #ifndef G2N_HL_LOAD_PCT  // experiment builds: the lean table's maximum load, percent
@@ -1383,7 +1392,8 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
   G2N_HIP(hipMemsetAsync(table, 0xFF, cap * sizeof(DictEntry), c->stream));
   auto* noff = dget<uint64_t>(c, S_NOFF, n_s);
   auto* nlen = dget<uint32_t>(c, S_NLEN, n_s);
-  const HashLeanArgs H{tbase, tcnt, table, cap - 1, cap, noff, nlen, rows, cols, ktrip};
+  HashLeanArgs H{tbase, tcnt, table, cap - 1, cap, noff, nlen, rows, cols, ktrip};
+  lean_ext_args(H, X);
   phase(c, "table_init");
 #ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
@@ -1402,8 +1412,12 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 #ifdef G2N_K2_STAMPS
   G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));  // the claim pass stamped too
 #endif
-  hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
-                     ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  if (H.bidir || H.has_wt)
+    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                       len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  else
+    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
+                       ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "insert_lookup");
 #ifdef G2N_K2_STAMPS
   if (const char* out = std::getenv("G2N_HL_STAMPS_OUT")) {  // diagnostics build only: the edge pass
@@ -1434,7 +1448,7 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 // input is not S-first: the lean hash tier runs next.
 static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
                               const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
-                              const NamePattern& np, uint64_t** noff_out, uint32_t** nlen_out,
+                              const NamePattern& np, const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out,
                               uint64_t* names_len) {
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   const uint64_t cap = std::min<uint64_t>(1ull << 28, std::max<uint64_t>(4 * n_s, 1ull << 16));
@@ -1450,6 +1464,7 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
   H.suf = np.suf;
   H.suf_len = np.suf_len;
   H.width = np.width;
+  lean_ext_args(H, X);
   phase(c, "table_init");
 #ifdef G2N_K2_STAMPS  // every k_tile_lean launch stamps: the buffer must be this build's
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
@@ -1465,8 +1480,13 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
     return false;
   }
   *names_len = c->h_ctl->names_len;
-  hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
-                     len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  if (H.bidir || H.has_wt)
+    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream,
+                       in, len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr,
+                       (uint64_t)0, H);
+  else
+    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+                       len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "direct_lookup");
   sync_ctl(c);
   if (c->h_ctl->int_fail) {
@@ -1624,16 +1644,23 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   uint64_t* hl_noff = nullptr;
   uint32_t* hl_nlen = nullptr;
   uint64_t hl_names_len = 0;
-  const bool lean_hash_ok = n_tiles && !local_done && !int_ids && !bidir && !op.has_wt && !op.strip && !shard_dec &&
-                            !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s;
+  // (bidirected keys and / or one integer weight tag: the edge passes' extended instance)
+  const bool lean_hash_ok = n_tiles && !local_done && !int_ids && (!op.has_wt || wtl <= 8) && !op.strip &&
+                            !shard_dec && !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s;
+  HashLeanArgs X{};
+  X.bidir = bidir ? 1 : 0;
+  X.has_wt = op.has_wt;
+  X.wt_len = (uint32_t)wtl;
+  X.wt_pack = xo.wt_pack;
+  X.ew = E.w;
   // decimal names out of S order (or behind one prefix): the direct-address tier first
   NamePattern np;
   const bool direct_done = lean_hash_ok && !(c->test_flags & (kTestDictHash | kTestNoDirect)) &&
                            first_segment_pattern(c, in, len, &np) &&
                            direct_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, np,
-                                             &hl_noff, &hl_nlen, &hl_names_len);
+                                             X, &hl_noff, &hl_nlen, &hl_names_len);
   const bool hash_done = direct_done || (lean_hash_ok && hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s,
-                                                                          (uint32_t)ktrip, rows, cols, &hl_noff,
+                                                                          (uint32_t)ktrip, rows, cols, X, &hl_noff,
                                                                           &hl_nlen, &hl_names_len));
   bool lean_done = local_done || hash_done;  // rows / cols hold the stream-order COO already
   if (lean && !local_done) {
@@ -1730,7 +1757,19 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   R->n_nodes = (int64_t)n_nodes;
   phase(c, "ids");
   const bool throw_after_ids = (c->test_flags & kTestThrowAfterIds) != 0;
-  if (o->want_node_names && hash_done) {  // node k's name: S line k's (noff / nlen from the claims)
+  if (o->want_node_names && hash_done && bidir) {  // nodes 2k / 2k + 1: S line k's name + ":+" / ":-"
+    auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
+    auto* soff = dget<int64_t>(c, S_TEMP, n_s + 1);
+    scan_excl<uint32_t, int64_t>(c, hl_nlen, soff, n_s, soff + n_s);
+    const uint64_t names_len = 2 * hl_names_len + 4 * n_s;
+    auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
+    hipLaunchKernelGGL(k_names_lean_bidir, dim3(grid_for(n_s + 1)), dim3(kTPB), 0, c->stream, in,
+                       (const uint64_t*)hl_noff, (const uint32_t*)hl_nlen, (const int64_t*)soff, n_s, offs, blob);
+    R->names_bytes = names_len;
+    R->names_blob = blob;
+    R->names_offsets = offs;
+    phase(c, "names");
+  } else if (o->want_node_names && hash_done) {  // node k's name: S line k's (noff / nlen from the claims)
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
     scan_excl<uint32_t, int64_t>(c, hl_nlen, offs, n_nodes);
     hipLaunchKernelGGL(k_names_total, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)hl_nlen, n_nodes, offs, c->ctl);

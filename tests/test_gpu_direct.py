@@ -219,3 +219,66 @@ def test_extended_lean_parse_equals_oracle(gpu, oracle_lib, monkeypatch, case):
             monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_EXT_LEAN)
             assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, wt, dtype, "K1 path")
             monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+
+
+# ---- bidirected / weighted builds on the lean hash and direct tiers (round 5) ----
+def _ext_tier_case(name):
+    r = random.Random(sum(name.encode()))
+    n_s = 3000
+    if name.startswith("permuted"):
+        names = [str(v) for v in r.sample(range(1, n_s + 1), n_s)]
+    else:
+        seen = set()
+        while len(seen) < n_s:
+            seen.add("ctg_%08x" % r.getrandbits(32))
+        names = sorted(seen, key=lambda _: r.random())
+    S = [f"S\t{k}\t{'ACGT' * r.randint(0, 2)}\n" for k in names]
+
+    def link(tag=True):
+        a = r.randrange(n_s)
+        b = min(n_s - 1, a + r.randint(0, 4))
+        t = f"\tRC:i:{r.randint(-50, 99)}" if tag and r.random() < 0.9 else ""
+        return f"L\t{names[a]}\t{r.choice('+-')}\t{names[b]}\t{r.choice('+-')}\t0M{t}\n"
+    L = [link() for _ in range(12000)]
+    tier = "direct_lookup" if name.startswith("permuted") else "insert_lookup"
+    if name in ("permuted", "hashed"):
+        return S + L, tier
+    if name in ("permuted_float_tag", "hashed_float_tag"):
+        return S + L[:100] + [f"L\t{names[1]}\t+\t{names[2]}\t-\t0M\tRC:f:1.5\n"] + L[100:], None
+    if name == "hashed_two_tags":
+        return S + L[:100] + [f"L\t{names[1]}\t+\t{names[2]}\t-\t0M\tRC:i:3\tRC:i:4\n"] + L[100:], None
+    if name == "hashed_no_tags":
+        return S + [link(False) for _ in range(12000)], tier
+    raise KeyError(name)
+
+
+EXT_TIER_CASES = ["permuted", "hashed", "permuted_float_tag", "hashed_float_tag", "hashed_two_tags", "hashed_no_tags"]
+
+
+@pytest.mark.parametrize("case", EXT_TIER_CASES)
+def test_extended_lean_tiers_equal_oracle(gpu, oracle_lib, monkeypatch, case):
+    """Names that are not the decimal ids, built bidirected and / or with a weight tag: the direct and
+    lean hash tiers' edge passes in their extended instance ("name:o" ids 2i + o and the reverse
+    twins, one canonical integer tag per edge; builders.py:199-234, parser.py:179-204).  Every mode x
+    dtype equals the oracle and the classic tiers (TEST_NO_HASH_LEAN); a tag the lean shape refuses
+    sends the build to the full parse when the build reads that tag."""
+    from gfa2network_amd import _native as nat
+
+    lines, tier = _ext_tier_case(case)
+    data = "".join(lines).encode()
+    for mode, wt in EXT_MODES:
+        raw = nat.build_from_buffer(data, nat.make_options(weight_tag=wt, **mode))
+        if raw.status == 0:
+            ph = raw.phase_ms  # (a failed lean pass leaves its phase, then the full parse runs)
+            took = (None if "parse" in ph else "insert_lookup" if "insert_lookup" in ph else
+                    "direct_lookup" if "direct_lookup" in ph else None)
+            want = tier if (tier or wt is None) else None
+            if want is None and wt is None:
+                want = "direct_lookup" if case.startswith("permuted") else "insert_lookup"
+            assert took == want, (case, mode, wt, sorted(ph))
+        for dtype in ("float64", "float32", "int8", "bool"):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, wt)), (case, mode, wt, dtype)
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_HASH_LEAN)
+            assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, wt, dtype, "classic")
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)

@@ -40,11 +40,13 @@ for step in "$@"; do
     pmc)
       OUT_JSON=$R/gpurun_out/${TAG}_pmc.json COMMIT=${COMMIT:-unknown} BENCH_ARGS="$args" \
         bash tools/gpu_counters.sh ${TAG}_ctr "g2n::" || exit 1 ;;
-    ab)  # ab:<lib,lib,...> <bench.py args>: each library in turn (main = libg2n.so, x = exp_x.so), twice
+    ab)  # ab:<lib,lib,...> <bench.py args>: each library in turn (main = libg2n.so, x = exp_x.so; lib@F runs
+         # it with G2N_TEST_FLAGS=F), twice
       libs=${args%% *}; bargs=${args#* }
       for rep in 1 2; do for l in ${libs//,/ }; do
-        lp=$R/gfa2network_amd/_lib/$([ "$l" = main ] && echo libg2n.so || echo exp_$l.so)
-        G2N_LIB=$lp timeout -k 10 ${T_BENCH:-600} python -u bench.py $bargs > ${base}_${l}_$rep.json 2>> $base.err ||
+        ln=${l%@*}; fl=0; [ "$ln" != "$l" ] && fl=${l#*@}
+        lp=$R/gfa2network_amd/_lib/$([ "$ln" = main ] && echo libg2n.so || echo exp_$ln.so)
+        G2N_TEST_FLAGS=$fl G2N_LIB=$lp timeout -k 10 ${T_BENCH:-600} python -u bench.py $bargs > ${base}_${l}_$rep.json 2>> $base.err ||
           { tail -20 $base.err; exit 1; }
         python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d.get('device_ms_per_step'), d.get('phase_ms'))" ${base}_${l}_$rep.json $l
       done; done ;;
