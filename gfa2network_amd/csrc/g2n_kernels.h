@@ -83,7 +83,7 @@ struct Ctl {
   unsigned long long ev_vmax;           //   and its largest edge key
   unsigned long long w_inexact;         // the weighted bucket SUM's exactness broke (k_weight_encode / k_sumw_finish)
   unsigned long long warn_tile;         // tile-local lean parse: the first tile holding an unsupported record
-  unsigned long long warn_off;          //   and that record's byte offset (k_lean_warn; warn_line its line)
+  unsigned long long warn_off;          //   and that record's byte offset (k_tile_lean_check; warn_line its line)
 };
 
 struct ParseOpts {

@@ -1407,8 +1407,16 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restr
                                                           const TileCnt* __restrict__ tbase,
                                                           const TileLean* __restrict__ tlean, uint64_t n_tiles,
                                                           uint64_t n_seg, const TileCnt* __restrict__ tot,
-                                                          uint64_t s_base, Ctl* ctl) {
+                                                          uint64_t s_base, const uint32_t* __restrict__ tunk, Ctl* ctl) {
   const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  if (t == 0 && tunk) {  // the one-shot unsupported-record warning (ParseOpts::tunk): the first such
+    const unsigned long long w = ctl->warn_tile;  // tile's record -> its line and byte offset
+    if (w != ~0ull) {
+      const uint32_t u = tunk[w];
+      ctl->warn_line = tbase[w].lines + (u >> 15);
+      ctl->warn_off = w * kTile + (u & 0x7FFFu);
+    }
+  }
   if (t >= n_tiles) return;
   if (!n_seg) n_seg = tot->segs;  // a whole file: its S lines (the tile scan's total)
   const TileLean e = tlean[t];
@@ -1424,17 +1432,6 @@ __global__ void __launch_bounds__(kTPB) k_tile_lean_check(const TileCnt* __restr
 // once the ranges' counts are exchanged); no edge may precede an S line inside the range; the
 // range's largest edge key goes to the caller too (checked against the file's S count).  d is
 // biased by 2^62 for the unsigned atomics.
-// The one-shot unsupported-record warning of a tile-local lean parse (parser.py:125-131): the first
-// tile holding such a record, its rank among the tile's lines and its offset -> the record's line and
-// byte offset (ctl->warn_line / warn_off), after the tile bases are known.
-__global__ void k_lean_warn(const uint32_t* __restrict__ tunk, const TileCnt* __restrict__ tbase, Ctl* ctl) {
-  const unsigned long long w = ctl->warn_tile;
-  if (w == ~0ull) return;
-  const uint32_t u = tunk[w];
-  ctl->warn_line = tbase[w].lines + (u >> 15);
-  ctl->warn_off = w * kTile + (u & 0x7FFFu);
-}
-
 __global__ void __launch_bounds__(kTPB) k_tile_lean_evidence(const TileCnt* __restrict__ cnt,
                                                              const TileCnt* __restrict__ tbase,
                                                              const TileLean* __restrict__ tlean, uint64_t n_tiles,
@@ -2040,7 +2037,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   // the first kLeanBatch starts: offsets, then every first / second byte load in flight at once,
   // then the kinds (2-bit codes kept for the record pass); any further start one by one.  An
   // unsupported record (parser.py:125-131) fails the pass unless op.tunk takes it: its index among
-  // the thread's starts and its offset, ranked after the scan (the warning's line, k_lean_warn) —
+  // the thread's starts and its offset, ranked after the scan (the warning's line, k_tile_lean_check) —
   // a first byte >= 0x80 still fails (its warning is a UnicodeDecodeError: the full parse decides)
   uint32_t codes = 0, q_unk = ~0u, o_unk = 0;
   auto unsupported = [&](uint32_t q, uint32_t o, uint32_t b0) {

@@ -1248,7 +1248,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
   lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
-  // a whole-file build takes the unsupported-record warning itself (k_lean_warn); a sharded range
+  // a whole-file build takes the unsupported-record warning itself (k_tile_lean_check); a sharded range
   // leaves it to the general protocol
   uint32_t* tunk = warn_ok ? dget<uint32_t>(c, S_TUNK, n_tiles) : nullptr;
   lo.tunk = tunk;
@@ -1315,14 +1315,13 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL(k_struct_scan_parts<TileCnt>, dim3(1), dim3(256), 0, c->stream, part, n_parts, part + n_parts);
     hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
-    if (tunk) hipLaunchKernelGGL(k_lean_warn, dim3(1), dim3(1), 0, c->stream, (const uint32_t*)tunk, (const TileCnt*)tbase, c->ctl);
     if (deferred)  // the range's offset evidence, checked by the caller across ranges
       hipLaunchKernelGGL(k_tile_lean_evidence, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream,
                          (const TileCnt*)tcnt, (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, c->ctl);
     else  // (the file's S count: n_seg_all, or the total the scan just wrote)
       hipLaunchKernelGGL(k_tile_lean_check, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt,
                          (const TileCnt*)tbase, (const TileLean*)tlean, n_tiles, n_seg_all,
-                         (const TileCnt*)(part + n_parts), s_base, c->ctl);
+                         (const TileCnt*)(part + n_parts), s_base, (const uint32_t*)tunk, c->ctl);
     TileCnt tot;
     G2N_HIP(hipMemcpyAsync(&tot, part + n_parts, sizeof(TileCnt), hipMemcpyDeviceToHost, c->stream));
     sync_ctl(c);
@@ -1705,7 +1704,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const uint64_t warn_line = o->unknown_warned ? ~0ull : c->h_ctl->warn_line;
   if (warn_line != ~0ull) R->warn_line = (int64_t)warn_line;  // first unsupported line, warned or not
   if (warn_line != ~0ull && warn_line < err_line) {
-    // (a tile-local lean build has no line starts: k_lean_warn found the record's offset)
+    // (a tile-local lean build has no line starts: k_tile_lean_check found the record's offset)
     uint64_t off = local_done ? c->h_ctl->warn_off : read_dev(c, ls + warn_line);
     uint8_t b = read_dev(c, in + off);
     if (b >= 0x80) {  // parser.py:127 line[:1].decode() raises

@@ -427,9 +427,9 @@ def test_decimal_ids_equal_hash_dictionary(gpu, monkeypatch):
                 monkeypatch.setattr(nat, "TEST_FLAGS", flag)
                 st, ph = _phases(data, **mode)
                 hashed = bool(flag & nat.TEST_DICT_HASH)
-                # the lean S-first hash pass writes the COO itself (no triplets phase) where it applies:
-                # plain (not bidirected) unweighted builds
-                lean_hash = hashed and not (flag & nat.TEST_NO_HASH_LEAN) and not mode.get("bidirected")
+                # the lean S-first hash pass writes the COO itself (no triplets phase): plain builds and,
+                # since round 5, bidirected ones (the extended edge pass)
+                lean_hash = hashed and not (flag & nat.TEST_NO_HASH_LEAN)
                 assert ("insert_lookup" in ph) == hashed and ("triplets" in ph) == (not lean_hash), \
                     (flag, mode, sorted(ph))
                 b = outcome(gpu_run(data, mode, "float64", wt))

@@ -4,7 +4,7 @@ its one-shot warning (GFA 1.1 W lines, comments, blank lines; parser.py:114-131)
 the full parse (K1 + k_tile_parse) before: a line running past a tile's staged window, or any
 unsupported record, failed the lean pass.  Now an S / P / O line needs only its first fields in view,
 and the first unsupported record (ASCII first byte) is located per tile and ranked after the tile
-scan (k_lean_warn).  Every case x mode x dtype equals the oracle and the full parse
+scan (k_tile_lean_check).  Every case x mode x dtype equals the oracle and the full parse
 (TEST_NO_TILE_LOCAL); the eligible ones must take the tile-local path ("tiles" phase absent).
 """
 import random
