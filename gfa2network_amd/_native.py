@@ -37,6 +37,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    "g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_keyset_free",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
 
@@ -261,7 +262,12 @@ def load() -> ctypes.CDLL:
                                             ctypes.POINTER(Result)]
     lib.g2n_order_keys.argtypes = [P, P, P, U64, P, U32, P]
     lib.g2n_rank_keys.argtypes = [P, P, U64, P, P, U32, U32, P]
-    for f in ("g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    lib.g2n_keyset_create.argtypes = [P, ctypes.POINTER(P)]
+    lib.g2n_keyset_add.argtypes = [P, P, U64, P, U64, P, ctypes.POINTER(U64)]
+    lib.g2n_keyset_view.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    lib.g2n_keyset_free.argtypes = [P]
+    lib.g2n_keyset_free.restype = None
+    for f in ("g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
               "g2n_upload_file_range", "g2n_count_device", "g2n_build_decimal_range", "g2n_order_keys",
               "g2n_rank_keys"):
         getattr(lib, f).restype = ctypes.c_int

@@ -32,6 +32,7 @@
 #include "g2n_sym.hip"
 #include "g2n_route.hip"
 #include "g2n_inflate.hip"
+#include "g2n_keyset.hip"
 
 #define G2N_HIP(call)                                                                                      \
   do {                                                                                                     \
@@ -2360,6 +2361,100 @@ void partition_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, ui
   G2N_HIP(hipStreamSynchronize(c->stream));
 }
 
+}  // namespace g2n
+
+// The chunked build's growing key set (g2n_keyset.hip): its own device buffers (the context's arena
+// is reused by the builds between calls), per-call scratch from the context.
+struct g2n_keyset {
+  g2n_context* ctx = nullptr;
+  int device = 0;  // (free needs no context: it may be gone by then)
+  g2n::KsEntry* table = nullptr;
+  uint64_t cap = 0;  // entries, a power of two
+  uint8_t* blob = nullptr;
+  uint64_t blob_len = 0, blob_cap = 0;
+  int64_t* offs = nullptr;  // n + 1
+  uint64_t n = 0, offs_cap = 0;
+};
+
+namespace g2n {
+
+template <class T>
+static void ks_grow(g2n_context* c, T** p, uint64_t* cap, uint64_t used, uint64_t want) {  // keep the first used
+  if (want <= *cap) return;
+  uint64_t nc = *cap ? *cap : 1024;
+  while (nc < want) nc *= 2;
+  T* q = nullptr;
+  if (hipMalloc(&q, nc * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Failure(G2N_E_NOMEM, "keyset: hipMalloc failed");
+  }
+  if (used) G2N_HIP(hipMemcpyAsync(q, *p, used * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  if (*p) G2N_HIP(hipFree(*p));
+  *p = q;
+  *cap = nc;
+}
+
+static void keyset_rehash(g2n_keyset* ks, uint64_t want_keys) {
+  g2n_context* c = ks->ctx;
+  uint64_t cap = ks->cap ? ks->cap : 1024;
+  while (cap < 2 * want_keys) cap *= 2;
+  if (cap == ks->cap) return;
+  if (ks->table) G2N_HIP(hipFree(ks->table));
+  ks->table = nullptr;
+  if (hipMalloc(&ks->table, cap * sizeof(KsEntry)) != hipSuccess) {
+    (void)hipGetLastError();
+    ks->cap = 0;
+    throw Failure(G2N_E_NOMEM, "keyset: hipMalloc of the table failed");
+  }
+  ks->cap = cap;
+  G2N_HIP(hipMemsetAsync(ks->table, 0xFF, cap * sizeof(KsEntry), c->stream));
+  if (ks->n)  // every key again, from the set's own blob
+    hipLaunchKernelGGL(k_ks_insert, dim3(grid_for(ks->n, 256)), dim3(256), 0, c->stream, ks->blob,
+                       (const int64_t*)ks->offs, ks->n, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                       (const int64_t*)nullptr, (uint64_t)0, (uint64_t)0, ks->table, cap - 1, ks->blob, ks->offs,
+                       (uint32_t*)nullptr, 1);
+}
+
+uint64_t keyset_add(g2n_keyset* ks, const uint8_t* blob, const int64_t* offs, uint64_t n, uint32_t* ids) {
+  g2n_context* c = ks->ctx;
+  begin_call(c);
+  if (ks->n + n >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 keys");
+  if (!ks->offs) {
+    ks_grow(c, &ks->offs, &ks->offs_cap, 0, 1024);
+    G2N_HIP(hipMemsetAsync(ks->offs, 0, sizeof(int64_t), c->stream));
+  }
+  if (n == 0) return ks->n;
+  keyset_rehash(ks, ks->n + n);  // load <= 1/2 even if every key is new
+  auto* fresh = dget<uint32_t>(c, S_KEYS0, n);
+  auto* pos = dget<uint32_t>(c, S_KEYS1, n + 1);
+  auto* lens = dget<int64_t>(c, S_FOFF64, n + 1);
+  auto* bpos = dget<int64_t>(c, S_RSCR, n + 1);
+  hipLaunchKernelGGL(k_ks_lookup, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, blob, offs, n,
+                     (const KsEntry*)ks->table, ks->cap - 1, (const uint8_t*)ks->blob, ids, fresh);
+  hipLaunchKernelGGL(k_ks_new_lens, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, offs, (const uint32_t*)fresh, n,
+                     lens);
+  scan_excl<uint32_t, uint32_t>(c, fresh, pos, n, pos + n);
+  G2N_HIP(hipMemsetAsync(lens + n, 0, sizeof(int64_t), c->stream));
+  scan_excl<int64_t, int64_t>(c, lens, bpos, n + 1);
+  uint32_t n_new = 0;
+  int64_t new_bytes = 0;
+  G2N_HIP(hipMemcpyAsync(&n_new, pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipMemcpyAsync(&new_bytes, bpos + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  if (n_new) {
+    ks_grow(c, &ks->blob, &ks->blob_cap, ks->blob_len, ks->blob_len + (uint64_t)new_bytes + 16);
+    ks_grow(c, &ks->offs, &ks->offs_cap, ks->n + 1, ks->n + n_new + 1);
+    hipLaunchKernelGGL(k_ks_insert, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, blob, offs, n,
+                       (const uint32_t*)fresh, (const uint32_t*)pos, (const int64_t*)bpos, ks->n, ks->blob_len,
+                       ks->table, ks->cap - 1, ks->blob, ks->offs, ids, 0);
+    ks->n += n_new;
+    ks->blob_len += (uint64_t)new_bytes;
+  }
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  return ks->n;
+}
+
 uint64_t gather_keys(g2n_context* c, const uint8_t* blob, const int64_t* offs, const uint32_t* index, uint64_t n,
                      uint8_t* oblob, uint64_t oblob_cap, int64_t* ooffs) {
   begin_call(c);
@@ -2639,6 +2734,45 @@ int g2n_gather_keys(g2n_context* ctx, const uint8_t* d_blob, const int64_t* d_of
   G2N_CTX_CALL(ctx, *out_len = g2n::gather_keys(ctx, d_blob, d_offsets, d_index, n, d_out_blob, out_cap,
                                                 d_out_offsets));
   return G2N_OK;
+}
+
+int g2n_keyset_create(g2n_context* ctx, g2n_keyset** out) {
+  if (!ctx || !out) return G2N_E_ARG;
+  *out = new g2n_keyset();
+  (*out)->ctx = ctx;
+  (*out)->device = ctx->device;
+  return G2N_OK;
+}
+
+int g2n_keyset_add(g2n_keyset* ks, const uint8_t* d_blob, uint64_t blob_len, const int64_t* d_offsets, uint64_t n,
+                   uint32_t* d_ids, uint64_t* n_total) {
+  if (!ks || !n_total || (n && (!d_offsets || !d_ids || (blob_len && !d_blob)))) return G2N_E_ARG;
+  g2n_context* ctx = ks->ctx;
+  G2N_CTX_CALL(ctx, *n_total = g2n::keyset_add(ks, d_blob, d_offsets, n, d_ids));
+  return G2N_OK;
+}
+
+int g2n_keyset_view(g2n_keyset* ks, const uint8_t** d_blob, const int64_t** d_offsets, uint64_t* n,
+                    uint64_t* blob_len) {
+  if (!ks || !d_blob || !d_offsets || !n || !blob_len) return G2N_E_ARG;
+  if (!ks->offs) {
+    g2n_context* ctx = ks->ctx;
+    G2N_CTX_CALL(ctx, (void)g2n::keyset_add(ks, nullptr, nullptr, 0, nullptr));
+  }
+  *d_blob = ks->blob;
+  *d_offsets = ks->offs;
+  *n = ks->n;
+  *blob_len = ks->blob_len;
+  return G2N_OK;
+}
+
+void g2n_keyset_free(g2n_keyset* ks) {
+  if (!ks) return;
+  (void)hipSetDevice(ks->device);
+  if (ks->table) (void)hipFree(ks->table);
+  if (ks->blob) (void)hipFree(ks->blob);
+  if (ks->offs) (void)hipFree(ks->offs);
+  delete ks;
 }
 
 int g2n_order_keys(g2n_context* ctx, const uint32_t* d_first_of, const int64_t* d_src_idx, uint64_t nd,

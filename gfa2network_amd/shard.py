@@ -214,6 +214,38 @@ class DevArray:
         return DevArray(self.ptr + a * self.itemsize, max(b - a, 0), self.itemsize)
 
 
+class _HipKeyset:
+    """g2n_keyset on an engine's context: add(blob, offsets) -> (ids int32 of the keys, keys in the set);
+    names() -> the set's keys in id order (copies); close()."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.h = ctypes.c_void_p()
+        eng._check(eng.lib.g2n_keyset_create(eng.ctx, ctypes.byref(self.h)), "g2n_keyset_create")
+
+    def add(self, blob, offsets):
+        torch, eng = self.eng.torch, self.eng
+        n = offsets.numel() - 1
+        ids = torch.empty(max(n, 1), dtype=torch.int32, device=eng.device)
+        tot = ctypes.c_uint64(0)
+        eng._sync()
+        eng._check(eng.lib.g2n_keyset_add(self.h, blob.data_ptr() if blob.numel() else None, blob.numel(),
+                                          offsets.data_ptr(), n, ids.data_ptr(), ctypes.byref(tot)), "g2n_keyset_add")
+        return ids[:n], int(tot.value)
+
+    def names(self):
+        torch, eng = self.eng.torch, self.eng
+        pb, po, n, nb = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        eng._check(eng.lib.g2n_keyset_view(self.h, ctypes.byref(pb), ctypes.byref(po), ctypes.byref(n),
+                                           ctypes.byref(nb)), "g2n_keyset_view")
+        return eng._copy_out(pb.value, int(nb.value), torch.uint8), eng._copy_out(po.value, int(n.value) + 1, torch.int64)
+
+    def close(self):
+        if self.h:
+            self.eng.lib.g2n_keyset_free(self.h)
+            self.h = ctypes.c_void_p()
+
+
 class HipEngine:
     """The product engine: libg2n.so on one GPU; buffers are torch device tensors (or DevArray
     views of a context's arena)."""
@@ -433,6 +465,10 @@ class HipEngine:
                                             offsets.data_ptr(), n, ids.data_ptr(), first.data_ptr(),
                                             ctypes.byref(nd)), "g2n_dedup_keys")
         return ids[:n], first[:nd.value], nd.value
+
+    def keyset(self):
+        """A growing device set of byte keys, ids in insertion order (g2n_keyset_*)."""
+        return _HipKeyset(self)
 
     def gather_keys(self, blob, offsets, index, nbytes: int):
         """Keys index[j] of the blob in that order: (blob of nbytes, offsets)."""
@@ -1008,8 +1044,6 @@ def _chunked_general(src, *, engine, chunk_bytes: int, directed, bidirected, kee
     and every later chunk is built with it already warned (options.unknown_warned)."""
     import time
 
-    import torch
-
     src = _as_source(src)
     free_hbm = free_hbm or engine.free_memory
     opts = dict(directed=directed, bidirected=bidirected, keep_directed_bidir=keep_directed_bidir,
@@ -1021,8 +1055,8 @@ def _chunked_general(src, *, engine, chunk_bytes: int, directed, bidirected, kee
     n_chunks = max(1, -(-src.size // max(1, int(chunk_bytes))))
     t0 = time.perf_counter()
     dev = engine.device
-    g_blob = torch.zeros(0, dtype=torch.uint8, device=dev)  # the file's distinct keys so far, in global id order
-    g_offs = torch.zeros(1, dtype=torch.int64, device=dev)
+    ks = engine.keyset()  # the file's distinct keys so far, in global id order
+    n_g = 0
     parts = []
     n_lines = n_records = n_edges = overflow = n_trip = 0
     warned = None      # (global warn line, warn byte) of the first unsupported record
@@ -1034,73 +1068,67 @@ def _chunked_general(src, *, engine, chunk_bytes: int, directed, bidirected, kee
         return time.perf_counter()
 
     def result(**kw):
-        r = ShardResult(n_lines=n_lines, n_records=n_records, n_edges=n_edges, n_nodes=int(g_offs.numel()) - 1,
+        r = ShardResult(n_lines=n_lines, n_records=n_records, n_edges=n_edges, n_nodes=n_g,
                         n_cast_overflow=overflow, **kw)
         if warned is not None:
             r.has_warning, r.warn_line, r.warn_byte = True, warned[0], warned[1]
         return r
 
-    for lo, hi in src.ranges(n_chunks):
-        t = time.perf_counter()
-        buf = src.upload(engine, lo, hi)
-        t = lap("read", t)
-        sh = engine.local_build(buf, opts, unknown_warned=warned is not None)
-        if warned is None and sh.has_warning and not (sh.status == 8 and sh.err_line == sh.warn_line):
-            warned = (n_lines + sh.warn_line, sh.warn_byte)
-        del buf
-        t = lap("local_build", t)
-        if sh.status != 0 and sh.status not in CAST_ERRORS:  # a parse error: the build ends here
-            if warned is not None and warned[0] >= n_lines + sh.err_line:
-                warned = None  # (the warning would have come after the error)
-            out = result(status=int(sh.status), err_line=n_lines + int(sh.err_line), err_detail=sh.err_detail)
-            out.n_lines, out.n_records = n_lines + int(sh.n_lines), n_records + int(sh.n_records)
-            out.n_records_before_error = n_records + int(sh.n_records_before_error)
-            return out
-        n_lines += int(sh.n_lines)
-        n_records += int(sh.n_records)
-        if sh.status in CAST_ERRORS:
-            if cast_err is None:
-                cast_err = (int(sh.status), n_trip + int(sh.err_index), float(sh.err_value))
-            continue
-        n_edges += int(sh.n_edges)
-        overflow += int(sh.n_cast_overflow)
+    try:
+        for lo, hi in src.ranges(n_chunks):
+            t = time.perf_counter()
+            buf = src.upload(engine, lo, hi)
+            t = lap("read", t)
+            sh = engine.local_build(buf, opts, unknown_warned=warned is not None)
+            if warned is None and sh.has_warning and not (sh.status == 8 and sh.err_line == sh.warn_line):
+                warned = (n_lines + sh.warn_line, sh.warn_byte)
+            del buf
+            t = lap("local_build", t)
+            if sh.status != 0 and sh.status not in CAST_ERRORS:  # a parse error: the build ends here
+                if warned is not None and warned[0] >= n_lines + sh.err_line:
+                    warned = None  # (the warning would have come after the error)
+                out = result(status=int(sh.status), err_line=n_lines + int(sh.err_line), err_detail=sh.err_detail)
+                out.n_lines, out.n_records = n_lines + int(sh.n_lines), n_records + int(sh.n_records)
+                out.n_records_before_error = n_records + int(sh.n_records_before_error)
+                return out
+            n_lines += int(sh.n_lines)
+            n_records += int(sh.n_records)
+            if sh.status in CAST_ERRORS:
+                if cast_err is None:
+                    cast_err = (int(sh.status), n_trip + int(sh.err_index), float(sh.err_value))
+                continue
+            n_edges += int(sh.n_edges)
+            overflow += int(sh.n_cast_overflow)
+            if cast_err is not None:
+                continue  # (the build raises the cast error; only later parse errors still matter)
+            n_l = int(sh.n_local_nodes)
+            ids, n_g = ks.add(sh.names_blob.to(dev), sh.names_offsets.to(dev))
+            t = lap("merge_keys", t)
+            rows, cols = sh.rows, sh.cols
+            if n_l and rows.numel():
+                rows, cols = engine.remap_pairs(rows, cols, ids[:n_l].contiguous())
+            t = lap("remap", t)
+            n_trip += int(rows.numel())
+            parts.append(_keep_part(keep_host, rows, cols, sh.data))
+            del rows, cols, sh
         if cast_err is not None:
-            continue  # (the build raises the cast error; only later parse errors still matter)
-        n_g, n_l = int(g_offs.numel()) - 1, int(sh.n_local_nodes)
-        blob = torch.cat([g_blob, sh.names_blob.to(dev)])
-        offs = torch.cat([g_offs, sh.names_offsets.to(dev)[1:] + g_offs[-1]])
-        ids, first_of, nd = engine.dedup_keys(blob, offs)
-        if nd > n_g:  # the chunk's new keys, in global id order, appended to the file's names
-            idx = first_of[n_g:nd]
-            idx64 = idx.to(torch.int64)
-            nbytes = int((offs[idx64 + 1] - offs[idx64]).sum().item())
-            nb, no = engine.gather_keys(blob, offs, idx, nbytes)
-            g_blob = torch.cat([g_blob, nb[:nbytes]])
-            g_offs = torch.cat([g_offs, no[1:] + g_offs[-1]])
-        del blob, offs
-        t = lap("merge_keys", t)
-        rows, cols = sh.rows, sh.cols
-        if n_l and rows.numel():
-            rows, cols = engine.remap_pairs(rows, cols, ids[n_g:n_g + n_l].contiguous())
-        t = lap("remap", t)
-        n_trip += int(rows.numel())
-        parts.append(_keep_part(keep_host, rows, cols, sh.data))
-        del rows, cols, sh
-    if cast_err is not None:
-        return result(status=cast_err[0], err_index=cast_err[1], err_value=cast_err[2])
-    n = int(g_offs.numel()) - 1
-    if n >= INT32_MAX:
-        return None
-    tm["build"] = (time.perf_counter() - t0) * 1e3
-    out = result(status=0)
-    out.n_records_before_error = n_records
-    if gather_names:
-        out.names_blob, out.names_offsets = g_blob.cpu().numpy(), g_offs.cpu().numpy()
-    del g_blob, g_offs
-    _finish_chunked(engine, out, parts, n, maxsym, uniform, dtype, keep_coo, tm, free_hbm, bands)
-    out.parse_path = "chunked general"
-    out.timings_ms = tm
-    return out
+            return result(status=cast_err[0], err_index=cast_err[1], err_value=cast_err[2])
+        n = n_g
+        if n >= INT32_MAX:
+            return None
+        tm["build"] = (time.perf_counter() - t0) * 1e3
+        out = result(status=0)
+        out.n_records_before_error = n_records
+        if gather_names:
+            nb, no = ks.names()
+            out.names_blob, out.names_offsets = nb.cpu().numpy(), no.cpu().numpy()
+        ks.close()  # before the assembly: its memory goes, and the engine's reset replaces the context
+        _finish_chunked(engine, out, parts, n, maxsym, uniform, dtype, keep_coo, tm, free_hbm, bands)
+        out.parse_path = "chunked general"
+        out.timings_ms = tm
+        return out
+    finally:
+        ks.close()
 
 
 def _chunked_decimal(src, *, engine, chunk_bytes: int, directed=True, keep_directed_bidir=False, asymmetric=False,

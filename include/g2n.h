@@ -312,6 +312,22 @@ int g2n_build_device(g2n_context *ctx, const void *d_input, size_t len, const g2
 int g2n_dedup_keys(g2n_context *ctx, const uint8_t *d_blob, uint64_t blob_len, const int64_t *d_offsets,
                    uint64_t n, uint32_t *d_ids, uint32_t *d_first, uint64_t *n_distinct);
 
+/* A growing device set of byte keys with dense ids in insertion order (the chunked build's
+ * file-wide names, gfa2network_amd/shard.py _chunked_general; replaces re-running
+ * g2n_dedup_keys over every key so far for each chunk).  g2n_keyset_add looks up keys i < n
+ * (d_blob / d_offsets as for g2n_dedup_keys; DISTINCT within one call): d_ids[i] = the key's id,
+ * a key not in the set yet taking the next id in call order (builders.py:194-198 first-touch
+ * minting); *n_total = keys in the set after the call.  g2n_keyset_view: the set's keys in id
+ * order (device pointers owned by the set, valid until its next add or free).  The set works on
+ * ctx's device and stream; ctx must outlive every add / view (g2n_keyset_free does not use it). */
+typedef struct g2n_keyset g2n_keyset;
+int g2n_keyset_create(g2n_context *ctx, g2n_keyset **out);
+int g2n_keyset_add(g2n_keyset *ks, const uint8_t *d_blob, uint64_t blob_len, const int64_t *d_offsets, uint64_t n,
+                   uint32_t *d_ids, uint64_t *n_total);
+int g2n_keyset_view(g2n_keyset *ks, const uint8_t **d_blob, const int64_t **d_offsets, uint64_t *n,
+                    uint64_t *blob_len);
+void g2n_keyset_free(g2n_keyset *ks);
+
 /* Key i of the names blob goes to rank (FNV-1a of its bytes) mod n_ranks: the keys, grouped
  * by rank (order kept within a rank), to d_out_blob / d_out_offsets (n + 1); d_out_index[j] =
  * the input index of output key j; d_starts[r] = first output key of rank r. */

@@ -17,6 +17,32 @@ from gfa2network_amd.shard import TORCH_DTYPES, LocalShard
 NP = {"bool": np.uint8, "int8": np.int8, "int32": np.int32, "float32": np.float32, "float64": np.float64}
 
 
+class _CpuKeyset:
+    """HipEngine.keyset's contract on the host: ids in insertion order, the keys of one add distinct."""
+
+    def __init__(self):
+        self.ids, self.keys = {}, []
+
+    def add(self, blob, offsets):
+        b, off = blob.numpy().tobytes(), offsets.numpy()
+        out = []
+        for i in range(len(off) - 1):
+            k = b[off[i]:off[i + 1]]
+            if k not in self.ids:
+                self.ids[k] = len(self.keys)
+                self.keys.append(k)
+            out.append(self.ids[k])
+        return torch.tensor(out, dtype=torch.int32), len(self.keys)
+
+    def names(self):
+        offs = np.zeros(len(self.keys) + 1, dtype=np.int64)
+        np.cumsum([len(k) for k in self.keys], out=offs[1:])
+        return torch.from_numpy(np.frombuffer(b"".join(self.keys), dtype=np.uint8).copy()), torch.from_numpy(offs)
+
+    def close(self):
+        pass
+
+
 class CpuEngine:
     device = torch.device("cpu")
 
@@ -170,6 +196,9 @@ class CpuEngine:
                 first.append(i)
             ids.append(seen[k])
         return (torch.tensor(ids, dtype=torch.int32), torch.tensor(first, dtype=torch.int32), len(first))
+
+    def keyset(self):
+        return _CpuKeyset()
 
     def gather_keys(self, blob, offsets, index, nbytes):
         b, off = blob.numpy().tobytes(), offsets.numpy()
