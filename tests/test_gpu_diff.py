@@ -687,3 +687,20 @@ def test_convert_format_int64_path_equals_oracle(gpu, oracle_lib, monkeypatch, c
                         and C.data.tobytes() == ref.data.tobytes()):
                     bad.append((mode, dtype, fmt))
     assert not bad, bad[:4]
+
+
+def test_scan_status_epochs_wrap(gpu, oracle_lib):
+    """The single-pass scans reuse their status buffers by epoch (g2n_scan.hip: 4095 epochs, then
+    the buffer is cleared): 1500 builds on one context — several scans each, past the wrap on every
+    slot — all equal the first and the oracle (a stale word taken as published would shift offsets)."""
+    from gfa2network_amd import _native as nat
+
+    data = _canonical_gfa(3, 700, 2500, False, False)
+    want = outcome(oracle_run(oracle_lib, data, {"directed": False}, "float64", None))
+    first = None
+    for i in range(1500):
+        raw = nat.build_from_buffer(data, nat.make_options(directed=False, output=nat.OUT_CSR))
+        key = (raw.status, raw.indptr.tobytes(), raw.indices.tobytes(), raw.data.tobytes())
+        first = first or key
+        assert key == first, i
+    assert outcome(gpu_run(data, {"directed": False}, "float64", None)) == want
