@@ -784,6 +784,7 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   // partition buffer's 8 bytes per element, values in their own array
   auto* tcol = (uint32_t*)(el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1);
   T* tval = dget<T>(c, S_TVAL, 2 * n_el);
+  fork_side(c);  // the deferred names beside the finish (as csr_partition), not after the CSR
   hipLaunchKernelGGL((k_sumw_finish<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el, ew,
                      (const uint32_t*)bst, (uint32_t)low, n_rows, btot, tcol, tval, indptr, c->ctl);
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
@@ -1590,8 +1591,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const size_t wtl = o->weight_tag ? std::strlen(o->weight_tag) : 0;
   op.has_wt = wtl > 0;
   op.wt_len = (uint32_t)wtl;
-  if (wtl) {
-    auto* wt = dget<uint8_t>(c, S_WT, wtl);
+  if (wtl && !local_done) {  // (the full parse's copy; a tile-local build compared the tag in place: a pageable
+    auto* wt = dget<uint8_t>(c, S_WT, wtl);  // H2D copy is a host wait)
     G2N_HIP(hipMemcpyAsync(wt, o->weight_tag, wtl, hipMemcpyHostToDevice, c->stream));
     op.wt = wt;
   }
@@ -1859,9 +1860,12 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     }
     phase(c, "triplets");
   }
-  sync_ctl(c);
-  const uint64_t cast_key = c->h_ctl->cast_key;
-  R->n_cast_overflow = (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip);
+  // the cast's verdict needs a host wait only when a cast ran (a build whose values are all dtype(1)
+  // and unread — C2, C4 — goes on to the assembly without one)
+  const bool cast_ran = !coords_done || (n_e && (coo_out || !uni) && !no_values);
+  if (cast_ran) sync_ctl(c);
+  const uint64_t cast_key = cast_ran ? c->h_ctl->cast_key : ~0ull;
+  R->n_cast_overflow = cast_ran ? (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip) : 0;
   if (cast_key != ~0ull) {  // np.array(data, dtype) raises at the first bad element
     R->status = (int)(cast_key & 15);
     R->err_index = (int64_t)(cast_key >> 4);
