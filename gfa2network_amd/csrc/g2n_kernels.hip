@@ -1783,6 +1783,22 @@ struct HashLeanArgs {
   double* ew;
 };
 
+#ifndef G2N_DIRECT_STORE  // kLeanDirClaim: 1 = plain stores + a count of the filled slots, 0 = CAS per S line
+#define G2N_DIRECT_STORE 1
+#endif
+
+// the direct array's filled slots (!= ~0u), added to *out: the claim pass's duplicate check
+__global__ void __launch_bounds__(256) k_direct_filled(const uint4* __restrict__ a, uint64_t n4,
+                                                       unsigned long long* out) {
+  uint32_t c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256) {
+    const uint4 v = a[i];
+    c += (v.x != ~0u) + (v.y != ~0u) + (v.z != ~0u) + (v.w != ~0u);
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
 #ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)
 #define G2N_DIRECT_LINES 4
 #endif
@@ -2371,11 +2387,17 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
           continue;
         }
         const uint32_t id = (uint32_t)(sbase + pref);
-        // (plain stores plus a verify pass measured slower: 4.13 against 3.70 ms on C4's 50M S lines)
+#if G2N_DIRECT_STORE
+        // a plain store: a repeated value leaves fewer filled slots than S lines, which one count of
+        // the array after the pass finds (k_direct_filled; a verify pass re-staging the tiles measured
+        // slower: 4.13 against 3.70 ms)
+        H.direct[v] = id;
+#else
         if (atomicCAS(H.direct + v, ~0u, id) != ~0u) {  // a repeated S name: the classic tiers decide
           is.fail = 1;
           continue;
         }
+#endif
         H.noff[id] = t0 + x;
         H.nlen[id] = l;
         claimed_bytes += l;

@@ -1474,9 +1474,14 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
 #endif
   hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
                      len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+#if G2N_DIRECT_STORE  // (cap is a multiple of 4)
+  G2N_HIP(hipMemsetAsync(&c->ctl->n_keep, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(k_direct_filled, dim3((unsigned)std::min<uint64_t>(grid_for(cap / 4, 256), 4096)), dim3(256), 0,
+                     c->stream, (const uint4*)direct, cap / 4, &c->ctl->n_keep);
+#endif
   phase(c, "direct_claim");
   sync_ctl(c);
-  if (c->h_ctl->int_fail) {
+  if (c->h_ctl->int_fail || (G2N_DIRECT_STORE && c->h_ctl->n_keep != n_s)) {  // (a repeated value: fewer filled)
     reset_ctl(c);
     return false;
   }
