@@ -1768,6 +1768,8 @@ struct HashLeanArgs {
   int32_t* rows;         // kLeanEdges: stream-order COO, ktrip entries per edge line
   int32_t* cols;
   uint32_t ktrip;
+  const uint32_t* tlist; // the launch's tiles (k_tile_lists; block b parses tile tlist[b]), or null: tile b
+  uint32_t* tnb;         // kLeanClaim / kLeanDirClaim: name bytes claimed per block (< 2^15 per tile)
   uint32_t* direct;      // kLeanDir*: name value -> node id (~0u: no S line names it)
   uint64_t direct_cap;   //            values below this
   uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
@@ -1786,6 +1788,50 @@ struct HashLeanArgs {
 #ifndef G2N_DIRECT_STORE  // kLeanDirClaim: 1 = plain stores + a count of the filled slots, 0 = CAS per S line
 #define G2N_DIRECT_STORE 1
 #endif
+
+// The lean hash / direct passes' tiles, from K1's counts: lists[0] / lists[1] = how many tiles hold
+// S or P / O lines (the claim passes) / edge lines (the edge passes), their indices at lists + 2 /
+// lists + 2 + n_tiles (one atomic per wave: ascending within a wave).  A pass launched over its list
+// instead of every tile: ~158K of C4's 192K tiles hold no S line, and a block that only reads its
+// counts and exits still costs its dispatch (a claim pass over all tiles measured 3.2 ms with the
+// stores taken out).
+__global__ void __launch_bounds__(kTPB) k_tile_lists(const TileCnt* __restrict__ tcnt, uint64_t n_tiles,
+                                                     uint32_t* __restrict__ lists) {
+  const uint64_t t = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+  bool cl = false, ed = false;
+  if (t < n_tiles) {
+    const TileCnt c = tcnt[t];
+    cl = !(c.segs == 0 && c.recs == c.segs + c.edges);
+    ed = c.edges != 0;
+  }
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1;
+  const unsigned long long bc = __ballot(cl), be = __ballot(ed);
+  uint32_t pc = 0, pe = 0;
+  if (lane == 0) {
+    if (bc) pc = atomicAdd(&lists[0], (uint32_t)__popcll(bc));
+    if (be) pe = atomicAdd(&lists[1], (uint32_t)__popcll(be));
+  }
+  pc = __shfl(pc, 0, 64);
+  pe = __shfl(pe, 0, 64);
+  if (cl) lists[2 + pc + __popcll(bc & below)] = (uint32_t)t;
+  if (ed) lists[2 + n_tiles + pe + __popcll(be & below)] = (uint32_t)t;
+}
+
+// *out = a[0] + ... + a[n - 1] (one block)
+__global__ void __launch_bounds__(1024) k_u32_total(const uint32_t* __restrict__ a, uint64_t n,
+                                                    unsigned long long* out) {
+  __shared__ unsigned long long red[16];
+  unsigned long long x = 0;
+  for (uint64_t i = threadIdx.x; i < n; i += 1024) x += a[i];
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; w++) x += red[w];
+    *out = x;
+  }
+}
 
 // the direct array's filled slots (!= ~0u), added to *out: the claim pass's duplicate check
 __global__ void __launch_bounds__(256) k_direct_filled(const uint4* __restrict__ a, uint64_t n4,
@@ -2452,9 +2498,16 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
     if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
     if constexpr (kMode == kLeanClaim || kMode == kLeanDirClaim) {
+      // the block's name bytes at H.tnb[block] (k_u32_total sums them): one atomic per wave on one
+      // address measured ~2.7 ms of a 3.3 ms claim pass (34K tiles x 8 waves, serialised)
       unsigned long long nb = claimed_bytes;
       for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
-      if ((threadIdx.x & 63) == 0 && nb) atomicAdd(&ctl->names_len, nb);
+      if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = nb;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < kW; w++) nb += red64[w];
+        H.tnb[blockIdx.x] = (uint32_t)nb;
+      }
     }
 #ifdef G2N_K2_STAMPS
     K2_LEAN_STAMP(6);
@@ -2533,7 +2586,7 @@ template <int kMode, bool kGrouped, bool kExt = false>
 __global__ void G2N_LEAN_ATTR
     k_tile_lean(const uint8_t* __restrict__ in, uint64_t len, ParseOpts op, Ctl* ctl, TileCnt* __restrict__ tcnt_out,
                 TileLean* __restrict__ tlean, uint32_t* __restrict__ gcount, uint64_t gcap, HashLeanArgs H) {
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = kMode != kLeanDecimal && H.tlist ? (uint64_t)H.tlist[blockIdx.x] : (uint64_t)blockIdx.x;
   if constexpr (kMode != kLeanDecimal) {  // a pass that already failed elsewhere: the rest is wasted work
     if (*(volatile const unsigned long long*)&ctl->int_fail) return;
   }

@@ -51,7 +51,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_TUNK, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_TLIST, S_TNB, S_NSLOTS
 };
 
 #ifndef G2N_PTILE_SMALL_DIV  // partition blocks below 2^24 elements: kPartTile / this many (C2: 8 and 4 alike, 2 slower)
@@ -1373,13 +1373,23 @@ static void lean_ext_args(HashLeanArgs& H, const HashLeanArgs& X) {
   H.ew = X.ew;
 }
 
+// the lean hash / direct passes' tiles (k_tile_lists): claim = tiles with S or P / O lines, edge = with edge lines
+struct TileLists {
+  const uint32_t* claim = nullptr;
+  uint64_t n_claim = 0;
+  const uint32_t* edge = nullptr;
+  uint64_t n_edge = 0;
+};
+
 // The S-first hash dictionary on the lean front end (k_tile_lean kLeanClaim / kLeanEdges, after K1):
 // S names claimed with node id = S index, then every edge line's names found straight from its
 // staged tile and the stream-order COO written.  False (and a clean slate) when the input is not
 // S-first with unique names in the lean shapes: the classic parse + dictionary tiers run instead.
-static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
+static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, const TileLists& TL, const TileCnt* tcnt,
                             const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
                             const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
+  const uint64_t n_tiles = (len + kTile - 1) / kTile;
+  (void)n_tiles;
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
 #ifndef G2N_HL_LOAD_PCT  // experiment builds: the lean table's maximum load, percent
@@ -1401,8 +1411,12 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
   G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_k2_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
                                  c->stream));
 #endif
-  hipLaunchKernelGGL((k_tile_lean<kLeanClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
+  H.tlist = TL.claim;
+  H.tnb = dget<uint32_t>(c, S_TNB, TL.n_claim);
+  hipLaunchKernelGGL((k_tile_lean<kLeanClaim, false>), dim3((unsigned)TL.n_claim), dim3(kLeanTPB), 0, c->stream, in, len,
                      ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
+  hipLaunchKernelGGL(k_u32_total, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)H.tnb, TL.n_claim,
+                     &c->ctl->names_len);
   phase(c, "insert_claim");
   sync_ctl(c);
   if (c->h_ctl->int_fail) {
@@ -1413,11 +1427,13 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 #ifdef G2N_K2_STAMPS
   G2N_HIP(hipMemsetAsync(stamps, 0, n_tiles * kK2Stamps * 8, c->stream));  // the claim pass stamped too
 #endif
-  if (H.bidir || H.has_wt)
-    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+  H.tlist = TL.edge;
+  if (!TL.n_edge) {
+  } else if (H.bidir || H.has_wt)
+    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false, true>), dim3((unsigned)TL.n_edge), dim3(kLeanTPB), 0, c->stream, in,
                        len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   else
-    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in, len,
+    hipLaunchKernelGGL((k_tile_lean<kLeanEdges, false>), dim3((unsigned)TL.n_edge), dim3(kLeanTPB), 0, c->stream, in, len,
                        ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "insert_lookup");
 #ifdef G2N_K2_STAMPS
@@ -1447,10 +1463,12 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uin
 // lines (at least 64 Ki, at most 2^28 values: 1 GiB): ids "1".."N" out of order, or with gaps, fit.
 // False (and a clean slate) when any name breaks the shape, a value repeats or passes cap, or the
 // input is not S-first: the lean hash tier runs next.
-static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, const TileCnt* tcnt,
+static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, const TileLists& TL, const TileCnt* tcnt,
                               const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
                               const NamePattern& np, const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out,
                               uint64_t* names_len) {
+  const uint64_t n_tiles = (len + kTile - 1) / kTile;
+  (void)n_tiles;
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   const uint64_t cap = std::min<uint64_t>(1ull << 28, std::max<uint64_t>(4 * n_s, 1ull << 16));
   auto* direct = dget<uint32_t>(c, S_DIRECT, cap);
@@ -1472,13 +1490,17 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
   G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_k2_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
                                  c->stream));
 #endif
-  hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+  H.tlist = TL.claim;
+  H.tnb = dget<uint32_t>(c, S_TNB, TL.n_claim);
+  hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)TL.n_claim), dim3(kLeanTPB), 0, c->stream, in,
                      len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
 #if G2N_DIRECT_STORE  // (cap is a multiple of 4)
   G2N_HIP(hipMemsetAsync(&c->ctl->n_keep, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(k_direct_filled, dim3((unsigned)std::min<uint64_t>(grid_for(cap / 4, 256), 4096)), dim3(256), 0,
                      c->stream, (const uint4*)direct, cap / 4, &c->ctl->n_keep);
 #endif
+  hipLaunchKernelGGL(k_u32_total, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)H.tnb, TL.n_claim,
+                     &c->ctl->names_len);
   phase(c, "direct_claim");
   sync_ctl(c);
   if (c->h_ctl->int_fail || (G2N_DIRECT_STORE && c->h_ctl->n_keep != n_s)) {  // (a repeated value: fewer filled)
@@ -1486,12 +1508,14 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, u
     return false;
   }
   *names_len = c->h_ctl->names_len;
-  if (H.bidir || H.has_wt)
-    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream,
+  H.tlist = TL.edge;
+  if (!TL.n_edge) {
+  } else if (H.bidir || H.has_wt)
+    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false, true>), dim3((unsigned)TL.n_edge), dim3(kLeanTPB), 0, c->stream,
                        in, len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr,
                        (uint64_t)0, H);
   else
-    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0, c->stream, in,
+    hipLaunchKernelGGL((k_tile_lean<kLeanDirEdges, false>), dim3((unsigned)TL.n_edge), dim3(kLeanTPB), 0, c->stream, in,
                        len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
   phase(c, "direct_lookup");
   sync_ctl(c);
@@ -1560,7 +1584,10 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
                        shard_deferred, ext ? &xo : nullptr, !shard_dec);
   if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
     throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
-  // ---- K1: per-tile counts -> tile bases
+  // ---- K1: per-tile counts -> tile bases (and the lean hash / direct passes' tile lists: names that
+  // are not the decimal ids)
+  TileLists TL;
+  const bool lists_wanted = !first_one && !shard_dec;
   if (n_tiles && !local_done) {
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
     const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
@@ -1570,7 +1597,18 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     hipLaunchKernelGGL(k_struct_scan_parts<TileCnt>, dim3(1), dim3(256), 0, c->stream, part, n_parts, part + n_parts);
     hipLaunchKernelGGL(k_struct_scan_chunks<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
                        (const TileCnt*)tcnt, n_tiles, (const TileCnt*)part, tbase);
-    tot = read_dev(c, part + n_parts);
+    if (lists_wanted) {  // (read with the total: no second wait)
+      auto* lists = dget<uint32_t>(c, S_TLIST, 2 + 2 * n_tiles);
+      G2N_HIP(hipMemsetAsync(lists, 0, 2 * sizeof(uint32_t), c->stream));
+      hipLaunchKernelGGL(k_tile_lists, dim3(grid_for(n_tiles)), dim3(kTPB), 0, c->stream, (const TileCnt*)tcnt, n_tiles,
+                         lists);
+      uint32_t n2[2];
+      G2N_HIP(hipMemcpyAsync(n2, lists, sizeof(n2), hipMemcpyDeviceToHost, c->stream));
+      tot = read_dev(c, part + n_parts);
+      TL = TileLists{lists + 2, n2[0], lists + 2 + n_tiles, n2[1]};
+    } else {
+      tot = read_dev(c, part + n_parts);
+    }
   }
   const uint64_t n_lines = tot.lines;
   const uint64_t n_e = tot.edges, n_s = tot.segs;
@@ -1652,7 +1690,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   uint64_t hl_names_len = 0;
   // (bidirected keys and / or one integer weight tag: the edge passes' extended instance)
   const bool lean_hash_ok = n_tiles && !local_done && !int_ids && (!op.has_wt || wtl <= 8) && !op.strip &&
-                            !shard_dec && !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s;
+                            !shard_dec && !(c->test_flags & (kTestDictGeneral | kTestNoHashLean)) && n_s && TL.claim;
   HashLeanArgs X{};
   X.bidir = bidir ? 1 : 0;
   X.has_wt = op.has_wt;
@@ -1663,9 +1701,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   NamePattern np;
   const bool direct_done = lean_hash_ok && !(c->test_flags & (kTestDictHash | kTestNoDirect)) &&
                            first_segment_pattern(c, in, len, &np) &&
-                           direct_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, np,
+                           direct_lean_build(c, in, len, TL, tcnt, tbase, n_s, (uint32_t)ktrip, rows, cols, np,
                                              X, &hl_noff, &hl_nlen, &hl_names_len);
-  const bool hash_done = direct_done || (lean_hash_ok && hash_lean_build(c, in, len, n_tiles, tcnt, tbase, n_s,
+  const bool hash_done = direct_done || (lean_hash_ok && hash_lean_build(c, in, len, TL, tcnt, tbase, n_s,
                                                                           (uint32_t)ktrip, rows, cols, X, &hl_noff,
                                                                           &hl_nlen, &hl_names_len));
   bool lean_done = local_done || hash_done;  // rows / cols hold the stream-order COO already
