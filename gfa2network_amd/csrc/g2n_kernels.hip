@@ -365,6 +365,82 @@ __global__ void __launch_bounds__(kTPB) k_tile_count(const uint8_t* __restrict__
   }
 }
 
+// K1 without LDS (G2N_K1_REG): thread t of a tile's 512 holds the 16-byte chunks t + 512 j in
+// registers (coalesced loads), the byte before / after a chunk from lane t - 1 / t + 1 (one global
+// byte read per wave and chunk row at each end), each line start's first two bytes picked from the
+// registers.  k_tile_count stages the tile in LDS and reads the starts' bytes back from it.
+#ifndef G2N_K1_REG
+#define G2N_K1_REG 1
+#endif
+constexpr uint32_t kK1TPB = 512;
+constexpr uint32_t kK1Per = (uint32_t)(kTile / 16) / kK1TPB;
+__device__ inline uint32_t chunk_byte(uint4 c, uint32_t b) {  // byte b (< 16) of a chunk
+  const uint32_t q = b >> 2;
+  const uint32_t w = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
+  return (w >> (8 * (b & 3u))) & 0xFFu;
+}
+__global__ void __launch_bounds__(kK1TPB) k_tile_count_r(const uint8_t* __restrict__ in, uint64_t len, uint32_t tps,
+                                                         uint32_t tpe, TileCnt* __restrict__ out) {
+  __shared__ unsigned long long red[2][kK1TPB / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  uint4 v[kK1Per];
+#pragma unroll
+  for (uint32_t j = 0; j < kK1Per; j++) {
+    const uint64_t pos = t0 + 16ull * (j * kK1TPB + threadIdx.x);
+    v[j] = pos < len ? load16(in, pos, len) : make_uint4(0, 0, 0, 0);
+  }
+  const int lane = threadIdx.x & 63;
+  uint32_t n_nl = 0, n_st = 0, segs = 0, edges = 0, po = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kK1Per; j++) {
+    const uint64_t r0 = t0 + 16ull * (j * kK1TPB + threadIdx.x);
+    uint32_t prev_b = (uint32_t)__shfl_up((int)(v[j].w >> 24), 1, 64);
+    uint32_t next_b = (uint32_t)__shfl_down((int)(v[j].x & 0xFFu), 1, 64);
+    if (lane == 0) prev_b = r0 == 0 ? (uint32_t)'\n' : (r0 - 1 < len ? in[r0 - 1] : 0u);
+    if (lane == 63) next_b = r0 + 16 < len ? in[r0 + 16] : 0u;
+    const uint32_t valid = r0 >= len ? 0u : (len - r0 >= 16 ? 0xFFFFu : ((1u << (uint32_t)(len - r0)) - 1u));
+    const uint32_t nl = mask16(v[j], 0x0A0A0A0Au) & valid;
+    uint32_t st = ((nl << 1) | (prev_b == '\n' ? 1u : 0u)) & valid;
+    n_nl += __popc(nl);
+    n_st += __popc(st);
+    while (st) {
+      const uint32_t b = (uint32_t)__builtin_ctz(st);
+      st &= st - 1;
+      const uint32_t c0 = chunk_byte(v[j], b), c1 = b < 15 ? chunk_byte(v[j], b + 1) : next_b;
+      const uint8_t k = line_kind((uint8_t)c0, r0 + b + 1 >= len || c0 == '\n' || c1 == '\t' || c1 == '\n');
+      segs += k == kS;
+      edges += k == kEdge;
+      po += k == kPO;
+    }
+  }
+  unsigned long long a = (unsigned long long)n_nl | ((unsigned long long)n_st << 16) |
+                         ((unsigned long long)segs << 32) | ((unsigned long long)edges << 48);
+  unsigned long long bpo = po;
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    bpo += __shfl_xor(bpo, o, 64);
+  }
+  if (lane == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = bpo;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < kK1TPB / 64; w++) {
+      a += red[0][w];
+      bpo += red[1][w];
+    }
+    TileCnt cnt;
+    cnt.nl = a & 0xFFFF;
+    cnt.lines = (a >> 16) & 0xFFFF;
+    cnt.segs = (a >> 32) & 0xFFFF;
+    cnt.edges = a >> 48;
+    cnt.touches = cnt.segs * tps + cnt.edges * tpe;
+    cnt.recs = cnt.segs + cnt.edges + bpo;
+    out[blockIdx.x] = cnt;
+  }
+}
+
 // ================================================================ K2: parse =======
 __device__ inline void record_error(Ctl* ctl, uint64_t line, uint32_t code) {
   atomicMin(&ctl->err_key, (unsigned long long)((line << 5) | code));

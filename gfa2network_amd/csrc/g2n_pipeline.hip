@@ -1589,7 +1589,10 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   TileLists TL;
   const bool lists_wanted = !first_one && !shard_dec;
   if (n_tiles && !local_done) {
-    hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
+    if (G2N_K1_REG)
+      hipLaunchKernelGGL(k_tile_count_r, dim3((unsigned)n_tiles), dim3(kK1TPB), 0, c->stream, in, len, tps, tpe, tcnt);
+    else
+      hipLaunchKernelGGL(k_tile_count, dim3((unsigned)n_tiles), dim3(kTPB), 0, c->stream, in, len, tps, tpe, tcnt);
     const uint64_t n_parts = (n_tiles + kStructChunk - 1) / kStructChunk;
     auto* part = dget<TileCnt>(c, S_TEMP, n_parts + 1);  // chunk sums, then the total
     hipLaunchKernelGGL(k_struct_reduce<TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, c->stream,
@@ -2875,7 +2878,7 @@ int g2n_count_device(g2n_context* ctx, const void* d_input, size_t len, int64_t*
       auto* tcnt = g2n::dget<g2n::TileCnt>(ctx, g2n::S_TILE_CNT, n_tiles + 1);
       const uint64_t n_parts = (n_tiles + g2n::kStructChunk - 1) / g2n::kStructChunk;
       auto* part = g2n::dget<g2n::TileCnt>(ctx, g2n::S_TEMP, n_parts + 1);
-      hipLaunchKernelGGL(g2n::k_tile_count, dim3((unsigned)n_tiles), dim3(g2n::kTPB), 0, ctx->stream,
+      hipLaunchKernelGGL(g2n::k_tile_count_r, dim3((unsigned)n_tiles), dim3(g2n::kK1TPB), 0, ctx->stream,
                          (const uint8_t*)d_input, (uint64_t)len, 1u, 2u, tcnt);
       hipLaunchKernelGGL(g2n::k_struct_reduce<g2n::TileCnt>, dim3((unsigned)n_parts), dim3(256), 0, ctx->stream,
                          (const g2n::TileCnt*)tcnt, n_tiles, part);
