@@ -1909,16 +1909,21 @@ __global__ void __launch_bounds__(1024) k_u32_total(const uint32_t* __restrict__
   }
 }
 
-// the direct array's filled slots (!= ~0u), added to *out: the claim pass's duplicate check
+// the direct array's filled slots (!= ~0u), added to *out: the claim pass's duplicate check (one
+// atomic per block: atomics on one address serialise, ~7 ns each)
 __global__ void __launch_bounds__(256) k_direct_filled(const uint4* __restrict__ a, uint64_t n4,
                                                        unsigned long long* out) {
+  __shared__ uint32_t red[4];
   uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256) {
     const uint4 v = a[i];
     c += (v.x != ~0u) + (v.y != ~0u) + (v.z != ~0u) + (v.w != ~0u);
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0 && red[0] + red[1] + red[2] + red[3])
+    atomicAdd(out, (unsigned long long)(red[0] + red[1] + red[2] + red[3]));
 }
 
 #ifndef G2N_DIRECT_LINES  // kLeanDirEdges: edge lines per thread per step (2 random reads each in flight)

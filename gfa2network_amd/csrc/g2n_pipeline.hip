@@ -1496,7 +1496,7 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, c
                      len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
 #if G2N_DIRECT_STORE  // (cap is a multiple of 4)
   G2N_HIP(hipMemsetAsync(&c->ctl->n_keep, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL(k_direct_filled, dim3((unsigned)std::min<uint64_t>(grid_for(cap / 4, 256), 4096)), dim3(256), 0,
+  hipLaunchKernelGGL(k_direct_filled, dim3((unsigned)std::min<uint64_t>(grid_for(cap / 4, 256), 2048)), dim3(256), 0,
                      c->stream, (const uint4*)direct, cap / 4, &c->ctl->n_keep);
 #endif
   hipLaunchKernelGGL(k_u32_total, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)H.tnb, TL.n_claim,
