@@ -89,6 +89,14 @@ def _case(name):
         return L[:7000] + ["W\tsample\t1\tchr1\t0\t10\t>x\n"] + L[7000:], False
     if name == "malformed_link":
         return L[:7000] + ["L\t" + names[1] + "\t+\n"] + L[7000:], False
+    # the passes' tile lists (k_tile_lists): no edge line at all; tiles holding only P lines at the
+    # end (claim list, no edge list); an S line in a tile far past the edge-only tiles
+    if name == "s_lines_only":
+        return L[:n], True
+    if name == "p_only_tiles_at_end":
+        return L + ["P\tp%d\t%s+,%s-\t*\n" % (i, names[i], names[i + 1]) for i in range(4000)], True
+    if name == "s_line_in_a_late_tile":
+        return L + ["S\t%d\tAC\n" % (n + 1)] + L[n:n + 3000], False
     raise KeyError(name)
 
 
@@ -96,7 +104,8 @@ CASES = ["permuted", "prefix_s", "prefix_8_bytes_gaps", "hifiasm_utg_in_order", 
          "canonical_with_suffix", "width_break", "suffix_break", "suffix_with_digit", "padded_edge_unpadded",
          "ten_digit_values", "p_and_header_lines", "repeated_value",
          "other_prefix", "leading_zero", "zero", "eleven_digits", "value_past_table", "s_after_edges",
-         "edge_to_undefined_value", "edge_to_non_decimal", "unsupported_record", "malformed_link"]
+         "edge_to_undefined_value", "edge_to_non_decimal", "unsupported_record", "malformed_link",
+         "s_lines_only", "p_only_tiles_at_end", "s_line_in_a_late_tile"]
 
 
 @pytest.mark.parametrize("case", CASES)

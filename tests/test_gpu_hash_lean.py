@@ -61,11 +61,20 @@ def _case(name):
         return L[:7000] + ["W\tsample\t1\tchr1\t0\t10\t>x\n"] + L[7000:], False
     if name == "malformed_link":
         return L[:7000] + ["L\t" + names[1] + "\t+\n"] + L[7000:], False
+    # the passes' tile lists (k_tile_lists): no edge line at all; tiles holding only P lines at the
+    # end (claim list, no edge list); an S line in a tile far past the edge-only tiles
+    if name == "s_lines_only":
+        return L[:6000], True
+    if name == "p_only_tiles_at_end":
+        return L + ["P\tp%d\t%s+,%s-\t*\n" % (i, names[i], names[i + 1]) for i in range(4000)], True
+    if name == "s_line_in_a_late_tile":
+        return L[:6000] + L[6000:] + ["S\tlate_one\tAC\n"] + L[6000:9000], False
     raise KeyError(name)
 
 
 CASES = ["canonical", "p_and_header_lines", "names_of_16_and_17_bytes", "empty_name", "name_only_s_line",
-         "repeated_s_name", "s_after_edges", "edge_to_undefined_name", "unsupported_record", "malformed_link"]
+         "repeated_s_name", "s_after_edges", "edge_to_undefined_name", "unsupported_record", "malformed_link",
+         "s_lines_only", "p_only_tiles_at_end", "s_line_in_a_late_tile"]
 
 
 @pytest.mark.parametrize("case", CASES)
