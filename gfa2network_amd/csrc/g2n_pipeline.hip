@@ -2091,9 +2091,20 @@ static g2n_context* context_create(int device) {
   std::unique_ptr<g2n_context> c(new g2n_context());
   c->device = device;
   G2N_HIP(hipSetDevice(device));
-  G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  G2N_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-  G2N_HIP(hipStreamCreateWithFlags(&c->place, hipStreamNonBlocking));
+#ifndef G2N_SIDE_PRIO  // the side stream (names beside the finish) at the lowest priority, the pipeline at the
+#define G2N_SIDE_PRIO 1  // highest: C4 8.21-8.28 -> 8.05-8.11 ms in a same-box A/B (the names' interference 0.33 ms)
+#endif
+  if (G2N_SIDE_PRIO) {
+    int least = 0, greatest = 0;
+    G2N_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    G2N_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+    G2N_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
+  } else {
+    G2N_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    G2N_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  }
+  G2N_HIP(hipStreamCreateWithFlags(&c->place, hipStreamNonBlocking));  // (F2 at the pipeline's priority or the
+                                                                          // lowest measured slower: 8.11-8.38 ms)
   for (auto& e : c->side_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : c->ov_ev) G2N_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   G2N_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
