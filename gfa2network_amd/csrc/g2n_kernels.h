@@ -84,6 +84,7 @@ struct Ctl {
   unsigned long long w_inexact;         // the weighted bucket SUM's exactness broke (k_weight_encode / k_sumw_finish)
   unsigned long long warn_tile;         // tile-local lean parse: the first tile holding an unsupported record
   unsigned long long warn_off;          //   and that record's byte offset (k_tile_lean_check; warn_line its line)
+  unsigned long long dir_vmax;          // the lean claim passes: the largest claimed value (direct tier)
 };
 
 struct ParseOpts {

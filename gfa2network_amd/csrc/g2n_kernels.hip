@@ -1845,7 +1845,7 @@ struct HashLeanArgs {
   int32_t* cols;
   uint32_t ktrip;
   const uint32_t* tlist; // the launch's tiles (k_tile_lists; block b parses tile tlist[b]), or null: tile b
-  uint32_t* tnb;         // kLeanClaim / kLeanDirClaim: name bytes claimed per block (< 2^15 per tile)
+  unsigned long long* tnb;  // kLeanClaim / kLeanDirClaim, per block: name bytes claimed | the largest value << 32
   uint32_t* direct;      // kLeanDir*: name value -> node id (~0u: no S line names it)
   uint64_t direct_cap;   //            values below this
   uint64_t pre;          //            the names' common prefix, little-endian (pre_len <= 8 bytes)
@@ -1894,26 +1894,41 @@ __global__ void __launch_bounds__(kTPB) k_tile_lists(const TileCnt* __restrict__
   if (ed) lists[2 + n_tiles + pe + __popcll(be & below)] = (uint32_t)t;
 }
 
-// *out = a[0] + ... + a[n - 1] (one block)
-__global__ void __launch_bounds__(1024) k_u32_total(const uint32_t* __restrict__ a, uint64_t n,
-                                                    unsigned long long* out) {
-  __shared__ unsigned long long red[16];
-  unsigned long long x = 0;
-  for (uint64_t i = threadIdx.x; i < n; i += 1024) x += a[i];
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+// the claim pass's per-block (bytes | vmax << 32): *bytes = their sum, *vmax = their largest value (one block)
+__global__ void __launch_bounds__(1024) k_claim_totals(const unsigned long long* __restrict__ a, uint64_t n,
+                                                       unsigned long long* bytes, unsigned long long* vmax) {
+  __shared__ unsigned long long red[16], redm[16];
+  unsigned long long x = 0, m = 0;
+  for (uint64_t i = threadIdx.x; i < n; i += 1024) {
+    x += a[i] & 0xFFFFFFFFull;
+    m = max(m, a[i] >> 32);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    x += __shfl_xor(x, o, 64);
+    m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = x;
+    redm[threadIdx.x >> 6] = m;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 16; w++) x += red[w];
-    *out = x;
+    for (int w = 1; w < 16; w++) {
+      x += red[w];
+      m = max(m, redm[w]);
+    }
+    *bytes = x;
+    *vmax = m;
   }
 }
 
 // the direct array's filled slots (!= ~0u), added to *out: the claim pass's duplicate check (one
 // atomic per block: atomics on one address serialise, ~7 ns each)
-__global__ void __launch_bounds__(256) k_direct_filled(const uint4* __restrict__ a, uint64_t n4,
+__global__ void __launch_bounds__(256) k_direct_filled(const uint4* __restrict__ a, uint64_t cap4,
+                                                       const unsigned long long* __restrict__ vmax,
                                                        unsigned long long* out) {
   __shared__ uint32_t red[4];
+  const uint64_t n4 = min(cap4, *vmax / 4 + 1);  // no claimed value past vmax (the claim pass's largest)
   uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256) {
     const uint4 v = a[i];
@@ -2156,6 +2171,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   K2_LEAN_STAMP(1);
   IntState is;
   uint32_t claimed_bytes = 0;  // kLeanClaim: name bytes of the S lines this thread claimed (names blob size)
+  uint32_t claimed_vmax = 0;   // kLeanDirClaim: the largest value it claimed
   // (2) this thread's region: chunks c0 .. c0 + 3, its starts as one 64-bit mask
   const uint32_t c0 = kLeanRegion * threadIdx.x;
   unsigned long long st;
@@ -2519,6 +2535,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
         // the array after the pass finds (k_direct_filled; a verify pass re-staging the tiles measured
         // slower: 4.13 against 3.70 ms)
         H.direct[v] = id;
+        claimed_vmax = (uint32_t)v > claimed_vmax ? (uint32_t)v : claimed_vmax;
 #else
         if (atomicCAS(H.direct + v, ~0u, id) != ~0u) {  // a repeated S name: the classic tiers decide
           is.fail = 1;
@@ -2579,15 +2596,21 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   if constexpr (kMode != kLeanDecimal) {  // K1 counted the tile already
     if (__ballot(is.fail) && (threadIdx.x & 63) == 0) ctl->int_fail = 1;
     if constexpr (kMode == kLeanClaim || kMode == kLeanDirClaim) {
-      // the block's name bytes at H.tnb[block] (k_u32_total sums them): one atomic per wave on one
-      // address measured ~2.7 ms of a 3.3 ms claim pass (34K tiles x 8 waves, serialised)
-      unsigned long long nb = claimed_bytes;
-      for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
-      if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = nb;
+      // the block's name bytes and largest value at H.tnb[block] (k_claim_totals adds / maxes them): one
+      // atomic per wave on one address measured ~2.7 ms of a 3.3 ms claim pass (34K tiles x 8 waves,
+      // serialised)
+      uint32_t nb = claimed_bytes, vm = claimed_vmax;
+      for (int o = 32; o > 0; o >>= 1) {
+        nb += (uint32_t)__shfl_xor((int)nb, o, 64);
+        vm = max(vm, (uint32_t)__shfl_xor((int)vm, o, 64));
+      }
+      if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = nb | ((unsigned long long)vm << 32);
       __syncthreads();
       if (threadIdx.x == 0) {
-        for (uint32_t w = 1; w < kW; w++) nb += red64[w];
-        H.tnb[blockIdx.x] = (uint32_t)nb;
+        unsigned long long t = red64[0];
+        for (uint32_t w = 1; w < kW; w++)
+          t = ((t & 0xFFFFFFFFull) + (red64[w] & 0xFFFFFFFFull)) | (max(t >> 32, red64[w] >> 32) << 32);
+        H.tnb[blockIdx.x] = t;
       }
     }
 #ifdef G2N_K2_STAMPS
@@ -3003,16 +3026,32 @@ __global__ void k_names_total(const uint32_t* __restrict__ klen, uint64_t n_node
 }
 
 // names blob in id order (builders.py:284-288 node_list): node `id` <- the key bytes of inv[id]
-__global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, TouchIn T, uint64_t n_nodes,
-                                                const uint32_t* __restrict__ inv, const int64_t* __restrict__ offs,
-                                                int bidir, uint8_t* __restrict__ blob) {
+// A name of at most 16 bytes comes from three aligned 8-byte loads (all in flight together) and goes
+// out as predicated byte stores; a longer one, or one within 24 bytes of the input's end, byte by
+// byte (a dependent load per byte held the kernel at ~2 ms for C4's 50M names beside the finish)
+__global__ void __launch_bounds__(kTPB) k_names(const uint8_t* __restrict__ in, uint64_t in_len, TouchIn T,
+                                                uint64_t n_nodes, const uint32_t* __restrict__ inv,
+                                                const int64_t* __restrict__ offs, int bidir,
+                                                uint8_t* __restrict__ blob) {
   const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (id >= n_nodes) return;
   const uint64_t t = inv ? inv[id] : id;  // S-prefix dictionary: id == touch
   const uint64_t o = (uint64_t)offs[id];
   const uint64_t no = T.noff[t];
   const uint32_t nl = T.nlen[t];
-  for (uint32_t j = 0; j < nl; j++) blob[o + j] = in[no + j];
+  // (aligned on the address itself: the input may start anywhere in its allocation, which is aligned)
+  const uint8_t* p = in + no;
+  const uint64_t* w = (const uint64_t*)((uintptr_t)p & ~(uintptr_t)7);
+  if (nl <= 16 && (const uint8_t*)(w + 3) <= in + in_len) {
+    const uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 7) * 8;
+    const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0, hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++)
+      if (j < nl) blob[o + j] = (uint8_t)((j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8))) & 0xFF);
+  } else {
+    for (uint32_t j = 0; j < nl; j++) blob[o + j] = in[no + j];
+  }
   if (bidir) {
     const uint64_t oo = T.ooff[t];
     const uint32_t ol = T.olen[t];

@@ -1412,11 +1412,11 @@ static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, con
                                  c->stream));
 #endif
   H.tlist = TL.claim;
-  H.tnb = dget<uint32_t>(c, S_TNB, TL.n_claim);
+  H.tnb = dget<unsigned long long>(c, S_TNB, TL.n_claim);
   hipLaunchKernelGGL((k_tile_lean<kLeanClaim, false>), dim3((unsigned)TL.n_claim), dim3(kLeanTPB), 0, c->stream, in, len,
                      ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
-  hipLaunchKernelGGL(k_u32_total, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)H.tnb, TL.n_claim,
-                     &c->ctl->names_len);
+  hipLaunchKernelGGL(k_claim_totals, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long*)H.tnb, TL.n_claim,
+                     &c->ctl->names_len, &c->ctl->dir_vmax);
   phase(c, "insert_claim");
   sync_ctl(c);
   if (c->h_ctl->int_fail) {
@@ -1491,16 +1491,17 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, c
                                  c->stream));
 #endif
   H.tlist = TL.claim;
-  H.tnb = dget<uint32_t>(c, S_TNB, TL.n_claim);
+  H.tnb = dget<unsigned long long>(c, S_TNB, TL.n_claim);
   hipLaunchKernelGGL((k_tile_lean<kLeanDirClaim, false>), dim3((unsigned)TL.n_claim), dim3(kLeanTPB), 0, c->stream, in,
                      len, ParseOpts{}, c->ctl, (TileCnt*)nullptr, (TileLean*)nullptr, (uint32_t*)nullptr, (uint64_t)0, H);
-#if G2N_DIRECT_STORE  // (cap is a multiple of 4)
+  hipLaunchKernelGGL(k_claim_totals, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long*)H.tnb, TL.n_claim,
+                     &c->ctl->names_len, &c->ctl->dir_vmax);
+#if G2N_DIRECT_STORE  // (cap is a multiple of 4; the count stops past the largest claimed value)
   G2N_HIP(hipMemsetAsync(&c->ctl->n_keep, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(k_direct_filled, dim3((unsigned)std::min<uint64_t>(grid_for(cap / 4, 256), 2048)), dim3(256), 0,
-                     c->stream, (const uint4*)direct, cap / 4, &c->ctl->n_keep);
+                     c->stream, (const uint4*)direct, cap / 4, (const unsigned long long*)&c->ctl->dir_vmax,
+                     &c->ctl->n_keep);
 #endif
-  hipLaunchKernelGGL(k_u32_total, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)H.tnb, TL.n_claim,
-                     &c->ctl->names_len);
   phase(c, "direct_claim");
   sync_ctl(c);
   if (c->h_ctl->int_fail || (G2N_DIRECT_STORE && c->h_ctl->n_keep != n_s)) {  // (a repeated value: fewer filled)
@@ -1825,8 +1826,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     if (n_nodes) {  // the copy on the side stream, overlapping the assembly's finish (fork_side)
       const uint64_t* no = hl_noff;
       const uint32_t* nl = hl_nlen;
-      c->side_work = [c, in, no, nl, n_nodes, offs, blob]() {
-        hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->side, in,
+      c->side_work = [c, in, len, no, nl, n_nodes, offs, blob]() {
+        hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->side, in, len,
                            TouchIn{(uint64_t*)no, (uint32_t*)nl, nullptr, nullptr}, n_nodes, (const uint32_t*)nullptr,
                            (const int64_t*)offs, 0, blob);
       };
@@ -1858,7 +1859,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     const uint64_t names_len = read_dev(c, &c->ctl->names_len);
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
     if (n_nodes)
-      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, TI, n_nodes, D.inv,
+      hipLaunchKernelGGL(k_names, dim3(grid_for(n_nodes)), dim3(kTPB), 0, c->stream, in, len, TI, n_nodes, D.inv,
                          offs, (int)bidir, blob);
     R->names_bytes = names_len;
     R->names_blob = blob;
