@@ -2095,9 +2095,8 @@ static g2n_context* context_create(int device) {
 #ifndef G2N_SIDE_PRIO  // the side stream (names beside the finish) at the lowest priority, the pipeline at the
 #define G2N_SIDE_PRIO 1  // highest: C4 8.21-8.28 -> 8.05-8.11 ms in a same-box A/B (the names' interference 0.33 ms)
 #endif
-  if (G2N_SIDE_PRIO) {
-    int least = 0, greatest = 0;
-    G2N_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  int least = 0, greatest = 0;  // (no priority range: plain streams)
+  if (G2N_SIDE_PRIO && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest) {
     G2N_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
     G2N_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
   } else {
