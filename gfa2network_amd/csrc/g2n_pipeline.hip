@@ -1388,8 +1388,9 @@ struct TileLists {
 static bool hash_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, const TileLists& TL, const TileCnt* tcnt,
                             const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
                             const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out, uint64_t* names_len) {
-  const uint64_t n_tiles = (len + kTile - 1) / kTile;
-  (void)n_tiles;
+#ifdef G2N_K2_STAMPS
+  const uint64_t n_tiles = (len + kTile - 1) / kTile;  // (the stamps buffer)
+#endif
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   uint64_t cap = 1024;
 #ifndef G2N_HL_LOAD_PCT  // experiment builds: the lean table's maximum load, percent
@@ -1467,8 +1468,9 @@ static bool direct_lean_build(g2n_context* c, const uint8_t* in, uint64_t len, c
                               const TileCnt* tbase, uint64_t n_s, uint32_t ktrip, int32_t* rows, int32_t* cols,
                               const NamePattern& np, const HashLeanArgs& X, uint64_t** noff_out, uint32_t** nlen_out,
                               uint64_t* names_len) {
-  const uint64_t n_tiles = (len + kTile - 1) / kTile;
-  (void)n_tiles;
+#ifdef G2N_K2_STAMPS
+  const uint64_t n_tiles = (len + kTile - 1) / kTile;  // (the stamps buffer)
+#endif
   if (n_s == 0 || n_s >= 0x7FFFFFFFull) return false;
   const uint64_t cap = std::min<uint64_t>(1ull << 28, std::max<uint64_t>(4 * n_s, 1ull << 16));
   auto* direct = dget<uint32_t>(c, S_DIRECT, cap);
