@@ -35,7 +35,7 @@ FMT_COO, FMT_CSR, FMT_TEXT = 0, 1, 2
 EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_device_memory", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
-    "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream",
+    "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream", "g2n_context_trim",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
     "g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_keyset_free",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
@@ -220,6 +220,9 @@ def load() -> ctypes.CDLL:
     lib.g2n_context_destroy.restype = None
     lib.g2n_context_stream.argtypes = [ctypes.c_void_p]
     lib.g2n_context_stream.restype = ctypes.c_void_p
+    lib.g2n_context_trim.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    lib.g2n_context_trim.restype = ctypes.c_int
     lib.g2n_build_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(Options), ctypes.POINTER(Result)]
     lib.g2n_build_device.restype = ctypes.c_int

@@ -602,7 +602,8 @@ def parse_gfa_sharded(path, *, directed: bool = True, weight_tag: str | None = N
     res = build_sharded(buf, engine=eng, group=group, directed=directed, bidirected=bidirected,
                         keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,
                         strip_orientation=strip_orientation, dtype=dt.name, weight_tag=weight_tag or None,
-                        gather_names=return_node_list, keep_coo=not maxsym and output == "parse", names_root=root)
+                        gather_names=return_node_list, keep_coo=not maxsym and output == "parse", names_root=root,
+                        trim=True)  # (a sharded file is one too large for a GPU: free each stage's dead buffers)
     del buf
     raw = RawResult(status=res.status, err_line=res.err_line, err_index=res.err_index, err_value=res.err_value,
                     err_detail=res.err_detail, has_warning=res.has_warning, warn_byte=res.warn_byte,

@@ -106,6 +106,7 @@ class ShardResult:
     fast_path: bool = False  # the decimal-id fast path built it
     parse_path: str = ""  # fast path: how this rank's range was parsed ("tile_local" or "k1")
     coo: tuple | None = None  # keep_coo: this range's stream-order triplets over global ids
+    a2a_bytes_sent: int = 0  # bytes this rank's all-to-all-v calls sent to other ranks (diagnostics)
 
     @property
     def names(self) -> list | None:
@@ -289,6 +290,21 @@ class HipEngine:
     def empty(self, n, dtype):
         return self.torch.empty(n, dtype=getattr(self.torch, dtype) if isinstance(dtype, str) else dtype,
                                 device=self.device)
+
+    def trim(self, keep=(), build_ctx: bool = False) -> int:
+        """Release the context's arena buffers except those holding the device pointers in `keep`
+        (g2n_context_trim) and torch's cached blocks: a sharded rank's dictionary, touch descriptors
+        and partition buffers between protocol stages.  Returns the bytes the arena released."""
+        ctx = self.ctx_b if build_ctx else self.ctx
+        if not ctx:
+            return 0
+        ptrs = [int(p) for p in keep if p]
+        arr = (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs)
+        freed = ctypes.c_uint64(0)
+        self._sync()
+        self._check(self.lib.g2n_context_trim(ctx, arr, len(ptrs), ctypes.byref(freed)), "g2n_context_trim")
+        self.torch.cuda.empty_cache()
+        return int(freed.value)
 
     def _build_ctx(self):
         if self.ctx_b is None:
@@ -579,6 +595,7 @@ class Comm:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.host = dist.get_backend(group) == "gloo"
+        self.sent = 0  # bytes the all-to-all-v calls sent to other ranks (ShardResult.a2a_bytes_sent)
 
     def _c(self, x):
         return x.cpu() if self.host and x.is_cuda else x
@@ -607,6 +624,7 @@ class Comm:
                 outs.append(None)
                 continue
             xc = self._c(x.contiguous())
+            self.sent += (sum(send_counts) - send_counts[self.rank]) * xc.element_size()
             out = torch.empty(sum(recv), dtype=xc.dtype, device=xc.device)
             self.dist.all_to_all_single(out, xc, output_split_sizes=recv, input_split_sizes=list(send_counts),
                                         group=self.group)
@@ -835,6 +853,7 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     if gather_names and names_root in (None, rank):  # node k is str(k + 1) (bidirected: k // 2 + 1 and ":+" / ":-")
         out.names_blob, out.names_offsets = nat.decimal_names(n_global, bool(opts.get("bidirected")))
     out.timings_ms = tm
+    out.a2a_bytes_sent = C.sent
     out.fast_path = True
     out.parse_path = getattr(local, "parse_path", "")
     if keep_coo:
@@ -1195,7 +1214,7 @@ def _chunked_decimal(src, *, engine, chunk_bytes: int, directed=True, keep_direc
 def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, keep_directed_bidir=False,
                   asymmetric=False, strip_orientation=False, dtype="float64", weight_tag=None,
                   gather_names=False, keep_coo=False, names_root=None, force_protocol=False,
-                  copy_out=True) -> ShardResult:
+                  copy_out=True, trim=False) -> ShardResult:
     """Build this rank's byte range `buf` (uint8 tensor on the engine's device) as part of one
     file split over `group` in rank order; returns this rank's CSR row slice (and, keep_coo, the
     range's stream-order triplets over global ids: res.coo = (rows, cols, data)).
@@ -1203,7 +1222,10 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     on rank `names_root` only.  force_protocol: run the general exchange even on one rank (whose
     local ids are the global ones; measurement of the protocol's cost only).  copy_out=False: the slice's
     indptr / indices / data are views of the engine's context (no device copy; valid until the engine's
-    next call) — the bench's timed steps, which never read them."""
+    next call) — the bench's timed steps, which never read them.  trim: release each context's dead
+    buffers between the general protocol's stages (engine.trim: the local dictionary once the range's
+    COO and names are out, the owners' dedup table once the global ids are known) — the HBM of a
+    rank that shares its GPU, at the cost of re-allocating them on the next build."""
     import time
 
     import torch
@@ -1244,6 +1266,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         local.has_warning = False
     if first_unk is not None:  # a range may have been rebuilt: its counts again
         allst = C.allgather_list(stats(local))
+    if trim and view and local.status == 0 and hasattr(engine, "trim"):  # keep the COO views only
+        engine.trim([local.rows.data_ptr(), local.cols.data_ptr(), local.data.data_ptr()], build_ctx=True)
     line_base = np.concatenate([[0], np.cumsum([int(s[3]) for s in allst])])
     out = ShardResult(status=0, n_lines=int(line_base[-1]), n_records=int(sum(s[4] for s in allst)),
                       n_edges=int(sum(s[6] for s in allst)))
@@ -1347,6 +1371,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         if local.n_local_nodes:
             gmap[pidx.to(torch.int64)] = back
     tm["global_ids"] = (time.perf_counter() - t2) * 1e3
+    if trim and hasattr(engine, "trim"):  # the dedup table and key partition: their outputs are tensors
+        engine.trim()
     out.n_nodes = n_global
     if gather_names:
         # the owner's distinct keys (bytes at r_off[first_of]) with their global ids, to the
@@ -1399,6 +1425,7 @@ def _finish(engine, C, out, a, tstream, maxsym, dtype, weight_tag, tm, n_trip, c
     nnz, trip = C.allreduce_sum([int(indices.numel()), n_trip], engine.device)
     out.index_maxval = nnz if maxsym else trip
     out.timings_ms = tm
+    out.a2a_bytes_sent = C.sent
     return out
 
 

@@ -80,6 +80,27 @@ def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = Fals
         lib.g2n_synth_free_host(ptr)
 
 
+def write_file(path, n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, threads: int = 0,
+               names: str = "decimal", far_links: bool = False) -> int:
+    """host_bytes(...) written to `path` straight from the generator's buffer (no Python bytes copy:
+    a 16 GB C5 file needs 16 GB of host memory, not 32).  Returns the byte count."""
+    lib = _lib()
+    spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names], int(far_links))
+    ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = lib.g2n_synth_host(ctypes.byref(spec), threads, ctypes.byref(ptr), ctypes.byref(n))
+    if rc:
+        raise RuntimeError(f"g2n_synth_host failed ({rc})")
+    try:
+        view = memoryview((ctypes.c_char * n.value).from_address(ptr.value)).cast("B") if n.value else b""
+        with open(path, "wb") as fh:
+            step = 1 << 30
+            for a in range(0, n.value, step):
+                fh.write(view[a:a + step])
+        return n.value
+    finally:
+        lib.g2n_synth_free_host(ptr)
+
+
 class DeviceInput:
     """Synthetic GFA generated directly in HBM; owns the device buffer."""
 

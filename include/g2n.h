@@ -295,6 +295,12 @@ void *g2n_context_stream(g2n_context *ctx);    /* the hipStream_t the pipeline r
  * stream has drained (counts must be read back); phase timings are hipEvent-based. */
 int g2n_build_device(g2n_context *ctx, const void *d_input, size_t len, const g2n_options *opts,
                      g2n_result *out);
+/* Release ctx's grow-only arena buffers except those holding one of the n_keep device pointers
+ * (results the caller still reads, e.g. a build's rows / cols): the working set of one sharded rank
+ * between protocol stages (its dictionary, touch descriptors, partition buffers), which would
+ * otherwise stay allocated until ctx's next build needs them.  *freed (optional) = bytes released.
+ * No reference counterpart (the reference has no device memory); a later call re-allocates. */
+int g2n_context_trim(g2n_context *ctx, const void *const *keep, uint64_t n_keep, uint64_t *freed);
 
 /* ---- sharded build: device-side steps of one file split over ranks --------
  * Each rank builds its byte range with output = G2N_OUT_COO (local ids = first-touch order
