@@ -52,7 +52,7 @@ def _args():
                     help="skip the end-to-end leg (file on the page cache -> scipy CSR + node list in host memory)")
     ap.add_argument("--e2e-only", action="store_true", help="only the end-to-end leg")
     ap.add_argument("--no-alt", action="store_true", help="skip the hash-dictionary comparison build")
-    ap.add_argument("--names", default="decimal", choices=["decimal", "hashed", "permuted"],
+    ap.add_argument("--names", default="decimal", choices=["decimal", "hashed", "permuted", "prefixed"],
                     help="segment names of the synthetic file: decimal ids 1..N (the configs' layout), hashed "
                          "(unique non-decimal names: the hash dictionary / the general sharded protocol) or permuted "
                          "(decimal names out of S order: the direct-address dictionary)")
@@ -708,9 +708,19 @@ def main():
         t_h = time.perf_counter()
         hash_ph = step(hopts)
         t_h = time.perf_counter() - t_h
-    # decimal names out of S order (a permutation of 1..N): the direct-address dictionary tier
-    if not args.no_alt and args.names == "decimal":
-        perm = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local, names="permuted")
+    # decimal names out of S order (a permutation of 1..N), and minigraph's prefixed names "s1".."sN" in S
+    # order: the direct-address dictionary tier (S lines claim direct[v], each edge name one 4-byte read)
+    alt_names = {}
+    name_legs = {
+        "permuted_names": ("permuted", "same dimensions and flags, segment names a permutation of 1..N (synth "
+                           "names='permuted'): the direct-address dictionary (S lines claim direct[v], each edge "
+                           "name one 4-byte read)"),
+        "prefixed_names": ("prefixed", "same dimensions and flags, segment names 's1'..'sN' in S order (synth "
+                           "names='prefixed', minigraph's layout): the direct-address dictionary with a one-byte "
+                           "prefix"),
+    }
+    for leg, (nm, note) in (name_legs.items() if not args.no_alt and args.names == "decimal" else ()):
+        perm = synth.DeviceInput(n_s, n_l, seed=rank, rc_tag=wl.rc_tag, device=local, names=nm)
         try:
             pph = []
             for i in range(1 + max(2, min(args.steps, 5))):
@@ -724,16 +734,12 @@ def main():
                                  if not res.phase_names[k].decode().startswith("_")}, t_p))
             p_avg = {k: sum(p[0].get(k, 0.0) for p in pph) / len(pph) for k in pph[0][0]}
             p_ms = sum(p[1] for p in pph) / len(pph) * 1e3
-            line_alt_perm = {
+            alt_names[leg] = {
                 "ms_per_step": round(p_ms, 3), "m_edges_per_s": round(int(res.n_edges) / (p_ms / 1e3) / 1e6, 2),
                 "device_ms_per_step": round(sum(p_avg.values()), 3), "input_bytes": perm.len, "nnz": int(res.nnz),
-                "phase_ms": {k: round(v, 3) for k, v in p_avg.items()},
-                "note": "same dimensions and flags, segment names a permutation of 1..N (synth names='permuted'): the "
-                        "direct-address dictionary (S lines claim direct[v], each edge name one 4-byte read)"}
+                "phase_ms": {k: round(v, 3) for k, v in p_avg.items()}, "note": note}
         finally:
             perm.free()
-    else:
-        line_alt_perm = None
     # export --format edge-list on the same input (the text rendered in HBM)
     t_x, x_ph, x_bytes = None, None, 0
     if not args.no_alt:
@@ -804,8 +810,8 @@ def main():
             "phase_ms": {k: round(v, 3) for k, v in hash_ph.items()},
             "note": "options.test_flags = G2N_TEST_DICT_HASH: segment names resolved through the GPU hash table (inputs whose S lines "
                     "are not named 1..N in order)"}}
-    if line_alt_perm is not None:
-        line.setdefault("alt_paths", {})["permuted_names"] = line_alt_perm
+    for leg, rec in alt_names.items():
+        line.setdefault("alt_paths", {})[leg] = rec
     if t_x is not None:
         xt = x_ph.get("edge_text", 0.0)
         line.setdefault("alt_paths", {})["export_edge_list"] = {

@@ -35,7 +35,7 @@ FMT_COO, FMT_CSR, FMT_TEXT = 0, 1, 2
 EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_device_memory", "g2n_last_error",
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
-    "g2n_coo_to_csr", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream", "g2n_context_trim",
+    "g2n_coo_to_csr", "g2n_coo_to_csr_band", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream", "g2n_context_trim",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
     "g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_keyset_free",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
@@ -58,6 +58,7 @@ TEST_DICT_DIRECT = 2048  # decimal ids in S order through the direct-address tie
 TEST_NO_DIRECT = 4096    # never the direct-address tier: the lean hash tier instead
 TEST_NO_EXT_LEAN = 8192  # bidirected / weighted decimal builds through K1 + the lean parse (not tile-local)
 TEST_NO_DEC_TEXT = 16384  # edge-list export of decimal ids through the names blob (not the arithmetic render)
+TEST_NO_DEC_PREFIX = 32768  # prefixed names "P1".."PN" in S order through the direct tier (not the tile-local parse)
 TEST_FLAGS = int(os.environ.get("G2N_TEST_FLAGS", "0"), 0)  # (diagnostics: force the paths below for a whole run)
 # options.range_flags (include/g2n.h G2N_RANGE_*): set by the sharded / chunked protocol (shard.py)
 RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)
@@ -174,6 +175,12 @@ def hip_runtime() -> ctypes.CDLL:
     hip = ctypes.CDLL("libamdhip64.so.7")
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMalloc.restype = ctypes.c_int
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    hip.hipFree.restype = ctypes.c_int
+    hip.hipSetDevice.argtypes = [ctypes.c_int]
+    hip.hipSetDevice.restype = ctypes.c_int
     return hip
 
 
@@ -214,6 +221,10 @@ def load() -> ctypes.CDLL:
                                    ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(Result))]
     lib.g2n_coo_to_csr.restype = ctypes.c_int
+    lib.g2n_coo_to_csr_band.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.g2n_coo_to_csr_band.restype = ctypes.c_int
     lib.g2n_context_create.argtypes = [ctypes.c_int]
     lib.g2n_context_create.restype = ctypes.c_void_p
     lib.g2n_context_destroy.argtypes = [ctypes.c_void_p]
@@ -425,10 +436,15 @@ def build_from_buffer(data: bytes | bytearray | memoryview | np.ndarray, opts: O
     return _from_result(res, rc)
 
 
+BAND_ENTRIES = 2**31 - 2  # entries one g2n_coo_to_csr_band call takes (the weighted row-sum path's limit)
+
+
 def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int, n_cols: int,
-               device: int = 0, test_flags: int | None = None) -> RawResult:
+               device: int = 0, test_flags: int | None = None, band_entries: int | None = None) -> RawResult:
     """scipy coo.tocsr() on the GPU (g2n_coo_to_csr): indptr / indices in scipy's index dtype
-    (int64 past 2^31 - 1 entries)."""
+    (int64 past 2^31 - 1 entries).  A COO past what one call takes (a weighted matrix past 2^31 - 2
+    entries, any past 2^32 - 2) is converted in row bands (_coo_to_csr_bands); band_entries forces
+    bands of at most that many entries (tests)."""
     lib = load()
     dt = np.dtype(data.dtype)
     if dt.name not in DTYPE_CODES:
@@ -438,15 +454,84 @@ def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int
     r = np.ascontiguousarray(rows, dtype=np.int32)
     c = np.ascontiguousarray(cols, dtype=np.int32)
     d = np.ascontiguousarray(data)
-    res = ctypes.POINTER(Result)()
     flags = TEST_FLAGS if test_flags is None else test_flags
+    if band_entries is not None:
+        return _coo_to_csr_bands(r, c, d, n_rows, n_cols, device, band_entries)
+    if flags & TEST_INDEX64 and len(d) and not bool(np.all(d == 1)):
+        # the past-2^31 route of a weighted COO on a small input: three row bands, int64 indices
+        return _coo_to_csr_bands(r, c, d, n_rows, n_cols, device, len(d) // 3 + 1, index64=True)
+    res = ctypes.POINTER(Result)()
     rc = lib.g2n_coo_to_csr(r.ctypes.data, c.ctypes.data, d.ctypes.data, len(d), n_rows, n_cols, 4,
                             DTYPE_CODES[dt.name], device, flags, ctypes.byref(res))
+    if rc == E_UNSUPPORTED and len(d) > BAND_ENTRIES:  # past one call's limit: row bands
+        return _coo_to_csr_bands(r, c, d, n_rows, n_cols, device, BAND_ENTRIES)
     if rc == E_UNSUPPORTED:  # a documented size limit (include/g2n.h)
         raise NotImplementedError(f"GPU COO->CSR: {last_error()}")
     out = _from_result(res, rc)
     if out.status != OK:
         raise RuntimeError(f"{status_name(out.status)}: {out.message}")
+    return out
+
+
+def _coo_to_csr_bands(r, c, d, n_rows: int, n_cols: int, device: int, limit: int, index64: bool = False) -> RawResult:
+    """coo.tocsr() (utils.py:55) of a COO too large for one g2n_coo_to_csr call, in row bands of at most
+    `limit` entries (g2n_coo_to_csr_band).  Each band's triplets keep their stream order (a stable
+    selection), so each row's duplicates meet in scipy's order; scipy's has_sorted_indices verdict is
+    the whole matrix's — when some band holds an unsorted row, csr_sort_indices reorders every row —
+    so bands that were sorted on their own are re-run with the matrix's verdict.  indptr / indices in
+    scipy's dtype for the whole COO (int64 once its entries pass 2^31 - 1: _coo_to_compressed)."""
+    lib = load()
+    n = len(d)
+    dt = np.dtype(d.dtype)
+    counts = np.bincount(r, minlength=n_rows) if n else np.zeros(n_rows, dtype=np.int64)
+    if n_rows and int(counts.max()) > limit:
+        raise NotImplementedError("GPU COO->CSR: a row holds more entries than one band takes")
+    cum = np.cumsum(counts, dtype=np.int64)
+    cuts = [0]
+    while cuts[-1] < n_rows:
+        base = int(cum[cuts[-1] - 1]) if cuts[-1] else 0
+        nxt = int(np.searchsorted(cum, base + limit, side="right"))
+        cuts.append(min(max(nxt, cuts[-1] + 1), n_rows))
+    if n_rows == 0:
+        cuts.append(0)
+    bands = list(zip(cuts[:-1], cuts[1:]))
+
+    def run(lo, hi, force):
+        sel = np.flatnonzero((r >= lo) & (r < hi)) if len(bands) > 1 else None
+        br = (r[sel] - lo) if sel is not None else r
+        bc, bd = (c[sel], d[sel]) if sel is not None else (c, d)
+        br = np.ascontiguousarray(br, dtype=np.int32)
+        bc, bd = np.ascontiguousarray(bc), np.ascontiguousarray(bd)
+        res = ctypes.POINTER(Result)()
+        rc = lib.g2n_coo_to_csr_band(br.ctypes.data, bc.ctypes.data, bd.ctypes.data, len(bd), hi - lo, n_cols,
+                                     DTYPE_CODES[dt.name], device, force, ctypes.byref(res))
+        if rc == E_UNSUPPORTED:
+            raise NotImplementedError(f"GPU COO->CSR band: {last_error()}")
+        out = _from_result(res, rc)
+        if out.status != OK:
+            raise RuntimeError(f"{status_name(out.status)}: {out.message}")
+        # (copies: the next band's call reuses the context the result views point into)
+        return (np.array(out.indptr), np.array(out.indices), np.array(out.data),
+                None if out.sum_buckets else not out.sum_sorted)
+
+    parts = [run(lo, hi, -1) for lo, hi in bands]
+    if any(p[3] is True for p in parts):  # the matrix is unsorted: scipy sorts every row of it
+        parts = [run(lo, hi, 1) if p[3] is False else p for (lo, hi), p in zip(bands, parts)]
+    idt = np.int64 if index64 or max(n, n_rows) > 2**31 - 1 else np.int32
+    nnz = sum(len(p[1]) for p in parts)
+    indptr = np.empty(n_rows + 1, dtype=idt)
+    indices = np.empty(nnz, dtype=idt)
+    vals = np.empty(nnz, dtype=dt)
+    indptr[0] = 0
+    pos = 0
+    for (lo, hi), p in zip(bands, parts):
+        k = len(p[1])
+        indptr[lo + 1:hi + 1] = p[0][1:].astype(np.int64) + pos
+        indices[pos:pos + k] = p[1]
+        vals[pos:pos + k] = p[2]
+        pos += k
+    out = RawResult(status=OK, format="csr", dtype=dt, n_nodes=n_rows, indptr=indptr, indices=indices, data=vals)
+    out.sum_sorted = not any(p[3] is True for p in parts)
     return out
 
 

@@ -457,7 +457,7 @@ def _parse_gfa_chunked(source, chunk_bytes: int, *, directed: bool, weight_tag, 
 
     gd = keep_directed_bidir or (not bidirected and directed)  # builders.py:143
     maxsym = gd and not asymmetric                               # builders.py:282
-    eng = engine or HipEngine(device)
+    eng = engine or HipEngine(device, torch_buffers=False)  # one GPU, no collective: no torch on this path
     try:
         res = build_chunked(source, engine=eng, chunk_bytes=chunk_bytes, directed=directed, bidirected=bidirected,
                             keep_directed_bidir=keep_directed_bidir, asymmetric=asymmetric,

@@ -123,6 +123,10 @@ struct ParseOpts {
   // ASCII) as its line rank in the tile << 15 | its tile offset, the tile index atomicMin'd into
   // ctl->warn_tile (the one-shot warning without the full parse); null: such a record fails the pass
   uint32_t* tunk;
+  // the tile-local decimal parse behind one constant prefix (round 6: minigraph's "s1".."sN" in S order):
+  // every name is these dpre_len (<= 8, no digit) bytes, little-endian, then the canonical decimal
+  uint64_t dpre;
+  uint32_t dpre_len;
 };
 constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
 

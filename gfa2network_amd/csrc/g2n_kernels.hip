@@ -207,12 +207,30 @@ constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // chunks per thread
 // t + 256 j; all loads are issued before the first LDS write.  (A persistent variant that loads
 // tile i + G while parsing tile i measured slower on gfx950: the prefetch registers took K2 from
 // 80 to 212 VGPRs, 2 waves/SIMD, 6.3 -> 10.7 ms on C4.)
+#ifndef G2N_LEAN_LINK  // experiment builds: 0 = the edge line's five tabs by five ctz (round 5)
+#define G2N_LEAN_LINK 1
+#endif
+#ifndef G2N_EDGE_ONLY  // experiment builds: 0 = no edge-only parse loop in k_tile_lean (round 5)
+#define G2N_EDGE_ONLY 1
+#endif
+#ifndef G2N_LOAD_UNIFORM  // experiment builds: 0 = per-chunk bounds on every tile load (round 5)
+#define G2N_LOAD_UNIFORM 1
+#endif
+
 template <uint32_t kHalo, uint32_t kT = kTPB>
 struct TileRegs {
   static constexpr uint32_t kChunks = (uint32_t)((kTile + kHalo) / 16);
   static constexpr uint32_t kPer = (kChunks + kT - 1) / kT;
   uint4 r[kPer];
   __device__ inline void load(const uint8_t* __restrict__ in, uint64_t len, uint64_t t0) {
+    if (G2N_LOAD_UNIFORM && t0 + (uint64_t)kChunks * 16 <= len) {  // (block-uniform) every chunk is input
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t c = j * kT + threadIdx.x;
+        r[j] = c < kChunks ? *(const uint4*)(in + t0 + (uint64_t)c * 16) : make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {  // every load in flight before any is used
       const uint32_t c = j * kT + threadIdx.x;
@@ -975,6 +993,26 @@ __device__ inline bool dec_lds(const uint8_t* buf, uint32_t x, uint32_t l, uint6
   return true;
 }
 
+// The first p <= 8 bytes at tile offset x of the staged tile, little-endian (aligned 8-byte LDS reads)
+__device__ inline uint64_t lds_prefix8(const uint8_t* buf, uint32_t x, uint32_t p) {
+  const uint32_t a = x & ~7u, sh = (x & 7u) * 8;
+  uint64_t w = *(const uint64_t*)(buf + a) >> sh;
+  if (sh && (x & 7u) + p > 8) w |= *(const uint64_t*)(buf + a + 8) << (64 - sh);
+  return p >= 8 ? w : (w & ((1ull << (8 * p)) - 1));
+}
+
+// a segment name of the decimal-id layout at tile offset x (length l): op.dpre then the canonical
+// decimal (no prefix: the decimal alone) — its value
+__device__ inline bool dec_name(const uint8_t* buf, uint32_t x, uint32_t l, const ParseOpts& op, uint64_t* v) {
+  const uint32_t p = op.dpre_len;
+  if (p) {
+    if (l <= p || lds_prefix8(buf, x, p) != op.dpre) return false;
+    x += p;
+    l -= p;
+  }
+  return dec_lds(buf, x, l, v);
+}
+
 // dec_lds's 1-8 digit case on words already loaded: w0 / w1 = the aligned 8-byte LDS words at
 // (x & ~7) and (x & ~7) + 8.  false for anything else (the caller takes dec_lds for 9-10 digits).
 __device__ inline bool dec_words(uint64_t w0, uint64_t w1, uint32_t x, uint32_t l, uint64_t* v) {
@@ -1045,6 +1083,24 @@ __device__ inline bool lean_int_tag(const uint8_t* buf, uint32_t x, uint32_t l, 
   return true;
 }
 
+// An L / E / C line in the link_fast shape "L\t<a>\t<o>\t<b>\t<o>[\t...]" from its tab bits m (bit k =
+// byte so + k; the '\n' excluded): the two names' lengths.  The record-kind check put a tab at byte 1
+// (a '\n' there leaves m without a name: false), so the five tabs are byte 1; p1 = the first after it;
+// p1 + 2 (the orientation byte between must be '+' / '-'); p3 = the first after p1 + 2; p3 + 2 — two
+// ctz instead of one per tab (round 6).  Name a at so + 2, length la; name b at so + 5 + la, length lb.
+__device__ __forceinline__ bool lean_link(const uint8_t* buf, uint64_t m, uint32_t so, uint32_t& la, uint32_t& lb) {
+  m >>= 2;  // tabs from byte 2: the first name's
+  if (!m) return false;
+  la = (uint32_t)__builtin_ctzll(m);  // < 46
+  if (!((m >> (la + 2)) & 1)) return false;
+  const uint64_t m2 = m >> (la + 3);  // from the second name
+  if (!m2) return false;
+  lb = (uint32_t)__builtin_ctzll(m2);
+  if (!((m2 >> (lb + 2)) & 1)) return false;
+  const uint32_t c2 = buf[so + 3 + la], c4 = buf[so + 6 + la + lb];
+  return (c2 == '+' || c2 == '-') && (c4 == '+' || c4 == '-');
+}
+
 // kExt: the extended instance (bidirected keys, one integer weight tag), tile-local builds only
 template <bool kExt = false>
 __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint32_t so, uint32_t next, uint8_t k,
@@ -1065,12 +1121,35 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
     // one that breaks it re-parses in full
     if (op.tid && !is.fail) {
       uint64_t v;
-      if (eb != 0 || !dec_lds(buf, so + t1 + 1, t2 - t1 - 1, &v)) is.fail = 1;
+      if (eb != 0 || !dec_name(buf, so + t1 + 1, t2 - t1 - 1, op, &v)) is.fail = 1;
       else is.s_name(op, v, tb);
     }
     return true;
   }
-  if (k != kEdge || __popcll(m) < 5) return false;
+  if (k != kEdge) return false;
+  if constexpr (!kExt && G2N_LEAN_LINK) {  // the plain decimal build: two tab searches (lean_link)
+    uint32_t la, lb;
+    if (!lean_link(buf, m, so, la, lb)) return false;
+    if (op.tile_pad && eb >= op.tile_pad) is.fail = 1;  // the tile's slot is full: give up
+    if (is.fail) return true;
+    uint64_t a, b;
+    if (!dec_name(buf, so + 2, la, op, &a) || !dec_name(buf, so + 5 + la, lb, op, &b) || a > op.n_seg ||
+        b > op.n_seg) {  // not an S key: the premise breaks (int_edge_id)
+      is.fail = 1;
+      return true;
+    }
+    const uint32_t vm = (uint32_t)(a > b ? a : b);
+    is.vmax = vm > is.vmax ? vm : is.vmax;
+    const uint64_t o = ((op.tile_pad && !op.grouped ? (uint64_t)blockIdx.x * op.tile_pad : 0ull) + eb) * op.ktrip;
+    op.rows[o] = (int32_t)(a - 1);
+    op.cols[o] = (int32_t)(b - 1);
+    if (op.ktrip >= 2) {
+      op.rows[o + 1] = (int32_t)(b - 1);
+      op.cols[o + 1] = (int32_t)(a - 1);
+    }
+    return true;
+  }
+  if (__popcll(m) < 5) return false;
   uint32_t p[6];
 #pragma unroll
   for (int j = 0; j < 6; j++) {
@@ -1083,7 +1162,7 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
   if (op.tile_pad && eb >= op.tile_pad) is.fail = 1;  // the tile's slot is full: give up
   if (is.fail) return true;
   uint64_t a, b;
-  if (!dec_lds(buf, so + p[0] + 1, p[1] - p[0] - 1, &a) || !dec_lds(buf, so + p[2] + 1, p[3] - p[2] - 1, &b) ||
+  if (!dec_name(buf, so + p[0] + 1, p[1] - p[0] - 1, op, &a) || !dec_name(buf, so + p[2] + 1, p[3] - p[2] - 1, op, &b) ||
       a > op.n_seg || b > op.n_seg) {  // not an S key: the premise breaks (int_edge_id)
     is.fail = 1;
     return true;
@@ -1774,7 +1853,15 @@ __device__ inline bool tail_eq(const uint8_t* __restrict__ in, const TouchIn& T,
 #endif
 constexpr uint32_t kLeanTPB = G2N_LEAN_TPB;                             // threads per tile
 constexpr uint32_t kLeanRegion = (uint32_t)(kTile / 16) / kLeanTPB;     // chunks per thread (4)
-constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kTileHalo) / 16);  // staged chunks
+// the lean front end's halo: a lean edge line ends at most 48 bytes + its '\n' past its start, and an S /
+// P / O line whose end is out of view needs only its first 48 bytes (round 6: 64 bytes staged past the
+// tile instead of K1 / k_tile_parse's 2 KiB — 0.2 % of the input re-read and masked, not 6.25 %)
+#ifndef G2N_LEAN_HALO
+#define G2N_LEAN_HALO 64
+#endif
+constexpr uint32_t kLeanHalo = G2N_LEAN_HALO;
+static_assert(kLeanHalo >= 64 && kLeanHalo % 16 == 0, "an edge line's 49 bytes past its start");
+constexpr uint32_t kLeanChunks = (uint32_t)((kTile + kLeanHalo) / 16);  // staged chunks
 constexpr uint32_t kLeanLines = 2048;                                   // line records per window
 #ifndef G2N_LEAN_PAIR  // experiment builds: the decimal parse two lines per lane per step
 #define G2N_LEAN_PAIR 0
@@ -2116,7 +2203,7 @@ __device__ inline uint32_t lean_find(const uint8_t* __restrict__ in, const HashL
   return ~0u;
 }
 
-using LeanRegs = TileRegs<kTileHalo, kLeanTPB>;
+using LeanRegs = TileRegs<kLeanHalo, kLeanTPB>;
 #ifndef G2N_K2_PREFETCH
 #define G2N_K2_PREFETCH 0
 #endif
@@ -2130,7 +2217,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
                                           uint32_t* __restrict__ gcount, uint64_t gcap, const HashLeanArgs& H,
                                           const uint64_t tile, LeanRegs& R, uint64_t next_tile, uint64_t n_tiles) {
   constexpr uint32_t kW = kLeanTPB / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kTileHalo + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTile + kLeanHalo + 16];
   __shared__ __attribute__((aligned(16))) uint16_t tabm[kLeanChunks + 8];
   __shared__ __attribute__((aligned(16))) uint16_t nlm[kLeanChunks + 8];
   __shared__ uint32_t rec[kLeanLines + 1];
@@ -2254,7 +2341,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
                  e_tot = (uint32_t)(tot >> 40);
   if (q_unk != ~0u) atomicMin(&s_unk, (((uint32_t)(ex & 0xFFFFFu) + q_unk) << 15) | o_unk);  // (read at the finish)
   K2_LEAN_STAMP(3);
-  const uint32_t lim = (uint32_t)(len - t0 < kTile + kTileHalo ? len - t0 : kTile + kTileHalo);  // staged bytes
+  const uint32_t lim = (uint32_t)(len - t0 < kTile + kLeanHalo ? len - t0 : kTile + kLeanHalo);  // staged bytes
   if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
     s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
   // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
@@ -2501,6 +2588,17 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       continue;  // next window
     }
 #endif
+    if (G2N_EDGE_ONLY && kMode == kLeanDecimal && !kExt && e_tot == n_lines) {  // (block-uniform) edge lines only: no
+#pragma unroll 1                                               // record-kind branches (round 6)
+      for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
+        const uint32_t x = rec[j];
+        const uint32_t o = x & 0x7FFFu;
+        const uint32_t next = line_next(j, o);
+        if (!next || !lean_line<false>(buf, tabm, o, next, kEdge, t0, 0ull, x >> 17, op, TouchOut{}, is))
+          is.fail = 1;
+      }
+      continue;  // next window
+    }
 #pragma unroll 1
     for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
       const uint32_t x = rec[j];
@@ -2712,7 +2810,7 @@ __global__ void G2N_LEAN_ATTR
   // line, into a sink register kept live (and drained) to the end, so no later value shares it
   uint32_t sink = 0;
   const uint64_t pf = (tile + op.pf_dist) * kTile + 128ull * threadIdx.x;
-  const bool do_pf = op.pf_dist && threadIdx.x < (kTile + kTileHalo) / 128 && pf < len;
+  const bool do_pf = op.pf_dist && threadIdx.x < (kTile + kLeanHalo) / 128 && pf < len;
   if (do_pf) asm volatile("global_load_dword %0, %1, off" : "=v"(sink) : "v"(in + pf) : "memory");
 #endif
   lean_tile<kMode, kGrouped, kExt>(in, len, op, ctl, tcnt_out, tlean, gcount, gcap, H, tile, R, ~0ull, 0);
@@ -3115,13 +3213,16 @@ __device__ __host__ inline uint64_t dec_name_off(uint64_t id, int bidir) {  // o
 // the names' run found by arithmetic: +0.3 ms, VALU-heavy beside F1), the names written by the
 // tile-local parse as it meets each S line (K2 +0.34 ms, F1 -0.3: no gain), the names forked beside
 // the partition instead of F1 (+0.4 ms on it), non-temporal stores (+0.2-0.5 ms).
+// (pl bytes of pre before every key: the prefixed decimal layout, ParseOpts::dpre)
 __global__ void __launch_bounds__(kTPB) k_names_dec(uint64_t n_nodes, int bidir, int64_t* __restrict__ offs,
-                                                    uint8_t* __restrict__ blob) {
+                                                    uint8_t* __restrict__ blob, uint64_t pre, uint32_t pl) {
   const uint64_t id = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (id > n_nodes) return;
-  const uint64_t o = dec_name_off(id, bidir);
+  uint64_t o = dec_name_off(id, bidir) + (uint64_t)pl * id;
   offs[id] = (int64_t)o;
   if (id == n_nodes) return;
+  for (uint32_t j = 0; j < pl; j++) blob[o + j] = (uint8_t)(pre >> (8 * j));
+  o += pl;
   uint32_t v = (uint32_t)((bidir ? id >> 1 : id) + 1);  // node ids < 2^31
   const uint32_t d = dec_digits(v);
   for (uint32_t j = d; j-- > 0;) {

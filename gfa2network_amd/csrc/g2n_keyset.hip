@@ -20,6 +20,7 @@ struct KsEntry {
 };
 constexpr unsigned long long kKsEmpty = ~0ull;
 constexpr unsigned long long kKsOffMask = (1ull << 40) - 1;
+constexpr uint64_t kKsMaxKeyLen = (1ull << 24) - 1;  // loc's length field (a longer key: G2N_E_UNSUPPORTED)
 
 __device__ inline uint64_t ks_hash(const uint8_t* __restrict__ p, uint64_t n) {  // FNV-1a, 64-bit
   uint64_t h = 0xcbf29ce484222325ull;
@@ -98,6 +99,17 @@ __global__ void __launch_bounds__(256) k_ks_new_lens(const int64_t* __restrict__
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   lens[i] = fresh[i] ? offs[i + 1] - offs[i] : 0;
+}
+
+// the longest of n key lengths, into *out (atomicMax per block: only run when the new keys' bytes
+// could hold one longer than kKsMaxKeyLen)
+__global__ void __launch_bounds__(256) k_ks_max_len(const int64_t* __restrict__ lens, uint64_t n,
+                                                    unsigned long long* out) {
+  unsigned long long m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    m = max(m, (unsigned long long)lens[i]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
 }  // namespace g2n

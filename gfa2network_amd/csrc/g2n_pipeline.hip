@@ -84,6 +84,7 @@ constexpr uint32_t kTestDictDirect = G2N_TEST_DICT_DIRECT;
 constexpr uint32_t kTestNoDirect = G2N_TEST_NO_DIRECT;
 constexpr uint32_t kTestNoExtLean = G2N_TEST_NO_EXT_LEAN;
 constexpr uint32_t kTestNoDecText = G2N_TEST_NO_DEC_TEXT;
+constexpr uint32_t kTestNoDecPrefix = G2N_TEST_NO_DEC_PREFIX;
 
 
 struct DevBuf {
@@ -812,7 +813,7 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
 
 template <class T, bool kU>
 static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
-                       uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R) {
+                       uint64_t n_rows, uint64_t n_cols, bool maxsym, g2n_result* R, int force_unsorted = -1) {
   if constexpr (kU) {
     if (n_trip && n_rows && (n_rows == n_cols || !maxsym) && !(c->test_flags & kTestNoBuckets) &&
         csr_partition<T>(c, rows, cols, n_trip, n_rows, !maxsym, R))
@@ -829,8 +830,10 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
   // the row-sum path (weighted / float sums, or a partition that declined) keeps int32 positions
   if (n_trip >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 weighted matrix entries");
   const T one = (T)1;
-  RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0);
-  R->sum_sorted = A.unsorted ? 0 : 1;
+  // (force_unsorted >= 0: a row band of a larger COO, g2n_coo_to_csr_band — scipy's verdict is the whole
+  // matrix's; sum_sorted still reports this band's own)
+  RowSide<T, kU> A = row_sums<T, kU>(c, rows, cols, data, n_trip, n_rows, 0, 0, 0, force_unsorted);
+  R->sum_sorted = A.local_unsorted ? 0 : 1;
   phase(c, "sum");
   auto* indptr = dget<int32_t>(c, S_INDPTR, n_rows + 1);
   if (n_rows == 0) G2N_HIP(hipMemsetAsync(indptr, 0, sizeof(int32_t), c->stream));
@@ -949,9 +952,10 @@ static void assemble_pair_t(g2n_context* c, const int32_t* ar, const int32_t* ac
 
 template <class T>
 static void assemble(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t n_trip,
-                     uint64_t n_rows, uint64_t n_cols, bool maxsym, bool uniform, g2n_result* R) {
-  if (uniform) assemble_t<T, true>(c, rows, cols, data, n_trip, n_rows, n_cols, maxsym, R);
-  else assemble_t<T, false>(c, rows, cols, data, n_trip, n_rows, n_cols, maxsym, R);
+                     uint64_t n_rows, uint64_t n_cols, bool maxsym, bool uniform, g2n_result* R,
+                     int force_unsorted = -1) {
+  if (uniform) assemble_t<T, true>(c, rows, cols, data, n_trip, n_rows, n_cols, maxsym, R, force_unsorted);
+  else assemble_t<T, false>(c, rows, cols, data, n_trip, n_rows, n_cols, maxsym, R, force_unsorted);
 }
 
 template <class T>
@@ -1161,6 +1165,36 @@ static bool first_segment_is_one(g2n_context* c, const uint8_t* in, uint64_t len
   return true;  // no S line seen yet (long header lines): try
 }
 
+// Is the first S line's name (within the first 64 KiB) a constant prefix then "1" — minigraph's "s1"?
+// The prefix (1-8 bytes, no digit, no tab) is then tried as the decimal-id layout's (ParseOpts::dpre:
+// names P + str(k + 1) in S order); a wrong guess costs one tile-local pass, never the result.
+static bool first_segment_prefixed(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t* pre, uint32_t* pl) {
+  const size_t n = (size_t)std::min<uint64_t>(len, 1 << 16);
+  if (n == 0) return false;
+  std::vector<uint8_t> h(n);
+  G2N_HIP(hipMemcpyAsync(h.data(), in, n, hipMemcpyDeviceToHost, c->stream));
+  G2N_HIP(hipStreamSynchronize(c->stream));
+  for (size_t p = 0; p + 3 < n;) {
+    if (h[p] == 'S' && h[p + 1] == '\t') {
+      size_t e = p + 2;
+      while (e < n && h[e] != '\t' && h[e] != '\n') e++;
+      if (e >= n || e - (p + 2) < 2 || e - (p + 2) > 9 || h[e - 1] != '1') return false;
+      uint64_t v = 0;
+      for (size_t k = p + 2; k + 1 < e; k++) {
+        if (h[k] - (uint32_t)'0' <= 9u) return false;
+        v |= (uint64_t)h[k] << (8 * (k - p - 2));
+      }
+      *pre = v;
+      *pl = (uint32_t)(e - 1 - (p + 2));
+      return true;
+    }
+    const void* q = std::memchr(h.data() + p, '\n', n - p);
+    if (!q) break;
+    p = (size_t)((const uint8_t*)q - h.data()) + 1;
+  }
+  return false;
+}
+
 // The first S line's name (in the first 64 KiB) as the direct-address tier's premise: a prefix of
 // at most 8 non-digit bytes, a run of at most 10 digits, a suffix of at most 8 bytes without a digit
 // ("s123", "utg000123l", "node_42").  A run that starts with '0' fixes the width (zero-padded
@@ -1226,7 +1260,7 @@ constexpr uint32_t kTileEdgeCap = (uint32_t)(kTile / 12) + 6;  // a lean edge li
 static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, uint64_t n_tiles, uint32_t ktrip,
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
                              uint64_t n_seg_all = 0, bool deferred = false, const ParseOpts* xo = nullptr,
-                             bool warn_ok = false) {
+                             bool warn_ok = false, uint64_t dpre = 0, uint32_t dpre_len = 0) {
   if (xo) grouped = false;
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
@@ -1249,6 +1283,8 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.tile_pad = kTileEdgeCap;
   lo.tid = (uint32_t*)rows_p;  // only a flag here: the lean parse writes no per-touch ids
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
+  lo.dpre = dpre;              // names behind one constant prefix (first_segment_prefixed)
+  lo.dpre_len = dpre_len;
   lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
   // a whole-file build takes the unsupported-record warning itself (k_tile_lean_check); a sharded range
   // leaves it to the general protocol
@@ -1563,6 +1599,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool first_one =
       !shard_dec && !(c->test_flags & (kTestDictHash | kTestDictGeneral | kTestDictDirect)) &&
       first_segment_is_one(c, in, len);
+  // ... or "P1": the same layout behind a constant prefix P (tile-local pass only: a failed one goes to
+  // the direct / hash tiers, which take any prefix)
+  uint64_t dpre = 0;
+  uint32_t dpre_len = 0;
+  const bool first_pre = !first_one && !shard_dec && !(c->test_flags & (kTestDictHash | kTestDictGeneral |
+                                                                        kTestDictDirect | kTestNoDecPrefix)) &&
+                         first_segment_prefixed(c, in, len, &dpre, &dpre_len);
   // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
   // group slots when the COO's only reader is the unweighted bucket partition (a CSR output)
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
@@ -1580,11 +1623,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   const bool ext_ok = !shard_dec && wt_bytes <= 8 && !(c->test_flags & kTestNoExtLean);
   // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
   const bool local_done =
-      n_tiles && (first_one || (shard_dec && (shard_deferred || (o->range_s_base >= 0 && o->range_n_segments > 0)))) &&
+      n_tiles && (first_one || first_pre ||
+                  (shard_dec && (shard_deferred || (o->range_s_base >= 0 && o->range_n_segments > 0)))) &&
       (!ext || ext_ok) && !o->strip_orientation && !(c->test_flags & (kTestNoLean | kTestNoTileLocal)) &&
       tile_local_parse(c, in, len, n_tiles, tpe == 4 ? 4u : (gd ? 1u : 2u), tcnt, tbase, &tot, grouped,
                        shard_dec ? (uint64_t)o->range_s_base : 0, shard_dec ? (uint64_t)o->range_n_segments : 0,
-                       shard_deferred, ext ? &xo : nullptr, !shard_dec);
+                       shard_deferred, ext ? &xo : nullptr, !shard_dec, dpre, first_pre ? dpre_len : 0u);
+  const uint32_t name_pre_len = local_done && first_pre ? dpre_len : 0u;  // node k's name: P + str(k + 1)
   if (shard_deferred && n_tiles && !local_done)  // the caller counts the ranges and builds with K1 instead
     throw Failure(G2N_E_UNSUPPORTED, "sharded decimal-id range: the one-pass parse declined");
   // ---- K1: per-tile counts -> tile bases (and the lean hash / direct passes' tile lists: names that
@@ -1838,17 +1883,19 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     R->names_blob = blob;
     R->names_offsets = offs;
     phase(c, "names");
-  } else if (o->want_node_names && lean_done && c->edge_text) {
+  } else if (o->want_node_names && lean_done && c->edge_text && !name_pre_len) {
     c->names_dec = true;  // k_edge_dec_text renders them from the ids
   } else if (o->want_node_names && lean_done) {
     auto* offs = dget<int64_t>(c, S_OFFS, n_nodes + 1);
-    const uint64_t names_len = dec_name_off(n_nodes, (int)bidir);
+    const uint64_t names_len = dec_name_off(n_nodes, (int)bidir) + (uint64_t)name_pre_len * n_nodes;
     auto* blob = dget<uint8_t>(c, S_BLOB, names_len);
     // no input but n_nodes: on the side stream, overlapping the assembly's finish (fork_side in
     // csr_partition; joined in finish_timings)
     const int bd = (int)bidir;
-    c->side_work = [c, n_nodes, bd, offs, blob]() {
-      hipLaunchKernelGGL(k_names_dec, dim3(grid_for(n_nodes + 1)), dim3(kTPB), 0, c->side, n_nodes, bd, offs, blob);
+    const uint32_t pl = name_pre_len;
+    c->side_work = [c, n_nodes, bd, offs, blob, dpre, pl]() {
+      hipLaunchKernelGGL(k_names_dec, dim3(grid_for(n_nodes + 1)), dim3(kTPB), 0, c->side, n_nodes, bd, offs, blob,
+                         dpre, pl);
     };
     R->names_bytes = names_len;
     R->names_blob = blob;
@@ -1977,7 +2024,7 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
     g2n_context* c;
     ~TextFlag() { c->edge_text = false; }
   } guard{c};
-  c->edge_text = !(c->test_flags & kTestNoDecText);
+  c->edge_text = !(o->test_flags & kTestNoDecText);  // (this call's flags: run_build copies them only later)
   c->names_dec = false;
   const int rc = run_build(c, in, len, &b, R);
   c->edge_text = false;
@@ -2300,15 +2347,18 @@ __global__ void k_values_not_one(const T* __restrict__ d, uint64_t n, unsigned i
 
 template <class T>
 static void coo_to_csr_t(g2n_context* c, const int32_t* rows, const int32_t* cols, const T* data, uint64_t nnz,
-                         uint64_t n_rows, uint64_t n_cols, bool uniform, g2n_result* R) {
+                         uint64_t n_rows, uint64_t n_cols, bool uniform, g2n_result* R, int force_unsorted) {
   // uniform (every value T(1): what parse_gfa returns without a weight tag): the copy count per
   // entry is the sum, through the unweighted bucket partition — the path with int64 results past
   // 2^31 - 1 entries (scipy's _coo_to_compressed sizes its index dtype by coo.nnz)
-  assemble<T>(c, rows, cols, data, nnz, n_rows, n_cols, false, uniform, R);
+  assemble<T>(c, rows, cols, data, nnz, n_rows, n_cols, false, uniform, R, force_unsorted);
 }
 
+// force_unsorted: -1 = this COO is the whole matrix (scipy's has_sorted_indices verdict is its own),
+// 0 / 1 = one row band of a larger COO, the whole matrix's verdict given (g2n_coo_to_csr_band)
 int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows, int64_t n_cols,
-               int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags, g2n_result** out) {
+               int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags, g2n_result** out,
+               int force_unsorted = -1) {
   if (index_width != 4) throw Failure(G2N_E_UNSUPPORTED, "only int32 COO indices are supported");
   if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) throw Failure(G2N_E_ARG, "unsupported dtype");
   if (nnz < 0 || n_rows < 0 || n_cols < 0) throw Failure(G2N_E_ARG, "negative size");
@@ -2355,11 +2405,11 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   D.index_width = 4;
   D.n_nodes = n_rows;
   switch (dtype) {
-    case G2N_BOOL: coo_to_csr_t<uint8_t>(c, dr, dc, (const uint8_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
-    case G2N_INT8: coo_to_csr_t<int8_t>(c, dr, dc, (const int8_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
-    case G2N_INT32: coo_to_csr_t<int32_t>(c, dr, dc, (const int32_t*)dd, nnz, n_rows, n_cols, uniform, &D); break;
-    case G2N_FLOAT32: coo_to_csr_t<float>(c, dr, dc, (const float*)dd, nnz, n_rows, n_cols, uniform, &D); break;
-    default: coo_to_csr_t<double>(c, dr, dc, (const double*)dd, nnz, n_rows, n_cols, uniform, &D); break;
+    case G2N_BOOL: coo_to_csr_t<uint8_t>(c, dr, dc, (const uint8_t*)dd, nnz, n_rows, n_cols, uniform, &D, force_unsorted); break;
+    case G2N_INT8: coo_to_csr_t<int8_t>(c, dr, dc, (const int8_t*)dd, nnz, n_rows, n_cols, uniform, &D, force_unsorted); break;
+    case G2N_INT32: coo_to_csr_t<int32_t>(c, dr, dc, (const int32_t*)dd, nnz, n_rows, n_cols, uniform, &D, force_unsorted); break;
+    case G2N_FLOAT32: coo_to_csr_t<float>(c, dr, dc, (const float*)dd, nnz, n_rows, n_cols, uniform, &D, force_unsorted); break;
+    default: coo_to_csr_t<double>(c, dr, dc, (const double*)dd, nnz, n_rows, n_cols, uniform, &D, force_unsorted); break;
   }
   finish_timings(c, &D);
   HostResult* H = new_host_result();
@@ -2505,6 +2555,20 @@ uint64_t keyset_add(g2n_keyset* ks, const uint8_t* blob, const int64_t* offs, ui
   G2N_HIP(hipMemcpyAsync(&n_new, pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
   G2N_HIP(hipMemcpyAsync(&new_bytes, bpos + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   G2N_HIP(hipStreamSynchronize(c->stream));
+  // an entry packs the key length in 24 bits and its blob offset in 40 (KsEntry.loc): refuse what
+  // would not fit rather than store a truncated length
+  if (ks->blob_len + (uint64_t)new_bytes > kKsOffMask)
+    throw Failure(G2N_E_UNSUPPORTED, "key set blob past 2^40 bytes");
+  if ((uint64_t)new_bytes > kKsMaxKeyLen) {
+    auto* mx = dget<unsigned long long>(c, S_TEMP, 1);
+    G2N_HIP(hipMemsetAsync(mx, 0, sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(k_ks_max_len, dim3(std::min<uint64_t>(grid_for(n, 256), 1024)), dim3(256), 0, c->stream,
+                       (const int64_t*)lens, n, mx);
+    unsigned long long longest = 0;
+    G2N_HIP(hipMemcpyAsync(&longest, mx, sizeof(longest), hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (longest > kKsMaxKeyLen) throw Failure(G2N_E_UNSUPPORTED, "a key of 2^24 bytes or more");
+  }
   if (n_new) {
     ks_grow(c, &ks->blob, &ks->blob_cap, ks->blob_len, ks->blob_len + (uint64_t)new_bytes + 16);
     ks_grow(c, &ks->offs, &ks->offs_cap, ks->n + 1, ks->n + n_new + 1);
@@ -2691,6 +2755,41 @@ void g2n_context_destroy(g2n_context* ctx) { g2n::context_destroy(ctx); }
 
 void* g2n_context_stream(g2n_context* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+int g2n_context_trim(g2n_context* ctx, const void* const* keep, uint64_t n_keep, uint64_t* freed) {
+  if (!ctx || (n_keep && !keep)) {
+    g2n::set_last_error("g2n_context_trim: null argument");
+    return G2N_E_ARG;
+  }
+  try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    G2N_HIP(hipSetDevice(ctx->device));
+    G2N_HIP(hipStreamSynchronize(ctx->stream));
+    uint64_t total = 0;
+    for (int s = 0; s < g2n::S_NSLOTS; s++) {
+      g2n::DevBuf& b = ctx->bufs[s];
+      if (!b.p) continue;
+      bool held = false;  // a buffer holding any kept pointer stays (a result the caller still reads)
+      for (uint64_t k = 0; k < n_keep && !held; k++) {
+        const uintptr_t p = (uintptr_t)keep[k], a = (uintptr_t)b.p;
+        held = p && p >= a && p < a + b.cap;
+      }
+      if (held) continue;
+      G2N_HIP(hipFree(b.p));
+      total += b.cap;
+      b.p = nullptr;
+      b.cap = 0;
+      ctx->scan_slot[s] = g2n::ScanSlot{};  // a later allocation at the same address must be cleared again
+    }
+    ctx->wenc = nullptr;
+    ctx->gcoo = g2n::GroupedCoo{};
+    if (freed) *freed = total;
+    return G2N_OK;
+  } catch (const g2n::Failure& f) {
+    g2n::set_last_error(f.what());
+    return f.status;
+  }
+}
+
 int g2n_build_device(g2n_context* ctx, const void* d_input, size_t len, const g2n_options* opts, g2n_result* out) {
   if (!ctx || !opts || !out || (len && !d_input)) {
     g2n::set_last_error("g2n_build_device: null argument");
@@ -2737,6 +2836,21 @@ int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, c
     ev6[5] = (int64_t)ctx->range_vmax;
   }
   return rc;
+}
+
+int g2n_coo_to_csr_band(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows,
+                        int64_t n_cols, int32_t dtype, int32_t device, int32_t force_unsorted, g2n_result** out) {
+  if (!out || force_unsorted < -1 || force_unsorted > 1) return G2N_E_ARG;
+  *out = nullptr;
+  try {
+    return g2n::coo_to_csr(rows, cols, data, nnz, n_rows, n_cols, 4, dtype, device, 0, out, force_unsorted);
+  } catch (const g2n::Failure& f) {
+    g2n::set_last_error(f.what());
+    return f.status;
+  } catch (const std::exception& e) {
+    g2n::set_last_error(e.what());
+    return G2N_E_DEVICE;
+  }
 }
 
 int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz, int64_t n_rows,

@@ -6,7 +6,8 @@
 //   line 0:            H\tVN:Z:1.0
 //   S lines i=1..N_S:  S\t{name(i)}\t{seq}  |seq| ~ Geometric(1/8) over ACGT;
 //                      name(i) = "i", or (names = 1) "s" + 8 hex digits of a u32 bijection of i,
-//                      or (names = 2) the decimal of a permutation of 1..N_S (affine mod N_S)
+//                      or (names = 2) the decimal of a permutation of 1..N_S (affine mod N_S),
+//                      or (names = 3) "s" + the decimal of i (minigraph's layout: prefixed, in S order)
 //   L lines j:         L\t{name(src)}\t{o1}\t{name(dst)}\t{o2}\t0M[\tRC:i:{k}]
 //                      src ~ U[1,N_S], dst = min(src + Geometric(5/16), N_S) (far = 1: dst ~ U[1,N_S]),
 //                      o = '+' with probability 922/1024, k ~ U[1,99]
@@ -25,7 +26,8 @@ namespace g2n {
 struct SynthSpec {
   uint64_t n_s, n_l, seed;
   int32_t rc;
-  int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32); 2: permuted decimal
+  int32_t names;  // 0: decimal "i"; 1: hashed "s%08x" of synth_name_mix(i) (n_s < 2^32); 2: permuted decimal;
+                  // 3: prefixed "s" + "i" in S order
   int32_t far;    // 1: dst ~ U[1, N_S] instead of src + Geometric(5/16)
   uint64_t pmul;  // names = 2: multiplier coprime to n_s (synth_perm_mul)
 };
@@ -143,12 +145,16 @@ G2N_HD inline uint32_t synth_name_mix(uint32_t x) {
 }
 
 G2N_HD inline uint32_t synth_name_len(const SynthSpec& s, uint64_t i) {
-  return s.names == 1 ? 9u : synth_digits(s.names == 2 ? synth_perm(s, i) : i);
+  return s.names == 1 ? 9u : (s.names == 3 ? 1u : 0u) + synth_digits(s.names == 2 ? synth_perm(s, i) : i);
 }
 
 G2N_HD inline char* synth_put_name(const SynthSpec& s, char* o, uint64_t i) {
   if (!s.names) return synth_put_u64(o, i);
   if (s.names == 2) return synth_put_u64(o, synth_perm(s, i));
+  if (s.names == 3) {
+    *o++ = 's';
+    return synth_put_u64(o, i);
+  }
   const uint32_t h = synth_name_mix((uint32_t)i);
   *o++ = 's';
   for (int k = 7; k >= 0; k--) {

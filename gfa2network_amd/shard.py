@@ -215,6 +215,81 @@ class DevArray:
         return DevArray(self.ptr + a * self.itemsize, max(b - a, 0), self.itemsize)
 
 
+class _HostView:
+    """What DevBuf.cpu() returns: .numpy() of the host copy (the torch-tensor idiom the protocol uses)."""
+
+    def __init__(self, arr):
+        self.arr = arr
+
+    def numpy(self):
+        return self.arr
+
+
+class _HipAlloc:
+    """One hipMalloc'd block, freed with the last DevBuf viewing it."""
+
+    def __init__(self, hip, device: int, nbytes: int):
+        self.hip, self.ptr = hip, ctypes.c_void_p()
+        if hip.hipSetDevice(device) != 0 or hip.hipMalloc(ctypes.byref(self.ptr), max(int(nbytes), 16)) != 0:
+            raise MemoryError(f"hipMalloc of {nbytes} bytes failed on device {device}")
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.hip.hipFree(self.ptr)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+class DevBuf:
+    """A 1-D device array owned through the HIP runtime (hipMalloc / hipFree over ctypes) — the
+    one-GPU chunked build's buffers without torch.  Exposes what the engine and
+    the chunked code read: numel, data_ptr, element_size, dtype, 1-D slices (views), contiguous / to
+    (itself), cpu().numpy() / numpy() / tolist() (host copies)."""
+
+    def __init__(self, n: int, dtype, device: int = 0, _alloc=None, _ptr=None):
+        self.dtype, self.n, self.device = np.dtype(dtype), int(n), device
+        self.hip = nat.hip_runtime()
+        self._alloc = _alloc if _alloc is not None else _HipAlloc(self.hip, device, self.n * self.dtype.itemsize)
+        self.ptr = _ptr if _ptr is not None else self._alloc.ptr.value
+
+    def numel(self):
+        return self.n
+
+    def data_ptr(self):
+        return self.ptr
+
+    def element_size(self):
+        return self.dtype.itemsize
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, sl: slice):
+        a, b, step = sl.indices(self.n)
+        if step != 1:
+            raise IndexError("DevBuf: unit-stride slices only")
+        return DevBuf(max(b - a, 0), self.dtype, self.device, self._alloc, self.ptr + a * self.dtype.itemsize)
+
+    def contiguous(self):
+        return self
+
+    def to(self, device):
+        return self
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.n, dtype=self.dtype)
+        if self.n and self.hip.hipMemcpy(out.ctypes.data, self.ptr, out.nbytes, 2) != 0:  # device to host
+            raise RuntimeError("hipMemcpy failed")
+        return out
+
+    def cpu(self):
+        return _HostView(self.numpy())
+
+    def tolist(self):
+        return self.numpy().tolist()
+
+
 class _HipKeyset:
     """g2n_keyset on an engine's context: add(blob, offsets) -> (ids int32 of the keys, keys in the set);
     names() -> the set's keys in id order (copies); close()."""
@@ -225,9 +300,9 @@ class _HipKeyset:
         eng._check(eng.lib.g2n_keyset_create(eng.ctx, ctypes.byref(self.h)), "g2n_keyset_create")
 
     def add(self, blob, offsets):
-        torch, eng = self.eng.torch, self.eng
+        eng = self.eng
         n = offsets.numel() - 1
-        ids = torch.empty(max(n, 1), dtype=torch.int32, device=eng.device)
+        ids = eng._empty(max(n, 1), "int32")
         tot = ctypes.c_uint64(0)
         eng._sync()
         eng._check(eng.lib.g2n_keyset_add(self.h, blob.data_ptr() if blob.numel() else None, blob.numel(),
@@ -235,11 +310,11 @@ class _HipKeyset:
         return ids[:n], int(tot.value)
 
     def names(self):
-        torch, eng = self.eng.torch, self.eng
+        eng = self.eng
         pb, po, n, nb = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64(0), ctypes.c_uint64(0)
         eng._check(eng.lib.g2n_keyset_view(self.h, ctypes.byref(pb), ctypes.byref(po), ctypes.byref(n),
                                            ctypes.byref(nb)), "g2n_keyset_view")
-        return eng._copy_out(pb.value, int(nb.value), torch.uint8), eng._copy_out(po.value, int(n.value) + 1, torch.int64)
+        return eng._copy_out(pb.value, int(nb.value), "uint8"), eng._copy_out(po.value, int(n.value) + 1, "int64")
 
     def close(self):
         if self.h:
@@ -249,17 +324,22 @@ class _HipKeyset:
 
 class HipEngine:
     """The product engine: libg2n.so on one GPU; buffers are torch device tensors (or DevArray
-    views of a context's arena)."""
+    views of a context's arena) — or, torch_buffers=False (the one-GPU chunked build: no collective,
+    so no torch), DevBuf arrays allocated through the HIP runtime."""
 
     supports_views = True
 
-    def __init__(self, device: int = 0):
-        import torch
+    def __init__(self, device: int = 0, torch_buffers: bool = True):
+        if torch_buffers:
+            import torch
 
-        self.torch = torch
+            self.torch = torch
+            self.device = torch.device("cuda", device)
+        else:
+            self.torch = None
+            self.device = device
         self.lib = nat.load()
         self.device_index = device
-        self.device = torch.device("cuda", device)
         self.ctx = self.lib.g2n_context_create(device)
         if not self.ctx:
             raise nat.NativeUnavailable(nat.last_error())
@@ -273,23 +353,47 @@ class HipEngine:
                 setattr(self, name, None)
 
     def _sync(self):
-        self.torch.cuda.current_stream(self.device).synchronize()
+        # (DevBuf work is synchronous — hipMemcpy, and every g2n call returns after its stream drained)
+        if self.torch is not None:
+            self.torch.cuda.current_stream(self.device).synchronize()
 
     def _check(self, rc: int, what: str):
         if rc != 0:
             raise RuntimeError(f"{what}: {nat.status_name(rc)}: {nat.last_error()}")
 
-    def _copy_out(self, ptr, n, dtype):
-        t = self.torch.empty(n, dtype=dtype, device=self.device)
+    def _empty(self, n, dtype: str):
+        """n elements of numpy dtype name `dtype` on this GPU: a torch tensor or a DevBuf."""
+        if self.torch is None:
+            return DevBuf(n, dtype, self.device_index)
+        return self.torch.empty(n, dtype=getattr(self.torch, dtype), device=self.device)
+
+    def _copy_out(self, ptr, n, dtype: str):
+        t = self._empty(n, dtype)
         nbytes = n * t.element_size()
         if nbytes:
             if self._hip.hipMemcpy(t.data_ptr(), ptr, nbytes, 3) != 0:  # device to device
                 raise RuntimeError("hipMemcpy failed")
         return t
 
+    def cat(self, xs):
+        """1-D device arrays of one dtype, concatenated (torch.cat, or D2D copies into one DevBuf)."""
+        if len(xs) == 1:
+            return xs[0]
+        if self.torch is not None:
+            return self.torch.cat(xs)
+        out = DevBuf(sum(x.numel() for x in xs), xs[0].dtype, self.device_index)
+        pos = 0
+        for x in xs:
+            nb = x.numel() * x.element_size()
+            if nb and self._hip.hipMemcpy(out.ptr + pos, x.data_ptr(), nb, 3) != 0:
+                raise RuntimeError("hipMemcpy failed")
+            pos += nb
+        return out
+
     def empty(self, n, dtype):
-        return self.torch.empty(n, dtype=getattr(self.torch, dtype) if isinstance(dtype, str) else dtype,
-                                device=self.device)
+        if self.torch is None or isinstance(dtype, str):
+            return self._empty(n, dtype if isinstance(dtype, str) else str(dtype).replace("torch.", ""))
+        return self.torch.empty(n, dtype=dtype, device=self.device)
 
     def trim(self, keep=(), build_ctx: bool = False) -> int:
         """Release the context's arena buffers except those holding the device pointers in `keep`
@@ -303,7 +407,8 @@ class HipEngine:
         freed = ctypes.c_uint64(0)
         self._sync()
         self._check(self.lib.g2n_context_trim(ctx, arr, len(ptrs), ctypes.byref(freed)), "g2n_context_trim")
-        self.torch.cuda.empty_cache()
+        if self.torch is not None:
+            self.torch.cuda.empty_cache()
         return int(freed.value)
 
     def _build_ctx(self):
@@ -319,7 +424,6 @@ class HipEngine:
         context (valid until its next build; remap_pairs rewrites them in place), the names copied.
         values=False: a build without a weight tag leaves its values unwritten (options.range_flags
         G2N_RANGE_NO_VALUES) — the caller routes coordinates only and never reads them."""
-        torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=True, device=self.device_index, **opts)
         o.unknown_warned = int(unknown_warned)
         o.range_flags = 0 if values else nat.RANGE_NO_VALUES
@@ -340,26 +444,26 @@ class HipEngine:
             if not name.startswith("_"):
                 sh.phase_ms[name] = sh.phase_ms.get(name, 0.0) + res.phase_ms[j]
         if rc == 8 and res.err_detail_len:  # the bytes whose decode raises, for the message
-            sh.err_detail = bytes(self._copy_out(res.err_detail, res.err_detail_len, torch.uint8).cpu().numpy())
+            sh.err_detail = bytes(self._copy_out(res.err_detail, res.err_detail_len, "uint8").cpu().numpy())
         if rc != 0:
             return sh
         n = res.nnz
-        tdt = getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")])
+        tdt = TORCH_DTYPES[opts.get("dtype", "float64")]
         if view:
             sh.rows, sh.cols = DevArray(res.rows or 0, n, 4), DevArray(res.cols or 0, n, 4)
-            sh.data = DevArray(res.data or 0, n, torch.empty(0, dtype=tdt).element_size())
+            sh.data = DevArray(res.data or 0, n, np.dtype(tdt).itemsize)
         else:
-            sh.rows = self._copy_out(res.rows, n, torch.int32)
-            sh.cols = self._copy_out(res.cols, n, torch.int32)
+            sh.rows = self._copy_out(res.rows, n, "int32")
+            sh.cols = self._copy_out(res.cols, n, "int32")
             sh.data = self._copy_out(res.data, n, tdt)
-        sh.names_offsets = self._copy_out(res.names_offsets, res.n_nodes + 1, torch.int64)
-        sh.names_blob = self._copy_out(res.names_blob, int(res.names_bytes), torch.uint8)
+        sh.names_offsets = self._copy_out(res.names_offsets, res.n_nodes + 1, "int64")
+        sh.names_blob = self._copy_out(res.names_blob, int(res.names_bytes), "uint8")
         return sh
 
     def read_range(self, path: str, offset: int, length: int):
         """Bytes [offset, offset + length) of the file, pread into pinned staging and copied to this
         rank's HBM (g2n_upload_file_range): a rank never reads the other ranks' bytes."""
-        t = self.torch.empty(length, dtype=self.torch.uint8, device=self.device)
+        t = self._empty(length, "uint8")
         if length:
             self._sync()
             self._check(self.lib.g2n_upload_file_range(os.fsencode(path), offset, length, t.data_ptr(),
@@ -369,7 +473,7 @@ class HipEngine:
     def upload(self, arr):
         """Host bytes (a numpy uint8 array: a chunk of text inflated / read into host memory) to this
         GPU's HBM."""
-        t = self.torch.empty(len(arr), dtype=self.torch.uint8, device=self.device)
+        t = self._empty(len(arr), "uint8")
         if len(arr):
             a = np.ascontiguousarray(arr)
             self._sync()
@@ -386,7 +490,8 @@ class HipEngine:
         context: before a chunked build's whole-matrix assembly, whose buffers then
         have the GPU to themselves.  Views of earlier results become invalid."""
         self.close()
-        self.torch.cuda.empty_cache()
+        if self.torch is not None:
+            self.torch.cuda.empty_cache()
         self.ctx = self.lib.g2n_context_create(self.device_index)
         if not self.ctx:
             raise nat.NativeUnavailable(nat.last_error())
@@ -403,7 +508,6 @@ class HipEngine:
         """The range parsed straight into GLOBAL decimal ids (S lines s_base.. of n_seg), or None when
         it needs the general protocol (ids that are not decimal, errors, warnings, slow weights).
         view: the COO as DevArray views of the build context (valid until the next build_decimal)."""
-        torch = self.torch
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
         o.range_s_base, o.range_n_segments = int(s_base), int(n_seg)
         o.range_flags = nat.RANGE_DECIMAL | (0 if values else nat.RANGE_NO_VALUES)
@@ -438,19 +542,18 @@ class HipEngine:
         return self._decimal_shard(res, opts, view), [int(v) for v in ev]
 
     def _decimal_shard(self, res, opts: dict, view: bool) -> LocalShard:
-        torch = self.torch
         n = res.nnz
         sh = LocalShard(status=0, err_line=-1, err_index=-1, err_value=0.0, err_detail=b"", warn_line=-1,
                         has_warning=False, warn_byte=0, n_lines=res.n_lines, n_records=res.n_records,
                         n_records_before_error=res.n_records, n_edges=res.n_edges, n_local_nodes=res.n_nodes,
                         n_cast_overflow=res.n_cast_overflow)
-        tdt = getattr(torch, TORCH_DTYPES[opts.get("dtype", "float64")])
+        tdt = TORCH_DTYPES[opts.get("dtype", "float64")]
         if view:
             sh.rows, sh.cols = DevArray(res.rows or 0, n, 4), DevArray(res.cols or 0, n, 4)
-            sh.data = DevArray(res.data or 0, n, torch.empty(0, dtype=tdt).element_size())
+            sh.data = DevArray(res.data or 0, n, np.dtype(tdt).itemsize)
         else:
-            sh.rows = self._copy_out(res.rows, n, torch.int32)
-            sh.cols = self._copy_out(res.cols, n, torch.int32)
+            sh.rows = self._copy_out(res.rows, n, "int32")
+            sh.cols = self._copy_out(res.cols, n, "int32")
             sh.data = self._copy_out(res.data, n, tdt)
         sh.parse_path = "k1" if any(res.phase_names[k] == b"tiles" for k in range(res.n_phases)) else "tile_local"
         return sh
@@ -536,13 +639,12 @@ class HipEngine:
         return rows, cols
 
     def route_triplets(self, rows, cols, data, dtype: str, gmap, n_global: int, n_ranks: int, transposed: bool):
-        torch = self.torch
         n = rows.numel()
-        orows = torch.empty(n, dtype=torch.int32, device=self.device)
-        ocols = torch.empty(n, dtype=torch.int32, device=self.device)
+        orows = self._empty(n, "int32")
+        ocols = self._empty(n, "int32")
         # data None: uniform values (unweighted), nothing to route
-        odata = None if data is None else torch.empty(n, dtype=getattr(torch, TORCH_DTYPES[dtype]), device=self.device)
-        starts = torch.empty(n_ranks + 1, dtype=torch.int32, device=self.device)
+        odata = None if data is None else self._empty(n, TORCH_DTYPES[dtype])
+        starts = self._empty(n_ranks + 1, "int32")
         self._sync()
         nz = n > 0
         self._check(self.lib.g2n_route_triplets(
@@ -557,7 +659,6 @@ class HipEngine:
                  force_unsorted: int, copy: bool = True):
         """The slice's CSR; copy=False: DevArray views of the context's result (valid until its next
         call — what a caller that reads the slice right away, or never, needs: no device copy)."""
-        torch = self.torch
         res = nat.Result()
         t = t if t is not None else (a[0][:0], a[1][:0], None)
 
@@ -569,13 +670,13 @@ class HipEngine:
                                                    p(t[1]), p(t[2]), t[0].numel(), int(maxsym), row_base, n_rows,
                                                    n_cols, nat.DTYPE_CODES[dtype], int(uniform), force_unsorted,
                                                    ctypes.byref(res)), "g2n_csr_from_coo_pair")
-        tdt = getattr(torch, TORCH_DTYPES[dtype])
+        tdt = TORCH_DTYPES[dtype]
         if not copy:
-            w = torch.empty(0, dtype=tdt).element_size()
+            w = np.dtype(tdt).itemsize
             iw = 8 if res.index_width == 8 else 4  # (a whole matrix past 2^31 - 1 entries: int64 views)
             return (DevArray(res.indptr or 0, n_rows + 1, iw), DevArray(res.indices or 0, res.nnz, iw),
                     DevArray(res.data or 0, res.nnz, w), not res.sum_sorted, bool(maxsym) and not res.sum_t_sorted)
-        idx = torch.int64 if res.index_width == 8 else torch.int32  # (a whole matrix past 2^31 - 1 entries)
+        idx = "int64" if res.index_width == 8 else "int32"  # (a whole matrix past 2^31 - 1 entries)
         indptr = self._copy_out(res.indptr, n_rows + 1, idx)
         indices = self._copy_out(res.indices, res.nnz, idx)
         vals = self._copy_out(res.data, res.nnz, tdt)
@@ -923,7 +1024,6 @@ def _assemble_csr(engine, parts, n: int, maxsym: bool, uniform: bool, dtype: str
     (indptr, indices, data, index_maxval) — device tensors (one piece) or numpy (bands)."""
     import time
 
-    torch = engine.torch if hasattr(engine, "torch") else __import__("torch")
     t1 = time.perf_counter()
     n_trip = sum(int(p[0].numel()) for p in parts)
     w = _ITEMSIZE[dtype]
@@ -945,7 +1045,7 @@ def _assemble_csr(engine, parts, n: int, maxsym: bool, uniform: bool, dtype: str
         bands = max(2, -(-per // int(room * 0.8)))
     d = lambda x: None if uniform else x  # noqa: E731  (uniform values are never read)
     if bands == 1:
-        cat = (lambda xs: torch.cat(xs) if len(xs) > 1 else xs[0])
+        cat = engine.cat
         rows, cols = cat([p[0] for p in parts]), cat([p[1] for p in parts])
         data = None if uniform else cat([p[2] for p in parts])
         parts.clear()
@@ -967,7 +1067,7 @@ def _assemble_csr(engine, parts, n: int, maxsym: bool, uniform: bool, dtype: str
     def band(routed, starts, k):
         pieces = [(g[0][s[k]:s[k + 1]], g[1][s[k]:s[k + 1]], None if g[2] is None else g[2][s[k]:s[k + 1]])
                   for g, s in zip(routed, starts)]
-        cat = (lambda xs: torch.cat(xs) if len(xs) > 1 else xs[0])
+        cat = engine.cat
         return (cat([p[0] for p in pieces]), cat([p[1] for p in pieces]),
                 None if uniform else cat([p[2] for p in pieces]))
 

@@ -59,7 +59,7 @@ def _lib():
     return lib
 
 
-NAME_MODES = {"decimal": 0, "hashed": 1, "permuted": 2}
+NAME_MODES = {"decimal": 0, "hashed": 1, "permuted": 2, "prefixed": 3}
 
 
 def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = False, threads: int = 0,
@@ -67,7 +67,8 @@ def host_bytes(n_segments: int, n_links: int, seed: int = 0, rc_tag: bool = Fals
     """The synthetic GFA as bytes, generated on the CPU.  names="hashed": segment i is named
     "s" + 8 hex digits of a bijection of i (unique, not the decimal ids "1".."N"); names="permuted":
     the decimal of a permutation of 1..N (decimal names, not in S order).  far_links: an L
-    line's second segment is uniform over all segments (no id locality)."""
+    line's second segment is uniform over all segments (no id locality); names="prefixed": "s" + the
+    decimal of i in S order (minigraph's s1..sN)."""
     lib = _lib()
     spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names], int(far_links))
     ptr, n = ctypes.c_void_p(), ctypes.c_size_t()

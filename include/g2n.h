@@ -133,8 +133,10 @@ enum {
   G2N_TEST_NO_DIRECT = 4096,    /* never the direct-address tier (the lean hash tier instead) */
   G2N_TEST_NO_EXT_LEAN = 8192,  /* bidirected / weighted decimal builds: K1 + the lean parse, not the
                                    extended tile-local parse */
-  G2N_TEST_NO_DEC_TEXT = 16384  /* edge-list export of a decimal-id build through the names blob, not
+  G2N_TEST_NO_DEC_TEXT = 16384, /* edge-list export of a decimal-id build through the names blob, not
                                    the arithmetic render */
+  G2N_TEST_NO_DEC_PREFIX = 32768 /* names "P1".."PN" in S order through the direct-address tier, not
+                                   the tile-local decimal parse behind the prefix */
 };
 
 #define G2N_MAX_PHASES 40
@@ -284,6 +286,17 @@ int64_t g2n_first_bad_utf8(const uint8_t *blob, const int64_t *offsets, uint64_t
 int g2n_coo_to_csr(const void *rows, const void *cols, const void *data, int64_t nnz, int64_t n_rows,
                    int64_t n_cols, int32_t index_width, int32_t dtype, int32_t device, uint32_t test_flags,
                    g2n_result **out);
+
+/* One row band of a COO too large for g2n_coo_to_csr's weighted limit (rows band-local, 0..n_rows-1,
+ * in the whole COO's stream order): the band's CSR.  force_unsorted = -1: the band's own sortedness
+ * decides (as for a whole matrix); 0 / 1: scipy's has_sorted_indices verdict of the WHOLE matrix
+ * (coo.tocsr -> sum_duplicates sorts every row when any is unsorted, utils.py:55), which decides
+ * the order float duplicates are summed in.  result.sum_sorted: this band's own verdict (-1: the
+ * band's sums cannot depend on order).  The caller (gfa2network_amd/_native.py coo_to_csr) cuts the
+ * bands, asks each for its verdict, re-runs the sorted ones with 1 when another is unsorted, and
+ * concatenates them with int64 indptr / indices as scipy returns past 2^31 - 1 entries. */
+int g2n_coo_to_csr_band(const void *rows, const void *cols, const void *data, int64_t nnz, int64_t n_rows,
+                        int64_t n_cols, int32_t dtype, int32_t device, int32_t force_unsorted, g2n_result **out);
 
 /* ---- device-resident entry points (the measured hot path) ------------------------------ */
 typedef struct g2n_context g2n_context;

@@ -22,7 +22,8 @@ typedef struct g2n_synth_spec {
   int32_t names;       /* 0: segment i is "i"; 1: "s" + 8 hex digits of a bijection of i
                           (unique, not decimal: the hash-dictionary / general sharded paths);
                           2: the decimal of a permutation of 1..n_segments (decimal names out of
-                          order: the direct-address dictionary tier) */
+                          order: the direct-address dictionary tier); 3: "s" + the decimal of i
+                          (minigraph's s1..sN: prefixed names in S order) */
   int32_t far_links;   /* 1: an L line's second segment is uniform over all segments (no id
                           locality: every edge's two rows fall in different CSR buckets) */
 } g2n_synth_spec;

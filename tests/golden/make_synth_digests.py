@@ -31,6 +31,8 @@ CASES = {  # name -> (n_segments, n_links, rc_tag, seed, mode[, segment names])
     "C4": (50_000_000, 200_000_000, False, 0, {}),
     # C4's dimensions with the decimal names permuted (synth names="permuted"): the direct-address tier
     "C4P": (50_000_000, 200_000_000, False, 0, {}, "permuted"),
+    # ... and minigraph's prefixed names "s1".."sN" in S order (synth names="prefixed"): the direct tier
+    "C4X": (50_000_000, 200_000_000, False, 0, {}, "prefixed"),
 }
 
 

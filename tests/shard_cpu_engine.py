@@ -49,6 +49,9 @@ class CpuEngine:
     def __init__(self, oracle_mod):
         self.oracle = oracle_mod
 
+    def cat(self, xs):  # (HipEngine.cat's contract)
+        return torch.cat(xs) if len(xs) > 1 else xs[0]
+
     def local_build(self, buf, opts, unknown_warned=False):
         o = self.oracle.run(bytes(buf.numpy()), **opts)
         if unknown_warned and o.status == 8:

@@ -230,7 +230,7 @@ def _cpu_engine_factory(monkeypatch, oracle_mod, free=None):
     from gfa2network_amd import shard
     from shard_cpu_engine import CpuEngine
 
-    def make(device=0):
+    def make(device=0, torch_buffers=True):
         e = CpuEngine(oracle_mod)
         if free is not None:
             e.free_bytes = free

@@ -658,7 +658,8 @@ def test_convert_format_int64_path_equals_oracle(gpu, oracle_lib, monkeypatch, c
     """convert_format(A, "csr" | "csc") of a COO parse_gfa returns (utils.py:55; cli.py:239 for
     `convert --undirected`) through the int64 index path g2n_coo_to_csr takes past 2^31 - 1 entries
     (TEST_INDEX64 forces it on a small input): int64 indptr / indices holding exactly scipy's values, in
-    every COO mode and every CLI dtype; a weighted COO keeps its own path (int32, equal values)."""
+    every COO mode and every CLI dtype; a weighted COO takes the row-band route a weighted COO past
+    2^31 - 2 entries takes (three bands here): int64 too, equal values."""
     from gfa2network_amd import _native as nat
     from gfa2network_amd import convert_format, parse_gfa
     from gfa2network_amd import synth
@@ -679,8 +680,8 @@ def test_convert_format_int64_path_equals_oracle(gpu, oracle_lib, monkeypatch, c
             for fmt, ref in (("csr", R), ("csc", Rc)):
                 C = convert_format(A, fmt)
                 # every value dtype(1) (no weight tag, or an RC tag absent from every line): the
-                # bucket partition's int64 path; other values keep int32 below 2^31 - 1 entries
-                want = np.int64 if bool(np.all(A.data == 1)) else np.int32
+                # bucket partition's int64 path; other values: the row bands (_coo_to_csr_bands)
+                want = np.int64
                 if C.indptr.dtype != want or C.indices.dtype != want:
                     bad.append((mode, dtype, fmt, "dtype", C.indptr.dtype))
                 if not (np.array_equal(C.indptr, ref.indptr) and np.array_equal(C.indices, ref.indices)
@@ -704,3 +705,45 @@ def test_scan_status_epochs_wrap(gpu, oracle_lib):
         first = first or key
         assert key == first, i
     assert outcome(gpu_run(data, {"directed": False}, "float64", None)) == want
+
+
+def _band_coo(seed, n, m, dtype, sorted_rows):
+    """A COO whose float duplicates sum differently in stream and in sorted order (1e16, 1, -1e16),
+    and whose rows below n // 2 are in column order (sorted_rows) while the rest are not."""
+    r = np.random.default_rng(seed)
+    rows = np.sort(r.integers(0, n, m)).astype(np.int32)
+    cols = r.integers(0, n, m).astype(np.int32)
+    if sorted_rows:  # the first half of the rows sorted by column inside each row
+        lo = rows < n // 2
+        order = np.lexsort((cols[lo], rows[lo]))
+        cols[lo] = cols[lo][order]
+    vals = r.choice(np.array([1e16, 1.0, -1e16, 0.5, 3.0, -2.0]), m)
+    dup = r.integers(0, m, m // 4)  # duplicates of existing (row, col) pairs
+    rows = np.concatenate([rows, rows[dup]])
+    cols = np.concatenate([cols, cols[dup]])
+    vals = np.concatenate([vals, r.choice(np.array([1e16, -1e16, 1.0]), len(dup))])
+    perm = np.argsort(rows, kind="stable")  # stream order: rows grouped, duplicates later in their row
+    return rows[perm], cols[perm], vals[perm].astype(dtype)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "int32", "int8", "bool"])
+@pytest.mark.parametrize("shape", ["sorted_and_unsorted", "all_sorted", "uniform"])
+def test_coo_to_csr_row_bands_equal_scipy(gpu, dtype, shape):
+    """The row-band route of convert_format past one call's limit (_coo_to_csr_bands,
+    g2n_coo_to_csr_band) on a small COO cut into 2..7 bands: equal to scipy's coo.tocsr() bit for bit —
+    including float sums whose order depends on scipy's WHOLE-matrix has_sorted_indices verdict (a
+    band sorted on its own is re-run when another band is not) and the uniform partition's bands."""
+    from gfa2network_amd import _native as nat
+
+    n = 4000
+    rows, cols, vals = _band_coo(5, n, 60000, dtype, shape != "sorted_and_unsorted")
+    if shape == "all_sorted":  # every row in column order: scipy sorts nothing
+        order = np.lexsort((cols, rows))
+        rows, cols, vals = rows[order], cols[order], vals[order]
+    if shape == "uniform":
+        vals = np.ones(len(rows), dtype=dtype)
+    want = sp.coo_matrix((vals, (rows, cols)), shape=(n, n)).tocsr()
+    for limit in (len(vals) // 2 + 1, len(vals) // 7 + 1):
+        raw = nat.coo_to_csr(rows, cols, vals, n, n, band_entries=limit)
+        assert np.array_equal(raw.indptr, want.indptr) and np.array_equal(raw.indices, want.indices), limit
+        assert raw.data.tobytes() == want.data.tobytes(), (dtype, shape, limit)

@@ -291,3 +291,101 @@ def test_extended_lean_tiers_equal_oracle(gpu, oracle_lib, monkeypatch, case):
             monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_HASH_LEAN)
             assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, wt, dtype, "classic")
             monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+
+
+# ---- the decimal-id layout behind one constant prefix (round 6: minigraph's "s1".."sN" in S order) ----
+def _prefixed_case(name):
+    r = random.Random(41)
+    n_s, n_l = 5000, 20000
+
+    def gfa(pre, rc=False, n=n_s):
+        S = [f"S\t{pre}{k}\t{'ACGT' * r.randint(0, 3)}\n" for k in range(1, n + 1)]
+        L = []
+        for _ in range(n_l):
+            a = r.randint(1, n)
+            b = min(n, a + r.randint(0, 5))
+            t = f"\tRC:i:{r.randint(-9, 99)}" if rc else ""
+            L.append(f"L\t{pre}{a}\t{r.choice('+-')}\t{pre}{b}\t{r.choice('+-')}\t0M{t}\n")
+        return S, L
+    if name == "s_in_order":
+        S, L = gfa("s")
+        return S + L, True
+    if name == "eight_byte_prefix":
+        S, L = gfa("node_id_")
+        return S + L, True
+    if name == "nine_byte_prefix":  # longer than the layout takes: the hash tiers
+        S, L = gfa("contig_id")
+        return S + L, False
+    if name == "weights_and_header":
+        S, L = gfa("s", rc=True)
+        return ["H\tVN:Z:1.0\n"] + S + L, True
+    if name == "edge_without_prefix":
+        S, L = gfa("s")
+        return S + L[:500] + ["L\t7\t+\ts8\t-\t0M\n"] + L[500:], False
+    if name == "s_without_prefix":
+        S, L = gfa("s")
+        return S[:40] + ["S\t41\t*\n"] + S[41:] + L, False
+    if name == "leading_zero":
+        S, L = gfa("s")
+        return S + L[:500] + ["L\ts07\t+\ts8\t-\t0M\n"] + L[500:], False
+    if name == "empty_decimal":
+        S, L = gfa("s")
+        return S + L[:500] + ["L\ts\t+\ts8\t-\t0M\n"] + L[500:], False
+    if name == "other_prefix":
+        S, L = gfa("s")
+        return S[:40] + ["S\tt41\t*\n"] + S[41:] + L, False
+    if name == "past_the_segments":
+        S, L = gfa("s")
+        return S + L[:500] + [f"L\ts{n_s + 3}\t+\ts8\t-\t0M\n"] + L[500:], False
+    if name == "repeated_name":
+        S, L = gfa("s")
+        return S + ["S\ts77\t*\n"] + L, False
+    if name == "out_of_order":
+        S, L = gfa("s")
+        return S[:10] + [S[11], S[10]] + S[12:] + L, False
+    if name == "s_after_edges":
+        S, L = gfa("s")
+        return S[:-5] + L[:100] + S[-5:] + L[100:], False
+    raise KeyError(name)
+
+
+PREFIXED = ["s_in_order", "eight_byte_prefix", "nine_byte_prefix", "weights_and_header", "edge_without_prefix",
+            "s_without_prefix", "leading_zero", "empty_decimal", "other_prefix", "past_the_segments",
+            "repeated_name", "out_of_order", "s_after_edges"]
+
+
+@pytest.mark.parametrize("case", PREFIXED)
+def test_prefixed_decimal_layout_equals_oracle(gpu, oracle_lib, monkeypatch, case):
+    """Names P + str(k + 1) in S order (P: 1-8 bytes without a digit): the tile-local decimal-id parse
+    strips P (ParseOpts::dpre; names P + str(k + 1) by arithmetic) — no K1, no dictionary.  Against
+    the oracle and against the direct / hash tiers (TEST_NO_DEC_PREFIX), every mode family, bidirected
+    and weighted builds (the extended instance); premise breaks fall back with the same answer."""
+    from gfa2network_amd import _native as nat
+
+    lines, eligible = _prefixed_case(case)
+    data = "".join(lines).encode()
+    wt = "RC" if case == "weights_and_header" else None
+    for mode in MODES + [{"bidirected": True}, {"bidirected": True, "directed": False}]:
+        raw = nat.build_from_buffer(data, nat.make_options(weight_tag=wt, **mode))
+        ph = raw.phase_ms
+        took = not any(k in ph for k in ("tiles", "direct_lookup", "insert_lookup", "insert_claim"))
+        if raw.status == 0:
+            assert took == eligible, (case, mode, sorted(ph))
+        for dtype in ("float64", "int8"):
+            a = outcome(gpu_run(data, mode, dtype, wt))
+            assert a == outcome(oracle_run(oracle_lib, data, mode, dtype, wt)), (case, mode, dtype)
+            monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_DEC_PREFIX)
+            assert a == outcome(gpu_run(data, mode, dtype, wt)), (case, mode, dtype, "direct / hash tiers")
+            monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+
+
+def test_prefixed_decimal_export_equals_oracle(gpu, oracle_lib):
+    """export --format edge-list of a prefixed build: the names come from the blob (the arithmetic
+    render knows only the bare decimals) — the oracle's bytes."""
+    from gfa2network_amd import _native as nat
+
+    data = "".join(_prefixed_case("s_in_order")[0]).encode()
+    for bidir in (False, True):
+        raw = nat.build_from_buffer(data, nat.make_options(bidirected=bidir, output=nat.OUT_EDGE_LIST))
+        want, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
+        assert err is None and raw.status == 0 and bytes(raw.data) == want, bidir

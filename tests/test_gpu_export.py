@@ -145,10 +145,13 @@ def test_gpu_export_decimal_render(gpu, oracle_lib, monkeypatch, case):
         text = bytes(raw.data) if raw.format == "text" else b""
         if raw.status == 0:
             assert ("names" not in raw.phase_ms) == dec, (case, sorted(raw.phase_ms))
-        monkeypatch.setattr(nat, "TEST_FLAGS", nat.TEST_NO_DEC_TEXT)
-        ref = nat.build_from_buffer(data, opts)
-        monkeypatch.setattr(nat, "TEST_FLAGS", 0)
+        # the blob render forced through this call's own options (a flag set after
+        # make_options never reached the build)
+        ref = nat.build_from_buffer(data, nat.make_options(bidirected=bidir, output=nat.OUT_EDGE_LIST,
+                                                           test_flags=nat.TEST_NO_DEC_TEXT))
         assert (raw.status, raw.err_line) == (ref.status, ref.err_line), case
+        if ref.status == 0:
+            assert "names" in ref.phase_ms, (case, sorted(ref.phase_ms))  # the blob path ran
         assert text == (bytes(ref.data) if ref.format == "text" else b""), (case, bidir)
         want, err, _ = oracle_lib.export_edge_list(data, bidirected=bidir)
         assert text == want, (case, bidir)

@@ -156,6 +156,19 @@ def test_c4_permuted_names_full_size_equals_oracle(gpu):
     assert hashlib.sha256(out["blob"].tobytes()).hexdigest() == d["names"]
 
 
+def test_c4_prefixed_names_full_size_equals_oracle(gpu):
+    """C4's dimensions with minigraph's names "s1".."sN" in S order (synth names="prefixed"): the
+    direct-address tier with a one-byte prefix, bit for bit against the oracle's digest of the same
+    bytes (tests/golden/make_synth_digests.py C4X)."""
+    from gfa2network_amd import _native as nat
+
+    d = DIGESTS["C4X"]
+    out = _device_build(d["n_segments"], d["n_links"], names="prefixed", output=nat.OUT_PARSE)
+    assert out["format"] == nat.FMT_CSR and out["n"] == d["n_nodes"] and out["nnz"] == d["parse"]["nnz"]
+    assert _digest(out["indptr"], out["indices"], out["data"]) == d["parse"]["digest"]
+    assert hashlib.sha256(out["blob"].tobytes()).hexdigest() == d["names"]
+
+
 def test_c5_single_gpu_properties(gpu):
     """C5 at full size on one GPU (16 GB in HBM): the undirected SUM CSR's size-independent
     properties, and the stream-order COO (parse_gfa's return value for directed=False)."""
@@ -311,3 +324,52 @@ def test_convert_format_int64_past_2_31_entries(gpu):
         assert bool(np.all(inc | starts[1:len(seg)]))
         total += float(C.data[k:k + step].sum())
     assert total == 2.0 * n_l
+
+
+def test_convert_format_weighted_past_2_31_entries(gpu):
+    """`convert --undirected --weight-tag RC` at more than 2^31 - 1 COO entries (VERDICT r05 item 5;
+    utils.py:55, cli.py:239): 275M S / 1.1G L with RC:i tags through parse_gfa(directed=False,
+    weight_tag="RC") — a 2.2G-triplet weighted COO in host memory — then convert_format(A, "csr"),
+    which converts a weighted COO past one call's limit in row bands (_coo_to_csr_bands).  Checked:
+    int64 indptr / indices (scipy's _coo_to_compressed sizes by coo.nnz), indptr from 0 to nnz and
+    non-decreasing, every row's columns strictly increasing and < n, and the values' exact sum equal
+    to the COO's (integer weights: exact in float64).  Parity beyond these properties: the banded
+    route bit for bit against scipy (test_gpu_diff.py::test_coo_to_csr_row_bands_equal_scipy) and the
+    forced int64 route (::test_convert_format_int64_path_equals_oracle)."""
+    from gfa2network_amd import convert_format, parse_gfa
+    from gfa2network_amd import synth
+
+    n_s, n_l = 275_000_000, 1_100_000_000
+    dev = synth.DeviceInput(n_s, n_l, seed=0, rc_tag=True)
+    try:
+        text = np.empty(dev.len, dtype=np.uint8)
+        assert synth._lib().g2n_synth_download(text.ctypes.data, dev.ptr, dev.len) == 0
+    finally:
+        dev.free()
+    A = parse_gfa(_Reader(text), build_graph=False, build_matrix=True, directed=False, weight_tag="RC")
+    del text
+    assert A.format == "coo" and A.shape == (n_s, n_s) and A.nnz == 2 * n_l > 2**31 - 1
+    step = 1 << 28
+    want = 0.0
+    for k in range(0, A.nnz, step):
+        want += float(A.data[k:k + step].sum())
+    assert not np.all(A.data[:1000] == 1.0)
+    C = convert_format(A, "csr")
+    del A
+    assert C.format == "csr" and C.indptr.dtype == np.int64 and C.indices.dtype == np.int64
+    ip, ix = C.indptr, C.indices
+    nnz = int(ip[-1])
+    assert int(ip[0]) == 0 and nnz == len(ix) == len(C.data) and bool(np.all(ip[1:] >= ip[:-1]))
+    total = 0.0
+    starts = np.zeros(step + 1, dtype=bool)
+    for k in range(0, nnz, step):
+        seg = ix[k:k + step + 1]
+        assert int(seg.min()) >= 0 and int(seg.max()) < n_s
+        starts[:] = False
+        lo, hi = np.searchsorted(ip, [k, k + len(seg)])
+        rs = ip[lo:hi] - k
+        starts[rs[(rs > 0) & (rs < len(seg))]] = True
+        inc = seg[1:] > seg[:-1]
+        assert bool(np.all(inc | starts[1:len(seg)]))
+        total += float(C.data[k:k + step].sum())
+    assert total == want

@@ -46,3 +46,33 @@ def test_keyset_matches_dict(gpu):
     finally:
         ks.close()
         eng.close()
+
+
+def test_keyset_refuses_keys_past_its_length_field(gpu):
+    """A key of 2^24 bytes or more does not fit KsEntry's 24-bit length: the add is refused
+    (G2N_E_UNSUPPORTED) instead of storing a truncated length that later lookups would miss
+    (ADVICE r05); one byte shorter is accepted and found again."""
+    import torch
+
+    from gfa2network_amd.shard import HipEngine
+
+    eng = HipEngine(0)
+    ks = eng.keyset()
+    try:
+        for n, ok in ((1 << 24) - 1, True), (1 << 24, False):
+            key = np.full(n, ord("a"), dtype=np.uint8)
+            key[-1] = ord("z") if ok else ord("y")
+            offs = np.array([0, 1, 1 + n], dtype=np.int64)
+            blob = np.concatenate([np.array([ord("k")], dtype=np.uint8), key])
+            args = (torch.from_numpy(blob).to(eng.device), torch.from_numpy(offs).to(eng.device))
+            if ok:
+                ids, n_tot = ks.add(*args)
+                assert ids.cpu().numpy().tolist() == [0, 1] and n_tot == 2
+                ids, n_tot = ks.add(*args)  # found again, nothing new
+                assert ids.cpu().numpy().tolist() == [0, 1] and n_tot == 2
+            else:
+                with pytest.raises(RuntimeError, match="UNSUPPORTED"):
+                    ks.add(*args)
+    finally:
+        ks.close()
+        eng.close()
