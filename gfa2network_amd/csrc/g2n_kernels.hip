@@ -1877,6 +1877,60 @@ __device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S
   return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
 }
 
+#ifndef G2N_DPP_SCAN  // experiment builds: 0 = the lean tile's scan / reductions by ds_bpermute shuffles (round 5)
+#define G2N_DPP_SCAN 1
+#endif
+// Wave-wide inclusive scans / reductions by DPP (gfx9 row_shr within 16-lane rows, then row_bcast:15 /
+// row_bcast:31 across rows): one VALU op per step, no LDS crossbar round trip (__shfl_up / __shfl_xor
+// compile to ds_bpermute).  Lanes a step has no source for take the identity (old operand).
+template <class Op>
+__device__ __forceinline__ uint32_t wave_dpp_incl(uint32_t v, uint32_t id, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint32_t dpp_add(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t dpp_max(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t dpp_smin(uint32_t a, uint32_t b) { return (int32_t)a < (int32_t)b ? a : b; }
+__device__ __forceinline__ uint32_t dpp_smax(uint32_t a, uint32_t b) { return (int32_t)a > (int32_t)b ? a : b; }
+// the wave's reduction (every lane gets it: lane 63's inclusive value)
+template <class Op>
+__device__ __forceinline__ uint32_t wave_dpp_reduce(uint32_t v, uint32_t id, Op op) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_dpp_incl(v, id, op), 63);
+}
+
+// The lean tile's block scan of (starts, S lines, edge lines), each < 2^16 per tile: two 32-bit DPP wave
+// scans, the waves' totals through LDS.  Returns the exclusive prefix packed as block_excl_scan_n64's.
+template <uint32_t kN>
+__device__ inline unsigned long long lean_block_scan(uint32_t n_st, uint32_t n_s, uint32_t n_e, unsigned long long* tot,
+                                                     unsigned long long* lds /* >= kN / 64 */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t a = n_st | (n_s << 16), ia = wave_dpp_incl(a, 0u, dpp_add), ie = wave_dpp_incl(n_e, 0u, dpp_add);
+  if (lane == 63) lds[wid] = (unsigned long long)ia | ((unsigned long long)ie << 32);
+  __syncthreads();
+  uint32_t ba = 0, be = 0, ta = 0, te = 0;
+#pragma unroll
+  for (int q = 0; q < (int)(kN / 64); q++) {
+    const unsigned long long y = lds[q];
+    if (q < wid) {
+      ba += (uint32_t)y;
+      be += (uint32_t)(y >> 32);
+    }
+    ta += (uint32_t)y;
+    te += (uint32_t)(y >> 32);
+  }
+  __syncthreads();
+  auto pack = [](uint32_t x, uint32_t e) {
+    return (unsigned long long)(x & 0xFFFFu) | ((unsigned long long)(x >> 16) << 20) | ((unsigned long long)e << 40);
+  };
+  *tot = pack(ta, te);
+  return pack(ba + ia - a, be + ie - n_e);
+}
+
 template <uint32_t kN, class T>
 __device__ inline T block_excl_scan_n64(T v, T* tot, T* lds /* >= kN / 64 */) {  // exclusive; *tot = total
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2335,8 +2389,12 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   }
   K2_LEAN_STAMP(2);
   unsigned long long tot;
+#if G2N_DPP_SCAN
+  const unsigned long long ex = lean_block_scan<kLeanTPB>(n_st, n_s, n_e, &tot, red64);
+#else
   const unsigned long long ex = block_excl_scan_n64<kLeanTPB>(
       (unsigned long long)n_st | ((unsigned long long)n_s << 20) | ((unsigned long long)n_e << 40), &tot, red64);
+#endif
   const uint32_t n_lines = (uint32_t)(tot & 0xFFFFFu), s_tot = (uint32_t)((tot >> 20) & 0xFFFFFu),
                  e_tot = (uint32_t)(tot >> 40);
   if (q_unk != ~0u) atomicMin(&s_unk, (((uint32_t)(ex & 0xFFFFFu) + q_unk) << 15) | o_unk);  // (read at the finish)
@@ -2726,6 +2784,14 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   if (e_tot > op.tile_pad) is.fail = 1;  // more edges than the tile's slot holds
   uint32_t vm = is.vmax;
   int32_t dmn = is.dref == kNoS ? 0x7FFFFFFF : is.dref, dmx = is.dref;  // (kNoS is the int32 minimum)
+#if G2N_DPP_SCAN
+  // (n_nl <= 2^15 and n_po < 2^15 per tile: one packed 32-bit sum)
+  const uint32_t c32 = wave_dpp_reduce(n_nl | (n_po << 16), 0u, dpp_add);
+  unsigned long long cnt = (unsigned long long)(c32 & 0xFFFFu) | ((unsigned long long)(c32 >> 16) << 20);
+  vm = wave_dpp_reduce(vm, 0u, dpp_max);
+  dmn = (int32_t)wave_dpp_reduce((uint32_t)dmn, 0x7FFFFFFFu, dpp_smin);
+  dmx = (int32_t)wave_dpp_reduce((uint32_t)dmx, 0x80000000u, dpp_smax);
+#else
   unsigned long long cnt = (unsigned long long)n_nl | ((unsigned long long)n_po << 20);  // per tile < 2^20 each
   for (int o = 32; o > 0; o >>= 1) {
     vm = max(vm, (uint32_t)__shfl_xor(vm, o, 64));
@@ -2733,6 +2799,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     dmx = max(dmx, (int32_t)__shfl_xor(dmx, o, 64));
     cnt += __shfl_xor(cnt, o, 64);
   }
+#endif
   __shared__ uint32_t rv[kW];
   __shared__ int32_t rmn[kW], rmx[kW];
   __shared__ unsigned long long rc[kW];
