@@ -213,6 +213,9 @@ constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // chunks per thread
 #ifndef G2N_EDGE_ONLY  // experiment builds: 0 = no edge-only parse loop in k_tile_lean (round 5)
 #define G2N_EDGE_ONLY 1
 #endif
+#ifndef G2N_EDGE_FLAT  // experiment builds: 0 = the edge-only loop through lean_line (branch per check)
+#define G2N_EDGE_FLAT 1
+#endif
 #ifndef G2N_LOAD_UNIFORM  // experiment builds: 0 = per-chunk bounds on every tile load (round 5)
 #define G2N_LOAD_UNIFORM 1
 #endif
@@ -1099,6 +1102,71 @@ __device__ __forceinline__ bool lean_link(const uint8_t* buf, uint64_t m, uint32
   if (!((m2 >> (lb + 2)) & 1)) return false;
   const uint32_t c2 = buf[so + 3 + la], c4 = buf[so + 6 + la + lb];
   return (c2 == '+' || c2 == '-') && (c4 == '+' || c4 == '-');
+}
+
+// 64 bits of v (128 bits: lo, hi) from bit sh in [0, 63], without a branch on sh == 0
+__device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t sh) {
+  return (lo >> sh) | ((hi << 1) << (63u - sh));
+}
+
+// dec_lds's canonical 1-8 digit decimal at tile offset x, length l, branch-free: *ok false for any other
+// length (the caller takes dec_name for 9-10 digits) or a byte that is not a digit, or a leading '0'
+__device__ __forceinline__ uint32_t dec8_flat(const uint8_t* buf, uint32_t x, uint32_t l, bool* ok) {
+  const uint32_t a = x & ~7u, sh = (x & 7u) * 8;
+  const uint64_t w0 = *(const uint64_t*)(buf + a), w1 = *(const uint64_t*)(buf + a + 8);
+  const uint32_t lc = l - 1u < 8u ? l : 8u;  // (1..8; another length fails below)
+  const uint64_t keep = ~0ull >> (64u - 8u * lc);
+  const uint64_t w = funnel64(w0, w1, sh) & keep;
+  const uint64_t zeros = 0x3030303030303030ull & keep;
+  *ok = l - 1u < 8u && (w & 0xF0F0F0F0F0F0F0F0ull & keep) == zeros &&
+        (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) == 0 &&
+        (w & 0xFF) != '0';
+  const uint64_t d = (w - zeros) << (8u * (8u - lc));
+  auto four = [](uint32_t y) {
+    y = ((y << 3) + (y << 1) + (y >> 8)) & 0x00FF00FFu;
+    return ((y << 6) + (y << 5) + (y << 2) + (y >> 16)) & 0xFFFFu;
+  };
+  return four((uint32_t)d) * 10000u + four((uint32_t)(d >> 32));
+}
+
+// An edge line of an edge-only tile (k_tile_lean's edge-only loop): lean_line<false>'s edge shape and
+// checks as straight-line code — one verdict, no branch per check (the exec-mask bookkeeping of the
+// early returns was most of the loop's scalar instructions).  next == 0: past the staged window (fails).
+// Returns false when the general path must decide (the caller fails the tile); *a / *b the name values.
+__device__ __forceinline__ bool lean_edge_flat(const uint8_t* buf, const uint16_t* tabm, uint32_t o, uint32_t next,
+                                               const ParseOpts& op, uint64_t* a, uint64_t* b) {
+  const uint32_t n = next - 1u - o;  // (next == 0: huge)
+  const uint32_t q = o >> 4, qa = q & ~3u;
+  const uint64_t tlo = *(const uint64_t*)(tabm + qa), thi = *(const uint64_t*)(tabm + qa + 4);
+  const uint64_t w = funnel64(tlo, thi, (q & 3u) * 16u + (o & 15u));  // tab bits from byte o
+  const uint64_t m1 = (w & (~0ull >> (64u - (n <= 48u ? (n ? n : 1u) : 48u)))) >> 2;  // from byte 2
+  const uint32_t la = m1 ? (uint32_t)__builtin_ctzll(m1) : 60u;
+  bool ok = n <= 48u && n >= 2u && m1 != 0 && ((m1 >> (la + 2u)) & 1u);
+  const uint64_t m2 = m1 >> (la + 3u);  // (la <= 60)
+  const uint32_t lb = m2 ? (uint32_t)__builtin_ctzll(m2) : 0u;
+  ok = ok && m2 != 0 && ((m2 >> (lb + 2u)) & 1u);
+  const uint32_t c2 = buf[o + 3u + la], c4 = buf[ok ? o + 6u + la + lb : o];
+  ok = ok && ((c2 - '+') & ~2u) == 0 && ((c4 - '+') & ~2u) == 0;  // '+' or '-'
+  if (!ok) return false;
+  uint32_t xa = o + 2u, xb = o + 5u + la, lna = la, lnb = lb;
+  if (op.dpre_len) {  // (uniform) the names' constant prefix
+    const uint32_t p = op.dpre_len;
+    if (lna <= p || lnb <= p || lds_prefix8(buf, xa, p) != op.dpre || lds_prefix8(buf, xb, p) != op.dpre)
+      return false;
+    xa += p;
+    xb += p;
+    lna -= p;
+    lnb -= p;
+  }
+  bool oka, okb;
+  const uint32_t va = dec8_flat(buf, xa, lna, &oka), vb = dec8_flat(buf, xb, lnb, &okb);
+  if (oka && okb) {
+    *a = va;
+    *b = vb;
+    return true;
+  }
+  // 9-10 digits (or not a decimal): the exact form
+  return dec_lds(buf, xa, lna, a) && dec_lds(buf, xb, lnb, b);
 }
 
 // kExt: the extended instance (bidirected keys, one integer weight tag), tile-local builds only
@@ -2278,6 +2346,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   __shared__ unsigned long long red64[kW];
   __shared__ uint32_t s_gbase;
   __shared__ uint32_t s_unk;  // the tile's first unsupported record (op.tunk): rank << 15 | offset
+  __shared__ uint32_t s_last_end;  // the tile's last line's end (see line_next)
   const uint64_t t0 = tile * kTile;
   if (!kGrouped && op.tile_pad) {  // this tile's slot (positions relative to it, as in a group slot)
     const uint64_t b = tile * (uint64_t)op.tile_pad * op.ktrip;
@@ -2402,6 +2471,16 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   const uint32_t lim = (uint32_t)(len - t0 < kTile + kLeanHalo ? len - t0 : kTile + kLeanHalo);  // staged bytes
   if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
     s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
+  // the tile's last line's end (1 + its '\n', a virtual one at EOF; 0: past the staged window), found
+  // once by the thread holding that line's start, so every line's end is a record read (line_next)
+  if (n_st && (uint32_t)(ex & 0xFFFFFu) + n_st == n_lines) {  // (published by the records' barrier)
+    const uint32_t o = 16 * c0 + 63u - (uint32_t)__builtin_clzll(st);
+    uint32_t c = o >> 4;
+    uint32_t mm = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
+    const uint32_t ce = (lim + 15) / 16;
+    while (!mm && ++c < ce) mm = nlm[c];
+    s_last_end = mm ? 16 * c + (uint32_t)__builtin_ctz(mm) + 1 : (lim == len - t0 ? lim + 1 : 0u);
+  }
   // windows of kLeanLines lines (one for lines of >= 16 bytes on average): each thread writes the
   // records of its lines ranked in [w0, w0 + kLeanLines] (one past: the window's last line ends where
   // the next one starts), then the window's lines are parsed
@@ -2433,14 +2512,9 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     // (3) lane-parallel lines
     const uint32_t n_win = n_lines - w0 < kLeanLines ? n_lines - w0 : kLeanLines;
     // line j's end: 1 + its '\n' (a virtual one at EOF), tile-local; 0 = past the staged window
-    auto line_next = [&](uint32_t j, uint32_t o) -> uint32_t {
-      if (w0 + j + 1 < n_lines) return rec[j + 1] & 0x7FFFu;
-      uint32_t c = o >> 4;
-      uint32_t mm = (uint32_t)nlm[c] & ~((1u << (o & 15)) - 1u);
-      const uint32_t ce = (lim + 15) / 16;
-      while (!mm && ++c < ce) mm = nlm[c];
-      if (mm) return 16 * c + (uint32_t)__builtin_ctz(mm) + 1;
-      return lim == len - t0 ? lim + 1 : 0u;
+    auto line_next = [&](uint32_t j, uint32_t o) -> uint32_t {  // (rec[n_win] is in bounds: a select, no branch)
+      const uint32_t nx = rec[j + 1] & 0x7FFFu, last = s_last_end;
+      return w0 + j + 1 < n_lines ? nx : last;
     };
     if constexpr (kMode == kLeanDirEdges) {
       // kDL lines per thread per step: their 2 kDL random reads all in flight at once (the pass is
@@ -2650,10 +2724,27 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
 #pragma unroll 1                                               // record-kind branches (round 6)
       for (uint32_t j = threadIdx.x; j < n_win; j += kLeanTPB) {
         const uint32_t x = rec[j];
-        const uint32_t o = x & 0x7FFFu;
+        const uint32_t o = x & 0x7FFFu, eb = x >> 17;
         const uint32_t next = line_next(j, o);
-        if (!next || !lean_line<false>(buf, tabm, o, next, kEdge, t0, 0ull, x >> 17, op, TouchOut{}, is))
+#if G2N_EDGE_FLAT
+        uint64_t a, b;
+        if (!lean_edge_flat(buf, tabm, o, next, op, &a, &b) || eb >= op.tile_pad || a > op.n_seg || b > op.n_seg) {
+          is.fail = 1;  // (the general path decides; a key past the S lines is not an S key: int_edge_id)
+          continue;
+        }
+        const uint32_t vm = (uint32_t)(a > b ? a : b);
+        is.vmax = vm > is.vmax ? vm : is.vmax;
+        const uint64_t eo = (uint64_t)eb * op.ktrip;  // (grouped: the tile's base is in rows / cols)
+        op.rows[eo] = (int32_t)(a - 1);
+        op.cols[eo] = (int32_t)(b - 1);
+        if (op.ktrip >= 2) {
+          op.rows[eo + 1] = (int32_t)(b - 1);
+          op.cols[eo + 1] = (int32_t)(a - 1);
+        }
+#else
+        if (!next || !lean_line<false>(buf, tabm, o, next, kEdge, t0, 0ull, eb, op, TouchOut{}, is))
           is.fail = 1;
+#endif
       }
       continue;  // next window
     }

@@ -41,6 +41,9 @@ namespace g2n {
 #ifndef G2N_PART_PREFETCH
 #define G2N_PART_PREFETCH 1
 #endif
+#ifndef G2N_SYM_DPP  // experiment builds: 1 = the partition / finish scans by DPP (g2n_kernels.hip) — measured
+#define G2N_SYM_DPP 0  // slower for the finish (maxsym 2.44 -> 2.54 ms on C4, same box): shuffles kept here
+#endif
 constexpr uint32_t kPartTPB = G2N_PART_TPB;       // threads of a partition block
 constexpr uint32_t kSubPer = 8;                    // elements per thread in one sub-tile
 constexpr uint32_t kSub = kSubPer * kPartTPB;      // 8192 elements per sub-tile
@@ -73,11 +76,15 @@ constexpr uint32_t kSymReg = G2N_FIN_REG;         // stored elements per thread 
 template <uint32_t kN>
 __device__ inline uint32_t block_excl_scan_n(uint32_t v, uint32_t* excl, uint32_t* lds /* >= kN / 64 */) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#if G2N_DPP_SCAN && G2N_SYM_DPP  // (g2n_kernels.hip: DPP row_shr / row_bcast, no ds_bpermute round trips)
+  const uint32_t x = wave_dpp_incl(v, 0u, dpp_add);
+#else
   uint32_t x = v;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
+#endif
   if (lane == 63) lds[wid] = x;
   __syncthreads();
   uint32_t wbase = 0, tot = 0;
@@ -793,7 +800,11 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
   {  // one network per wave: the longest short row of the wave picks it (no divergent sorts)
     uint32_t wm = (live && shortrow) ? my : 0u;
+#if G2N_DPP_SCAN && G2N_SYM_DPP
+    wm = wave_dpp_reduce(wm, 0u, dpp_max);
+#else
     for (int o = 32; o > 0; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor(wm, o, 64));
+#endif
     if (wm > 8) net_sort<16>(k);
     else if (wm > 4) net_sort<8>(k);
     else if (wm > 1) net_sort<4>(k);
@@ -1172,7 +1183,11 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
   for (int i = 0; i < kR; i++) r[i] = (live && i < (int)my) ? sg[i] : ~0ull;  // padding sorts last
   {  // one network per wave: the longest in-register row of the wave picks it (no divergent sorts)
     uint32_t wm = (live && inreg) ? my : 0u;
+#if G2N_DPP_SCAN && G2N_SYM_DPP
+    wm = wave_dpp_reduce(wm, 0u, dpp_max);
+#else
     for (int o = 32; o > 0; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor(wm, o, 64));
+#endif
     if (wm > 8) sumw_sort_net<16>(r);
     else if (wm > 4) sumw_sort_net<8>(r);
     else if (wm > 1) sumw_sort_net<4>(r);
