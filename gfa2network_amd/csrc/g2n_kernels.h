@@ -127,8 +127,10 @@ struct ParseOpts {
   // every name is these dpre_len (<= 8, no digit) bytes, little-endian, then the canonical decimal
   uint64_t dpre;
   uint32_t dpre_len;
+  // group slots: 2^gshift tiles per slot (kGroupShift, fewer for small inputs: group_shift_for)
+  uint32_t gshift;
 };
-constexpr uint32_t kGroupShift = 5;  // 32 tiles per group slot
+constexpr uint32_t kGroupShift = 5;  // at most 32 tiles per group slot
 
 // per-tile evidence of the decimal-id premise in a tile-local parse: every S line's name value
 // minus (its S index within the tile + 1), min and max (equal, = the S lines before the tile, when

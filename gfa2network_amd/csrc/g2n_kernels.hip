@@ -213,6 +213,9 @@ constexpr uint32_t kChunkIters = kTileChunks / kTPB;       // chunks per thread
 #ifndef G2N_EDGE_ONLY  // experiment builds: 0 = no edge-only parse loop in k_tile_lean (round 5)
 #define G2N_EDGE_ONLY 1
 #endif
+#ifndef G2N_MASK2  // experiment builds: 0 = the lean tile's two bitmaps by two mask16 (round 5)
+#define G2N_MASK2 1
+#endif
 #ifndef G2N_EDGE_FLAT  // experiment builds: 0 = the edge-only loop through lean_line (branch per check)
 #define G2N_EDGE_FLAT 1
 #endif
@@ -278,6 +281,31 @@ __device__ inline uint32_t mask16(uint4 v, uint32_t pat) {
   x ^= t1 ^ (t1 << 3);
   const uint32_t t2 = (x ^ (x >> 6)) & 0x00CCu;
   x ^= t2 ^ (t2 << 6);
+  return x;
+}
+
+// Both bitmaps of a 16-byte chunk at once: tab bits (byte order) in the low 16 bits, newline bits in the
+// high 16 (round 6; == mask16(v, 0x09..) | mask16(v, 0x0A..) << 16).  t = byte ^ 0x08 maps tab to 1 and
+// newline to 2; one exact "byte < 4" test (no carry between bytes) then bit 0 / bit 1 of t pick tab /
+// newline; the four words' tab bits go to bits 8b + k and newline bits to 8b + 4 + k of one word, a
+// nibble unshuffle separates them into two 16-bit halves, and the 4 x 4 bit transposes of both halves
+// run in the same two delta swaps (about 56 VALU for both bitmaps against about 90 for two mask16).
+__device__ inline uint32_t tabnl_word(uint32_t w) {  // bit 8b + 3: byte b is a tab; bit 8b + 7: a newline
+  const uint32_t t = w ^ 0x08080808u;
+  const uint32_t lt4 = ~(((t & 0x7F7F7F7Fu) + 0x7C7C7C7Cu) | t) & 0x80808080u;  // bytes t < 4
+  const uint32_t a = t << 7, b = t << 6;
+  return ((lt4 & a & ~b) >> 4) | (lt4 & b & ~a);
+}
+__device__ inline uint32_t mask16x2(uint4 v) {
+  uint32_t x = (tabnl_word(v.x) >> 3) | (tabnl_word(v.y) >> 2) | (tabnl_word(v.z) >> 1) | tabnl_word(v.w);
+  uint32_t d = ((x >> 4) ^ x) & 0x00F000F0u;  // nibble unshuffle: tab nibbles low, newline nibbles high
+  x ^= d ^ (d << 4);
+  d = ((x >> 8) ^ x) & 0x0000FF00u;
+  x ^= d ^ (d << 8);
+  d = (x ^ (x >> 3)) & 0x0A0A0A0Au;  // 4 x 4 transposes: bit 4 b + k -> 4 k + b, both halves
+  x ^= d ^ (d << 3);
+  d = (x ^ (x >> 6)) & 0x00CC00CCu;
+  x ^= d ^ (d << 6);
   return x;
 }
 
@@ -1109,64 +1137,83 @@ __device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t 
   return (lo >> sh) | ((hi << 1) << (63u - sh));
 }
 
-// dec_lds's canonical 1-8 digit decimal at tile offset x, length l, branch-free: *ok false for any other
-// length (the caller takes dec_name for 9-10 digits) or a byte that is not a digit, or a leading '0'
-__device__ __forceinline__ uint32_t dec8_flat(const uint8_t* buf, uint32_t x, uint32_t l, bool* ok) {
-  const uint32_t a = x & ~7u, sh = (x & 7u) * 8;
+// 4 digit values (bytes, the first in byte 0) -> their decimal value, all full-rate: the two pairs' values
+// by 4-way byte dot products (b0 * 10 + b1, b2 * 10 + b3: <= 99, no carry), packed, then one 2-way
+// 16-bit dot product (pair 0 * 100 + pair 1)
+typedef unsigned short g2n_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dig4(uint32_t x) {
+  const uint32_t p = __builtin_amdgcn_udot4(x, 0x0000010Au, 0u, false) |
+                     (__builtin_amdgcn_udot4(x, 0x010A0000u, 0u, false) << 16);
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(g2n_u16x2, p), __builtin_bit_cast(g2n_u16x2, 0x00010064u), 0u,
+                                false);
+}
+
+// dec_lds's canonical decimal of 1-10 digits at tile offset x, length l, as straight-line code (round 6):
+// the last min(l, 8) digits from one 16-byte window (their value by dot products); the first one or two
+// of a 9-10 digit name from two byte loads, only in a wave that has such a name (C4's ids have at most 8
+// digits, C5's up to 9).  *ok false for another length, a byte that is not a digit, a leading '0' or a
+// 10-digit value past 2.2e9 (no segment index; the caller's n_seg bound rejects the rest).  xmax: the
+// last offset the staged tile may be read at (addresses of a failed line are clamped).
+__device__ __forceinline__ uint32_t dec10_flat(const uint8_t* buf, uint32_t x, uint32_t l, uint32_t xmax, bool* ok) {
+  x = x < xmax ? x : xmax;
+  const bool longer = l - 9u < 2u;  // 9 or 10 digits
+  const uint32_t lt = l < 8u ? l : 8u, lc = lt ? lt : 1u;
+  const uint32_t xt = x + (longer ? l - 8u : 0u);  // the last lt digits
+  const uint32_t a = xt & ~7u, sh = (xt & 7u) * 8;
   const uint64_t w0 = *(const uint64_t*)(buf + a), w1 = *(const uint64_t*)(buf + a + 8);
-  const uint32_t lc = l - 1u < 8u ? l : 8u;  // (1..8; another length fails below)
   const uint64_t keep = ~0ull >> (64u - 8u * lc);
   const uint64_t w = funnel64(w0, w1, sh) & keep;
-  const uint64_t zeros = 0x3030303030303030ull & keep;
-  *ok = l - 1u < 8u && (w & 0xF0F0F0F0F0F0F0F0ull & keep) == zeros &&
-        (((w & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull & keep) == 0 &&
-        (w & 0xFF) != '0';
-  const uint64_t d = (w - zeros) << (8u * (8u - lc));
-  auto four = [](uint32_t y) {
-    y = ((y << 3) + (y << 1) + (y >> 8)) & 0x00FF00FFu;
-    return ((y << 6) + (y << 5) + (y << 2) + (y >> 16)) & 0xFFFFu;
-  };
-  return four((uint32_t)d) * 10000u + four((uint32_t)(d >> 32));
+  const uint64_t dv = w & 0x0F0F0F0F0F0F0F0Full;
+  bool good = (l - 1u < 10u) & ((w & 0xF0F0F0F0F0F0F0F0ull) == (0x3030303030303030ull & keep)) &
+              (((dv + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) == 0) & (longer | ((w & 0xFFu) != '0'));
+  uint32_t head = 0;
+  if (__any(longer)) {  // (wave-uniform)
+    const uint32_t h0 = (uint32_t)buf[x] - '0', h1 = (uint32_t)buf[x + 1] - '0';
+    good = good & (!longer | ((h0 - 1u <= 8u) & ((l == 9u) | ((h1 <= 9u) & (h0 * 10u + h1 <= 21u)))));
+    head = longer ? (l == 10u ? h0 * 10u + h1 : h0) & 0x7Fu : 0u;  // (<= 21 when good)
+  }
+  *ok = good;
+  const uint64_t d = dv << (8u * (8u - lc));  // the units digit in byte 7
+  // (head * 10^4 + digits 1-4 of the tail) * 10^4 + digits 5-8: two 24-bit multiply-adds
+  return ((head * 10000u + (dig4((uint32_t)d) & 0x3FFFu)) & 0xFFFFFFu) * 10000u + dig4((uint32_t)(d >> 32));
 }
 
 // An edge line of an edge-only tile (k_tile_lean's edge-only loop): lean_line<false>'s edge shape and
-// checks as straight-line code — one verdict, no branch per check (the exec-mask bookkeeping of the
-// early returns was most of the loop's scalar instructions).  next == 0: past the staged window (fails).
-// Returns false when the general path must decide (the caller fails the tile); *a / *b the name values.
+// checks as straight-line code — one verdict, every LDS load of the line issued before any check (the
+// exec-mask bookkeeping of early returns was most of the loop's scalar instructions, and each early
+// return serialised the next load behind it).  next == 0: past the staged window (fails).  Returns false
+// when the general path must decide (the caller fails the tile); *a / *b the name values.
 __device__ __forceinline__ bool lean_edge_flat(const uint8_t* buf, const uint16_t* tabm, uint32_t o, uint32_t next,
-                                               const ParseOpts& op, uint64_t* a, uint64_t* b) {
+                                               const ParseOpts& op, uint32_t xmax, uint64_t* a, uint64_t* b) {
   const uint32_t n = next - 1u - o;  // (next == 0: huge)
   const uint32_t q = o >> 4, qa = q & ~3u;
   const uint64_t tlo = *(const uint64_t*)(tabm + qa), thi = *(const uint64_t*)(tabm + qa + 4);
   const uint64_t w = funnel64(tlo, thi, (q & 3u) * 16u + (o & 15u));  // tab bits from byte o
-  const uint64_t m1 = (w & (~0ull >> (64u - (n <= 48u ? (n ? n : 1u) : 48u)))) >> 2;  // from byte 2
+  const uint32_t nc = n < 48u ? (n ? n : 1u) : 48u;
+  const uint64_t m1 = (w & (~0ull >> (64u - nc))) >> 2;  // tabs from byte 2 (byte 1's is the record check's)
   const uint32_t la = m1 ? (uint32_t)__builtin_ctzll(m1) : 60u;
-  bool ok = n <= 48u && n >= 2u && m1 != 0 && ((m1 >> (la + 2u)) & 1u);
-  const uint64_t m2 = m1 >> (la + 3u);  // (la <= 60)
+  const uint64_t m2 = m1 >> (la + 3u);  // (la <= 60) tabs from the second name
   const uint32_t lb = m2 ? (uint32_t)__builtin_ctzll(m2) : 0u;
-  ok = ok && m2 != 0 && ((m2 >> (lb + 2u)) & 1u);
-  const uint32_t c2 = buf[o + 3u + la], c4 = buf[ok ? o + 6u + la + lb : o];
-  ok = ok && ((c2 - '+') & ~2u) == 0 && ((c4 - '+') & ~2u) == 0;  // '+' or '-'
-  if (!ok) return false;
+  const uint32_t oa = o + 3u + la, ob = o + 6u + la + lb;  // the orientation bytes
+  const uint32_t c2 = buf[oa < xmax ? oa : xmax], c4 = buf[ob < xmax ? ob : xmax];
+  // a tab after each orientation byte (a zero m1 / m2 has none either), each orientation '+' or '-'
+  bool ok = (n - 2u < 47u) & (((m1 >> (la + 2u)) & 1u) != 0) & (((m2 >> (lb + 2u)) & 1u) != 0) &
+            (((c2 - '+') & ~2u) == 0) & (((c4 - '+') & ~2u) == 0);
   uint32_t xa = o + 2u, xb = o + 5u + la, lna = la, lnb = lb;
   if (op.dpre_len) {  // (uniform) the names' constant prefix
     const uint32_t p = op.dpre_len;
-    if (lna <= p || lnb <= p || lds_prefix8(buf, xa, p) != op.dpre || lds_prefix8(buf, xb, p) != op.dpre)
-      return false;
+    const uint32_t pa = xa < xmax ? xa : xmax, pb = xb < xmax ? xb : xmax;
+    const uint64_t wa = lds_prefix8(buf, pa, p), wb = lds_prefix8(buf, pb, p);
+    ok = ok & (lna > p) & (lnb > p) & (wa == op.dpre) & (wb == op.dpre);
     xa += p;
     xb += p;
     lna -= p;
     lnb -= p;
   }
   bool oka, okb;
-  const uint32_t va = dec8_flat(buf, xa, lna, &oka), vb = dec8_flat(buf, xb, lnb, &okb);
-  if (oka && okb) {
-    *a = va;
-    *b = vb;
-    return true;
-  }
-  // 9-10 digits (or not a decimal): the exact form
-  return dec_lds(buf, xa, lna, a) && dec_lds(buf, xb, lnb, b);
+  *a = dec10_flat(buf, xa, lna, xmax, &oka);
+  *b = dec10_flat(buf, xb, lnb, xmax, &okb);
+  return ok & oka & okb;
 }
 
 // kExt: the extended instance (bidirected keys, one integer weight tag), tile-local builds only
@@ -1934,6 +1981,9 @@ constexpr uint32_t kLeanLines = 2048;                                   // line 
 #ifndef G2N_LEAN_PAIR  // experiment builds: the decimal parse two lines per lane per step
 #define G2N_LEAN_PAIR 0
 #endif
+#ifndef G2N_CLASSIFY_FLAT  // experiment builds: 0 = the lean classify's starts through line_kind's branches
+#define G2N_CLASSIFY_FLAT 1
+#endif
 #ifndef G2N_LEAN_BATCH  // experiment builds: starts classified per region with their loads batched
 #define G2N_LEAN_BATCH 4
 #endif
@@ -1943,6 +1993,18 @@ static_assert(kTile <= 32768 && (kLeanRegion == 4 || kLeanRegion == 2),
 
 __device__ inline uint32_t lean_code(uint8_t kd) {  // record kind: 0 other, 1 S, 2 edge, 3 P / O
   return kd == kS ? 1u : kd == kEdge ? 2u : kd == kPO ? 3u : 0u;
+}
+
+// lean_code(line_kind(c0, exact)) as straight-line code (round 6): one bit per record letter of
+// '@'..'_' tested against each kind's letters; *unk: kUnknown (not a record letter at all)
+__device__ __forceinline__ uint32_t lean_code_flat(uint32_t c0, bool exact, bool* unk) {
+  constexpr uint32_t kBS = 1u << ('S' - 64), kBE = (1u << ('L' - 64)) | (1u << ('E' - 64)) | (1u << ('C' - 64)),
+                     kBPO = (1u << ('P' - 64)) | (1u << ('O' - 64)), kBHF = (1u << ('H' - 64)) | (1u << ('F' - 64));
+  const uint32_t idx = c0 - 64u;
+  const uint32_t bit = idx < 32u ? 1u << idx : 0u;
+  *unk = (bit & (kBS | kBE | kBPO | kBHF)) == 0;
+  const uint32_t code = (bit & kBS ? 1u : 0u) | (bit & kBE ? 2u : 0u) | (bit & kBPO ? 3u : 0u);
+  return exact ? code : 0u;
 }
 
 #ifndef G2N_DPP_SCAN  // experiment builds: 0 = the lean tile's scan / reductions by ds_bpermute shuffles (round 5)
@@ -2367,8 +2429,14 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   for (uint32_t j = 0; j < R.kPer; j++) {
     const uint32_t c = j * kLeanTPB + threadIdx.x;
     if (c < kLeanChunks) {
+#if G2N_MASK2
+      const uint32_t tn = mask16x2(R.r[j]);
+      tabm[c] = (uint16_t)tn;
+      nlm[c] = (uint16_t)(tn >> 16);
+#else
       tabm[c] = (uint16_t)mask16(R.r[j], 0x09090909u);
       nlm[c] = (uint16_t)mask16(R.r[j], 0x0A0A0A0Au);
+#endif
     }
   }
   if (next_tile < n_tiles) R.load(in, len, next_tile * kTile);  // in flight through this tile's parse
@@ -2432,6 +2500,28 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       x0[q] = buf[o];
       x1[q] = buf[o + 1];
     }
+#if G2N_CLASSIFY_FLAT
+    // (round 6) branch-free: unsupported() as selects — the first unknown start that op.tunk takes, or
+    // the failure for one it cannot (a first byte >= 0x80 or no op.tunk)
+#pragma unroll
+    for (uint32_t q = 0; q < kLeanBatch; q++) {
+      const bool on = off[q] != 0xFFFFu;
+      const bool exact = (t0 + off[q] + 1 >= len) | (x0[q] == '\n') | (x1[q] == '\t') | (x1[q] == '\n');
+      bool unk = false;
+      uint32_t code = lean_code_flat(x0[q], exact, &unk);
+      code = on ? code : 0u;
+      unk = unk & on;
+      const bool hard = unk & ((op.tunk == nullptr) | (x0[q] >= 0x80u));
+      is.fail |= hard ? 1u : 0u;
+      const bool take = unk & !hard & (q_unk == ~0u);
+      q_unk = take ? q : q_unk;
+      o_unk = take ? off[q] : o_unk;
+      codes |= code << (2 * q);
+      n_s += code == 1;
+      n_e += code == 2;
+      n_po += code == 3;
+    }
+#else
 #pragma unroll
     for (uint32_t q = 0; q < kLeanBatch; q++) {
       if (off[q] == 0xFFFFu) continue;
@@ -2444,6 +2534,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
       n_e += code == 2;
       n_po += code == 3;
     }
+#endif
 #pragma unroll 1
     for (uint32_t q = kLeanBatch; m; q++) {  // more than kLeanBatch lines start in these 64 bytes
       const uint32_t o = 16 * c0 + (uint32_t)__builtin_ctzll(m);
@@ -2470,7 +2561,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   K2_LEAN_STAMP(3);
   const uint32_t lim = (uint32_t)(len - t0 < kTile + kLeanHalo ? len - t0 : kTile + kLeanHalo);  // staged bytes
   if (kGrouped && threadIdx.x == 0)  // this tile's place in its group slot (published by the barrier below)
-    s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> kGroupShift], e_tot * op.ktrip) : 0u;
+    s_gbase = n_lines && e_tot <= op.tile_pad ? atomicAdd(&gcount[tile >> op.gshift], e_tot * op.ktrip) : 0u;
   // the tile's last line's end (1 + its '\n', a virtual one at EOF; 0: past the staged window), found
   // once by the thread holding that line's start, so every line's end is a record read (line_next)
   if (n_st && (uint32_t)(ex & 0xFFFFFu) + n_st == n_lines) {  // (published by the records' barrier)
@@ -2504,7 +2595,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
     if (w0 == 0) {
       K2_LEAN_STAMP(4);
       if (kGrouped) {
-        const uint64_t b = (tile >> kGroupShift) * gcap + s_gbase;
+        const uint64_t b = (tile >> op.gshift) * gcap + s_gbase;
         op.rows += b;
         op.cols += b;
       }
@@ -2728,13 +2819,15 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
         const uint32_t next = line_next(j, o);
 #if G2N_EDGE_FLAT
         uint64_t a, b;
-        if (!lean_edge_flat(buf, tabm, o, next, op, &a, &b) || eb >= op.tile_pad || a > op.n_seg || b > op.n_seg) {
+        if (!lean_edge_flat(buf, tabm, o, next, op, kTile + kLeanHalo - 8u, &a, &b) | (eb >= op.tile_pad) |
+            (a > op.n_seg) | (b > op.n_seg)) {
           is.fail = 1;  // (the general path decides; a key past the S lines is not an S key: int_edge_id)
           continue;
         }
         const uint32_t vm = (uint32_t)(a > b ? a : b);
         is.vmax = vm > is.vmax ? vm : is.vmax;
-        const uint64_t eo = (uint64_t)eb * op.ktrip;  // (grouped: the tile's base is in rows / cols)
+        const uint32_t eo = (eb & 0xFFFFFu) * (op.ktrip & 0xFu);  // (24-bit: eb < tile_pad, ktrip <= 4; grouped:
+                                                                  // the tile's base is in rows / cols)
         op.rows[eo] = (int32_t)(a - 1);
         op.cols[eo] = (int32_t)(b - 1);
         if (op.ktrip >= 2) {

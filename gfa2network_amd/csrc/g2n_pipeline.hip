@@ -54,6 +54,9 @@ enum Slot {
   S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_TLIST, S_TNB, S_NSLOTS
 };
 
+#ifndef G2N_MIN_GROUPS  // group slots: fewer tiles per slot until the input has about this many slots
+#define G2N_MIN_GROUPS 1024
+#endif
 #ifndef G2N_PTILE_SMALL_DIV  // partition blocks below 2^24 elements: kPartTile / this many (C2: 8 and 4 alike, 2 slower)
 #define G2N_PTILE_SMALL_DIV 4
 #endif
@@ -1265,8 +1268,12 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
 #endif
-  const uint64_t n_groups = (n_tiles + (1u << kGroupShift) - 1) >> kGroupShift;
-  const uint64_t gcap = ((uint64_t)kTileEdgeCap << kGroupShift) * ktrip;  // entries per group slot
+  // 32 tiles per group slot; a small input takes fewer, so that the partition's first pass (one block
+  // per group) still has about G2N_MIN_GROUPS blocks (C2's 3.7K tiles: 115 groups of 32 left most CUs idle)
+  uint32_t gshift = kGroupShift;
+  while (gshift > 0 && (n_tiles >> gshift) < (uint64_t)G2N_MIN_GROUPS) gshift--;
+  const uint64_t n_groups = (n_tiles + (1u << gshift) - 1) >> gshift;
+  const uint64_t gcap = ((uint64_t)kTileEdgeCap << gshift) * ktrip;  // entries per group slot
   const uint64_t slots = grouped ? n_groups * gcap : n_tiles * kTileEdgeCap * ktrip;
   auto* rows_p = dget<int32_t>(c, S_ROWSP, slots);
   auto* cols_p = dget<int32_t>(c, S_COLSP, slots);
@@ -1285,6 +1292,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
   lo.n_seg = 0x7FFFFFFFull;    // the file's S count is known afterwards (k_tile_lean_check)
   lo.dpre = dpre;              // names behind one constant prefix (first_segment_prefixed)
   lo.dpre_len = dpre_len;
+  lo.gshift = gshift;
   lo.pf_dist = G2N_K2_PREFETCH ? (uint32_t)c->lean_blocks : 0u;
   // a whole-file build takes the unsupported-record warning itself (k_tile_lean_check); a sharded range
   // leaves it to the general protocol
