@@ -1159,10 +1159,10 @@ __device__ __forceinline__ uint32_t dec10_flat(const uint8_t* buf, uint32_t x, u
   const bool longer = l - 9u < 2u;  // 9 or 10 digits
   const uint32_t lt = l < 8u ? l : 8u, lc = lt ? lt : 1u;
   const uint32_t xt = x + (longer ? l - 8u : 0u);  // the last lt digits
-  const uint32_t a = xt & ~7u, sh = (xt & 7u) * 8;
-  const uint64_t w0 = *(const uint64_t*)(buf + a), w1 = *(const uint64_t*)(buf + a + 8);
+  const uint32_t* wp = (const uint32_t*)(buf + (xt & ~3u));  // three dwords hold the 8 bytes from xt
+  const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], sb = (xt & 3u) * 8u;
   const uint64_t keep = ~0ull >> (64u - 8u * lc);
-  const uint64_t w = funnel64(w0, w1, sh) & keep;
+  const uint64_t w = (((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sb) << 32) | __builtin_amdgcn_alignbit(w1, w0, sb)) & keep;
   const uint64_t dv = w & 0x0F0F0F0F0F0F0F0Full;
   bool good = (l - 1u < 10u) & ((w & 0xF0F0F0F0F0F0F0F0ull) == (0x3030303030303030ull & keep)) &
               (((dv + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) == 0) & (longer | ((w & 0xFFu) != '0'));
@@ -1186,9 +1186,10 @@ __device__ __forceinline__ uint32_t dec10_flat(const uint8_t* buf, uint32_t x, u
 __device__ __forceinline__ bool lean_edge_flat(const uint8_t* buf, const uint16_t* tabm, uint32_t o, uint32_t next,
                                                const ParseOpts& op, uint32_t xmax, uint64_t* a, uint64_t* b) {
   const uint32_t n = next - 1u - o;  // (next == 0: huge)
-  const uint32_t q = o >> 4, qa = q & ~3u;
-  const uint64_t tlo = *(const uint64_t*)(tabm + qa), thi = *(const uint64_t*)(tabm + qa + 4);
-  const uint64_t w = funnel64(tlo, thi, (q & 3u) * 16u + (o & 15u));  // tab bits from byte o
+  const uint32_t q = o >> 4;
+  const uint32_t* tp = (const uint32_t*)(tabm + (q & ~1u));  // three dwords: chunks q & ~1 .. + 5
+  const uint32_t t0 = tp[0], t1 = tp[1], t2 = tp[2], tb = (q & 1u) * 16u + (o & 15u);
+  const uint64_t w = ((uint64_t)__builtin_amdgcn_alignbit(t2, t1, tb) << 32) | __builtin_amdgcn_alignbit(t1, t0, tb);
   const uint32_t nc = n < 48u ? (n ? n : 1u) : 48u;
   const uint64_t m1 = (w & (~0ull >> (64u - nc))) >> 2;  // tabs from byte 2 (byte 1's is the record check's)
   const uint32_t la = m1 ? (uint32_t)__builtin_ctzll(m1) : 60u;
@@ -2973,8 +2974,10 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
   const uint32_t c32 = wave_dpp_reduce(n_nl | (n_po << 16), 0u, dpp_add);
   unsigned long long cnt = (unsigned long long)(c32 & 0xFFFFu) | ((unsigned long long)(c32 >> 16) << 20);
   vm = wave_dpp_reduce(vm, 0u, dpp_max);
-  dmn = (int32_t)wave_dpp_reduce((uint32_t)dmn, 0x7FFFFFFFu, dpp_smin);
-  dmx = (int32_t)wave_dpp_reduce((uint32_t)dmx, 0x80000000u, dpp_smax);
+  if (s_tot) {  // (block-uniform) no S line: every lane holds the identities already
+    dmn = (int32_t)wave_dpp_reduce((uint32_t)dmn, 0x7FFFFFFFu, dpp_smin);
+    dmx = (int32_t)wave_dpp_reduce((uint32_t)dmx, 0x80000000u, dpp_smax);
+  }
 #else
   unsigned long long cnt = (unsigned long long)n_nl | ((unsigned long long)n_po << 20);  // per tile < 2^20 each
   for (int o = 32; o > 0; o >>= 1) {
