@@ -129,6 +129,11 @@ struct ParseOpts {
   uint32_t dpre_len;
   // group slots: 2^gshift tiles per slot (kGroupShift, fewer for small inputs: group_shift_for)
   uint32_t gshift;
+  // a grouped weighted SUM CSR (round 6): each triplet's weight as the exact-int32 code the bucket
+  // partition sums (weight_enc of the dtype's value: wf32 = the value rounded through float32), written
+  // beside rows / cols in the group slots instead of one double per edge line (op.ew)
+  uint32_t* wenc;
+  uint32_t wf32;
 };
 constexpr uint32_t kGroupShift = 5;  // at most 32 tiles per group slot
 

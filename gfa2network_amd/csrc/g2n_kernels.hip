@@ -1296,7 +1296,12 @@ __device__ inline bool lean_line(const uint8_t* buf, const uint16_t* tabm, uint3
           return true;
         }
       }
-      op.ew[e] = wv;
+      if (op.wenc) {  // (grouped) the code beside each of the edge's triplets
+        const uint32_t code = op.wf32 ? (uint32_t)(int32_t)(float)wv : (uint32_t)(int32_t)wv;  // |wv| < 10^9
+        for (uint32_t k = 0; k < op.ktrip; k++) op.wenc[o + k] = code;
+      } else {
+        op.ew[e] = wv;
+      }
     }
     if (op.bidir) {  // builders.py:211-234: "name:o" keys, S line k minting 2k (+) and 2k + 1 (-)
       const uint32_t ia = 2u * (uint32_t)(a - 1) + (c2 == '-'), ib = 2u * (uint32_t)(b - 1) + (c4 == '-');
@@ -2599,6 +2604,7 @@ __device__ __forceinline__ void lean_tile(const uint8_t* __restrict__ in, uint64
         const uint64_t b = (tile >> op.gshift) * gcap + s_gbase;
         op.rows += b;
         op.cols += b;
+        if (kExt && op.wenc) op.wenc += b;
       }
     }
     // (3) lane-parallel lines

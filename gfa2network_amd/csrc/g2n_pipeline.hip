@@ -51,7 +51,7 @@ enum Slot {
   S_ROUT1, S_UCNT0, S_UCNT1, S_UOFF, S_MCNT, S_MOFF, S_RSCR, S_RFLAG0, S_RFLAG1, S_RVAL0, S_RVAL1, S_TID,
   S_INV, S_TUNK, S_DEFER, S_FOFF64, S_BTC, S_BTV, S_BTOT, S_EBAD, S_ELEN, S_EPOS, S_ETEXT, S_EFIRST, S_EMETA, S_EL0, S_EL1,
   S_PCNT, S_POFF, S_PGRP, S_BSTART, S_SCANST, S_RBOUND, S_ROWSP, S_COLSP, S_TLEAN, S_ZIN, S_ZMEM, S_ZBAD, S_RSK, S_RSV, S_RSCNT, S_RSOFF,
-  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_TLIST, S_TNB, S_NSLOTS
+  S_GCNT, S_TCN, S_FINLB, S_INDPTR64, S_INDICES64, S_WENC, S_W1, S_W2, S_TVAL, S_PW0, S_PW1, S_BSTARTA, S_DIRECT, S_RTOT, S_SCANST2, S_EWP, S_TLIST, S_TNB, S_WENCP, S_NSLOTS
 };
 
 #ifndef G2N_MIN_GROUPS  // group slots: fewer tiles per slot until the input has about this many slots
@@ -111,6 +111,7 @@ struct GroupedCoo {
   const int32_t* cols = nullptr;
   const uint32_t* gcount = nullptr;
   uint64_t gcap = 0, n_groups = 0;
+  const uint32_t* wenc = nullptr;  // a weighted build's codes beside rows / cols (ParseOpts::wenc)
 };
 
 }  // namespace g2n
@@ -744,7 +745,15 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   // pass 5: the entries with their values, adjacent transposed twins of one value as one element
   const uint32_t ptile = n_el >= (1ull << 24) ? kPartTile : kPartTile / G2N_PTILE_SMALL_DIV;  // as csr_partition
   src.tile = ptile;
-  const uint64_t n_blk1 = (n_el + ptile - 1) / ptile;
+  const bool grouped = c->gcoo.active;  // (with the parse's codes: run_build) one block per group slot
+  if (grouped) {
+    src.rows = (const uint32_t*)c->gcoo.rows;
+    src.cols = (const uint32_t*)c->gcoo.cols;
+    src.n_entries = c->gcoo.n_groups * c->gcoo.gcap;
+    src.gcount = c->gcoo.gcount;
+    src.gcap = c->gcoo.gcap;
+  }
+  const uint64_t n_blk1 = grouped ? c->gcoo.n_groups : (n_el + ptile - 1) / ptile;
   auto* cnt1 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig1 * n_blk1);
   auto* off1 = dget<uint32_t>(c, S_POFF, (uint64_t)n_dig1 * n_blk1);
   auto* el1 = dget<uint2>(c, S_EL0, n_el);
@@ -822,7 +831,7 @@ static void assemble_t(g2n_context* c, const int32_t* rows, const int32_t* cols,
         csr_partition<T>(c, rows, cols, n_trip, n_rows, !maxsym, R))
       return;
   } else {
-    if (n_trip && n_rows && !maxsym && !c->gcoo.active && !(c->test_flags & kTestNoBuckets) &&
+    if (n_trip && n_rows && !maxsym && (!c->gcoo.active || c->gcoo.wenc) && !(c->test_flags & kTestNoBuckets) &&
         csr_partition_w<T>(c, rows, cols, data, n_trip, n_rows, n_cols, R))
       return;
   }
@@ -1264,7 +1273,9 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
                              TileCnt* tcnt, TileCnt* tbase, TileCnt* tot_out, bool grouped, uint64_t s_base = 0,
                              uint64_t n_seg_all = 0, bool deferred = false, const ParseOpts* xo = nullptr,
                              bool warn_ok = false, uint64_t dpre = 0, uint32_t dpre_len = 0) {
-  if (xo) grouped = false;
+  // an extended build takes group slots when its only reader is the bucket partition: unweighted, or
+  // a weighted SUM CSR whose codes the parse writes (xo->wenc set by the caller as a flag)
+  if (xo && xo->has_wt && !xo->wenc) grouped = false;
 #if G2N_K2_OLD
   grouped = false;  // k_tile_parse<true> writes per-tile slots only
 #endif
@@ -1305,7 +1316,12 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     lo.has_wt = xo->has_wt;
     lo.wt_len = xo->wt_len;
     lo.wt_pack = xo->wt_pack;
-    if (xo->has_wt) lo.ew = ew_p = dget<double>(c, S_EWP, n_tiles * kTileEdgeCap);
+    if (xo->has_wt && grouped) {
+      lo.wenc = dget<uint32_t>(c, S_WENCP, slots);
+      lo.wf32 = xo->wf32;
+    } else if (xo->has_wt) {
+      lo.ew = ew_p = dget<double>(c, S_EWP, n_tiles * kTileEdgeCap);
+    }
   }
 #ifdef G2N_K2_STAMPS
   unsigned long long* stamps = dget<unsigned long long>(c, S_TEMP, n_tiles * kK2Stamps);
@@ -1328,7 +1344,10 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL((k_tile_lean_p<false>), dim3(grid), dim3(kLeanTPB), 0, c->stream, in, len, lo, c->ctl, tcnt,
                        tlean, (uint32_t*)nullptr, (uint64_t)0, n_tiles);
 #else
-  if (xo)
+  if (xo && grouped)
+    hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, true, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0,
+                       c->stream, in, len, lo, c->ctl, tcnt, tlean, gcount, gcap, HashLeanArgs{});
+  else if (xo)
     hipLaunchKernelGGL((k_tile_lean<kLeanDecimal, false, true>), dim3((unsigned)n_tiles), dim3(kLeanTPB), 0,
                        c->stream, in, len, lo, c->ctl, tcnt, tlean, (uint32_t*)nullptr, (uint64_t)0, HashLeanArgs{});
   else if (grouped)
@@ -1388,6 +1407,7 @@ static bool tile_local_parse(g2n_context* c, const uint8_t* in, uint64_t len, ui
       c->gcoo.gcount = gcount;
       c->gcoo.gcap = gcap;
       c->gcoo.n_groups = n_groups;
+      c->gcoo.wenc = lo.wenc;
       *tot_out = tot;
       return true;
     }
@@ -1628,6 +1648,15 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   xo.wt_len = (uint32_t)wt_bytes;
   for (size_t k = 0; k < wt_bytes && k < 8; k++) xo.wt_pack |= (uint64_t)(uint8_t)o->weight_tag[k] << (8 * k);
   const bool ext = bidir || wt_bytes > 0;
+  // a weighted SUM CSR in dtypes whose cast of a canonical <= 9-digit integer can neither fail nor lose
+  // the integer's exact-int32 code (float32: the code of the rounded value) takes group slots: the parse
+  // writes the codes, so neither k_tile_compact nor k_values runs (C3); a bucket partition that declines
+  // (an overfull bucket, an inexact float sum) redoes the build without groups
+  if (wt_bytes && grouped && !maxsym && o->output == G2N_OUT_CSR &&
+      (dt == G2N_FLOAT64 || dt == G2N_FLOAT32 || dt == G2N_INT32)) {
+    xo.wenc = reinterpret_cast<uint32_t*>(uintptr_t{1});  // (a flag here: tile_local_parse allocates them)
+    xo.wf32 = dt == G2N_FLOAT32 ? 1u : 0u;
+  }
   const bool ext_ok = !shard_dec && wt_bytes <= 8 && !(c->test_flags & kTestNoExtLean);
   // (a sharded range with global decimal ids takes it too — with or without S lines of its own)
   const bool local_done =
@@ -1702,7 +1731,9 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
              bidir ? dget<uint64_t>(c, S_OOFF, z(n_t)) : nullptr, bidir ? dget<uint32_t>(c, S_OLEN, z(n_t)) : nullptr,
              dget<uint8_t>(c, S_TKIND, z(n_t))};
   // (E.w is read by k_values only for weights: a tile-local build holds them there when it has a tag)
-  EdgeOut E{dget<double>(c, S_EW, local_done && !wt_bytes ? 1 : n_e), dget<uint32_t>(c, S_ETB, z(n_e))};
+  // (a grouped weighted build wrote exact-int32 codes instead: no per-edge weights at all)
+  const bool codes_done = local_done && c->gcoo.active && c->gcoo.wenc;
+  EdgeOut E{dget<double>(c, S_EW, local_done && (!wt_bytes || codes_done) ? 1 : n_e), dget<uint32_t>(c, S_ETB, z(n_e))};
   const int ktrip = tpe == 4 ? 4 : (gd ? 1 : 2);
   const uint64_t n_trip = n_e * (uint64_t)ktrip;
   // the stream-order COO holds int32 node ids (< 2^31 - 1, checked below) at 64-bit positions; the
@@ -1927,7 +1958,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
 
   // ---- triplets (K6): stream-order COO with the dtype cast
   // values: not for a grouped build whose every value is dtype(1) (the partition reads none)
-  void* data = dbuf(c, S_DATA, (in_groups && !o->weight_tag) ? 16 : n_trip * dtype_size(dt));
+  void* data = dbuf(c, S_DATA, (in_groups && (!o->weight_tag || codes_done)) ? 16 : n_trip * dtype_size(dt));
   const bool uni = !op.has_wt;  // no weight tag: every entry is dtype(1.0)
   const bool coo_out = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
   EdgeIn EI{E.w, E.tb};
@@ -1936,7 +1967,8 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   // caller routes coordinates only (uniform values, no COO result): the values array is left unwritten
   const bool no_values = uni && (o->range_flags & G2N_RANGE_NO_VALUES) != 0;
   if (coords_done) {  // values only, and only when the output or the sums read them
-    if (n_e && (coo_out || !uni) && !no_values) {
+    if (codes_done) c->wenc = c->gcoo.wenc;  // the partition sums the parse's codes; no value is cast
+    if (n_e && (coo_out || !uni) && !no_values && !codes_done) {
       // a weighted SUM CSR: the exact-int32 codes the bucket partition sums (csr_partition_w) beside
       uint32_t* enc = nullptr;
       if (!uni && !maxsym && o->output == G2N_OUT_CSR && !(c->test_flags & kTestNoBuckets) && n_trip <= 0x7FFFFFFFull)
@@ -1966,7 +1998,7 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   }
   // the cast's verdict needs a host wait only when a cast ran (a build whose values are all dtype(1)
   // and unread — C2, C4 — goes on to the assembly without one)
-  const bool cast_ran = !coords_done || (n_e && (coo_out || !uni) && !no_values);
+  const bool cast_ran = !coords_done || (n_e && (coo_out || !uni) && !no_values && !codes_done);
   if (cast_ran) sync_ctl(c);
   const uint64_t cast_key = cast_ran ? c->h_ctl->cast_key : ~0ull;
   R->n_cast_overflow = cast_ran ? (int64_t)(c->h_ctl->n_f32_overflow * (uint64_t)ktrip) : 0;
