@@ -452,8 +452,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
     src.pair_bits = (uint32_t)low + 1u;
     hipLaunchKernelGGL(k_part_hist<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, nm1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1 + nm1, off1 + nm1, nm1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, 2 * nm1);  // both streams' matrices (the scatter rebases A's)
     hipLaunchKernelGGL(k_part_scatter<4>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        (const uint32_t*)off1, n_blk1, el1, wa1);
   } else if (sum || pair) {  // one element per entry
@@ -465,8 +464,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   } else {
     hipLaunchKernelGGL(k_part_hist<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        cnt1, n_blk1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, nm1);
-    scan_excl<uint32_t, uint32_t>(c, cnt1 + nm1, off1 + nm1, nm1);
+    scan_excl<uint32_t, uint32_t>(c, cnt1, off1, 2 * nm1);  // both streams' matrices (the scatter rebases A's)
     hipLaunchKernelGGL(k_part_scatter<1>, dim3((unsigned)n_blk1), dim3(kPartTPB), 0, c->stream, src, shift1, n_dig1,
                        (const uint32_t*)off1, n_blk1, el1, wa1);
   }
@@ -476,60 +474,66 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
   const uint32_t* wa = wa1;
   if (bits2 == 0) {
     hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst);
+                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst, (const uint32_t*)nullptr);
     if (words)
       hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                         (const uint32_t*)(off1 + nm1), (const uint32_t*)(cnt1 + nm1), n_blk1, n_buckets, bstA);
+                         (const uint32_t*)(off1 + nm1), (const uint32_t*)(cnt1 + nm1), n_blk1, n_buckets, bstA,
+                         (const uint32_t*)(off1 + nm1));
   } else {  // pass 2 inside each pass-1 group (stream A's groups: the second half of S_PGRP)
     auto* grp = dget<uint32_t>(c, S_PGRP, 4 * ((uint64_t)n_dig1 + 1));
     uint32_t* grpA = grp + 2 * ((uint64_t)n_dig1 + 1);
     PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0};
     s2.tile = ptile;
-    hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
-                       n_blk1, n_dig1, grp, grp + n_dig1 + 1, ptile);
-    if (words)
-      hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)(off1 + nm1),
-                         (const uint32_t*)(cnt1 + nm1), n_blk1, n_dig1, grpA, grpA + n_dig1 + 1, ptile);
+    // (one launch for both streams' groups: stream A's at grpA = grp + 2 (n_dig1 + 1))
+    hipLaunchKernelGGL(k_part_groups, dim3(words ? 2 : 1), dim3(1024), 0, c->stream, (const uint32_t*)off1,
+                       (const uint32_t*)cnt1, n_blk1, n_dig1, grp, ptile);
     // >= the blocks the groups need (sum of ceil(group / ptile) <= n_el / ptile + n_dig1)
     const uint64_t n_blk2 = (n_el + ptile - 1) / ptile + n_dig1;
-    auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
-    auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));
+    const uint64_t n2 = (uint64_t)n_dig2 * n_blk2;  // one stream's pass-2 count matrix
+    const uint64_t ns = words ? 2 : 1;
+    auto* cnt2 = dget<uint32_t>(c, S_PCNT, ns * n2);
+    auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>(ns * n2, ns * nm1));
     auto* el2 = dget<uint2>(c, S_EL1, n_el);
-    if (bits2 > (int)kMaxDigitBits) {
+    // pass 7: stream A's words (its count matrix after pass 2's, both scanned by one launch; its
+    // offsets less the scan's value at its start, s2a.obase)
+    PartSrc s2a{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, nullptr, grpA, grpA + n_dig1 + 1, n_dig1,
+                nullptr, 0, (uint32_t)low + 1u, nullptr, wa1, ptile};
+    s2a.obase = off2 + n2;
+    uint32_t* wa2 = words ? dget<uint32_t>(c, S_PW1, n_trip) : nullptr;
+    const bool wide = bits2 > (int)kMaxDigitBits;
+    if (wide) {
       hipLaunchKernelGGL((k_part_hist<2, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2,
                          (uint32_t)low, n_dig2, cnt2, n_blk2);
-      scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
-      hipLaunchKernelGGL((k_part_scatter<2, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2,
-                         (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, el2);
+      if (words)
+        hipLaunchKernelGGL((k_part_hist<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream,
+                           s2a, 2u * (uint32_t)low, n_dig2, cnt2 + n2, n_blk2);
     } else {
       hipLaunchKernelGGL(k_part_hist<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
                          n_dig2, cnt2, n_blk2);
-      scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+      if (words)
+        hipLaunchKernelGGL(k_part_hist<7>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2a,
+                           2u * (uint32_t)low, n_dig2, cnt2 + n2, n_blk2);
+    }
+    scan_excl<uint32_t, uint32_t>(c, cnt2, off2, ns * n2);
+    if (wide)
+      hipLaunchKernelGGL((k_part_scatter<2, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2,
+                         (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, el2);
+    else
       hipLaunchKernelGGL(k_part_scatter<2>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2, (uint32_t)low,
                          n_dig2, (const uint32_t*)off2, n_blk2, el2);
-    }
     hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
                        (const uint32_t*)off2, s2, n_dig2, n_buckets, bst);
     el = el2;
-    if (words) {  // pass 7: stream A's words (same count / offset buffers, B's bucket starts are taken)
-      PartSrc s2a{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, nullptr, grpA, grpA + n_dig1 + 1, n_dig1,
-                  nullptr, 0, (uint32_t)low + 1u, nullptr, wa1, ptile};
-      auto* wa2 = dget<uint32_t>(c, S_PW1, n_trip);
-      if (bits2 > (int)kMaxDigitBits) {
-        hipLaunchKernelGGL((k_part_hist<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream,
-                           s2a, 2u * (uint32_t)low, n_dig2, cnt2, n_blk2);
-        scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+    if (words) {
+      if (wide)
         hipLaunchKernelGGL((k_part_scatter<7, kWideDigitBits>), dim3((unsigned)n_blk2), dim3(kPartTPB), 0,
-                           c->stream, s2a, 2u * (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, (uint2*)nullptr, wa2);
-      } else {
-        hipLaunchKernelGGL(k_part_hist<7>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2a,
-                           2u * (uint32_t)low, n_dig2, cnt2, n_blk2);
-        scan_excl<uint32_t, uint32_t>(c, cnt2, off2, (uint64_t)n_dig2 * n_blk2);
+                           c->stream, s2a, 2u * (uint32_t)low, n_dig2, (const uint32_t*)(off2 + n2), n_blk2,
+                           (uint2*)nullptr, wa2);
+      else
         hipLaunchKernelGGL(k_part_scatter<7>, dim3((unsigned)n_blk2), dim3(kPartTPB), 0, c->stream, s2a,
-                           2u * (uint32_t)low, n_dig2, (const uint32_t*)off2, n_blk2, (uint2*)nullptr, wa2);
-      }
+                           2u * (uint32_t)low, n_dig2, (const uint32_t*)(off2 + n2), n_blk2, (uint2*)nullptr, wa2);
       hipLaunchKernelGGL(k_part_bucket_starts, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                         (const uint32_t*)off2, s2a, n_dig2, n_buckets, bstA);
+                         (const uint32_t*)(off2 + n2), s2a, n_dig2, n_buckets, bstA);
       wa = wa2;
     }
   }
@@ -768,13 +772,13 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   const uint32_t* ew = w1;
   if (bits2 == 0) {
     hipLaunchKernelGGL(k_part_bucket_starts1, dim3(grid_for(n_buckets + 1)), dim3(kTPB), 0, c->stream,
-                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst);
+                       (const uint32_t*)off1, (const uint32_t*)cnt1, n_blk1, n_buckets, bst, (const uint32_t*)nullptr);
   } else {  // pass 6 inside each pass-5 group
     auto* grp = dget<uint32_t>(c, S_PGRP, 2 * ((uint64_t)n_dig1 + 1));
     PartSrc s2{nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, el1, grp, grp + n_dig1 + 1, n_dig1, nullptr, 0, 0,
                nullptr, w1, ptile};
     hipLaunchKernelGGL(k_part_groups, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)off1, (const uint32_t*)cnt1,
-                       n_blk1, n_dig1, grp, grp + n_dig1 + 1, ptile);
+                       n_blk1, n_dig1, grp, ptile);
     const uint64_t n_blk2 = (n_el + ptile - 1) / ptile + n_dig1;
     auto* cnt2 = dget<uint32_t>(c, S_PCNT, (uint64_t)n_dig2 * n_blk2);
     auto* off2 = dget<uint32_t>(c, S_POFF, std::max<uint64_t>((uint64_t)n_dig2 * n_blk2, (uint64_t)n_dig1 * n_blk1));

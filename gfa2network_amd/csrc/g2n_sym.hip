@@ -129,6 +129,9 @@ struct PartSrc {
   const uint32_t* vals = nullptr;  // weighted SUM (passes 5 / 6): the entries' values as exact int32
   const uint32_t* in_w = nullptr;  //   pass 6: the values beside `in`; pass 7: the pair words
   uint32_t tile = kPartTile;       // elements per block (a quarter for small inputs: more blocks than CUs)
+  // a count matrix scanned together with the one before it (one scan launch for passes 2 and 7): the
+  // device word holding that scan's value at this matrix's start, subtracted from every offset read
+  const uint32_t* obase = nullptr;
 };
 
 // Passes 5 / 6: passes 4 / 2 of the weighted SUM CSR (coo.tocsr of a weighted COO whose duplicate
@@ -394,8 +397,13 @@ __global__ void __launch_bounds__(kPartTPB)
   __shared__ uint32_t red[kPartTPB / 64];
   PartBlock B;
   if (!part_block<kPass>(S, blockIdx.x, B)) return;
-  const uint32_t nd = kStreams * n_dig;  // pass 1: stream A's cursors (own scan, from 0) after B's
-  for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB) cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)];
+  const uint32_t nd = kStreams * n_dig;  // pass 1: stream A's cursors after B's
+  // one scan covers both streams' matrices (round 6: one launch): stream A's offsets start at B's total,
+  // the scan's value at A's first count; a matrix scanned after another one subtracts S.obase's value
+  const uint32_t ob = S.obase ? *S.obase : 0u;
+  const uint32_t obA = kSplit<kPass> ? offs[(uint64_t)n_dig * n_blk] : 0u;
+  for (uint32_t d = threadIdx.x; d < nd; d += kPartTPB)
+    cur[d] = offs[part_slot<kPass>(S, B, d, n_dig, n_blk)] - (kSplit<kPass> && d >= n_dig ? obA : ob);
   const uint32_t dmask = n_dig - 1;
   const uint32_t low = S.pair_bits - 1;  // pass 1: the pair words' b bits
   PartRaw<kPass> raw, nraw;
@@ -471,16 +479,24 @@ __device__ inline uint32_t part_total(const uint32_t* offs, const uint32_t* coun
 }
 
 // pass-1 groups -> pass-2 block map: gstart[g] = offs[g * n_blk1] (the scan at digit g, block 0),
-// bstart = scan of the groups' block counts.  One block of 1024 threads (n_groups <= 1024).
-__global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs1,
-                                                      const uint32_t* __restrict__ cnt1, uint64_t n_blk1,
-                                                      uint32_t n_groups, uint32_t* __restrict__ gstart,
-                                                      uint32_t* __restrict__ bstart, uint32_t tile) {
+// bstart = scan of the groups' block counts.  One block of 1024 threads (n_groups <= 1024) per stream:
+// block s takes the s-th count matrix (stream A's after B's, both in one scan: its offsets less the
+// scan's value at its start) and writes gstart / bstart at gstart + 2 s (n_groups + 1).
+__global__ void __launch_bounds__(1024) k_part_groups(const uint32_t* __restrict__ offs_all,
+                                                      const uint32_t* __restrict__ cnt_all, uint64_t n_blk1,
+                                                      uint32_t n_groups, uint32_t* __restrict__ gstart_all,
+                                                      uint32_t tile) {
   __shared__ uint32_t red[16];
+  const uint64_t nm = (uint64_t)n_groups * n_blk1;
+  const uint32_t* offs1 = offs_all + blockIdx.x * nm;
+  const uint32_t* cnt1 = cnt_all + blockIdx.x * nm;
+  uint32_t* gstart = gstart_all + 2 * (uint64_t)blockIdx.x * (n_groups + 1);
+  uint32_t* bstart = gstart + n_groups + 1;
+  const uint32_t sub = blockIdx.x ? offs1[0] : 0u;
   const uint32_t g = threadIdx.x;
-  const uint32_t total = part_total(offs1, cnt1, (uint64_t)n_groups * n_blk1);
-  const uint32_t s = g < n_groups ? offs1[(uint64_t)g * n_blk1] : total;
-  const uint32_t e = g + 1 < n_groups ? offs1[(uint64_t)(g + 1) * n_blk1] : total;
+  const uint32_t total = part_total(offs1, cnt1, nm) - sub;
+  const uint32_t s = g < n_groups ? offs1[(uint64_t)g * n_blk1] - sub : total;
+  const uint32_t e = g + 1 < n_groups ? offs1[(uint64_t)(g + 1) * n_blk1] - sub : total;
   const uint32_t nb = g < n_groups ? (e - s + tile - 1) / tile : 0u;
   // block scan over 1024 threads (16 waves)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -518,16 +534,19 @@ __global__ void __launch_bounds__(kTPB) k_part_bucket_starts(const uint32_t* __r
   }
   const uint32_t g = (uint32_t)(q / n_dig2), d = (uint32_t)(q % n_dig2);
   const uint32_t nb = m.bstart[g + 1] - m.bstart[g];
-  bstart_out[q] = nb ? offs2[(uint64_t)m.bstart[g] * n_dig2 + (uint64_t)d * nb] : m.gstart[g];
+  bstart_out[q] = nb ? offs2[(uint64_t)m.bstart[g] * n_dig2 + (uint64_t)d * nb] - (m.obase ? *m.obase : 0u)
+                     : m.gstart[g];
 }
 
 // single pass: bucket q = digit q, start = offs1[q * n_blk1]
+// (sub: stream A's matrix, scanned after B's: the scan's value at its start, subtracted)
 __global__ void __launch_bounds__(kTPB) k_part_bucket_starts1(const uint32_t* __restrict__ offs1,
                                                               const uint32_t* __restrict__ cnt1, uint64_t n_blk1,
-                                                              uint64_t n_buckets, uint32_t* __restrict__ bstart_out) {
+                                                              uint64_t n_buckets, uint32_t* __restrict__ bstart_out,
+                                                              const uint32_t* __restrict__ sub) {
   const uint64_t q = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
   if (q > n_buckets) return;
-  bstart_out[q] = q == n_buckets ? part_total(offs1, cnt1, n_buckets * n_blk1) : offs1[q * n_blk1];
+  bstart_out[q] = (q == n_buckets ? part_total(offs1, cnt1, n_buckets * n_blk1) : offs1[q * n_blk1]) - (sub ? *sub : 0u);
 }
 
 // ---- F: bucket finish --------------------------------------------------------------------
