@@ -802,8 +802,25 @@ static bool csr_partition_w(g2n_context* c, const int32_t* rows, const int32_t* 
   auto* tcol = (uint32_t*)(el == el1 ? dget<uint2>(c, S_EL1, n_el) : el1);
   T* tval = dget<T>(c, S_TVAL, 2 * n_el);
   fork_side(c);  // the deferred names beside the finish (as csr_partition), not after the CSR
+#ifdef G2N_F1_STAMPS
+  unsigned long long* f1st = dget<unsigned long long>(c, S_TEMP, n_bk * kF1Stamps);
+  G2N_HIP(hipMemsetAsync(f1st, 0, n_bk * kF1Stamps * 8, c->stream));
+  G2N_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g2n_f1_stamps), &f1st, sizeof(f1st), 0, hipMemcpyHostToDevice,
+                                 c->stream));
+#endif
   hipLaunchKernelGGL((k_sumw_finish<T>), dim3((unsigned)n_bk), dim3(kFinTPB), 0, c->stream, el, ew,
                      (const uint32_t*)bst, (uint32_t)low, n_rows, btot, tcol, tval, indptr, c->ctl);
+#ifdef G2N_F1_STAMPS
+  if (const char* out = std::getenv("G2N_F1_STAMPS_OUT")) {  // diagnostics build only
+    std::vector<unsigned long long> h(n_bk * kF1Stamps);
+    G2N_HIP(hipMemcpyAsync(h.data(), f1st, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    G2N_HIP(hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(out, "wb")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
   scan_excl<uint32_t, uint32_t>(c, btot, boff, n_bk, boff + n_bk);
   // (an overflowed bucket or an inexact sum is found after F2w: its placement is then dropped)

@@ -1120,6 +1120,9 @@ __device__ inline void sumw_sort_row(unsigned long long* seg, uint32_t n) {
   }
 }
 
+#ifndef G2N_F1W_MID  // experiment builds: the longest row F1w sorts by a whole wave (16: none)
+#define G2N_F1W_MID 64
+#endif
 // F1w: one block per bucket of 2^low <= kFinTPB rows (thread = row): the bucket's entries (a kElPair
 // element is the twins (a, b) and (b, a) of one value) grouped by row as (column << 32 | value) in
 // LDS, each row sorted by its lane, its column runs summed; the merged entries staged at twice the
@@ -1136,6 +1139,11 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];
   __shared__ uint32_t red[kFinTPB / 64];
+  __shared__ uint16_t mlist[kFinTPB];  // the bucket's rows of kR + 1 .. kMidRow entries
+  __shared__ uint32_t mval[kFinTPB];   // per such row: its entries kept, then its output offset
+  __shared__ uint32_t mcount;
+  F1_STAMP(0);
+  if (threadIdx.x == 0) mcount = 0;
   const uint64_t b = blockIdx.x;
   const uint32_t e0 = bstart[b], n = bstart[b + 1] - e0;
   if (n > kSymCap) {  // block-uniform
@@ -1168,6 +1176,7 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
     }
   }
   __syncthreads();
+  F1_STAMP(1);
   const uint32_t my = cnt[threadIdx.x];
   uint32_t rs;
   const uint32_t nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
@@ -1178,6 +1187,7 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
     }
     return;
   }
+  cnt[threadIdx.x] = rs;  // row starts (the mid rows' waves read them)
   cur[threadIdx.x] = rs;
   __syncthreads();
 #pragma unroll
@@ -1190,16 +1200,24 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
     }
   }
   __syncthreads();
+  F1_STAMP(2);
   const uint64_t row = (b << low) + threadIdx.x;
   const bool live = threadIdx.x <= rmask && row < n_rows;
   unsigned long long* sg = seg + rs;
   // rows of <= kR entries are sorted in registers (one LDS read each: lanes' rows sit a few
-  // entries apart, so LDS passes over them conflict on the banks), longer ones by their lane in LDS
+  // entries apart, so LDS passes over them conflict on the banks); rows of kR + 1 .. kMidRow entries
+  // (a few per bucket of a graph with hubs) by a whole wave each, bitonic across the lanes (round 6: a
+  // lane-serial sort held its wave, and the block, for ~10 us — C3's slowest tenth of buckets); longer
+  // ones by their lane in LDS
   constexpr int kR = 16;
   const bool inreg = my <= (uint32_t)kR;
+  const bool midrow = live && !inreg && my <= G2N_F1W_MID;
+  const bool longrow = live && my > G2N_F1W_MID;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (midrow) mlist[atomicAdd(&mcount, 1u)] = (uint16_t)threadIdx.x;
   unsigned long long r[kR];
 #pragma unroll
-  for (int i = 0; i < kR; i++) r[i] = (live && i < (int)my) ? sg[i] : ~0ull;  // padding sorts last
+  for (int i = 0; i < kR; i++) r[i] = (live && inreg && i < (int)my) ? sg[i] : ~0ull;  // padding sorts last
   {  // one network per wave: the longest in-register row of the wave picks it (no divergent sorts)
     uint32_t wm = (live && inreg) ? my : 0u;
 #if G2N_DPP_SCAN && G2N_SYM_DPP
@@ -1211,42 +1229,126 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
     else if (wm > 4) sumw_sort_net<8>(r);
     else if (wm > 1) sumw_sort_net<4>(r);
   }
+  if (longrow) sumw_sort_row(sg, my);
+  __syncthreads();  // mlist
+  const uint32_t n_mid = mcount;  // block-uniform
+  // a mid row's lanes: entry `lane` of the row at s0 (sorted in place by the first visit); run ends and
+  // run starts by shuffles
+  auto mid_runs = [&](uint32_t s0, uint32_t nr, unsigned long long& x, bool& last, uint32_t& sl) {
+    const uint32_t col = (uint32_t)(x >> 32);
+    const bool valid = lane < nr;
+    const uint32_t pcol = (uint32_t)__shfl_up((int)col, 1, 64), ncol = (uint32_t)__shfl_down((int)col, 1, 64);
+    const bool start = valid && (lane == 0 || pcol != col);
+    last = valid && (lane + 1 == nr || ncol != col);
+    const unsigned long long upto = (2ull << lane) - 1ull;  // lanes 0..lane
+    sl = 63u - (uint32_t)__clzll((__ballot(start) & upto) | 1ull);
+  };
+  if (n_mid) {
+    for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
+      const uint32_t rr = mlist[i], s0 = cnt[rr], nr = (rr + 1 < kFinTPB ? cnt[rr + 1] : nx) - s0;
+      unsigned long long x = lane < nr ? seg[s0 + lane] : ~0ull;
+#pragma unroll
+      for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          const unsigned long long y = __shfl_xor(x, (int)j, 64);
+          x = (((lane & j) == 0) == ((lane & k) == 0)) ? (x < y ? x : y) : (x < y ? y : x);
+        }
+      if (lane < nr) seg[s0 + lane] = x;
+      bool last;
+      uint32_t sl;
+      mid_runs(s0, nr, x, last, sl);
+      const uint32_t kept = (uint32_t)__popcll(__ballot(last));  // (the whole wave's vote, outside the branch)
+      if (lane == 0) mval[rr] = kept;
+    }
+    __syncthreads();
+  }
   uint32_t m = 0;
   if (live) {
     if (inreg) {
 #pragma unroll
       for (int i = 0; i < kR; i++)
         m += (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) ? 1u : 0u;
+    } else if (midrow) {
+      m = mval[threadIdx.x];
     } else {
-      sumw_sort_row(sg, my);
       for (uint32_t i = 0; i < my; i++) m += (i + 1 == my || (sg[i + 1] >> 32) != (sg[i] >> 32)) ? 1u : 0u;
     }
   }
+  F1_STAMP(3);
   uint32_t off;
   const uint32_t tot = block_excl_scan_n<kFinTPB>(m, &off, red);
   if (threadIdx.x == 0) btot[b] = tot;
+  F1_STAMP(4);
   if (live) {
     indptr[row] = (int32_t)off;  // local: k_sumw_place adds the bucket's offset
     if (row == n_rows - 1) indptr[n_rows] = (int32_t)(off + m);
+    if (midrow) mval[threadIdx.x] = off;
   }
   uint32_t* oc = tcol + 2 * (uint64_t)e0;
   T* ov = tval + 2 * (uint64_t)e0;
   bool exact = true;
-  // every row in registers (block-uniform): the merged entries go through LDS (columns, then values,
-  // in seg, which no lane reads any more) and out coalesced; otherwise each lane writes its own row
-  if (!__syncthreads_or(live && !inreg)) {
+  // mid and long rows straight out (before the staging below reuses seg): a long row by its lane, a mid
+  // row by its wave (each run's last lane sums the run: consecutive lanes write consecutive entries)
+  if (longrow) {
+    WSum<T> acc;
+    uint32_t j = off;
+    for (uint32_t i = 0; i < my; i++) {
+      acc.add((uint32_t)sg[i]);
+      if (i + 1 == my || (sg[i + 1] >> 32) != (sg[i] >> 32)) {
+        exact &= acc.exact();
+        oc[j] = (uint32_t)(sg[i] >> 32);
+        ov[j] = acc.value();
+        j++;
+        acc = WSum<T>{};
+      }
+    }
+  }
+  if (n_mid) {
+    __syncthreads();  // mval offsets
+    for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
+      const uint32_t rr = mlist[i], s0 = cnt[rr], nr = (rr + 1 < kFinTPB ? cnt[rr + 1] : nx) - s0, o = mval[rr];
+      unsigned long long x = lane < nr ? seg[s0 + lane] : ~0ull;
+      bool last;
+      uint32_t sl;
+      mid_runs(s0, nr, x, last, sl);
+      const unsigned long long km = __ballot(last);
+      if (last) {
+        WSum<T> acc;
+        for (uint32_t q = sl; q <= lane; q++) acc.add((uint32_t)seg[s0 + q]);
+        exact &= acc.exact();
+        const uint32_t j = o + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+        oc[j] = (uint32_t)(x >> 32);
+        ov[j] = acc.value();
+      }
+    }
+  }
+  __syncthreads();  // every segment read before the staging overwrites them
+  // the in-register rows through LDS (columns, then values, in seg) and out coalesced; the positions
+  // of the rows written above are skipped (a column marker in the first pass, remembered per thread
+  // for the second: both passes visit the same positions with the same thread)
+  {
     uint32_t* sc = (uint32_t*)seg;
     if (live) {
       uint32_t j = off;
+      if (inreg) {
 #pragma unroll
-      for (int i = 0; i < kR; i++)
-        if (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) sc[j++] = (uint32_t)(r[i] >> 32);
+        for (int i = 0; i < kR; i++)
+          if (i < (int)my && (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32))) sc[j++] = (uint32_t)(r[i] >> 32);
+      } else {
+        for (uint32_t q = 0; q < m; q++) sc[off + q] = kStagedSkip;
+      }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) oc[i] = sc[i];
+    uint32_t skip = 0;  // bit k: position threadIdx.x + k kFinTPB belongs to a row written above
+    for (uint32_t i = threadIdx.x, k = 0; i < tot; i += kFinTPB, k++) {
+      const uint32_t c = sc[i];
+      if (c == kStagedSkip) skip |= 1u << k;
+      else oc[i] = c;
+    }
     __syncthreads();
     T* sv = (T*)seg;
-    if (live) {
+    if (live && inreg) {
       WSum<T> acc;
       uint32_t j = off;
 #pragma unroll
@@ -1262,38 +1364,20 @@ __global__ void __launch_bounds__(kFinTPB) k_sumw_finish(const uint2* __restrict
       }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += kFinTPB) ov[i] = sv[i];
-  } else if (live) {
-    WSum<T> acc;
-    uint32_t j = off;
-    if (inreg) {
-#pragma unroll
-      for (int i = 0; i < kR; i++) {
-        if (i < (int)my) {
-          acc.add((uint32_t)r[i]);
-          if (i + 1 == kR || (r[i + 1] >> 32) != (r[i] >> 32)) {
-            exact &= acc.exact();
-            oc[j] = (uint32_t)(r[i] >> 32);
-            ov[j] = acc.value();
-            j++;
-            acc = WSum<T>{};
-          }
-        }
-      }
-    } else {
-      for (uint32_t i = 0; i < my; i++) {
-        acc.add((uint32_t)sg[i]);
-        if (i + 1 == my || (sg[i + 1] >> 32) != (sg[i] >> 32)) {
-          exact &= acc.exact();
-          oc[j] = (uint32_t)(sg[i] >> 32);
-          ov[j] = acc.value();
-          j++;
-          acc = WSum<T>{};
-        }
-      }
-    }
+    for (uint32_t i = threadIdx.x, k = 0; i < tot; i += kFinTPB, k++)
+      if (!(skip >> k & 1u)) ov[i] = sv[i];
   }
   if (!exact) ctl->w_inexact = 1;
+#ifdef G2N_F1_STAMPS
+  F1_STAMP(5);
+  F1_STAMP(6);
+  if (threadIdx.x == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g2n_f1_stamps[blockIdx.x * kF1Stamps + 9] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // F2w: bucket b's staged entries (columns, values) to their CSR place, indptr rebased.
