@@ -952,7 +952,7 @@ def random_ceiling(records: int, ms: float):
             "source": "profiles/r01/randread_ceiling.jsonl"}
 
 
-PMC_SUMMARY = ROOT / "profiles" / "r05" / "pmc_c4.json"
+PMC_SUMMARY = ROOT / "profiles" / "r06" / "pmc_c4.json"
 
 
 def measured_traffic(kernel: str):
