@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -66,6 +67,9 @@ enum Slot {
 #ifndef G2N_F2_OVERLAP  // bucket finish: F1 / F2 in this many bucket ranges, F2 of one beside F1 of the next (1: off)
 #define G2N_F2_OVERLAP 4
 #endif
+#ifndef G2N_F2_GEOM  // 0: equal bucket ranges; r (1-99): each range r % of the one before it
+#define G2N_F2_GEOM 0
+#endif
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
 #define G2N_FIN_DIRECT 0
 #endif
@@ -93,6 +97,7 @@ constexpr uint32_t kTestNoDecPrefix = G2N_TEST_NO_DEC_PREFIX;
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  uint64_t call = 0;  // the entry-point call that last asked for it (g2n_context::call_id)
 };
 struct ScanSlot {  // a scan status slot (scan_excl): the buffer it last cleared, the epoch / ticket in use
   void* p = nullptr;
@@ -140,6 +145,8 @@ struct g2n_context {
   uint64_t range_nseg = 0;
   std::function<void()> side_work;  // launches deferred to the assembly's latency-bound finish (F1)
   std::vector<g2n::DevBuf> bufs;
+  uint64_t call_id = 0;  // entry-point calls so far (enter_call): a slot no call since asked for is stale
+  bool shared = false;   // a host entry points' cached context (shared_context): its callers hold no views
   g2n::Ctl* ctl = nullptr;    // device
   g2n::Ctl* h_ctl = nullptr;  // pinned host mirror
   hipEvent_t ev[G2N_MAX_PHASES + 1];
@@ -150,8 +157,34 @@ struct g2n_context {
 
 namespace g2n {
 
+// Every entry point that takes a context's lock opens a call here before its first dget: slots the
+// call asks for are stamped with it, so an allocation that fails in a shared context can release the
+// slots only earlier calls used (a grow-only arena keeps an earlier, larger build's buffers: 40 GB of
+// input text, say — beside which convert_format's 39 GB row band did not fit).  A caller's own
+// context (g2n_context_create) is never released behind its back: g2n_context_trim is its tool.
+static void enter_call(g2n_context* c) { c->call_id++; }
+
+// the slots no dget of the current call has touched, freed (their contents belong to finished calls;
+// results they held were valid only until this call).  Returns the bytes released.
+static uint64_t release_stale(g2n_context* c) {
+  for (hipStream_t s : {c->stream, c->side, c->place})
+    if (s) (void)hipStreamSynchronize(s);
+  uint64_t total = 0;
+  for (int s = 0; s < S_NSLOTS; s++) {
+    DevBuf& b = c->bufs[s];
+    if (!b.p || b.call == c->call_id) continue;
+    (void)hipFree(b.p);
+    total += b.cap;
+    b.p = nullptr;
+    b.cap = 0;
+    c->scan_slot[s] = ScanSlot{};  // a later allocation at the same address must be cleared again
+  }
+  return total;
+}
+
 static void* dbuf(g2n_context* c, int slot, size_t bytes) {
   DevBuf& b = c->bufs[slot];
+  b.call = c->call_id;
   if (bytes == 0) bytes = 16;
   if (b.cap < bytes) {
     if (b.p) G2N_HIP(hipFree(b.p));
@@ -160,7 +193,15 @@ static void* dbuf(g2n_context* c, int slot, size_t bytes) {
     size_t want = bytes + bytes / 8 + 256;
     if (hipMalloc(&b.p, want) != hipSuccess) {
       (void)hipGetLastError();
-      throw Failure(G2N_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+      // a host entry point's context (whose results were downloaded, whose inputs are host memory):
+      // once more without the earlier calls' buffers, and without the growth margin
+      b.p = nullptr;
+      if (c->shared && release_stale(c)) want = bytes + 256;
+      if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        throw Failure(G2N_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+      }
     }
     b.cap = want;
   }
@@ -591,12 +632,19 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                          n_bk >= 32768ull)
                             ? (uint32_t)std::min(G2N_F2_OVERLAP, 16)
                             : 1u;
+  // range k: buckets [rb(k), rb(k + 1)); G2N_F2_GEOM = r% makes each range r% of the one before it (the
+  // last F2, which nothing hides, shorter)
+  auto rb = [&](uint32_t k) -> uint64_t {
+    if (G2N_F2_GEOM <= 0 || G2N_F2_GEOM >= 100 || k == 0 || k >= n_ov) return n_bk * k / n_ov;
+    const double r = G2N_F2_GEOM / 100.0;
+    return (uint64_t)((double)n_bk * (1.0 - std::pow(r, (double)k)) / (1.0 - std::pow(r, (double)n_ov)));
+  };
   if (n_ov > 1) {
     auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
     auto* rtot = dget<uint32_t>(c, S_RTOT, n_ov);
     (void)dget<unsigned long long>(c, S_SCANST2, scan_tiles(n_bk) + 1);  // sized once, before the ranges' scans
     for (uint32_t k = 0; k < n_ov; k++) {
-      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov;
+      const uint64_t b0 = rb(k), b1 = rb(k + 1);
       if (sum)
         hipLaunchKernelGGL((k_sym_finish<T, true, false>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->stream, el,
                            (const uint32_t*)bst, (uint32_t)low, n_rows, (T)1, btot, tcol, tcn, indptr, c->ctl,
@@ -610,7 +658,7 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
       G2N_HIP(hipEventRecord(c->ov_ev[k], c->stream));
     }
     for (uint32_t k = 0; k < n_ov; k++) {
-      const uint64_t b0 = n_bk * k / n_ov, b1 = n_bk * (k + 1) / n_ov;
+      const uint64_t b0 = rb(k), b1 = rb(k + 1);
       G2N_HIP(hipStreamWaitEvent(c->place, c->ov_ev[k], 0));
       scan_excl<uint32_t, uint32_t>(c, (const uint32_t*)(btot + b0), boff + b0, b1 - b0, rtot + k, c->place, S_SCANST2);
       hipLaunchKernelGGL((k_sym_place<T, int32_t>), dim3((unsigned)(b1 - b0)), dim3(kFinTPB), 0, c->place,
@@ -2266,6 +2314,7 @@ static g2n_context* shared_context(int device) {
   auto it = g_ctx.find(device);
   if (it != g_ctx.end()) return it->second;
   g2n_context* c = context_create(device);
+  c->shared = true;
   g_ctx[device] = c;
   return c;
 }
@@ -2317,6 +2366,7 @@ static void download_result(g2n_context* c, const g2n_result& D, HostResult* H) 
 int build_host_fill(size_t len, const FillFn& fill, const g2n_options* opts, g2n_result** out, double read_ms) {
   g2n_context* c = shared_context(opts->device);
   std::lock_guard<std::mutex> lk(c->mu);
+  enter_call(c);
   G2N_HIP(hipSetDevice(c->device));
   double t0 = now_ms();
   auto* din = dget<uint8_t>(c, S_IN, len + 16);
@@ -2344,6 +2394,7 @@ int build_host_bgzf(const uint8_t* z, size_t zlen, const std::vector<ZMember>& m
                     const g2n_options* opts, g2n_result** out, double read_ms) {
   g2n_context* c = shared_context(opts->device);
   std::lock_guard<std::mutex> lk(c->mu);
+  enter_call(c);
   G2N_HIP(hipSetDevice(c->device));
   const double t0 = now_ms();
   auto* dz = dget<uint8_t>(c, S_ZIN, zlen + 16);
@@ -2427,6 +2478,7 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
   if ((uint64_t)nnz >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "2^32-1 or more entries");
   g2n_context* c = shared_context(device);
   std::lock_guard<std::mutex> lk(c->mu);
+  enter_call(c);
   G2N_HIP(hipSetDevice(c->device));
   clear_call_state(c);
   c->test_flags = test_flags & (kTestNoBuckets | kTestIndex64);  // the conversion's own rare paths
@@ -2858,6 +2910,7 @@ int g2n_build_device(g2n_context* ctx, const void* d_input, size_t len, const g2
   }
   try {
     std::lock_guard<std::mutex> lk(ctx->mu);
+    g2n::enter_call(ctx);
     G2N_HIP(hipSetDevice(ctx->device));
     return g2n::run_pipeline(ctx, (const uint8_t*)d_input, len, opts, out);
   } catch (const g2n::Failure& f) {
@@ -2938,6 +2991,7 @@ int g2n_coo_to_csr(const void* rows, const void* cols, const void* data, int64_t
     }                                                    \
     try {                                                \
       std::lock_guard<std::mutex> lk((ctx)->mu);         \
+      g2n::enter_call(ctx);                              \
       G2N_HIP(hipSetDevice((ctx)->device));              \
       body;                                              \
     } catch (const g2n::Failure& f) {                    \

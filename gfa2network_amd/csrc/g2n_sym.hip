@@ -71,6 +71,11 @@ constexpr uint32_t kSymPer = kSymCap / kFinTPB;    // 16 per thread
 #define G2N_FIN_REG 8
 #endif
 constexpr uint32_t kSymReg = G2N_FIN_REG;         // stored elements per thread kept in registers
+// F1 rows at 4-word starts (a bucket whose padded rows fit kSymCap): a short row is read with four
+// ds_read_b128 instead of up to 16 lane-irregular ds_read_b32 (most of F1's LDS bank conflicts)
+#ifndef G2N_F1_PAD
+#define G2N_F1_PAD 0
+#endif
 
 // exclusive scan of one u32 per thread over a kN-thread block; returns the block total
 template <uint32_t kN>
@@ -697,7 +702,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
                                                      int32_t* __restrict__ indices, T* __restrict__ data,
                                                      uint32_t row_base, const uint32_t* __restrict__ wa,
                                                      const uint32_t* __restrict__ bstA, uint32_t b0) {
-  __shared__ uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
+  __shared__ __attribute__((aligned(16))) uint32_t seg[kSymCap];  // values (column << 1 | side) grouped by row; then merged columns
   __shared__ uint32_t cnt[kFinTPB];
   __shared__ uint32_t cur[kFinTPB];    // placement cursors
   __shared__ uint32_t red[kFinTPB / 64];
@@ -729,6 +734,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   __syncthreads();
   const uint32_t rmask = (1u << low) - 1u;
   uint32_t my, rs, nx;  // nx: the bucket's entries, kElPair elements expanded
+  bool padded = false;  // (G2N_F1_PAD) rows at 4-word starts; block-uniform
   {
     // the first kSymReg elements per thread stay in registers from the count to the placement;
     // a bucket of more stored elements (rare: a skewed bucket) reads the rest again, so F1 keeps
@@ -781,7 +787,18 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
     __syncthreads();
     F1_STAMP(1);
     my = cnt[threadIdx.x];
-    nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
+    if constexpr (G2N_F1_PAD && !kDirect) {
+      // one scan of both layouts: the entries (low 16 bits, nx <= 2 kSymCap) and the rows rounded up
+      // to 4 words (high 16 bits); the padded layout when it fits
+      const uint32_t pm = (my + 3u) & ~3u;
+      uint32_t ex;
+      const uint32_t both = block_excl_scan_n<kFinTPB>(my | (pm << 16), &ex, red);
+      nx = both & 0xFFFFu;
+      padded = (both >> 16) <= kSymCap;
+      rs = padded ? ex >> 16 : ex & 0xFFFFu;
+    } else {
+      nx = block_excl_scan_n<kFinTPB>(my, &rs, red);
+    }
     if (nx > kSymCap) {  // block-uniform
       overflow();
       return;
@@ -815,8 +832,28 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   const uint32_t n_mid = mcount;  // block-uniform
   // short rows: registers; sorted ascending, padding sorts last
   uint32_t k[kShortRow];
+  if constexpr (G2N_F1_PAD && !kDirect) {
+    if (padded) {
 #pragma unroll
-  for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
+      for (uint32_t q4 = 0; q4 < kShortRow / 4; q4++) {
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (live && shortrow && 4 * q4 < my) v = *reinterpret_cast<const uint4*>(sg + 4 * q4);
+        k[4 * q4] = v.x;
+        k[4 * q4 + 1] = v.y;
+        k[4 * q4 + 2] = v.z;
+        k[4 * q4 + 3] = v.w;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kShortRow; q++)
+        if (!(live && shortrow && q < my)) k[q] = 0xFFFFFFFFu;
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < kShortRow; q++) k[q] = (live && shortrow && q < my) ? sg[q] : 0xFFFFFFFFu;
+  }
   {  // one network per wave: the longest short row of the wave picks it (no divergent sorts)
     uint32_t wm = (live && shortrow) ? my : 0u;
 #if G2N_DPP_SCAN && G2N_SYM_DPP
@@ -886,7 +923,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   auto none = [](uint32_t, uint32_t, uint32_t) {};
   if (n_mid) {
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : nx) - s0;
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = cur[r] - s0;  // (cur: the row's end after placement)
       uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       x = wave_sort64(x);
       if (lane < nr) seg[s0 + lane] = x;
@@ -949,7 +986,7 @@ __global__ void __launch_bounds__(kFinTPB) G2N_FIN_WAVES k_sym_finish(const uint
   __syncthreads();  // every segment read before the staging below overwrites them
   if (n_mid) {  // the wave-sorted rows, straight out (consecutive lanes write consecutive entries)
     for (uint32_t i = wv; i < n_mid; i += kFinTPB / 64) {
-      const uint32_t r = mlist[i], s0 = cnt[r], nr = (r + 1 < kFinTPB ? cnt[r + 1] : nx) - s0, o = mval[r];
+      const uint32_t r = mlist[i], s0 = cnt[r], nr = cur[r] - s0, o = mval[r];
       const uint32_t x = lane < nr ? seg[s0 + lane] : 0xFFFFFFFFu;
       wave_merge(x, nr, keep, [&](uint32_t j, uint32_t c, uint32_t kk) { out(o + j, c, kk); });
     }
