@@ -37,6 +37,7 @@ EXPORTED = [
     "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_coo_to_csr_band", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream", "g2n_context_trim",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+    "g2n_context_group_slots", "g2n_route_group_slots", "g2n_csr_from_group_slots",
     "g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_keyset_free",
     "g2n_gunzip", "g2n_gunzip_chunked", "g2n_free", "g2n_split_render", "g2n_split_get", "g2n_split_segments", "g2n_split_free", "g2n_join_names", "g2n_gather_names", "g2n_write_npz", "g2n_write_node_map", "g2n_first_bad_utf8",
 ]
@@ -64,6 +65,7 @@ TEST_FLAGS = int(os.environ.get("G2N_TEST_FLAGS", "0"), 0)  # (diagnostics: forc
 RANGE_DECIMAL = 1        # this byte range's ids are global decimals (range_s_base / range_n_segments)
 RANGE_EVIDENCE = 2       # report the range's evidence instead of checking (g2n_build_decimal_range sets it)
 RANGE_NO_VALUES = 4      # coordinates only: values left unwritten
+RANGE_SLOTS = 8          # with DECIMAL + NO_VALUES: the COO stays in the parse's group slots (no compaction)
 
 
 class Options(ctypes.Structure):
@@ -245,6 +247,9 @@ def load() -> ctypes.CDLL:
     lib.g2n_route_triplets.argtypes = [P, P, P, P, U64, I32, P, U64, U32, I32, P, P, P, P]
     lib.g2n_csr_from_coo_pair.argtypes = [P, P, P, P, U64, P, P, P, U64, I32, I64, U64, U64, I32, I32, I32,
                                           ctypes.POINTER(Result)]
+    lib.g2n_context_group_slots.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    lib.g2n_route_group_slots.argtypes = [P, P, P, P, U64, U64, U64, U64, U32, I32, P, P, P]
+    lib.g2n_csr_from_group_slots.argtypes = [P, P, P, P, U64, U64, U64, I32, U64, I32, ctypes.POINTER(Result)]
     lib.g2n_gunzip.argtypes = [P, ctypes.c_size_t, I32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
                                ctypes.POINTER(I32), ctypes.POINTER(I32)]
     lib.g2n_gunzip.restype = ctypes.c_int
@@ -282,6 +287,7 @@ def load() -> ctypes.CDLL:
     lib.g2n_keyset_free.argtypes = [P]
     lib.g2n_keyset_free.restype = None
     for f in ("g2n_keyset_create", "g2n_keyset_add", "g2n_keyset_view", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
+              "g2n_context_group_slots", "g2n_route_group_slots", "g2n_csr_from_group_slots",
               "g2n_upload_file_range", "g2n_count_device", "g2n_build_decimal_range", "g2n_order_keys",
               "g2n_rank_keys"):
         getattr(lib, f).restype = ctypes.c_int

@@ -127,6 +127,7 @@ struct g2n_context {
   uint32_t test_flags = 0;  // options.test_flags of the current build: forces rare paths (tests)
   uint64_t err_line_off = 0;  // byte offset of the last build's error line (edge-list prefix)
   g2n::GroupedCoo gcoo;       // the current build's COO, when it went to group slots
+  g2n::GroupedCoo slots;      // the last build's COO result when it stayed in group slots (G2N_RANGE_SLOTS)
   const uint32_t* wenc = nullptr;  // the current build's values as exact-int32 codes (k_values), if written
   bool no_group = false;      // redo of a build whose group-slot COO the partition refused
   g2n::ScanSlot scan_slot[g2n::S_NSLOTS];  // scan_excl's per-slot epoch / ticket state
@@ -1706,7 +1707,11 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
   // ---- the decimal-id lean parse without K1 (tile-local positions, checked and compacted after)
   // group slots when the COO's only reader is the unweighted bucket partition (a CSR output)
   const bool coo_wanted = (o->output == G2N_OUT_PARSE && !maxsym) || o->output == G2N_OUT_COO;
-  const bool grouped = !G2N_NO_GROUP_DEFAULT && !coo_wanted && !c->no_group &&
+  // ... or a sharded decimal range whose caller takes the COO as group slots (G2N_RANGE_SLOTS: unweighted,
+  // coordinates only — its route or slice CSR needs no stream order)
+  const bool slots_out = shard_dec && (o->range_flags & G2N_RANGE_SLOTS) && !(o->weight_tag && *o->weight_tag) && !bidir &&
+                         (o->range_flags & G2N_RANGE_NO_VALUES);
+  const bool grouped = !G2N_NO_GROUP_DEFAULT && (!coo_wanted || slots_out) && !c->no_group &&
                        !(c->test_flags & (kTestNoBuckets | kTestNoGroup));
   // bidirected keys / one integer weight tag: the extended tile-local instance (whole files only)
   const size_t wt_bytes = o->weight_tag ? std::strlen(o->weight_tag) : 0;
@@ -2084,6 +2089,13 @@ static int run_build(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_
     R->rows = rows;
     R->cols = cols;
     R->data = data;
+    c->slots = GroupedCoo{};
+    if (in_groups) {  // G2N_RANGE_SLOTS: the group slots themselves (g2n_context_group_slots)
+      c->slots = c->gcoo;
+      R->rows = c->gcoo.rows;
+      R->cols = c->gcoo.cols;
+      c->gcoo.active = false;
+    }
     finish_timings(c, R);
     return G2N_OK;
   }
@@ -2235,6 +2247,7 @@ static int run_edge_list(g2n_context* c, const uint8_t* in, uint64_t len, const 
 }
 
 static int run_pipeline(g2n_context* c, const uint8_t* in, uint64_t len, const g2n_options* o, g2n_result* R) {
+  c->slots = GroupedCoo{};  // (set again only by a build whose COO result stays in group slots)
   if (o->output == G2N_OUT_EDGE_LIST) return run_edge_list(c, in, len, o, R);
   return run_build(c, in, len, o, R);
 }
@@ -2751,20 +2764,31 @@ void remap_pairs(g2n_context* c, const uint32_t* map, uint64_t n_map, int32_t* r
   if (c->h_ctl->bad_id) throw Failure(G2N_E_ARG, "an id outside the map");
 }
 
+// grp (optional): rows / cols are a tile-local parse's group slots (G2N_RANGE_SLOTS) holding nnz entries
+// in all; no map, no values (their order inside an owner is then slot order, which an unweighted slice
+// CSR does not read)
 void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, const void* data, uint64_t nnz,
                     int dtype, const uint32_t* map, uint64_t n_global, uint32_t n_ranks, int transposed,
-                    int32_t* orows, int32_t* ocols, void* odata, uint32_t* starts) {
+                    int32_t* orows, int32_t* ocols, void* odata, uint32_t* starts, const GroupedCoo* grp = nullptr) {
   begin_call(c);
   if (n_ranks == 0 || n_ranks > 4096) throw Failure(G2N_E_ARG, "n_ranks out of range");
   if (nnz >= 0x7FFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^31-1 triplets");
+  if (grp && (map || data || n_ranks > kRouteMaxRanks))
+    throw Failure(G2N_E_ARG, "group slots route coordinates only, without a map, to at most 256 ranks");
   if (n_ranks <= kRouteMaxRanks) {  // stable owner partition (g2n_route.hip)
     std::vector<uint64_t> hb(n_ranks + 1);
     for (uint32_t k = 0; k <= n_ranks; k++) hb[k] = ((uint64_t)k * n_global + n_ranks - 1) / n_ranks;
     auto* bounds = dget<uint64_t>(c, S_RBOUND, n_ranks + 1);
     G2N_HIP(hipMemcpyAsync(bounds, hb.data(), hb.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-    const uint64_t n_blk = nnz ? (nnz + kRouteTile - 1) / kRouteTile : 0;
-    const uint32_t bits = n_ranks > 1 ? (uint32_t)bits_for(n_ranks) : 0u;
     RouteSrc s{rows, cols, map, nnz, n_ranks, transposed, bounds};
+    uint64_t n_blk = nnz ? (nnz + kRouteTile - 1) / kRouteTile : 0;
+    if (grp && nnz) {  // every group's tiles (those past its count exit at once)
+      s.gcount = grp->gcount;
+      s.gcap = grp->gcap;
+      s.tpg = (uint32_t)((grp->gcap + kRouteTile - 1) / kRouteTile);
+      n_blk = grp->n_groups * s.tpg;
+    }
+    const uint32_t bits = n_ranks > 1 ? (uint32_t)bits_for(n_ranks) : 0u;
     if (n_blk) {
       auto* cnt = dget<uint32_t>(c, S_PCNT, (uint64_t)n_ranks * n_blk);
       auto* off = dget<uint32_t>(c, S_POFF, (uint64_t)n_ranks * n_blk);
@@ -2816,6 +2840,46 @@ void route_triplets(g2n_context* c, const int32_t* rows, const int32_t* cols, co
   hipLaunchKernelGGL(k_row_start, dim3(grid_for((uint64_t)n_ranks + 1)), dim3(kTPB), 0, c->stream, owner_s, nnz,
                      (uint64_t)n_ranks, starts, (const Ctl*)c->ctl);
   G2N_HIP(hipStreamSynchronize(c->stream));
+}
+
+// The CSR of a one-rank sharded decimal build straight from its range build's group slots (G2N_RANGE_SLOTS:
+// with one rank every row is this rank's, so nothing routes and no stream-order COO is ever written) —
+// the one-GPU partition (csr_partition over GroupedCoo).  n_entries: the entries the slots hold in all.
+// G2N_E_UNSUPPORTED when the partition declines (an overfull bucket): the caller builds a stream COO.
+void csr_from_group_slots(g2n_context* c, const GroupedCoo& g, uint64_t n_entries, int maxsym, uint64_t n_rows,
+                          int dtype, g2n_result* R) {
+  fill_defaults(R);
+  begin_call(c);
+  if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) throw Failure(G2N_E_ARG, "unsupported dtype");
+  if ((maxsym ? 2 : 1) * n_entries >= 0xFFFFFFFFull) throw Failure(G2N_E_UNSUPPORTED, "more than 2^32-1 elements");
+  if (!n_entries || !n_rows || (c->test_flags & kTestNoBuckets))
+    throw Failure(G2N_E_UNSUPPORTED, "group slots: no entries (the stream-order route)");
+  R->dtype = dtype;
+  R->index_width = 4;
+  R->n_nodes = (int64_t)n_rows;
+  c->gcoo = g;
+  c->gcoo.active = true;
+  bool ok = false;
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    ok = csr_partition<T>(c, g.rows, g.cols, n_entries, n_rows, !maxsym, R);
+  };
+  try {
+    switch (dtype) {
+      case G2N_BOOL: go(uint8_t{}); break;
+      case G2N_INT8: go(int8_t{}); break;
+      case G2N_INT32: go(int32_t{}); break;
+      case G2N_FLOAT32: go(float{}); break;
+      default: go(double{}); break;
+    }
+  } catch (...) {
+    c->gcoo = GroupedCoo{};
+    throw;
+  }
+  c->gcoo = GroupedCoo{};
+  if (!ok) throw Failure(G2N_E_UNSUPPORTED, "group slots: the bucket partition declined (the stream-order route)");
+  R->sum_sorted = R->sum_t_sorted = 1;
+  finish_timings(c, R);
 }
 
 void csr_from_coo_pair(g2n_context* c, const int32_t* ar, const int32_t* ac, const void* ad, uint64_t an,
@@ -2895,6 +2959,7 @@ int g2n_context_trim(g2n_context* ctx, const void* const* keep, uint64_t n_keep,
     }
     ctx->wenc = nullptr;
     ctx->gcoo = g2n::GroupedCoo{};
+    ctx->slots = g2n::GroupedCoo{};
     if (freed) *freed = total;
     return G2N_OK;
   } catch (const g2n::Failure& f) {
@@ -2939,7 +3004,7 @@ int g2n_build_decimal_range(g2n_context* ctx, const void* d_input, size_t len, c
   o.range_s_base = 0;
   o.range_n_segments = 0;
   // sharded decimal ids, offset evidence instead of the check
-  o.range_flags = G2N_RANGE_DECIMAL | G2N_RANGE_EVIDENCE | (opts->range_flags & G2N_RANGE_NO_VALUES);
+  o.range_flags = G2N_RANGE_DECIMAL | G2N_RANGE_EVIDENCE | (opts->range_flags & (G2N_RANGE_NO_VALUES | G2N_RANGE_SLOTS));
   const int rc = g2n_build_device(ctx, d_input, len, &o, out);
   if (rc == G2N_OK) {
     ev6[0] = out->n_lines;
@@ -3097,6 +3162,45 @@ int g2n_route_triplets(g2n_context* ctx, const int32_t* d_rows, const int32_t* d
   if (dtype < G2N_BOOL || dtype > G2N_FLOAT64) return G2N_E_ARG;
   G2N_CTX_CALL(ctx, g2n::route_triplets(ctx, d_rows, d_cols, d_data, nnz, dtype, d_map, n_global, n_ranks, transposed,
                                         d_out_rows, d_out_cols, d_out_data, d_starts));
+  return G2N_OK;
+}
+
+int g2n_context_group_slots(g2n_context* ctx, const uint32_t** d_gcount, uint64_t* n_groups, uint64_t* gcap) {
+  if (!ctx || !d_gcount || !n_groups || !gcap) return G2N_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *d_gcount = ctx->slots.gcount;
+  *n_groups = ctx->slots.gcount ? ctx->slots.n_groups : 0;
+  *gcap = ctx->slots.gcount ? ctx->slots.gcap : 0;
+  return G2N_OK;
+}
+
+int g2n_route_group_slots(g2n_context* ctx, const int32_t* d_rows, const int32_t* d_cols, const uint32_t* d_gcount,
+                          uint64_t n_groups, uint64_t gcap, uint64_t nnz, uint64_t n_global, uint32_t n_ranks,
+                          int32_t transposed, int32_t* d_out_rows, int32_t* d_out_cols, uint32_t* d_starts) {
+  if (!d_starts || (nnz && (!d_rows || !d_cols || !d_gcount || !n_groups || !gcap || !d_out_rows || !d_out_cols)))
+    return G2N_E_ARG;
+  g2n::GroupedCoo g;
+  g.rows = d_rows;
+  g.cols = d_cols;
+  g.gcount = d_gcount;
+  g.n_groups = n_groups;
+  g.gcap = gcap;
+  G2N_CTX_CALL(ctx, g2n::route_triplets(ctx, d_rows, d_cols, nullptr, nnz, G2N_FLOAT64, nullptr, n_global, n_ranks,
+                                        transposed, d_out_rows, d_out_cols, nullptr, d_starts, &g));
+  return G2N_OK;
+}
+
+int g2n_csr_from_group_slots(g2n_context* ctx, const int32_t* d_rows, const int32_t* d_cols, const uint32_t* d_gcount,
+                             uint64_t n_groups, uint64_t gcap, uint64_t nnz, int32_t maxsym, uint64_t n_rows,
+                             int32_t dtype, g2n_result* out) {
+  if (!out || !d_rows || !d_cols || !d_gcount || !n_groups || !gcap) return G2N_E_ARG;
+  g2n::GroupedCoo g;
+  g.rows = d_rows;
+  g.cols = d_cols;
+  g.gcount = d_gcount;
+  g.n_groups = n_groups;
+  g.gcap = gcap;
+  G2N_CTX_CALL(ctx, g2n::csr_from_group_slots(ctx, g, nnz, maxsym, n_rows, dtype, out));
   return G2N_OK;
 }
 

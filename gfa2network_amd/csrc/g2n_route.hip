@@ -37,7 +37,25 @@ struct RouteSrc {
   uint32_t n_ranks;
   int transposed;
   const uint64_t* bounds;  // n_ranks + 1 row bounds (device)
+  // group slots (a tile-local parse's COO, G2N_RANGE_SLOTS): group g's entries are [g gcap, g gcap +
+  // gcount[g]); block b takes tile b % tpg of group b / tpg.  gcount null: entries [0, n)
+  const uint32_t* gcount = nullptr;
+  uint64_t gcap = 0;
+  uint32_t tpg = 1;
 };
+
+// block b's elements [e0, e1)
+__device__ __forceinline__ void route_range(const RouteSrc& s, uint64_t b, uint64_t& e0, uint64_t& e1) {
+  if (s.gcount) {
+    const uint64_t g = b / s.tpg, t = b % s.tpg;
+    const uint64_t end = g * s.gcap + s.gcount[g];
+    e0 = g * s.gcap + t * kRouteTile;
+    e1 = e0 + kRouteTile < end ? e0 + kRouteTile : end;
+  } else {
+    e0 = b * kRouteTile;
+    e1 = e0 + kRouteTile < s.n ? e0 + kRouteTile : s.n;
+  }
+}
 
 // owner of row x: the k with bounds[k] <= x < bounds[k + 1] (bounds in LDS)
 __device__ __forceinline__ uint32_t route_owner(const uint64_t* sb, uint32_t n_ranks, uint64_t x) {
@@ -74,17 +92,18 @@ __global__ void __launch_bounds__(kRouteTPB) k_route_count(RouteSrc s, uint32_t 
   for (uint32_t k = t; k <= s.n_ranks; k += kRouteTPB) sb[k] = s.bounds[k];
   for (uint32_t k = t; k < s.n_ranks; k += kRouteTPB) hist[k] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+  uint64_t base, end;
+  route_range(s, blockIdx.x, base, end);
   uint32_t own[kRouteRounds];
 #pragma unroll
   for (uint32_t r = 0; r < kRouteRounds; r++) {  // all loads in flight first
     const uint64_t i = base + r * kRouteTPB + t;
-    own[r] = i < s.n ? route_row(s, i) : 0u;
+    own[r] = i < end ? route_row(s, i) : 0u;
   }
 #pragma unroll
   for (uint32_t r = 0; r < kRouteRounds; r++) {
     const uint64_t i = base + r * kRouteTPB + t;
-    const bool valid = i < s.n;
+    const bool valid = i < end;
     const uint32_t o = valid ? route_owner(sb, s.n_ranks, own[r]) : 0u;
     const uint64_t m = route_match(o, bits, valid);
     if (valid && (m & ((1ull << lane) - 1)) == 0) atomicAdd(&hist[o], (uint32_t)__popcll(m));
@@ -106,13 +125,14 @@ __global__ void __launch_bounds__(kRouteTPB) k_route_scatter(RouteSrc s, uint32_
   for (uint32_t k = t; k <= s.n_ranks; k += kRouteTPB) sb[k] = s.bounds[k];
   for (uint32_t k = t; k < s.n_ranks; k += kRouteTPB) run[k] = off[(uint64_t)k * n_blk + blockIdx.x];
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+  uint64_t base, end;
+  route_range(s, blockIdx.x, base, end);
   int32_t ra[kRouteRounds], rb[kRouteRounds];
 #pragma unroll
   for (uint32_t r = 0; r < kRouteRounds; r++) {  // the tile's coordinates, all loads in flight first
     const uint64_t i = base + r * kRouteTPB + t;
     ra[r] = rb[r] = 0;
-    if (i < s.n) {
+    if (i < end) {
       ra[r] = s.rows[i];
       rb[r] = s.cols[i];
     }
@@ -120,7 +140,7 @@ __global__ void __launch_bounds__(kRouteTPB) k_route_scatter(RouteSrc s, uint32_
 #pragma unroll
   for (uint32_t r = 0; r < kRouteRounds; r++) {
     const uint64_t i = base + r * kRouteTPB + t;
-    const bool valid = i < s.n;
+    const bool valid = i < end;
     int32_t a = ra[r], b = rb[r];
     if (valid) {
       if (s.map) {
@@ -160,7 +180,7 @@ __global__ void __launch_bounds__(kRouteTPB) k_route_scatter(RouteSrc s, uint32_
   }
 }
 
-// starts[k] = first output of owner k (off[k * n_blk]), starts[n_ranks] = n
+// starts[k] = first output of owner k (off[k * n_blk]), starts[n_ranks] = n (the elements routed)
 __global__ void k_route_starts(const uint32_t* __restrict__ off, uint64_t n_blk, uint32_t n_ranks, uint64_t n,
                                uint32_t* __restrict__ starts) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;

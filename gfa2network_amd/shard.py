@@ -74,6 +74,14 @@ class LocalShard:
     n_cast_overflow: int = 0
     parse_path: str = ""  # build_decimal: "tile_local" (the one-pass lean parse) or "k1" (tile counts first)
     phase_ms: dict = field(default_factory=dict)  # the local build's device phases (hipEvents; diagnostics)
+    # G2N_RANGE_SLOTS: rows / cols are the parse's group slots (device pointer of the per-group counts,
+    # groups, entries per group) holding n_trip entries in all; None: rows / cols in stream order
+    slots: tuple | None = None
+    n_trip: int = -1
+
+    def triplets(self) -> int:
+        """The entries the COO holds (rows.numel(), unless it is in group slots)."""
+        return self.n_trip if self.slots is not None else int(self.rows.numel())
 
 
 @dataclass
@@ -107,6 +115,7 @@ class ShardResult:
     parse_path: str = ""  # fast path: how this rank's range was parsed ("tile_local" or "k1")
     coo: tuple | None = None  # keep_coo: this range's stream-order triplets over global ids
     a2a_bytes_sent: int = 0  # bytes this rank's all-to-all-v calls sent to other ranks (diagnostics)
+    coo_layout: str = ""  # fast path: "group_slots" (routed / assembled from the parse's slots) or "stream"
 
     @property
     def names(self) -> list | None:
@@ -328,6 +337,7 @@ class HipEngine:
     so no torch), DevBuf arrays allocated through the HIP runtime."""
 
     supports_views = True
+    supports_slots = True  # build_decimal_range(slots=True) / route_slots / csr_slots (G2N_RANGE_SLOTS)
 
     def __init__(self, device: int = 0, torch_buffers: bool = True):
         if torch_buffers:
@@ -522,13 +532,17 @@ class HipEngine:
             return None
         return self._decimal_shard(res, opts, view)
 
-    def build_decimal_range(self, buf, opts: dict, view: bool = False, values: bool = True):
+    def build_decimal_range(self, buf, opts: dict, view: bool = False, values: bool = True, slots: bool = False):
         """The range parsed into GLOBAL decimal ids before the ranges' counts are known (one pass, no
         count: g2n_build_decimal_range): (LocalShard, evidence [lines, S lines, edges, records, d,
         largest edge key]) — the caller checks d against the S lines before the range and the key
-        against the file's S count — or None when the one pass declines (count + build_decimal then)."""
+        against the file's S count — or None when the one pass declines (count + build_decimal then).
+        slots (view, no values): the COO may stay in the parse's group slots (LocalShard.slots), read
+        only by route_slots / csr_slots."""
         o = nat.make_options(output=nat.OUT_COO, want_node_names=False, device=self.device_index, **opts)
         o.range_flags = 0 if values else nat.RANGE_NO_VALUES  # values: the caller reads them (a COO result, weights)
+        if slots and view and not values:
+            o.range_flags |= nat.RANGE_SLOTS
         res = nat.Result()
         ev = (ctypes.c_int64 * 6)()
         self._build_ctx()
@@ -548,7 +562,14 @@ class HipEngine:
                         n_records_before_error=res.n_records, n_edges=res.n_edges, n_local_nodes=res.n_nodes,
                         n_cast_overflow=res.n_cast_overflow)
         tdt = TORCH_DTYPES[opts.get("dtype", "float64")]
-        if view:
+        gc, ng, cap = ctypes.c_void_p(), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        if view and self.lib.g2n_context_group_slots(self.ctx_b, ctypes.byref(gc), ctypes.byref(ng),
+                                                     ctypes.byref(cap)) == 0 and ng.value:
+            cap_all = ng.value * cap.value  # (the slots' capacity: views over every group's slot)
+            sh.rows, sh.cols = DevArray(res.rows or 0, cap_all, 4), DevArray(res.cols or 0, cap_all, 4)
+            sh.data = None
+            sh.slots, sh.n_trip = (gc.value, ng.value, cap.value), n
+        elif view:
             sh.rows, sh.cols = DevArray(res.rows or 0, n, 4), DevArray(res.cols or 0, n, 4)
             sh.data = DevArray(res.data or 0, n, np.dtype(tdt).itemsize)
         else:
@@ -654,6 +675,47 @@ class HipEngine:
             n_global, n_ranks, int(transposed), orows.data_ptr() if nz else None, ocols.data_ptr() if nz else None,
             odata.data_ptr() if nz and odata is not None else None, starts.data_ptr()), "g2n_route_triplets")
         return orows, ocols, odata, starts
+
+    def route_slots(self, local: LocalShard, n_global: int, n_ranks: int, transposed: bool):
+        """route_triplets of a group-slot COO (coordinates only): (rows, cols, None, starts)."""
+        n = local.n_trip
+        orows = self._empty(n, "int32")
+        ocols = self._empty(n, "int32")
+        starts = self._empty(n_ranks + 1, "int32")
+        gc, ng, cap = local.slots
+        self._sync()
+        nz = n > 0
+        self._check(self.lib.g2n_route_group_slots(
+            self.ctx, local.rows.data_ptr() if nz else None, local.cols.data_ptr() if nz else None, gc if nz else None,
+            ng, cap, n, n_global, n_ranks, int(transposed), orows.data_ptr() if nz else None,
+            ocols.data_ptr() if nz else None, starts.data_ptr()), "g2n_route_group_slots")
+        return orows, ocols, None, starts
+
+    def csr_slots(self, local: LocalShard, maxsym: bool, n_rows: int, dtype: str, copy: bool = True):
+        """A one-rank group's whole CSR straight from the range build's group slots
+        (g2n_csr_from_group_slots), or None when the partition declines (the caller then takes the
+        stream-order route)."""
+        res = nat.Result()
+        gc, ng, cap = local.slots
+        self._sync()
+        rc = self.lib.g2n_csr_from_group_slots(self.ctx, local.rows.data_ptr(), local.cols.data_ptr(), gc, ng, cap,
+                                               local.n_trip, int(maxsym), n_rows, nat.DTYPE_CODES[dtype],
+                                               ctypes.byref(res))
+        if rc == nat.E_UNSUPPORTED:
+            return None
+        self._check(rc, "g2n_csr_from_group_slots")
+        return self._csr_out(res, n_rows, dtype, copy)
+
+    def _csr_out(self, res, n_rows: int, dtype: str, copy: bool):
+        tdt = TORCH_DTYPES[dtype]
+        if not copy:
+            w = np.dtype(tdt).itemsize
+            iw = 8 if res.index_width == 8 else 4
+            return (DevArray(res.indptr or 0, n_rows + 1, iw), DevArray(res.indices or 0, res.nnz, iw),
+                    DevArray(res.data or 0, res.nnz, w))
+        idx = "int64" if res.index_width == 8 else "int32"
+        return (self._copy_out(res.indptr, n_rows + 1, idx), self._copy_out(res.indices, res.nnz, idx),
+                self._copy_out(res.data, res.nnz, tdt))
 
     def csr_pair(self, a, t, maxsym: bool, row_base: int, n_rows: int, n_cols: int, dtype: str, uniform: bool,
                  force_unsorted: int, copy: bool = True):
@@ -868,8 +930,11 @@ def _route(engine, C, local, dtype, gmap, n_global, maxsym, uniform, tm):
         return (local.rows, local.cols, d), ((local.cols, local.rows, d) if maxsym else None)
 
     def route(transposed):
-        rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, None if uniform else local.data,
-                                               local.dtype_name, gmap, n_global, C.world, transposed)
+        if local.slots is not None:  # group slots (G2N_RANGE_SLOTS, uniform): the route compacts them
+            rr, cc, dd, st = engine.route_slots(local, n_global, C.world, transposed)
+        else:
+            rr, cc, dd, st = engine.route_triplets(local.rows, local.cols, None if uniform else local.data,
+                                                   local.dtype_name, gmap, n_global, C.world, transposed)
         st_l = [int(v) for v in st.tolist()]
         cnt = [st_l[k + 1] - st_l[k] for k in range(C.world)]
         return tuple(C.a2av_multi([rr, cc, dd], cnt)[0])
@@ -901,11 +966,15 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
         return ok and 0 < n and n * tps < 2**31 - 1, n
 
     local, allc = None, None
+    # the COO left in the parse's group slots when nothing reads it in stream order (no COO result, unit
+    # values): routed straight from them, or at one rank turned into the CSR straight from them
+    slots = getattr(engine, "supports_slots", False) and not keep_coo
     if (hasattr(engine, "build_decimal_range") and not opts.get("bidirected") and not opts.get("weight_tag")
             and not opts.get("strip_orientation")):
         # one pass, no count: every range parses into global ids first and reports its evidence; one
         # all-gather decides for every rank at once (g2n_build_decimal_range)
-        got = engine.build_decimal_range(buf, opts, view=not keep_coo, values=keep_coo)
+        got = engine.build_decimal_range(buf, opts, view=not keep_coo, values=keep_coo,
+                                         **({"slots": True} if slots else {}))
         alle = C.allgather_list(got[1] if got is not None else [-1] * 6)
         tm["count"] = 0.0
         if all(e[0] >= 0 for e in alle):
@@ -942,10 +1011,26 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
         tm["build"] = (time.perf_counter() - t0) * 1e3 - tm["count"]
     n_global = n_seg * tps
     local.dtype_name = opts.get("dtype", "float64")
-    a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"), tm)
-    row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
-                                                   opts.get("weight_tag"), tm, copy_out)
-    sums = C.allreduce_sum([local.n_cast_overflow, int(indices.numel()), int(local.rows.numel())], engine.device)
+    n_trip = local.triplets()
+    got_csr = None
+    if C.world == 1 and local.slots is not None:
+        # one rank: no route, and the slice is the whole matrix — the single-GPU partition reads the slots
+        t4 = time.perf_counter()
+        tm["route"] = 0.0
+        got_csr = engine.csr_slots(local, maxsym, n_global, local.dtype_name, copy=copy_out)
+        if got_csr is None:  # the partition declined (an overfull bucket): the range's stream-order COO
+            local = engine.build_decimal_range(buf, opts, view=True, values=False)[0]
+            local.dtype_name = opts.get("dtype", "float64")
+        else:
+            tm["csr"] = (time.perf_counter() - t4) * 1e3
+            row_lo, row_hi = 0, n_global
+            indptr, indices, vals = got_csr
+    if got_csr is None:
+        a, tstream = _route(engine, C, local, local.dtype_name, None, n_global, maxsym, not opts.get("weight_tag"),
+                            tm)
+        row_lo, row_hi, indptr, indices, vals = _slice(engine, C, a, tstream, maxsym, n_global, local.dtype_name,
+                                                       opts.get("weight_tag"), tm, copy_out)
+    sums = C.allreduce_sum([local.n_cast_overflow, int(indices.numel()), n_trip], engine.device)
     out = ShardResult(status=0, n_lines=int(sum(c[0] for c in allc)), n_records=int(sum(c[3] for c in allc)),
                       n_edges=int(sum(c[2] for c in allc)), n_nodes=n_global, row_lo=row_lo, row_hi=row_hi,
                       indptr=indptr, indices=indices, data=vals, n_cast_overflow=sums[0],
@@ -957,6 +1042,7 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
     out.a2a_bytes_sent = C.sent
     out.fast_path = True
     out.parse_path = getattr(local, "parse_path", "")
+    out.coo_layout = "group_slots" if getattr(local, "slots", None) is not None else "stream"
     if keep_coo:
         out.coo = (local.rows, local.cols, local.data)
     return out

@@ -112,8 +112,13 @@ enum {
                                    weights) */
   G2N_RANGE_EVIDENCE = 2,       /* with DECIMAL: report the range's evidence instead of checking the
                                    premise (set by g2n_build_decimal_range) */
-  G2N_RANGE_NO_VALUES = 4       /* no weight tag and the caller reads coordinates only: the result's
+  G2N_RANGE_NO_VALUES = 4,      /* no weight tag and the caller reads coordinates only: the result's
                                    values are left unwritten */
+  G2N_RANGE_SLOTS = 8           /* with DECIMAL and NO_VALUES (unweighted, not bidirected): the COO stays
+                                   in the tile-local parse's group slots (no stream-order compaction);
+                                   result rows / cols are the slot arrays, nnz the entries they hold,
+                                   the layout from g2n_context_group_slots — what
+                                   g2n_route_group_slots and g2n_csr_from_group_slots read */
 };
 
 /* g2n_options.test_flags (tests only; every real build leaves 0): the same results through a path
@@ -388,6 +393,25 @@ int g2n_csr_from_coo_pair(g2n_context *ctx, const int32_t *a_rows, const int32_t
                           uint64_t a_nnz, const int32_t *t_rows, const int32_t *t_cols, const void *t_data,
                           uint64_t t_nnz, int32_t maxsym, int64_t row_base, uint64_t n_rows, uint64_t n_cols,
                           int32_t dtype, int32_t uniform, int32_t force_unsorted, g2n_result *out);
+
+/* Group slots (round 6): a sharded decimal range built with G2N_RANGE_SLOTS keeps its COO where the
+ * tile-local parse wrote it — group g's entries at [g * gcap, g * gcap + gcount[g]) of rows / cols —
+ * instead of compacting it into stream order.  g2n_context_group_slots reports the last build's layout
+ * on ctx (n_groups 0: the last build left none); valid until ctx's next build.
+ * g2n_route_group_slots: g2n_route_triplets of those slots (coordinates only, no map, n_ranks <= 256;
+ *   nnz = the entries they hold; within an owner the order is slot order, which an unweighted slice
+ *   CSR does not read).
+ * g2n_csr_from_group_slots: a ONE-rank group's whole CSR (row_base 0, n_rows rows) from the slots —
+ *   the SUM CSR (maxsym 0) or A.maximum(A.T) (maxsym 1) of unit values, the single-GPU bucket
+ *   partition; G2N_E_UNSUPPORTED when it declines (no entries, an overfull bucket): the caller then
+ *   builds the range's stream-order COO and calls g2n_csr_from_coo_pair. */
+int g2n_context_group_slots(g2n_context *ctx, const uint32_t **d_gcount, uint64_t *n_groups, uint64_t *gcap);
+int g2n_route_group_slots(g2n_context *ctx, const int32_t *d_rows, const int32_t *d_cols, const uint32_t *d_gcount,
+                          uint64_t n_groups, uint64_t gcap, uint64_t nnz, uint64_t n_global, uint32_t n_ranks,
+                          int32_t transposed, int32_t *d_out_rows, int32_t *d_out_cols, uint32_t *d_starts);
+int g2n_csr_from_group_slots(g2n_context *ctx, const int32_t *d_rows, const int32_t *d_cols, const uint32_t *d_gcount,
+                             uint64_t n_groups, uint64_t gcap, uint64_t nnz, int32_t maxsym, uint64_t n_rows,
+                             int32_t dtype, g2n_result *out);
 
 /* The general protocol's global node ids (shard.py step 4; builders.py:194-198 first-touch order
  * across byte ranges), on an owner rank's distinct keys (g2n_dedup_keys):

@@ -52,31 +52,40 @@ def _worker(rank, world, port, outdir):
         from oracle import oracle as orc
 
         eng = HipEngine(0)
-        for name, (data, modes) in _inputs().items():
+        cases = [(name, data, mode, False) for name, (data, modes) in _inputs().items() for mode in modes]
+        if world == 1:  # the one-rank slot partition declining (an overfull bucket): the stream-order route
+            cases += [(name, data, mode, True) for name, data, mode, _ in cases if name == "synthetic"]
+        for name, data, mode, decline in cases:
             lo, hi = line_ranges(data, world)[rank]
             buf = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy()).to(eng.device)
-            for mode in modes:
-                res = build_sharded(buf, engine=eng, gather_names=True, **mode)
-                assert res.status == 0, (name, mode, res.status)
-                assert res.fast_path == (name == "synthetic"), (name, mode)  # decimal ids: no id exchange
-                indptr, indices, vals = gather_csr(res)
-                if rank != 0:
-                    continue
-                full = orc.run(data, **mode)
-                want = [bytes(full.names_blob[full.names_offsets[i]:full.names_offsets[i + 1]])
-                        for i in range(full.n_nodes)]
-                assert res.names == want, (name, mode)
-                wp, wi, wd = ((full.ms_indptr, full.ms_indices, full.ms_data) if full.maxsym
-                              else (full.sum_indptr, full.sum_indices, full.sum_data))
-                assert np.array_equal(indptr, wp) and np.array_equal(indices, wi), (name, mode)
-                assert vals.tobytes() == np.ascontiguousarray(wd).tobytes(), (name, mode)
+            if decline:
+                eng.csr_slots = lambda *a, **k: None
+            res = build_sharded(buf, engine=eng, gather_names=True, **mode)
+            if decline:
+                del eng.csr_slots
+                assert res.coo_layout == "stream", (name, mode)
+            assert res.status == 0, (name, mode, res.status)
+            assert res.fast_path == (name == "synthetic"), (name, mode)  # decimal ids: no id exchange
+            if res.fast_path and not mode.get("bidirected") and not decline:  # the range parse's group slots,
+                assert res.coo_layout == "group_slots", (name, mode)  # routed / assembled in place
+            indptr, indices, vals = gather_csr(res)
+            if rank != 0:
+                continue
+            full = orc.run(data, **mode)
+            want = [bytes(full.names_blob[full.names_offsets[i]:full.names_offsets[i + 1]])
+                    for i in range(full.n_nodes)]
+            assert res.names == want, (name, mode)
+            wp, wi, wd = ((full.ms_indptr, full.ms_indices, full.ms_data) if full.maxsym
+                          else (full.sum_indptr, full.sum_indices, full.sum_data))
+            assert np.array_equal(indptr, wp) and np.array_equal(indices, wi), (name, mode)
+            assert vals.tobytes() == np.ascontiguousarray(wd).tobytes(), (name, mode)
         eng.close()
         np.save(os.path.join(outdir, f"ok{rank}.npy"), np.zeros(1))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_gpu_sharded_build_equals_single_file(gpu, oracle_lib, tmp_path, world):
     import torch.multiprocessing as mp
 
