@@ -10,7 +10,6 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
-#include <cmath>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -66,9 +65,6 @@ enum Slot {
 #endif
 #ifndef G2N_F2_OVERLAP  // bucket finish: F1 / F2 in this many bucket ranges, F2 of one beside F1 of the next (1: off)
 #define G2N_F2_OVERLAP 4
-#endif
-#ifndef G2N_F2_GEOM  // 0: equal bucket ranges; r (1-99): each range r % of the one before it
-#define G2N_F2_GEOM 0
 #endif
 #ifndef G2N_FIN_DIRECT  // bucket finish: 1 = F1 places its entries (look-back; measured slower), 0 = F1 stages + F2
 #define G2N_FIN_DIRECT 0
@@ -633,13 +629,9 @@ static bool csr_partition(g2n_context* c, const int32_t* rows, const int32_t* co
                          n_bk >= 32768ull)
                             ? (uint32_t)std::min(G2N_F2_OVERLAP, 16)
                             : 1u;
-  // range k: buckets [rb(k), rb(k + 1)); G2N_F2_GEOM = r% makes each range r% of the one before it (the
-  // last F2, which nothing hides, shorter)
-  auto rb = [&](uint32_t k) -> uint64_t {
-    if (G2N_F2_GEOM <= 0 || G2N_F2_GEOM >= 100 || k == 0 || k >= n_ov) return n_bk * k / n_ov;
-    const double r = G2N_F2_GEOM / 100.0;
-    return (uint64_t)((double)n_bk * (1.0 - std::pow(r, (double)k)) / (1.0 - std::pow(r, (double)n_ov)));
-  };
+  // range k: buckets [rb(k), rb(k + 1)), equal ranges (ranges shrinking geometrically, so that the last F2
+  // is shorter, measured slower: 70 % steps over 4 or 6 ranges, 55 % over 4, +0.06-0.18 ms per C4 build)
+  auto rb = [&](uint32_t k) -> uint64_t { return n_bk * k / n_ov; };
   if (n_ov > 1) {
     auto* boff = dget<uint32_t>(c, S_MOFF, n_bk + 1);
     auto* rtot = dget<uint32_t>(c, S_RTOT, n_ov);

@@ -72,7 +72,8 @@ constexpr uint32_t kSymPer = kSymCap / kFinTPB;    // 16 per thread
 #endif
 constexpr uint32_t kSymReg = G2N_FIN_REG;         // stored elements per thread kept in registers
 // F1 rows at 4-word starts (a bucket whose padded rows fit kSymCap): a short row is read with four
-// ds_read_b128 instead of up to 16 lane-irregular ds_read_b32 (most of F1's LDS bank conflicts)
+// ds_read_b128 instead of up to 16 lane-irregular ds_read_b32 — measured neutral on C4 (maxsym 2.427-2.441
+// against 2.442-2.444 ms, same box, round 6): the short-row reads are not what holds F1
 #ifndef G2N_F1_PAD
 #define G2N_F1_PAD 0
 #endif
