@@ -772,8 +772,8 @@ class Comm:
         """a2av of several tensors with the same per-rank counts: one count exchange for all of
         them (None entries pass through as None)."""
         torch = self.torch
-        if self.world == 1:  # everything stays: the tensors themselves (no caller writes into what it received)
-            return list(xs), list(send_counts)
+        if self.world == 1:  # a copy, as the send-to-self part of a real all-to-all (force_protocol times it)
+            return [None if x is None else x.clone() for x in xs], list(send_counts)
         ref = next(x for x in xs if x is not None)
         dev = ref.device
         host = self._c(ref[:0]).device
@@ -1550,9 +1550,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     else:
         n_global = nd
         gid = torch.arange(nd, dtype=torch.int64, device=dev)
-    # (one rank: rank 0's map is the identity, so nothing goes back)
-    back = (C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)[0]
-            if world > 1 else None)
+    back, _ = C.a2av(gid[ids.to(torch.int64)].to(torch.int32) if nd else gid[:0].to(torch.int32), r_kc)
     gmap = None
     if rank > 0:  # rank 0's map is the identity (step 5)
         gmap = torch.empty(local.n_local_nodes, dtype=torch.int32, device=dev)
