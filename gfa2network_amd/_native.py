@@ -34,7 +34,7 @@ FMT_COO, FMT_CSR, FMT_TEXT = 0, 1, 2
 # every symbol include/g2n.h declares (tests check the library exports all of them)
 EXPORTED = [
     "g2n_version", "g2n_abi_version", "g2n_options_init", "g2n_device_count", "g2n_device_memory", "g2n_last_error",
-    "g2n_status_name", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
+    "g2n_status_name", "g2n_release_shared", "g2n_build_from_path", "g2n_build_from_buffer", "g2n_result_free",
     "g2n_coo_to_csr", "g2n_coo_to_csr_band", "g2n_context_create", "g2n_context_destroy", "g2n_context_stream", "g2n_context_trim",
     "g2n_build_device", "g2n_build_decimal_range", "g2n_count_device", "g2n_order_keys", "g2n_rank_keys", "g2n_upload_file_range", "g2n_partition_keys", "g2n_dedup_keys", "g2n_gather_keys", "g2n_remap_pairs", "g2n_route_triplets", "g2n_csr_from_coo_pair",
     "g2n_context_group_slots", "g2n_route_group_slots", "g2n_csr_from_group_slots",
@@ -247,6 +247,8 @@ def load() -> ctypes.CDLL:
     lib.g2n_route_triplets.argtypes = [P, P, P, P, U64, I32, P, U64, U32, I32, P, P, P, P]
     lib.g2n_csr_from_coo_pair.argtypes = [P, P, P, P, U64, P, P, P, U64, I32, I64, U64, U64, I32, I32, I32,
                                           ctypes.POINTER(Result)]
+    lib.g2n_release_shared.argtypes = [I32, ctypes.POINTER(U64)]
+    lib.g2n_release_shared.restype = ctypes.c_int
     lib.g2n_context_group_slots.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]
     lib.g2n_route_group_slots.argtypes = [P, P, P, P, U64, U64, U64, U64, U32, I32, P, P, P]
     lib.g2n_csr_from_group_slots.argtypes = [P, P, P, P, U64, U64, U64, I32, U64, I32, ctypes.POINTER(Result)]
@@ -754,6 +756,15 @@ def device_memory(device: int = 0) -> tuple[int, int]:
     if rc != OK:
         raise RuntimeError(f"{status_name(rc)}: {last_error()}")
     return int(f.value), int(t.value)
+
+
+def release_shared(device: int = 0) -> int:
+    """Free the host entry points' cached buffers on `device` (g2n_release_shared): bytes released."""
+    freed = ctypes.c_uint64(0)
+    rc = load().g2n_release_shared(int(device), ctypes.byref(freed))
+    if rc != OK:
+        raise RuntimeError(f"{status_name(rc)}: {last_error()}")
+    return int(freed.value)
 
 
 def version() -> str:

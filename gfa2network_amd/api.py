@@ -373,11 +373,16 @@ def _gz_inflated_estimate(p: str, size: int) -> int:
     return max(isize, 4 * size)
 
 
-def _free_hbm(device: int) -> int | None:
+def _free_hbm(device: int, need: int = 0) -> int | None:
     """Free HBM of `device` (hipMemGetInfo through the C-ABI: no torch on the one-GPU path); None
-    without such a device (the build itself then raises G2N_E_DEVICE)."""
+    without such a device (the build itself then raises G2N_E_DEVICE).  When that is less than `need`,
+    the host entry points' cached buffers (an earlier build's arena, g2n_release_shared) are released
+    first and the free HBM read again: a cache must not send a build that fits to the chunked route."""
     try:
-        return nat.device_memory(device)[0]
+        free = nat.device_memory(device)[0]
+        if free < need and nat.release_shared(device):
+            free = nat.device_memory(device)[0]
+        return free
     except RuntimeError:
         return None
 
@@ -386,7 +391,7 @@ def _chunk_plan(size: int, device: int) -> int:
     """The chunk size that lets an input of `size` bytes whose working set (WORKING_SET_PER_INPUT_BYTE
     x its size) exceeds the GPU's free HBM be built on this GPU alone (shard.build_chunked), or 0 (the
     one-piece build): each chunk's working set is then about half the free HBM."""
-    free = _free_hbm(device)
+    free = _free_hbm(device, need=size * WORKING_SET_PER_INPUT_BYTE)
     if free is None or size * WORKING_SET_PER_INPUT_BYTE <= free:
         return 0
     return max(1 << 26, int(free // (2 * WORKING_SET_PER_INPUT_BYTE)))
@@ -425,7 +430,7 @@ def _one_gpu_chunked(path, chunk_bytes, device: int, **kw):
         return None, path  # the one-piece build raises the reference's OSError
     size = os.path.getsize(p)
     if p.endswith(".gz"):
-        free = None if chunk_bytes else _free_hbm(device)
+        free = None if chunk_bytes else _free_hbm(device, need=_gz_inflated_estimate(p, size) * WORKING_SET_PER_INPUT_BYTE)
         if not chunk_bytes and (free is None or _gz_inflated_estimate(p, size) * WORKING_SET_PER_INPUT_BYTE <= free):
             return None, path
         with open(p, "rb") as fh:
@@ -511,7 +516,7 @@ def _want_shard(path, shard: str, device: int) -> bool:
         p = str(path)
         size = os.path.getsize(p)
         work = (_gz_inflated_estimate(p, size) if p.endswith(".gz") else size) * WORKING_SET_PER_INPUT_BYTE
-        free = _free_hbm(device)
+        free = _free_hbm(device, need=work)
         need = int(free is not None and work > free)
     ident = zlib.crc32(os.fsencode(os.path.abspath(str(path)))) if here else 0
     size = os.path.getsize(str(path)) if here else -1

@@ -2960,6 +2960,18 @@ int g2n_context_trim(g2n_context* ctx, const void* const* keep, uint64_t n_keep,
   }
 }
 
+int g2n_release_shared(int32_t device, uint64_t* freed) {
+  g2n_context* c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g2n::g_ctx_mu);
+    auto it = g2n::g_ctx.find(device);
+    if (it != g2n::g_ctx.end()) c = it->second;
+  }
+  if (freed) *freed = 0;
+  if (!c) return G2N_OK;  // no host entry point has used this device yet: nothing cached
+  return g2n_context_trim(c, nullptr, 0, freed);
+}
+
 int g2n_build_device(g2n_context* ctx, const void* d_input, size_t len, const g2n_options* opts, g2n_result* out) {
   if (!ctx || !opts || !out || (len && !d_input)) {
     g2n::set_last_error("g2n_build_device: null argument");

@@ -239,8 +239,15 @@ class _HipAlloc:
 
     def __init__(self, hip, device: int, nbytes: int):
         self.hip, self.ptr = hip, ctypes.c_void_p()
-        if hip.hipSetDevice(device) != 0 or hip.hipMalloc(ctypes.byref(self.ptr), max(int(nbytes), 16)) != 0:
-            raise MemoryError(f"hipMalloc of {nbytes} bytes failed on device {device}")
+        if hip.hipSetDevice(device) != 0:
+            raise MemoryError(f"hipSetDevice({device}) failed")
+        if hip.hipMalloc(ctypes.byref(self.ptr), max(int(nbytes), 16)) != 0:
+            hip.hipGetLastError()
+            # once more without the host entry points' cached buffers (g2n_release_shared)
+            if not nat.release_shared(device) or hip.hipMalloc(ctypes.byref(self.ptr), max(int(nbytes), 16)) != 0:
+                hip.hipGetLastError()
+                self.ptr = ctypes.c_void_p()
+                raise MemoryError(f"hipMalloc of {nbytes} bytes failed on device {device}")
 
     def __del__(self):
         try:

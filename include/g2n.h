@@ -200,6 +200,11 @@ int g2n_device_count(void);                    /* HIP devices visible (0 without
 /* hipMemGetInfo of `device`: free / total HBM bytes (G2N_E_DEVICE without such a device).  What
  * parse_gfa sizes its one-GPU chunked build by (gfa2network_amd/api.py), without torch. */
 int g2n_device_memory(int32_t device, uint64_t *free_bytes, uint64_t *total_bytes);
+/* The host entry points (g2n_build_from_path / _buffer, g2n_coo_to_csr) keep one cached context per
+ * device whose grow-only buffers outlive the call (results are host copies).  This frees them all
+ * (*freed: the bytes released): what parse_gfa does before sizing a build against free HBM when an
+ * earlier, larger build's buffers would otherwise count as used. */
+int g2n_release_shared(int32_t device, uint64_t *freed);
 const char *g2n_last_error(void);              /* thread-local message of the last failure */
 const char *g2n_status_name(int status);
 

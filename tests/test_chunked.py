@@ -253,7 +253,7 @@ def test_parse_gfa_chunks_every_input_kind(oracle_lib, tmp_path, monkeypatch, ki
 
     data = _named_gfa(34, 200, 900, True)
     _cpu_engine_factory(monkeypatch, __import__("oracle.oracle", fromlist=["x"]))
-    monkeypatch.setattr(api, "_free_hbm", lambda device=0: 1000)  # every input is past the working set
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0, need=0: 1000)  # every input is past the working set
     monkeypatch.setattr(api, "_chunk_plan", lambda size, device: 1500 if size * 8 > 1000 else 0)
     calls = []
     real = api._parse_gfa_chunked
@@ -344,10 +344,10 @@ def test_chunk_plan_only_past_free_memory(tmp_path, monkeypatch):
 
     size = 10 << 20
     for free, want in ((size * api.WORKING_SET_PER_INPUT_BYTE + 1, False), (size, True)):
-        monkeypatch.setattr(api, "_free_hbm", lambda device=0, f=free: f)
+        monkeypatch.setattr(api, "_free_hbm", lambda device=0, need=0, f=free: f)
         got = api._chunk_plan(size, 0)
         assert bool(got) == want and (not got or got >= 1 << 26)
-    monkeypatch.setattr(api, "_free_hbm", lambda device=0: None)
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0, need=0: None)
     assert api._chunk_plan(size, 0) == 0
 
 

@@ -441,7 +441,7 @@ def test_gpu_chunked_gzip_and_default_route(gpu, oracle_lib, tmp_path, monkeypat
     calls = []
     real = api._parse_gfa_chunked
     monkeypatch.setattr(api, "_parse_gfa_chunked", lambda *a, **k: calls.append(a[1]) or real(*a, **k))
-    monkeypatch.setattr(api, "_free_hbm", lambda device=0: len(data) * 2)  # the working set does not fit
+    monkeypatch.setattr(api, "_free_hbm", lambda device=0, need=0: len(data) * 2)  # the working set does not fit
     monkeypatch.setattr(api, "_chunk_plan", lambda size, device: (len(data) // 3 + 1) if size * 8 > len(data) * 2 else 0)
     import io
 
@@ -550,7 +550,7 @@ import numpy as np
 from gfa2network_amd import api, parse_gfa
 
 path, out, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
-api._free_hbm = lambda device=0: n * 2  # the working set (8 x the input) does not fit
+api._free_hbm = lambda device=0, need=0: n * 2  # the working set (8 x the input) does not fit
 api._chunk_plan = lambda size, device: (n // 3 + 1) if size * 8 > n * 2 else 0
 res = {}
 for k, mode in enumerate(json.loads(sys.argv[4])):

@@ -314,10 +314,10 @@ def _want_worker(rank, world, port, paths, outdir):
 
         size = os.path.getsize(paths[0])
         free = size * api.WORKING_SET_PER_INPUT_BYTE * (4 if rank == 0 else 0.5)
-        api._free_hbm = lambda device=None: int(free)
+        api._free_hbm = lambda device=None, need=0: int(free)
         assert api._want_shard(paths[0], "auto", 0) is True
         assert api._want_shard(paths[0], "never", 0) is False
-        api._free_hbm = lambda device=None: 10**15
+        api._free_hbm = lambda device=None, need=0: 10**15
         assert api._want_shard(paths[0], "auto", 0) is False  # fits everywhere
         with pytest.raises(ValueError, match="same file"):
             api._want_shard(paths[rank], "always", 0)
