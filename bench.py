@@ -203,12 +203,14 @@ def config_leg(lib, nat, synth, wl, device: int, steps: int, warmup: int) -> dic
     avg = {k: sum(p.get(k, 0.0) for p in phases) / len(phases) for k in phases[0]}
     dev_ms = sum(avg.values())
     b_alg = algorithmic_bytes(int(res.input_bytes), int(res.n_nodes), int(res.nnz), 8)
+    traffic, src = build_traffic(wl.name)
     return {"workload": f"{wl.name}: {wl.note}", "ms_per_step": round(dt * 1e3, 3),
             "m_edges_per_s": round(int(res.n_edges) / dt / 1e6, 2),
             "gb_per_s_ingested": round(int(res.input_bytes) / dt / 1e9, 2), "nnz": int(res.nnz),
             "device_ms_per_step": round(dev_ms, 3), "phase_ms": {k: round(v, 3) for k, v in avg.items()},
             "pipeline_roofline": {"bound": "hbm", "b_alg_bytes": b_alg,
-                                  "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                                  "frac": round(b_alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "traffic": traffic, "traffic_source": src}}
 
 
 def cpu_baseline(workload, links: int) -> dict:
@@ -965,6 +967,25 @@ def measured_traffic(kernel: str):
         return None, None
     k = doc.get("kernels", {}).get(kernel, {})
     return k.get("traffic_bytes_per_launch"), {"file": str(PMC_SUMMARY.relative_to(ROOT)), "commit": doc.get("commit")}
+
+
+def build_traffic(workload: str):
+    """HBM bytes of one whole build of `workload` (every kernel's 2 x FETCH_SIZE + WRITE_SIZE times its
+    launches) from its committed PMC summary (profiles/r06/pmc_<workload>.json, one build:
+    tools/gpu_counters.sh with --steps 1 --warmup 0), or (None, None)."""
+    f = PMC_SUMMARY.parent / f"pmc_{workload.lower()}.json"
+    try:
+        doc = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return None, None
+    # (not the input generator's kernels: k_synth_len / k_synth_write and its 64-bit scan, which a CSR
+    # build of these configs never launches)
+    ks = [v for n, v in doc.get("kernels", {}).items()
+          if "synth" not in n and n != "g2n::k_scan_excl<unsigned long, unsigned long>"]
+    if not ks or any("launches" not in k or k.get("traffic_bytes_per_launch") is None for k in ks):
+        return None, None
+    return (int(sum(k["traffic_bytes_per_launch"] * k["launches"] for k in ks)),
+            {"file": str(f.relative_to(ROOT)), "commit": doc.get("commit"), "per": "build"})
 
 
 if __name__ == "__main__":

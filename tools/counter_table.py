@@ -28,7 +28,8 @@ for k, m in vals.items():
     for (disp, cn), v in m.items():
         per[cn].append(sum(v))  # summed over dimensions (XCDs / SEs) of one dispatch
     avg = {cn: sum(v) / len(v) for cn, v in per.items()}
-    row = {"ms": round(sorted(dur[k])[len(dur[k]) // 2], 3) if dur[k] else None}
+    row = {"ms": round(sorted(dur[k])[len(dur[k]) // 2], 3) if dur[k] else None,
+           "launches": max(len({disp for (disp, cn) in m if cn == c}) for c in {cn for (_, cn) in m})}
     if "FETCH_SIZE" in avg:  # KiB
         row["traffic_bytes_per_launch"] = round((2 * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024)
         row["hbm_GB"] = round((2 * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024 / 1e9, 3)
@@ -50,6 +51,7 @@ for k, r in sorted(out.items(), key=lambda kv: -(kv[1]["ms"] or 0)):
 if len(sys.argv) > 3:
     Path(sys.argv[2]).write_text(json.dumps({
         "commit": sys.argv[3], "source": "tools/gpu_counters.sh (rocprofv3 --pmc, one pass per counter group, "
-        "kernel-trace only) on `bench.py --steps 1 --warmup 0` (C4)",
+        "kernel-trace only) on `bench.py --steps 1 --warmup 0` (one build; launches = dispatches of the kernel "
+        "in one pass)",
         "correction": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: gfx950 FETCH_SIZE = 1/2 of a "
         "wide streaming read; WRITE_SIZE exact)", "kernels": out}, indent=1))
