@@ -144,6 +144,7 @@ struct g2n_context {
   std::vector<g2n::DevBuf> bufs;
   uint64_t call_id = 0;  // entry-point calls so far (enter_call): a slot no call since asked for is stale
   bool shared = false;   // a host entry points' cached context (shared_context): its callers hold no views
+  size_t hbm_total = 0;  // the device's HBM (hipMemGetInfo at creation)
   g2n::Ctl* ctl = nullptr;    // device
   g2n::Ctl* h_ctl = nullptr;  // pinned host mirror
   hipEvent_t ev[G2N_MAX_PHASES + 1];
@@ -177,6 +178,21 @@ static uint64_t release_stale(g2n_context* c) {
     c->scan_slot[s] = ScanSlot{};  // a later allocation at the same address must be cleared again
   }
   return total;
+}
+
+// After a host entry point's call (its results already downloaded): a shared context keeps its buffers
+// for the next call only while they hold at most a quarter of the device — a 1.1G-edge build's 100+ GB
+// arena would otherwise stay reserved behind every later allocation of the process.
+static void shrink_shared(g2n_context* c) {
+  if (!c->shared || !c->hbm_total) return;
+  uint64_t held = 0;
+  for (const DevBuf& b : c->bufs) held += b.p ? b.cap : 0;
+  if (held <= c->hbm_total / 4) return;
+  c->call_id++;  // (every slot is an earlier call's now)
+  (void)release_stale(c);
+  c->gcoo = GroupedCoo{};
+  c->slots = GroupedCoo{};
+  c->wenc = nullptr;
 }
 
 static void* dbuf(g2n_context* c, int slot, size_t bytes) {
@@ -2320,6 +2336,9 @@ static g2n_context* shared_context(int device) {
   if (it != g_ctx.end()) return it->second;
   g2n_context* c = context_create(device);
   c->shared = true;
+  size_t f = 0, t = 0;
+  if (hipMemGetInfo(&f, &t) == hipSuccess) c->hbm_total = t;
+  (void)hipGetLastError();
   g_ctx[device] = c;
   return c;
 }
@@ -2391,6 +2410,7 @@ int build_host_fill(size_t len, const FillFn& fill, const g2n_options* opts, g2n
   H->r.host_ms_read = read_ms;
   H->r.host_ms_h2d = t1 - t0;
   H->r.host_ms_d2h = now_ms() - t2;
+  shrink_shared(c);
   *out = &H->r;
   return H->r.status;
 }
@@ -2441,6 +2461,7 @@ int build_host_bgzf(const uint8_t* z, size_t zlen, const std::vector<ZMember>& m
     H->r.phase_names[H->r.n_phases] = "gz_inflate";
     H->r.phase_ms[H->r.n_phases++] = inflate_ms;
   }
+  shrink_shared(c);
   *out = &H->r;
   return H->r.status;
 }
@@ -2537,6 +2558,7 @@ int coo_to_csr(const void* rows, const void* cols, const void* data, int64_t nnz
     delete H;
     throw;
   }
+  shrink_shared(c);
   *out = &H->r;
   return G2N_OK;
 }

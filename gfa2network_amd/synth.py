@@ -111,6 +111,8 @@ class DeviceInput:
         spec = Spec(n_segments, n_links, seed, int(rc_tag), NAME_MODES[names], int(far_links))
         ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
         rc = lib.g2n_synth_device(device, ctypes.byref(spec), ctypes.byref(ptr), ctypes.byref(n))
+        if rc == _native.E_NOMEM and _native.release_shared(device):  # once more without the host cache
+            rc = lib.g2n_synth_device(device, ctypes.byref(spec), ctypes.byref(ptr), ctypes.byref(n))
         if rc:
             raise RuntimeError(f"g2n_synth_device failed ({_native.status_name(rc)})")
         self.ptr, self.len, self.device = ptr.value, n.value, device
