@@ -160,6 +160,39 @@ def _dtype_of(dtype) -> np.dtype:
     return dt
 
 
+def _unit_dtype(dtype) -> np.dtype | None:
+    """A dtype outside the five the kernels compute in, for a build whose every value is dtype(1.0) (no
+    weight tag: builders.py:224-228 appends 1.0): the build then runs in int32 and its values — copy counts
+    k of each entry (the SUM CSR's k, MAX-SYM's max(k_A, k_AT): builders.py:282-283) — become the sum of
+    k ones in that dtype (_unit_values).  None for the five native dtypes."""
+    dt = np.dtype(dtype)
+    return None if dt.name in nat.DTYPE_CODES else dt
+
+
+def _unit_values(counts: np.ndarray, dt: np.dtype) -> np.ndarray:
+    """The sum of k ones in dtype dt for each copy count k (scipy sums duplicates in the matrix dtype):
+    k itself while it is exact; an integer dtype whose sums would wrap raises NotImplementedError (a
+    documented limit); scipy.sparse's own dtype check raises first for what it does not support."""
+    sp.coo_matrix((np.zeros(0, dtype=dt), (np.zeros(0, np.int32), np.zeros(0, np.int32))), shape=(1, 1))
+    k = np.asarray(counts)
+    if k.size and dt.kind in "iu" and int(k.max()) > np.iinfo(dt).max:
+        raise NotImplementedError(f"copy counts up to {int(k.max())} wrap in {dt}: not supported by the GPU path")
+    return k.astype(dt)
+
+
+def _with_unit_dtype(out, dt: np.dtype, return_node_list: bool):
+    """An int32 unit-valued build's result in dtype dt (values: _unit_values of its copy counts)."""
+    A = out[0] if return_node_list else out
+    if A.format == "coo":  # every value is dtype(1.0)
+        A = sp.coo_matrix((_unit_values(np.ones(A.nnz, dtype=np.int32), dt), (A.row, A.col)), shape=A.shape)
+    else:
+        B = sp.csr_matrix((_unit_values(A.data, dt), A.indices, A.indptr), shape=A.shape)
+        if A.indptr.dtype == np.int64 and B.indptr.dtype != np.int64:  # (finalize's index-dtype rule)
+            B.indices, B.indptr = A.indices, A.indptr
+        A = B
+    return (A, out[1]) if return_node_list else A
+
+
 def parse_gfa(
     path,
     *,
@@ -214,6 +247,17 @@ def parse_gfa(
         raise ValueError("return_node_list requires build_matrix=True")
     if build_graph:
         raise NotImplementedError("graph objects (build_graph=True) are outside the GPU GFA->CSR path")
+    ext = _unit_dtype(dtype) if build_matrix else None
+    if ext is not None:  # another numpy dtype: unit values only, built in int32
+        if weight_tag:
+            raise NotImplementedError(f"dtype {ext} with a weight tag is not supported by the GPU path "
+                                      f"(supported: {', '.join(nat.DTYPE_CODES)})")
+        out = parse_gfa(path, build_graph=False, build_matrix=True, directed=directed, weight_tag=None,
+                        strip_orientation=strip_orientation, verbose=verbose, bidirected=bidirected,
+                        keep_directed_bidir=keep_directed_bidir, dtype="int32", asymmetric=asymmetric,
+                        raw_bytes_id=raw_bytes_id, return_node_list=return_node_list, device=device, shard=shard,
+                        chunk_bytes=chunk_bytes)
+        return _with_unit_dtype(out, ext, return_node_list)
     dt = _dtype_of(dtype) if build_matrix else np.dtype("float64")
     if shard not in ("auto", "always", "never"):
         raise ValueError("shard must be 'auto', 'always' or 'never'")
@@ -741,18 +785,34 @@ def _keep_index_dtype(M, raw):
     return M
 
 
+def _coo_data(A):
+    """The COO's values as the kernels take them: a dtype outside the native five only when every value
+    is 1 (then int32 ones, the sums mapped back by _unit_values), else NotImplementedError."""
+    ext = _unit_dtype(A.dtype)
+    if ext is None:
+        return A.data, None
+    if not bool(np.all(A.data == 1)):
+        raise NotImplementedError(f"GPU COO->CSR of dtype {ext} takes unit values only "
+                                  f"(any values: {', '.join(nat.DTYPE_CODES)})")
+    return np.ones(len(A.data), dtype=np.int32), ext
+
+
 def _native_tocsr(A, device: int = 0):
     """scipy coo.tocsr() on the GPU: duplicates summed in dtype in scipy's order."""
     n_rows, n_cols = A.shape
-    raw = nat.coo_to_csr(A.row, A.col, A.data, n_rows, n_cols, device)
-    return _keep_index_dtype(sp.csr_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
+    data, ext = _coo_data(A)
+    raw = nat.coo_to_csr(A.row, A.col, data, n_rows, n_cols, device)
+    vals = raw.data if ext is None else _unit_values(raw.data, ext)
+    return _keep_index_dtype(sp.csr_matrix((vals, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
 
 
 def _native_tocsc(A, device: int = 0):
     """scipy coo.tocsc(): the CSR of the transposed coordinates, read as CSC."""
     n_rows, n_cols = A.shape
-    raw = nat.coo_to_csr(A.col, A.row, A.data, n_cols, n_rows, device)
-    return _keep_index_dtype(sp.csc_matrix((raw.data, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
+    data, ext = _coo_data(A)
+    raw = nat.coo_to_csr(A.col, A.row, data, n_cols, n_rows, device)
+    vals = raw.data if ext is None else _unit_values(raw.data, ext)
+    return _keep_index_dtype(sp.csc_matrix((vals, raw.indices, raw.indptr), shape=A.shape, dtype=A.dtype), raw)
 
 
 def convert_format(A, fmt: str, *, verbose: bool = False):

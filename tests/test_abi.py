@@ -88,8 +88,8 @@ def test_out_of_scope_options_raise(tmp_path):
         parse_gfa(p, build_graph=False, build_matrix=True, backend="igraph")
     with pytest.raises(ValueError, match="return_node_list requires build_matrix=True"):
         parse_gfa(p, build_graph=False, build_matrix=False, return_node_list=True)
-    with pytest.raises(NotImplementedError):
-        parse_gfa(p, build_graph=False, build_matrix=True, dtype="float16")
+    with pytest.raises(NotImplementedError):  # another dtype with weights (unit values: test_unit_dtypes.py)
+        parse_gfa(p, build_graph=False, build_matrix=True, dtype="int64", weight_tag="RC")
 
 
 def test_join_names_matches_python():
