@@ -1026,7 +1026,10 @@ def _build_decimal_sharded(buf, engine, C, opts, gd, maxsym, gather_names, tm, k
         tm["route"] = 0.0
         got_csr = engine.csr_slots(local, maxsym, n_global, local.dtype_name, copy=copy_out)
         if got_csr is None:  # the partition declined (an overfull bucket): the range's stream-order COO
-            local = engine.build_decimal_range(buf, opts, view=True, values=False)[0]
+            again = engine.build_decimal_range(buf, opts, view=True, values=False)
+            if again is None:  # (one rank: the general protocol decides alone)
+                return None
+            local = again[0]
             local.dtype_name = opts.get("dtype", "float64")
         else:
             tm["csr"] = (time.perf_counter() - t4) * 1e3
