@@ -1533,7 +1533,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
     byte_counts = [int(po_l[k + 1] - po_l[k]) for k in range(world)]
     lens = (po[1:] - po[:-1]) if local.n_local_nodes else torch.zeros(0, dtype=torch.int64, device=dev)
     r_blob, _ = C.a2av(pb[:int(po_l[-1])] if local.n_local_nodes else pb[:0], byte_counts)
-    (r_lens, r_idx), r_kc = C.a2av_multi([lens, pidx.to(torch.int64)], key_counts)
+    # (the local ids travel as int32: order_keys widens the arrivals it reads)
+    (r_lens, r_idx), r_kc = C.a2av_multi([lens, pidx], key_counts)
     r_off = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
     if r_lens.numel():
         r_off[1:] = torch.cumsum(r_lens, 0)
@@ -1546,8 +1547,8 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         ids, first_of, nd = engine.dedup_keys(r_blob, r_off)
     tm["dedup_keys"] = (time.perf_counter() - t7) * 1e3
     # order key (source rank, local id) of each distinct key: global first-touch order
-    fo = first_of.to(torch.int64)
-    dkey = engine.order_keys(first_of, r_idx, r_kc) if nd and world > 1 else r_idx[:0]
+    dkey = (engine.order_keys(first_of, r_idx.to(torch.int64), r_kc) if nd and world > 1
+            else r_idx[:0].to(torch.int64))
     tm["owner_dedup"] = (time.perf_counter() - t1) * 1e3
 
     # 4. global ids: rank of each distinct key's order key among all owners' (one owner: its order)
@@ -1574,7 +1575,7 @@ def build_sharded(buf, *, engine, group=None, directed=True, bidirected=False, k
         # the owner's distinct keys (bytes at r_off[first_of]) with their global ids, to the
         # gathering rank(s) in one blob + lengths each; put in id order there (g2n_gather_names)
         t5 = time.perf_counter()
-        d_lens = r_lens[fo] if nd else r_lens[:0]
+        d_lens = r_lens[first_of.to(torch.int64)] if nd else r_lens[:0]
         d_off = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
         if nd:
             d_off[1:] = torch.cumsum(d_lens, 0)
