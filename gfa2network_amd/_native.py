@@ -471,6 +471,9 @@ def coo_to_csr(rows: np.ndarray, cols: np.ndarray, data: np.ndarray, n_rows: int
     res = ctypes.POINTER(Result)()
     rc = lib.g2n_coo_to_csr(r.ctypes.data, c.ctypes.data, d.ctypes.data, len(d), n_rows, n_cols, 4,
                             DTYPE_CODES[dt.name], device, flags, ctypes.byref(res))
+    if rc == E_NOMEM and release_shared(device):  # once more without what caches held
+        rc = lib.g2n_coo_to_csr(r.ctypes.data, c.ctypes.data, d.ctypes.data, len(d), n_rows, n_cols, 4,
+                                DTYPE_CODES[dt.name], device, flags, ctypes.byref(res))
     if rc == E_UNSUPPORTED and len(d) > BAND_ENTRIES:  # past one call's limit: row bands
         return _coo_to_csr_bands(r, c, d, n_rows, n_cols, device, BAND_ENTRIES)
     if rc == E_UNSUPPORTED:  # a documented size limit (include/g2n.h)
@@ -513,6 +516,9 @@ def _coo_to_csr_bands(r, c, d, n_rows: int, n_cols: int, device: int, limit: int
         res = ctypes.POINTER(Result)()
         rc = lib.g2n_coo_to_csr_band(br.ctypes.data, bc.ctypes.data, bd.ctypes.data, len(bd), hi - lo, n_cols,
                                      DTYPE_CODES[dt.name], device, force, ctypes.byref(res))
+        if rc == E_NOMEM and release_shared(device):  # once more without what caches held
+            rc = lib.g2n_coo_to_csr_band(br.ctypes.data, bc.ctypes.data, bd.ctypes.data, len(bd), hi - lo, n_cols,
+                                         DTYPE_CODES[dt.name], device, force, ctypes.byref(res))
         if rc == E_UNSUPPORTED:
             raise NotImplementedError(f"GPU COO->CSR band: {last_error()}")
         out = _from_result(res, rc)
@@ -759,12 +765,21 @@ def device_memory(device: int = 0) -> tuple[int, int]:
 
 
 def release_shared(device: int = 0) -> int:
-    """Free the host entry points' cached buffers on `device` (g2n_release_shared): bytes released."""
+    """Free the host entry points' cached buffers on `device` (g2n_release_shared) and, when torch is
+    already loaded in this process, its allocator's unused cached blocks — HBM that only caches held:
+    what an allocation that failed retries without.  Returns the library's bytes released (torch's
+    count 1 when it released any)."""
     freed = ctypes.c_uint64(0)
     rc = load().g2n_release_shared(int(device), ctypes.byref(freed))
     if rc != OK:
         raise RuntimeError(f"{status_name(rc)}: {last_error()}")
-    return int(freed.value)
+    n = int(freed.value)
+    torch = sys.modules.get("torch")  # (never imported here: the one-GPU path runs without torch)
+    if torch is not None and torch.cuda.is_initialized():
+        before = torch.cuda.memory_reserved(device)
+        torch.cuda.empty_cache()
+        n += 1 if torch.cuda.memory_reserved(device) < before else 0
+    return n
 
 
 def version() -> str:
