@@ -81,3 +81,18 @@ def test_dist_setup_without_a_group_refuses_more_gpus(monkeypatch):
     with pytest.raises(SystemExit, match="--gpus 4"):
         bench._dist_setup(4)
     assert bench._dist_setup(1) == (1, 0, 0)
+
+
+def test_build_traffic_sums_every_build_kernel_once_per_launch():
+    """The C2 / C3 legs' whole-build HBM traffic (bench.build_traffic): every kernel's per-launch
+    2 x FETCH_SIZE + WRITE_SIZE times its launches, the input generator's kernels left out — from the
+    committed summaries, and None for a workload without one."""
+    import json
+
+    for w in ("C2", "C3"):
+        t, src = bench.build_traffic(w)
+        doc = json.loads((bench.ROOT / src["file"]).read_text())
+        want = sum(k["traffic_bytes_per_launch"] * k["launches"] for n, k in doc["kernels"].items()
+                   if "synth" not in n and n != "g2n::k_scan_excl<unsigned long, unsigned long>")
+        assert t == want > 0 and src["commit"] == doc["commit"] and src["per"] == "build"
+    assert bench.build_traffic("C9") == (None, None)
